@@ -1,0 +1,202 @@
+#!/usr/bin/env python3
+"""Batched BPE encode throughput on MI355X -- the BASELINE.json metric.
+
+One step = one pass of the encode hot path (merge loop + id compaction, k_encode_tiles ->
+k_scan_tiles -> k_compact -> k_string_offsets) over one batch already resident in HBM:
+  N=1  BASELINE configs[1]/[2]: 1 GiB synthetic MIXED UTF-8, 1M strings (mean 1074 B), 32k-merge
+       byte-level table, cl100k pre-split on the host (the GPU pre-splitter is not built yet, so
+       this is reported as the C3 workload), GPU merge loop.
+  N>1  configs[3]: every rank encodes its own 1 GiB corpus (seed + rank; doc-sharded), then the
+       token-id buffers are reassembled on every rank with an RCCL all-gather (padded to the
+       largest rank's count) -- weak scaling, the gather is inside the step.
+Prints ONE JSON line (rank 0).  Launch for N>1:
+  python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \\
+      --master-port P bench.py --gpus N
+"""
+import argparse
+import ctypes
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "encoded MB/s (input bytes) + Mtokens/s at 32k merges, 1/2/4/8 MI355X vs CPU ref"
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (/opt/skills/guides/MI355X_MICROARCH.md)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--config", default="c3", choices=["c3", "c5"],
+                    help="c3: 1 GiB MIXED + 32k merges (configs[1]/[2]); c5: stress, 50k merges")
+    ap.add_argument("--strings", type=int, default=None)
+    ap.add_argument("--mean-len", type=int, default=None)
+    ap.add_argument("--pattern", default="cl100k", choices=["cl100k", "gpt2"])
+    ap.add_argument("--no-gather", action="store_true", help="N>1: skip the RCCL reassembly")
+    ap.add_argument("--cpu-sample-mb", type=float, default=96.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--threads", type=int, default=16, help="host threads for corpus/pre-split")
+    return ap.parse_args()
+
+
+def main():
+    args = parse()
+    rank = int(os.environ.get("RANK", 0))
+    world = int(os.environ.get("WORLD_SIZE", args.gpus))
+    local = int(os.environ.get("LOCAL_RANK", 0))
+    if world != args.gpus:
+        raise SystemExit("WORLD_SIZE=%d but --gpus %d" % (world, args.gpus))
+
+    import torch
+    import torch.distributed as dist
+
+    from shredword_amd import Tokenizer, _lib, corpus
+
+    if world > 1:
+        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+
+    c5 = args.config == "c5"
+    kind = corpus.STRESS if c5 else corpus.MIXED
+    n_str = args.strings or (1_000_000 if not c5 else 1_000_000)
+    mean = args.mean_len or (1074 if not c5 else 600)
+    model = "bl50k.model" if c5 else "bl32k.model"
+    pat = {"cl100k": _lib.SW_PAT_CL100K, "gpt2": _lib.SW_PAT_GPT2}[args.pattern]
+
+    t = time.time()
+    buf, off = corpus.synth(1_000_003 + rank, kind, n_str, mean, n_threads=args.threads)
+    bits, n_chunks = corpus.presplit(buf, off, pat, n_threads=args.threads)
+    t_prep = time.time() - t
+    n_bytes = int(off[-1])
+
+    tok = Tokenizer(device=local)
+    tok.load(os.path.join(ROOT, "tests", "golden", model))
+    tok.pattern = pat
+    L = _lib.lib()
+    h = tok._encoder()
+    _lib.check(L.sw_encoder_reserve(h, n_bytes, n_str))
+
+    cap = torch.tensor([n_bytes], dtype=torch.int64, device=dev)
+    if world > 1:
+        dist.all_reduce(cap, op=dist.ReduceOp.MAX)
+    d_buf = torch.from_numpy(buf).to(dev)
+    d_off = torch.from_numpy(off).to(dev)
+    d_bits = torch.from_numpy(bits.view(np.int64)).to(dev)
+    d_out = torch.empty(int(cap.item()), dtype=torch.int32, device=dev)
+    d_oo = torch.empty(n_str + 1, dtype=torch.int64, device=dev)
+    stream = torch.cuda.current_stream(dev).cuda_stream
+
+    def encode(n_tok_ptr=None):
+        _lib.check(L.sw_encode_device(h, d_buf.data_ptr(), n_bytes, d_off.data_ptr(), n_str, d_bits.data_ptr(),
+                                      d_out.data_ptr(), d_oo.data_ptr(), stream, n_tok_ptr))
+
+    n_tok_c = ctypes.c_int64()
+    encode(ctypes.byref(n_tok_c))
+    n_tok = int(n_tok_c.value)
+    gather = world > 1 and not args.no_gather
+    if gather:
+        counts = torch.zeros(world, dtype=torch.int64, device=dev)
+        dist.all_gather_into_tensor(counts, torch.tensor([n_tok], dtype=torch.int64, device=dev))
+        max_cnt = int(counts.max().item())
+        gathered = torch.empty(world * max_cnt, dtype=torch.int32, device=dev)
+        disp = torch.cumsum(counts, 0) - counts
+
+    def step():
+        encode()
+        if gather:
+            dist.all_gather_into_tensor(gathered, d_out[:max_cnt])
+
+    for _ in range(args.warmup):
+        step()
+    _lib.check(L.sw_encoder_set_timing(h, 1))
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    if world > 1:
+        dist.barrier()
+    k_ms = L.sw_encoder_last_kernel_ms(h)
+    _lib.check(L.sw_encoder_set_timing(h, 0))
+    elapsed = torch.tensor([t1 - t0], dtype=torch.float64, device=dev)
+    totals = torch.tensor([n_bytes, n_tok, n_str, n_chunks], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
+        dist.all_reduce(totals, op=dist.ReduceOp.SUM)
+    sec = float(elapsed.item())
+    all_bytes, all_tok, all_str, all_chunks = (float(x) for x in totals.tolist())
+    ms_step = sec / args.steps * 1e3
+    value = all_bytes * args.steps / sec / 1e6
+
+    # roofline of the dominant kernel (k_encode_tiles), rank-local, per launch
+    b_algo = n_bytes + 4 * n_tok + 16 * (n_str + 1) + (n_bytes + 7) // 8
+    achieved = b_algo / (k_ms * 1e-3) / 1e9 if k_ms > 0 else None
+    roofline = {"bound": "hbm", "achieved": round(achieved, 2) if achieved else None, "peak": HBM_PEAK_GBS,
+                "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5) if achieved else None,
+                "traffic": None, "kernel": "k_encode_tiles", "kernel_ms": round(k_ms, 4),
+                "algo_bytes_per_launch": int(b_algo)}
+
+    # parity spot-check + CPU baseline (rank 0, N=1 only): the oracle on a bounded prefix of the
+    # same corpus; the GPU ids for that prefix must be bit-identical
+    cpu = None
+    parity = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import oracle
+        k = int(np.searchsorted(off, args.cpu_sample_mb * 1e6, side="right")) - 1
+        k = max(1, min(k, n_str))
+        sbuf, soff = buf[:int(off[k])], off[:k + 1]
+        om = oracle.OracleModel(tok.merges)
+        tc = time.perf_counter()
+        ids_cpu, ooff_cpu = om.encode_batch(sbuf, soff, pat, n_threads=1)
+        dt1 = time.perf_counter() - tc
+        tc = time.perf_counter()
+        om.encode_batch(sbuf, soff, pat, n_threads=args.threads)
+        dtm = time.perf_counter() - tc
+        got = d_out[:int(ooff_cpu[-1])].cpu().numpy()
+        got_off = d_oo[:k + 1].cpu().numpy()
+        parity = bool(np.array_equal(got, ids_cpu) and np.array_equal(got_off, ooff_cpu))
+        cpu = {"value": round(len(sbuf) / dt1 / 1e6, 3), "unit": "MB/s", "cores": 1, "kind": "port",
+               "sample": "first %d strings (%.1f MB) of the same corpus, oracle/sw_oracle.c, 1 thread, "
+                         "host pre-split + merge loop" % (k, len(sbuf) / 1e6),
+               "value_all_threads": round(len(sbuf) / dtm / 1e6, 3), "threads_all": args.threads,
+               "python_reference_mb_s": 0.33}
+
+    if rank == 0:
+        line = {
+            "metric": METRIC, "value": round(value, 3), "unit": "MB/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(ms_step, 4), "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": "int32", "data": "synthetic",
+            "config": {"workload": ("C5 stress, 50k merges" if c5 else
+                                    "C3: configs[1] corpus (1 GiB MIXED UTF-8, 1M strings) + host %s pre-split, "
+                                    "GPU merge loop" % args.pattern) + (" + RCCL all-gather of ids" if gather else ""),
+                       "bytes_per_rank": n_bytes, "strings_per_rank": n_str, "merges": len(tok.merges),
+                       "model": model, "pattern": args.pattern, "parallelism": "doc-shard x%d" % world,
+                       "gather_in_step": gather},
+            "mtok_per_s": round(all_tok * args.steps / sec / 1e6, 3),
+            "bytes_per_token": round(all_bytes / max(all_tok, 1), 4),
+            "chunks": int(all_chunks),
+            "roofline": roofline,
+            "cpu_baseline": cpu,
+            "parity_vs_oracle_sample": parity,
+            "host_prep_s": round(t_prep, 2),
+        }
+        print(json.dumps(line), flush=True)
+    tok.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

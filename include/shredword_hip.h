@@ -1,0 +1,129 @@
+/* shredword_hip.h -- C-ABI of the MI355X-native BPE encode path.
+ *
+ * This is the drop-in boundary under shredword's Python tokenizer surface.  The reference
+ * binds its native code through ctypes (`shredword/cbase.py:5-59`: library discovery,
+ * `ctypes.CDLL`, per-function argtypes/restype, opaque `Trainer*` handle, int status codes
+ * mapped to Python exceptions in `shredword/trainer.py:14-25`).  The reference has no native
+ * encode: `BaseTokenizer.encode` is abstract (`shredword/base.py:108`) and its semantics are
+ * pinned by the primitives `get_stats` (base.py:10-20), `merge` (base.py:22-36) and
+ * `apply_regex` (base.py:38-58).  Each entry point below names the reference interface whose
+ * role it takes.
+ *
+ * Conventions
+ *   - Plain pointers and sizes; no torch types.  Status: SW_OK (0) or a negative SW_ERR_*.
+ *     Never exit(): the reference's `exit(EXIT_FAILURE)` paths (bpe.cpp:113-121) are replaced
+ *     by status codes plus sw_last_error() (thread-local message).
+ *   - The caller owns every buffer it passes.  The encoder handle owns its device copy of the
+ *     merge table, its workspace and its stream.
+ *   - One handle per host thread (a handle is not internally locked).
+ *   - Ids are int32.  Vocab ids 0..255 are raw bytes (base.py:74); a merge value is both the
+ *     pair's rank and the new token id (base.py:137,147).
+ */
+#ifndef SHREDWORD_HIP_H
+#define SHREDWORD_HIP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SW_OK 0
+#define SW_ERR_ARG (-1)     /* bad argument (null pointer, negative size, bad table) */
+#define SW_ERR_HIP (-2)     /* HIP runtime error (message has the HIP error string) */
+#define SW_ERR_ALLOC (-3)   /* host or device allocation failed */
+#define SW_ERR_CAP (-4)     /* output capacity too small */
+#define SW_ERR_NODEV (-5)   /* no usable gfx950 device */
+
+/* Pre-split patterns.  CL100K is the pattern apply_regex hard-codes (base.py:56); GPT2 is the
+ * alternative quoted in its docstring (base.py:46); NONE encodes each string as one chunk. */
+#define SW_PAT_CL100K 0
+#define SW_PAT_GPT2 1
+#define SW_PAT_NONE 2
+
+/* Synthetic corpus kinds (bench configs) */
+#define SW_CORPUS_ASCII 0
+#define SW_CORPUS_MIXED 1
+#define SW_CORPUS_STRESS 2
+
+typedef struct sw_encoder sw_encoder;
+
+typedef struct sw_stats {
+  int64_t n_bytes;      /* input bytes */
+  int64_t n_chunks;     /* pre-split chunks */
+  int64_t n_tokens;     /* output ids */
+  double ms_presplit;   /* host pre-split (0 if the caller supplied chunk_bits) */
+  double ms_h2d;        /* host->device copies */
+  double ms_kernels;    /* device time of the encode kernels (HIP events) */
+  double ms_d2h;        /* device->host copies */
+  double ms_total;      /* wall time of the call */
+} sw_stats;
+
+/* Last error message of this thread ("" if none).  Replaces the reference's stderr+exit. */
+const char* sw_last_error(void);
+
+/* Library / build identification, e.g. "shredword_hip 0.1 gfx950". */
+const char* sw_version(void);
+
+/* Number of visible HIP devices (0 if none / no runtime).  Never fails. */
+int32_t sw_device_count(void);
+
+/* ---- encoder lifecycle (role of create_trainer / bpe_trainer_destroy, bpe.h:62-64) ----
+ * pairs: n x 2 int32 (a, b); vals: n int32, the value merges[(a, b)] (rank == new id).
+ * Duplicate pairs: the LAST occurrence wins, as dict assignment does (base.py:145-148).
+ * Values must be in [0, 2^31-2].  device: HIP device ordinal. */
+int32_t sw_encoder_create(const int32_t* pairs, const int32_t* vals, int64_t n, int32_t device,
+                          sw_encoder** out);
+void sw_encoder_destroy(sw_encoder* h);
+
+/* Pre-allocate the device workspace for inputs up to max_bytes / max_strings (optional;
+ * encode grows it on demand otherwise). */
+int32_t sw_encoder_reserve(sw_encoder* h, int64_t max_bytes, int64_t max_strings);
+
+/* ---- host pre-split (apply_regex, base.py:38-58) ---------------------------------------
+ * Marks, for every string in bytes[str_off[0] .. str_off[n_str]), the first byte of each of
+ * its chunks in the bitmap chunk_bits (bit i of word i/64, LSB first; offsets are relative
+ * to str_off[0]).  chunk_bits must hold ceil(n_bytes/64) words.  Multithreaded over
+ * strings (n_threads <= 0: all hardware threads, capped at 64).  Returns the chunk count
+ * or a negative status. */
+int64_t sw_presplit_host(const uint8_t* bytes, const int64_t* str_off, int64_t n_str, int32_t pattern,
+                         uint64_t* chunk_bits, int32_t n_threads);
+
+/* ---- batched encode, host buffers (the Tokenizer.encode / encode_batch path) ------------
+ * Encodes n_str strings (bytes[str_off[s] .. str_off[s+1])) and writes their ids
+ * concatenated into out_ids, with out_off[0..n_str] the per-string offsets.
+ * chunk_bits: optional pre-split bitmap as produced by sw_presplit_host; NULL => the
+ * library pre-splits with `pattern`.  out_cap >= total input bytes always suffices.
+ * stats: optional.  Synchronous. */
+int32_t sw_encode_batch(sw_encoder* h, const uint8_t* bytes, const int64_t* str_off, int64_t n_str,
+                        int32_t pattern, const uint64_t* chunk_bits, int32_t* out_ids, int64_t out_cap,
+                        int64_t* out_off, sw_stats* stats);
+
+/* ---- batched encode, device-resident buffers (bench / multi-GPU driver) -----------------
+ * All pointers are device pointers on the encoder's device: d_bytes[n_bytes],
+ * d_str_off[n_str+1] (relative to d_bytes, d_str_off[0] == 0, d_str_off[n_str] == n_bytes),
+ * d_chunk_bits[ceil(n_bytes/64)], d_out_ids[n_bytes], d_out_off[n_str+1].
+ * stream: a hipStream_t on that device, or NULL for the encoder's own stream.
+ * Asynchronous: the work is enqueued on the stream.  n_tokens_host (optional) forces a
+ * synchronisation and receives the total id count. */
+int32_t sw_encode_device(sw_encoder* h, const uint8_t* d_bytes, int64_t n_bytes, const int64_t* d_str_off,
+                         int64_t n_str, const uint64_t* d_chunk_bits, int32_t* d_out_ids, int64_t* d_out_off,
+                         void* stream, int64_t* n_tokens_host);
+
+/* Timing of the dominant kernel (the merge-loop kernel, k_encode_tiles) with HIP events on the
+ * stream it is launched on.  sw_encoder_set_timing(h, 1) starts a new accumulation window (one
+ * event pair per launch, no host synchronisation per call); sw_encoder_last_kernel_ms returns the
+ * average device time per launch over that window (it synchronises on the last event), or -1. */
+int32_t sw_encoder_set_timing(sw_encoder* h, int32_t on);
+double sw_encoder_last_kernel_ms(const sw_encoder* h);
+
+/* ---- synthetic corpora (bench inputs; deterministic for any thread count) --------------
+ * Fills out_off[0..n_strings] with string offsets; when out_bytes is non-NULL also writes
+ * the bytes (cap >= out_off[n_strings]).  Returns the total byte count or SW_ERR_*. */
+int64_t sw_synth_corpus(uint64_t seed, int32_t kind, int64_t n_strings, int64_t mean_len,
+                        uint8_t* out_bytes, int64_t cap, int64_t* out_off, int32_t n_threads);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,135 @@
+"""ORACLE -- TEST INFRASTRUCTURE ONLY: ctypes wrapper of oracle/libsw_oracle.so (sw_oracle.c).
+
+May be imported only by tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg, and only
+as the checker (or the timed CPU baseline).  The product (shredword_amd) never imports it.
+"""
+import ctypes
+import os
+import subprocess
+from ctypes import POINTER, c_int, c_int32, c_int64, c_uint8, c_void_p
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB = os.path.join(HERE, "libsw_oracle.so")
+PAT_CL100K, PAT_GPT2, PAT_NONE = 0, 1, 2
+
+_lib = None
+
+
+def build():
+    subprocess.check_call(["make", "-s", "-C", HERE, "libsw_oracle.so"])
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB):
+            build()
+        L = ctypes.CDLL(LIB)
+        L.orc_model_new.restype = c_void_p
+        L.orc_model_new.argtypes = [POINTER(c_int32), POINTER(c_int32), c_int64]
+        L.orc_model_free.argtypes = [c_void_p]
+        L.orc_model_get.restype = c_int64
+        L.orc_model_get.argtypes = [c_void_p, c_int32, c_int32]
+        L.orc_ucd_class.restype = c_int
+        L.orc_ucd_class.argtypes = [ctypes.c_uint32]
+        L.orc_presplit.restype = c_int64
+        L.orc_presplit.argtypes = [POINTER(c_uint8), c_int64, c_int, POINTER(c_int64), c_int64]
+        L.orc_encode_chunk.restype = c_int64
+        L.orc_encode_chunk.argtypes = [c_void_p, POINTER(c_uint8), c_int64, POINTER(c_int32)]
+        L.orc_encode_ordinary.restype = c_int64
+        L.orc_encode_ordinary.argtypes = [c_void_p, POINTER(c_uint8), c_int64, c_int, POINTER(c_int32)]
+        L.orc_encode_batch.restype = c_int64
+        L.orc_encode_batch.argtypes = [c_void_p, POINTER(c_uint8), POINTER(c_int64), c_int64, c_int,
+                                       POINTER(c_int32), POINTER(c_int64), c_int]
+        L.orc_encode_with_specials.restype = c_int64
+        L.orc_encode_with_specials.argtypes = [c_void_p, POINTER(c_uint8), c_int64, c_int, POINTER(c_uint8),
+                                               POINTER(c_int64), POINTER(c_int32), c_int64, POINTER(c_int32)]
+        _lib = L
+    return _lib
+
+
+def _p(a, t):
+    return a.ctypes.data_as(POINTER(t))
+
+
+class OracleModel:
+    """merges dict -> oracle hash map."""
+
+    def __init__(self, merges):
+        n = len(merges)
+        pairs = np.array(list(merges.keys()), dtype=np.int32).reshape(n, 2)
+        vals = np.array(list(merges.values()), dtype=np.int32).reshape(n)
+        self._h = lib().orc_model_new(_p(pairs, c_int32), _p(vals, c_int32), n)
+
+    def __del__(self):
+        if getattr(self, "_h", None):
+            lib().orc_model_free(self._h)
+            self._h = None
+
+    def get(self, a, b):
+        r = lib().orc_model_get(self._h, a, b)
+        return None if r < 0 else int(r)
+
+    def encode_chunk(self, data):
+        buf = np.frombuffer(bytes(data), dtype=np.uint8) if len(data) else np.zeros(1, np.uint8)
+        out = np.empty(max(len(data), 1), dtype=np.int32)
+        n = lib().orc_encode_chunk(self._h, _p(buf, c_uint8), len(data), _p(out, c_int32))
+        return out[:n].tolist()
+
+    def encode_ordinary(self, data, pattern=PAT_CL100K):
+        if isinstance(data, str):
+            data = data.encode("utf-8")
+        buf = np.frombuffer(bytes(data), dtype=np.uint8) if len(data) else np.zeros(1, np.uint8)
+        out = np.empty(max(len(data), 1), dtype=np.int32)
+        n = lib().orc_encode_ordinary(self._h, _p(buf, c_uint8), len(data), pattern, _p(out, c_int32))
+        assert n >= 0
+        return out[:n].tolist()
+
+    def encode_batch(self, buf, off, pattern=PAT_CL100K, n_threads=1):
+        """-> (ids int32[total], out_off int64[n+1]) for strings buf[off[s]:off[s+1]]."""
+        buf = np.ascontiguousarray(buf, dtype=np.uint8)
+        off = np.ascontiguousarray(off, dtype=np.int64)
+        n = len(off) - 1
+        total = int(off[-1] - off[0]) if n > 0 else 0
+        out = np.empty(max(total, 1), dtype=np.int32)
+        out_off = np.empty(n + 1, dtype=np.int64)
+        if buf.size == 0:
+            buf = np.zeros(1, np.uint8)
+        t = lib().orc_encode_batch(self._h, _p(buf, c_uint8), _p(off, c_int64), n, pattern, _p(out, c_int32),
+                                   _p(out_off, c_int64), n_threads)
+        assert t >= 0
+        return out[:t], out_off
+
+    def encode_with_specials(self, text, special_tokens, pattern=PAT_CL100K):
+        data = text.encode("utf-8")
+        names = [s.encode("utf-8") for s in special_tokens]
+        sb = np.frombuffer(b"".join(names) or b"\0", dtype=np.uint8)
+        so = np.zeros(len(names) + 1, dtype=np.int64)
+        np.cumsum([len(x) for x in names], out=so[1:])
+        sid = np.array(list(special_tokens.values()) or [0], dtype=np.int32)
+        buf = np.frombuffer(data or b"\0", dtype=np.uint8)
+        out = np.empty(max(len(data), 1), dtype=np.int32)
+        n = lib().orc_encode_with_specials(self._h, _p(buf, c_uint8), len(data), pattern, _p(sb, c_uint8),
+                                           _p(so, c_int64), _p(sid, c_int32), len(names), _p(out, c_int32))
+        assert n >= 0
+        return out[:n].tolist()
+
+
+def presplit(data, pattern=PAT_CL100K):
+    """-> list of chunk start byte offsets."""
+    if isinstance(data, str):
+        data = data.encode("utf-8")
+    n = len(data)
+    if n == 0:
+        return []
+    buf = np.frombuffer(bytes(data), dtype=np.uint8)
+    starts = np.empty(n, dtype=np.int64)
+    c = lib().orc_presplit(_p(buf, c_uint8), n, pattern, _p(starts, c_int64), n)
+    assert c >= 0
+    return starts[:c].tolist()
+
+
+def ucd_class(cp):
+    return lib().orc_ucd_class(cp)

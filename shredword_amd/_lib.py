@@ -1,0 +1,113 @@
+"""ctypes binding of the C-ABI in include/shredword_hip.h.
+
+Follows the reference's native-binding pattern (`shredword/cbase.py:5-59`): search the package
+directory for the built library, `ctypes.CDLL` it, declare argtypes/restype per function, and map
+status codes to Python exceptions (as `shredword/trainer.py:14-25` does).  Two deliberate
+differences from the reference:
+  * the library is loaded lazily, on first use, so `import shredword_amd` never fails on a
+    machine without the built library (the reference's `import shredword` raises
+    FileNotFoundError at `cbase.py:20`);
+  * errors come back as negative status codes plus `sw_last_error()`, never `exit()`.
+"""
+import ctypes
+import os
+import sysconfig
+from ctypes import POINTER, Structure, c_char_p, c_double, c_int32, c_int64, c_uint8, c_uint64, c_void_p
+
+LIB_NAMES = ("libshredword_hip",)
+
+SW_OK = 0
+SW_ERR_ARG, SW_ERR_HIP, SW_ERR_ALLOC, SW_ERR_CAP, SW_ERR_NODEV = -1, -2, -3, -4, -5
+
+SW_PAT_CL100K, SW_PAT_GPT2, SW_PAT_NONE = 0, 1, 2
+SW_CORPUS_ASCII, SW_CORPUS_MIXED, SW_CORPUS_STRESS = 0, 1, 2
+
+
+class SwStats(Structure):
+    _fields_ = [("n_bytes", c_int64), ("n_chunks", c_int64), ("n_tokens", c_int64),
+                ("ms_presplit", c_double), ("ms_h2d", c_double), ("ms_kernels", c_double),
+                ("ms_d2h", c_double), ("ms_total", c_double)]
+
+
+class ShredwordError(RuntimeError):
+    """A C-ABI call returned a negative status."""
+
+    def __init__(self, code, msg):
+        super().__init__(f"[{code}] {msg}")
+        self.code = code
+
+
+def _get_lib_path():
+    """Locate the built library the way cbase.py:_get_lib_path does (package dir, lib/, build/)."""
+    pkg_dir = os.path.dirname(os.path.abspath(__file__))
+    exts = (".so", sysconfig.get_config_var("EXT_SUFFIX") or ".so")
+    for d in (pkg_dir, os.path.join(pkg_dir, "lib"), os.path.join(pkg_dir, "..", "build")):
+        if not os.path.isdir(d):
+            continue
+        for f in sorted(os.listdir(d)):
+            if f.startswith(LIB_NAMES) and f.endswith(exts):
+                return os.path.join(d, f)
+    raise FileNotFoundError(
+        "libshredword_hip.so not found next to shredword_amd/ -- run "
+        "`python -c 'import __graft_entry__ as g; g.build()'` or `make -C shredword_amd`")
+
+
+_lib = None
+
+# name: (restype, argtypes)
+_SIGNATURES = {
+    "sw_last_error": (c_char_p, []),
+    "sw_version": (c_char_p, []),
+    "sw_device_count": (c_int32, []),
+    "sw_encoder_create": (c_int32, [POINTER(c_int32), POINTER(c_int32), c_int64, c_int32, POINTER(c_void_p)]),
+    "sw_encoder_destroy": (None, [c_void_p]),
+    "sw_encoder_reserve": (c_int32, [c_void_p, c_int64, c_int64]),
+    "sw_presplit_host": (c_int64, [POINTER(c_uint8), POINTER(c_int64), c_int64, c_int32, POINTER(c_uint64), c_int32]),
+    "sw_encode_batch": (c_int32, [c_void_p, POINTER(c_uint8), POINTER(c_int64), c_int64, c_int32,
+                                  POINTER(c_uint64), POINTER(c_int32), c_int64, POINTER(c_int64),
+                                  POINTER(SwStats)]),
+    "sw_encode_device": (c_int32, [c_void_p, c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_void_p,
+                                   c_void_p, c_void_p, POINTER(c_int64)]),
+    "sw_encoder_set_timing": (c_int32, [c_void_p, c_int32]),
+    "sw_encoder_last_kernel_ms": (c_double, [c_void_p]),
+    "sw_synth_corpus": (c_int64, [c_uint64, c_int32, c_int64, c_int64, POINTER(c_uint8), c_int64,
+                                  POINTER(c_int64), c_int32]),
+}
+
+
+def lib():
+    """Load (once) and return the CDLL with every signature declared."""
+    global _lib
+    if _lib is None:
+        # If PyTorch is present, load it first: it ships its own libamdhip64.so.7 and the
+        # process must use ONE HIP runtime (same SONAME => the dynamic linker reuses it).
+        try:
+            import torch  # noqa: F401
+        except Exception:
+            pass
+        cdll = ctypes.CDLL(_get_lib_path())
+        for name, (res, args) in _SIGNATURES.items():
+            fn = getattr(cdll, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = cdll
+    return _lib
+
+
+def exported_symbols():
+    return tuple(_SIGNATURES)
+
+
+def check(code):
+    """Map a negative status to ShredwordError (the reference maps -1 to RuntimeError/IOError)."""
+    if code < 0:
+        msg = lib().sw_last_error()
+        raise ShredwordError(int(code), msg.decode("utf-8", "replace") if msg else "")
+    return code
+
+
+def ptr(arr, ctype):
+    """ctypes pointer to a contiguous numpy array (None for None)."""
+    if arr is None:
+        return None
+    return arr.ctypes.data_as(POINTER(ctype))

@@ -1,0 +1,212 @@
+"""HIP-backed BPE tokenizer behind shredword's BaseTokenizer surface.
+
+`Tokenizer.encode` is the abstract method of `shredword/base.py:108` made concrete, with the
+semantics of the reference's primitives: pre-split with apply_regex (base.py:38-58), bytes to
+ids, then repeatedly merge the lowest-ranked adjacent pair (get_stats base.py:10-20, merge
+base.py:22-36).  Pre-split runs in native host code, the merge loop in HIP kernels on a gfx950
+device.  There is no CPU fallback: without the library or a device, encode raises.
+"""
+import ctypes
+
+import numpy as np
+
+from . import _lib
+from .base import BaseTokenizer, build_vocab, pattern_id
+
+
+class _TrackedDict(dict):
+    """dict that counts its mutations, so the device copy of `merges` is rebuilt when edited."""
+    version = 0
+
+    def _bump(self):
+        self.version += 1
+
+    def __setitem__(self, k, v):
+        super().__setitem__(k, v)
+        self._bump()
+
+    def __delitem__(self, k):
+        super().__delitem__(k)
+        self._bump()
+
+    def update(self, *a, **k):
+        super().update(*a, **k)
+        self._bump()
+
+    def clear(self):
+        super().clear()
+        self._bump()
+
+    def pop(self, *a):
+        r = super().pop(*a)
+        self._bump()
+        return r
+
+    def popitem(self):
+        r = super().popitem()
+        self._bump()
+        return r
+
+    def setdefault(self, k, d=None):
+        r = super().setdefault(k, d)
+        self._bump()
+        return r
+
+
+def _pack_strings(datas):
+    """list of bytes -> (uint8 buffer, int64 offsets[n+1])."""
+    off = np.zeros(len(datas) + 1, dtype=np.int64)
+    np.cumsum([len(d) for d in datas], out=off[1:])
+    buf = np.frombuffer(b"".join(datas), dtype=np.uint8) if off[-1] else np.zeros(1, np.uint8)
+    return buf, off
+
+
+class Tokenizer(BaseTokenizer):
+    """shredword tokenizer whose encode runs on an MI355X.
+
+    Attributes are those of BaseTokenizer (merges, pattern, special_tokens, vocab).  `pattern`
+    selects the pre-split: "" (default) or the cl100k pattern = what apply_regex does; the GPT-2
+    pattern; anything else raises NotImplementedError at encode time.
+    """
+
+    def __init__(self, device=0):
+        self._merges = _TrackedDict()
+        super().__init__()
+        self.device = device
+        self._handle = None
+        self._handle_key = None
+        self.last_stats = None
+
+    # merges is tracked so that edits (README-style `tok.merges[(a, b)] = id`) reach the device
+    @property
+    def merges(self):
+        return self._merges
+
+    @merges.setter
+    def merges(self, value):
+        d = _TrackedDict(value)
+        d.version = self._merges.version + 1
+        self._merges = d
+
+    def __del__(self):
+        self.close()
+
+    def close(self):
+        h, self._handle = getattr(self, "_handle", None), None
+        if h:
+            _lib.lib().sw_encoder_destroy(h)
+
+    # ---------------------------------------------------------------- device table
+    def _encoder(self):
+        key = (id(self._merges), self._merges.version, self.device)
+        if self._handle is not None and self._handle_key == key:
+            return self._handle
+        self.close()
+        n = len(self._merges)
+        pairs = np.array(list(self._merges.keys()), dtype=np.int64).reshape(n, 2)
+        vals = np.array(list(self._merges.values()), dtype=np.int64).reshape(n)
+        if n and (pairs.min() < 0 or pairs.max() > 0x7FFFFFFF or vals.min() < 0 or vals.max() > 0x7FFFFFFD):
+            raise ValueError("merges must map non-negative int32 pairs to values in [0, 2^31-3]")
+        pairs = np.ascontiguousarray(pairs, dtype=np.int32)
+        vals = np.ascontiguousarray(vals, dtype=np.int32)
+        L = _lib.lib()
+        h = ctypes.c_void_p()
+        _lib.check(L.sw_encoder_create(_lib.ptr(pairs, ctypes.c_int32), _lib.ptr(vals, ctypes.c_int32),
+                                       n, int(self.device), ctypes.byref(h)))
+        self._handle, self._handle_key = h, key
+        return h
+
+    # ---------------------------------------------------------------- encode
+    def encode_ordinary_batch_np(self, datas):
+        """Encode a list of UTF-8 byte strings (no special-token handling) in one device batch.
+        Returns (ids int32[total], offsets int64[n+1])."""
+        buf, off = _pack_strings(datas)
+        return self.encode_packed(buf, off)
+
+    def encode_packed(self, buf, off, chunk_bits=None):
+        """Encode the strings buf[off[s]:off[s+1]] (uint8 buffer, int64 offsets) in one device
+        batch.  chunk_bits: optional host pre-split bitmap (sw_presplit_host layout).
+        Returns (ids int32[total], out_off int64[n+1])."""
+        buf = np.ascontiguousarray(buf, dtype=np.uint8)
+        off = np.ascontiguousarray(off, dtype=np.int64)
+        if buf.size == 0:
+            buf = np.zeros(1, np.uint8)
+        n = len(off) - 1
+        total = int(off[-1] - off[0]) if n > 0 else 0
+        out = np.empty(max(total, 1), dtype=np.int32)
+        out_off = np.empty(n + 1, dtype=np.int64)
+        stats = _lib.SwStats()
+        L = _lib.lib()
+        bits = None if chunk_bits is None else np.ascontiguousarray(chunk_bits, dtype=np.uint64)
+        _lib.check(L.sw_encode_batch(self._encoder(), _lib.ptr(buf, ctypes.c_uint8), _lib.ptr(off, ctypes.c_int64),
+                                     n, pattern_id(self.pattern), _lib.ptr(bits, ctypes.c_uint64),
+                                     _lib.ptr(out, ctypes.c_int32), total, _lib.ptr(out_off, ctypes.c_int64),
+                                     ctypes.byref(stats)))
+        self.last_stats = stats
+        return out[:int(out_off[-1])], out_off
+
+    def _split_specials(self, text):
+        """Split on special tokens: leftmost occurrence first, dictionary order breaking ties
+        (the reference stores special_tokens at base.py:103 but defines no split)."""
+        specials = [s for s in self.special_tokens if s]
+        if not specials:
+            return [text]
+        parts, seg, i, n = [], 0, 0, len(text)
+        while i < n:
+            hit = next((s for s in specials if text.startswith(s, i)), None)
+            if hit is None:
+                i += 1
+                continue
+            parts.append(text[seg:i])
+            parts.append(self.special_tokens[hit])
+            i += len(hit)
+            seg = i
+        parts.append(text[seg:])
+        return parts
+
+    def encode_batch(self, texts, allowed_special="all"):
+        """Encode many strings in one device batch; returns a list of id lists."""
+        if allowed_special not in ("all", "none"):
+            raise ValueError("allowed_special must be 'all' or 'none'")
+        pieces, layout = [], []
+        for t in texts:
+            parts = self._split_specials(t) if allowed_special == "all" else [t]
+            lay = []
+            for p in parts:
+                if isinstance(p, int):
+                    lay.append(p)
+                else:
+                    lay.append(-1 - len(pieces))
+                    pieces.append(p.encode("utf-8"))
+            layout.append(lay)
+        ids, off = self.encode_ordinary_batch_np(pieces)
+        out = []
+        for lay in layout:
+            r = []
+            for x in lay:
+                if x >= 0:
+                    r.append(x)
+                else:
+                    k = -1 - x
+                    r.extend(ids[off[k]:off[k + 1]].tolist())
+            out.append(r)
+        return out
+
+    def encode(self, text, allowed_special="all"):
+        return self.encode_batch([text], allowed_special)[0]
+
+    def encode_ordinary(self, text):
+        return self.encode_batch([text], "none")[0]
+
+    # ---------------------------------------------------------------- decode
+    def decode(self, ids):
+        """ids -> str via vocab bytes, undecodable bytes replaced (conventional minbpe decode)."""
+        if len(self.vocab) != 256 + len(self._merges) + len(self.special_tokens):
+            self.vocab = build_vocab(self._merges, self.special_tokens)
+        return b"".join(self.vocab[int(i)] for i in ids).decode("utf-8", errors="replace")
+
+    def load(self, model_file):
+        super().load(model_file)
+
+    def load_binary(self, model_file):
+        super().load_binary(model_file)

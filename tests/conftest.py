@@ -1,0 +1,55 @@
+"""Shared fixtures.  GPU tests carry @pytest.mark.gpu; everything else runs on a CPU-only box."""
+import json
+import os
+import sys
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+GOLD = os.path.join(ROOT, "tests", "golden")
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "oracle"))
+
+PATTERNS = {"cl100k": 0, "gpt2": 1, "none": 2}
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs a gfx950 device (run with -m gpu on the MI355X box)")
+
+
+def load_model_merges(name):
+    """merges dict of a committed table, parsed like shredword/base.py:135-149."""
+    path = os.path.join(GOLD, name)
+    if name.endswith(".json"):
+        return {(a, b): v for a, b, v in json.load(open(path))}
+    m, idx = {}, 256
+    with open(path, encoding="utf-8") as f:
+        assert f.readline().strip() == "shredword v1"
+        f.readline()
+        for _ in range(int(f.readline().strip())):
+            f.readline()
+        for line in f:
+            a, b = map(int, line.split())
+            m[(a, b)] = idx
+            idx += 1
+    return m
+
+
+def golden_index():
+    return json.load(open(os.path.join(GOLD, "index.json")))
+
+
+def load_fixture(entry):
+    z = np.load(os.path.join(GOLD, entry["file"]))
+    return {k: z[k] for k in z.files}
+
+
+@pytest.fixture(scope="session")
+def index():
+    return golden_index()
+
+
+@pytest.fixture(scope="session")
+def primitives():
+    return json.load(open(os.path.join(GOLD, "primitives.json"), encoding="utf-8"))

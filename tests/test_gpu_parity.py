@@ -1,0 +1,229 @@
+"""Parity of the HIP encode path with the reference semantics, on a gfx950 device.
+
+Bit-exact comparisons (integer work): against the golden vectors produced by the reference's own
+primitives (tests/golden), and against the oracle restatement (oracle/sw_oracle.c, itself pinned
+to those vectors by test_oracle_golden.py) on seeded inputs and edge cases.  All calls go
+through the C-ABI (shredword_amd -> libshredword_hip.so).
+"""
+import random
+
+import numpy as np
+import pytest
+
+import oracle
+import shredword_amd as sa
+from shredword_amd import _lib, corpus
+from conftest import PATTERNS, golden_index, load_fixture, load_model_merges
+
+pytestmark = pytest.mark.gpu
+
+FIXTURES = golden_index()["fixtures"]
+PAT_STR = {"cl100k": "", "gpt2": sa.GPT2_PATTERN, "none": 2}
+
+
+@pytest.fixture(scope="module", autouse=True)
+def need_device():
+    if _lib.lib().sw_device_count() < 1:
+        pytest.fail("no HIP device visible: -m gpu must run on the MI355X box")
+
+
+_TOKS = {}
+
+
+def tok_for(model, pattern="cl100k"):
+    key = (model, pattern)
+    if key not in _TOKS:
+        t = sa.Tokenizer(device=0)
+        t.merges = load_model_merges(model)
+        _TOKS[key] = t
+    t = _TOKS[key]
+    t.pattern = PAT_STR[pattern]
+    return t
+
+
+def gpu_encode(t, buf, off):
+    return t.encode_packed(buf, off)
+
+
+def oracle_encode(merges, buf, off, pattern):
+    return oracle.OracleModel(merges).encode_batch(buf, off, PATTERNS[pattern], n_threads=8)
+
+
+def pack(datas):
+    off = np.zeros(len(datas) + 1, dtype=np.int64)
+    np.cumsum([len(d) for d in datas], out=off[1:])
+    return np.frombuffer(b"".join(datas) or b"\0", dtype=np.uint8)[:max(int(off[-1]), 0)], off
+
+
+def assert_same(got, exp):
+    np.testing.assert_array_equal(got[1], exp[1])
+    np.testing.assert_array_equal(got[0], exp[0])
+
+
+@pytest.mark.parametrize("entry", FIXTURES, ids=[e["file"] for e in FIXTURES])
+def test_golden_bit_exact(entry):
+    fx = load_fixture(entry)
+    t = tok_for(entry["model"], entry["pattern"])
+    got = gpu_encode(t, fx["bytes"], fx["off"])
+    assert_same(got, (fx["ids"], fx["ids_off"]))
+
+
+def test_tokenizer_encode_decode_surface():
+    t = tok_for("bl32k.model")
+    text = "Hello world's 12345 \n\n  x 中文 😀"
+    ids = t.encode(text)
+    assert ids == oracle.OracleModel(t.merges).encode_ordinary(text)
+    assert t.decode(ids) == text
+    assert t.encode_batch([text, "", text]) == [ids, [], ids]
+    t.special_tokens = {"<|endoftext|>": 100257, "<|fim|>": 100258}
+    s = "a<|endoftext|>b<|fim|><|endoftext|>"
+    assert t.encode(s) == oracle.OracleModel(t.merges).encode_with_specials(s, t.special_tokens)
+    assert t.encode(s, allowed_special="none") == oracle.OracleModel(t.merges).encode_ordinary(s)
+    t.special_tokens = {}
+
+
+def test_empty_inputs():
+    t = tok_for("toy500.model")
+    ids, off = gpu_encode(t, np.zeros(0, np.uint8), np.zeros(1, np.int64))
+    assert len(ids) == 0 and off.tolist() == [0]
+    ids, off = gpu_encode(t, np.zeros(0, np.uint8), np.zeros(5, np.int64))
+    assert len(ids) == 0 and off.tolist() == [0] * 5
+    buf, off = pack([b"", b"a", b"", b"", b"hello there", b""])
+    assert_same(gpu_encode(t, buf, off), oracle_encode(t.merges, buf, off, "cl100k"))
+
+
+@pytest.mark.parametrize("model", ["toy500.model", "bl32k.model", "bl50k.model"])
+def test_tile_boundaries_and_long_chunks(model):
+    """Chunks that straddle the 2 KiB tiles, chunks longer than the per-lane limit (16 B), longer
+    than a tile, and a 200 KB single chunk; (a,a) runs of every parity."""
+    rng = random.Random(1)
+    t = tok_for(model)
+    datas = []
+    for L in (1, 2, 15, 16, 17, 31, 63, 64, 65, 127, 2047, 2048, 2049, 4095, 4096, 4097, 9000, 200_000):
+        datas.append(bytes(rng.choice(b"abcdefghij") for _ in range(L)))
+        datas.append(b"a" * L)
+        datas.append(b" " * L)
+    for shift in range(0, 40):  # push word boundaries across the 2048-byte tile edges
+        datas.append(b"x" * shift + b" hello world the of and" * 150)
+    buf, off = pack(datas)
+    assert_same(gpu_encode(t, buf, off), oracle_encode(t.merges, buf, off, "cl100k"))
+
+
+def test_self_pair_runs_exact():
+    """(a,a) overlap rule of merge(): [a,a,a]->[X,a], [a,a,a,a]->[X,X] (base.py:29-35)."""
+    merges = {(97, 97): 256, (256, 256): 257, (256, 97): 258, (257, 257): 259, (98, 98): 260}
+    t = sa.Tokenizer()
+    t.merges = merges
+    datas = [b"a" * n for n in range(0, 300)] + [b"b" * n + b"a" * m for n in range(0, 20) for m in range(0, 20)]
+    buf, off = pack(datas)
+    t.pattern = 2
+    assert_same(gpu_encode(t, buf, off), oracle_encode(merges, buf, off, "none"))
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_random_illformed_tables(seed):
+    """Exactness must not depend on well-formedness: random pairs, duplicate values, values
+    smaller than their pair members, ids > 255 referenced before they exist."""
+    r = random.Random(seed)
+    alpha = list(b"abcd ")
+    ids = alpha + list(range(256, 256 + 40))
+    merges = {}
+    for _ in range(r.randint(5, 300)):
+        merges[(r.choice(ids), r.choice(ids))] = r.randint(0, 300) if seed % 2 else r.randint(256, 295)
+    datas = [bytes(r.choice(b"abcd ") for _ in range(r.randint(0, 120))) for _ in range(400)]
+    datas.append(bytes(r.choice(b"abcd") for _ in range(5000)))
+    buf, off = pack(datas)
+    t = sa.Tokenizer()
+    t.merges = merges
+    for pat in ("none", "cl100k"):
+        t.pattern = PAT_STR[pat]
+        assert_same(gpu_encode(t, buf, off), oracle_encode(merges, buf, off, pat))
+
+
+def test_wide_ids_table():
+    """Ids > 65535 (e.g. vocabularies past 64k): the 16-byte-slot table path."""
+    base = load_model_merges("bl32k.model")
+    shift = lambda x: x if x < 256 else x + 70000  # noqa: E731
+    merges = {(shift(a), shift(b)): shift(v) for (a, b), v in base.items()}
+    fx = load_fixture(FIXTURES[1])
+    t = sa.Tokenizer()
+    t.merges = merges
+    got = gpu_encode(t, fx["bytes"], fx["off"])
+    exp_ids = np.where(fx["ids"] < 256, fx["ids"], fx["ids"] + 70000)
+    assert_same(got, (exp_ids, fx["ids_off"]))
+
+
+def test_invalid_utf8_bytes():
+    rng = random.Random(4)
+    datas = [bytes(rng.choice(b"ab \n\x80\xff\xc3\xa9\xe4\xb8\xf0\x9f") for _ in range(rng.randint(0, 80)))
+             for _ in range(500)]
+    buf, off = pack(datas)
+    for model in ("toy500.model", "bl32k.model"):
+        t = tok_for(model)
+        for pat in ("cl100k", "gpt2"):
+            t.pattern = PAT_STR[pat]
+            assert_same(gpu_encode(t, buf, off), oracle_encode(t.merges, buf, off, pat))
+        t.pattern = ""
+
+
+@pytest.mark.parametrize("kind,model", [(corpus.MIXED, "bl32k.model"), (corpus.STRESS, "bl50k.model")])
+def test_large_corpus_vs_oracle(kind, model):
+    """64 MB (MIXED) / 24 MB (STRESS) seeded corpora, bit-exact against the multithreaded oracle."""
+    n = 60000 if kind == corpus.MIXED else 40000
+    buf, off = corpus.synth(99, kind, n, 1074 if kind == corpus.MIXED else 600)
+    t = tok_for(model)
+    got = gpu_encode(t, buf, off)
+    assert_same(got, oracle_encode(t.merges, buf, off, "cl100k"))
+
+
+def test_full_size_properties():
+    """At the bench size class (256 MB here): decode(encode(x)) == x for a byte-level table,
+    token count bounds, determinism across calls."""
+    buf, off = corpus.synth(2024, corpus.MIXED, 250_000, 1074)
+    t = tok_for("bl32k.model")
+    ids1, off1 = gpu_encode(t, buf, off)
+    ids2, off2 = gpu_encode(t, buf, off)
+    np.testing.assert_array_equal(ids1, ids2)
+    np.testing.assert_array_equal(off1, off2)
+    assert off1[0] == 0 and np.all(np.diff(off1) >= 0) and np.all(np.diff(off1) <= np.diff(off))
+    # byte-level decode of the whole batch reproduces the input bytes exactly
+    vocab = sa.build_vocab(t.merges, {})
+    table = np.zeros(max(vocab) + 1, dtype=object)
+    lens = np.zeros(max(vocab) + 1, dtype=np.int64)
+    flat = bytearray()
+    starts = np.zeros(max(vocab) + 1, dtype=np.int64)
+    for i, b in vocab.items():
+        starts[i] = len(flat)
+        lens[i] = len(b)
+        flat.extend(b)
+    flat = np.frombuffer(bytes(flat), dtype=np.uint8)
+    L = lens[ids1]
+    pos = np.repeat(starts[ids1] - np.concatenate([[0], np.cumsum(L)[:-1]]), L) + np.arange(int(L.sum()))
+    np.testing.assert_array_equal(flat[pos], buf)
+    del table
+
+
+def test_device_api_with_torch_buffers():
+    """sw_encode_device on torch-allocated HBM buffers and torch's stream."""
+    import ctypes
+
+    import torch
+    buf, off = corpus.synth(7, corpus.MIXED, 3000, 1074)
+    bits, _ = corpus.presplit(buf, off)
+    t = tok_for("bl32k.model")
+    exp = gpu_encode(t, buf, off)
+    dev = torch.device("cuda", 0)
+    d_buf = torch.from_numpy(buf).to(dev)
+    d_off = torch.from_numpy(off).to(dev)
+    d_bits = torch.from_numpy(bits.view(np.int64)).to(dev)
+    d_out = torch.empty(len(buf), dtype=torch.int32, device=dev)
+    d_oo = torch.empty(len(off), dtype=torch.int64, device=dev)
+    n_tok = ctypes.c_int64()
+    L = _lib.lib()
+    _lib.check(L.sw_encode_device(t._encoder(), d_buf.data_ptr(), len(buf), d_off.data_ptr(), len(off) - 1,
+                                  d_bits.data_ptr(), d_out.data_ptr(), d_oo.data_ptr(),
+                                  torch.cuda.current_stream(dev).cuda_stream, ctypes.byref(n_tok)))
+    torch.cuda.synchronize()
+    assert n_tok.value == len(exp[0])
+    np.testing.assert_array_equal(d_out[:n_tok.value].cpu().numpy(), exp[0])
+    np.testing.assert_array_equal(d_oo.cpu().numpy(), exp[1])

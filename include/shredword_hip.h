@@ -71,7 +71,7 @@ int32_t sw_device_count(void);
 /* ---- encoder lifecycle (role of create_trainer / bpe_trainer_destroy, bpe.h:62-64) ----
  * pairs: n x 2 int32 (a, b); vals: n int32, the value merges[(a, b)] (rank == new id).
  * Duplicate pairs: the LAST occurrence wins, as dict assignment does (base.py:145-148).
- * Values must be in [0, 2^31-2].  device: HIP device ordinal. */
+ * Values must be in [0, 2^31-1].  device: HIP device ordinal. */
 int32_t sw_encoder_create(const int32_t* pairs, const int32_t* vals, int64_t n, int32_t device,
                           sw_encoder** out);
 void sw_encoder_destroy(sw_encoder* h);

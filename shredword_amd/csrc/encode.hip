@@ -131,6 +131,64 @@ int32_t ensure_workspace(sw_encoder* h, int64_t n_bytes) {
   return SW_OK;
 }
 
+// Two-choice cuckoo table (see table.h).  Narrow buckets hold 2 slots, wide buckets 1; the
+// bucket count starts at the load factor below and doubles (with fresh hash multipliers) until
+// every pair is placed.
+bool build_cuckoo(const std::unordered_map<uint64_t, int32_t>& dict, const std::vector<uint64_t>& order, bool wide,
+                  DevTable* t, std::vector<uint4>* out) {
+  const int slots = wide ? 1 : 2;
+  const double max_load = wide ? 0.40 : 0.80;
+  uint32_t log2b = 4;
+  while ((double)(1ull << log2b) * slots * max_load < (double)order.size()) ++log2b;
+  uint64_t rng = 0x243F6A8885A308D3ULL;
+  auto next = [&]() { rng ^= rng << 13; rng ^= rng >> 7; rng ^= rng << 17; return rng; };
+  for (int attempt = 0; attempt < 64; ++attempt) {
+    if (attempt && attempt % 4 == 0 && log2b < 30) ++log2b;
+    const size_t nb = (size_t)1 << log2b;
+    t->shift = 32 - log2b;
+    t->m1 = (uint32_t)next() | 1u;
+    t->m2 = (uint32_t)next() | 1u;
+    std::vector<uint4> b(nb, make_uint4(kEmptyKey, 0, kEmptyKey, 0));
+    bool ok = true;
+    for (uint64_t k : order) {
+      uint32_t a = (uint32_t)(k >> 32), c = (uint32_t)k, v = (uint32_t)dict.at(k);
+      for (int kick = 0;; ++kick) {
+        if (kick > 500) { ok = false; break; }
+        const uint32_t f = mix_key(a, c);
+        const uint32_t c1 = bucket1(f, *t), c2 = bucket2(f, *t);
+        bool placed = false;
+        for (uint32_t bk : {c1, c2}) {
+          uint4& q = b[bk];
+          if (wide) {
+            if (q.x == kEmptyKey) { q = make_uint4(a, c, v, 0); placed = true; break; }
+          } else {
+            const uint32_t key = (a << 16) | c;
+            if (q.x == kEmptyKey) { q.x = key; q.y = v; placed = true; break; }
+            if (q.z == kEmptyKey) { q.z = key; q.w = v; placed = true; break; }
+          }
+        }
+        if (placed) break;
+        // evict a random resident of a random candidate bucket and re-insert it
+        uint4& q = b[(next() & 1) ? c1 : c2];
+        if (wide) {
+          uint4 old = q;
+          q = make_uint4(a, c, v, 0);
+          a = old.x; c = old.y; v = old.z;
+        } else {
+          const uint32_t key = (a << 16) | c;
+          uint32_t ok_, ov;
+          if (next() & 1) { ok_ = q.x; ov = q.y; q.x = key; q.y = v; }
+          else { ok_ = q.z; ov = q.w; q.z = key; q.w = v; }
+          a = ok_ >> 16; c = ok_ & 0xFFFF; v = ov;
+        }
+      }
+      if (!ok) break;
+    }
+    if (ok) { out->swap(b); return true; }
+  }
+  return false;
+}
+
 }  // namespace
 
 extern "C" int32_t sw_encoder_create(const int32_t* pairs, const int32_t* vals, int64_t n, int32_t device,
@@ -150,7 +208,7 @@ extern "C" int32_t sw_encoder_create(const int32_t* pairs, const int32_t* vals, 
   for (int64_t i = 0; i < n; ++i) {
     int32_t a = pairs[2 * i], b = pairs[2 * i + 1], v = vals[i];
     if (a < 0 || b < 0) return fail(SW_ERR_ARG, "sw_encoder_create: negative token id in a pair");
-    if (v < 0 || (uint32_t)v >= kRecomp) return fail(SW_ERR_ARG, "sw_encoder_create: merge value out of range");
+    if (v < 0) return fail(SW_ERR_ARG, "sw_encoder_create: negative merge value");
     uint64_t k = ((uint64_t)(uint32_t)a << 32) | (uint32_t)b;
     auto it = dict.find(k);
     if (it == dict.end()) { dict.emplace(k, v); order.push_back(k); }
@@ -158,48 +216,26 @@ extern "C" int32_t sw_encoder_create(const int32_t* pairs, const int32_t* vals, 
     if (a > 0xFFFF || b > 0xFFFF || (a == 0xFFFF && b == 0xFFFF)) wide = true;
     if (a > 0xFFFD || b > 0xFFFD || v > 0xFFFD) ids16 = false;
   }
-  uint32_t log2cap = 4;
-  while ((1ull << log2cap) < 2 * (uint64_t)order.size() + 2) ++log2cap;
-  const uint64_t cap = 1ull << log2cap;
   sw_encoder* h = new sw_encoder();
   h->device = device;
   h->n_merges = (int64_t)order.size();
-  h->table.mask = (uint32_t)(cap - 1);
   h->table.wide = wide ? 1u : 0u;
   h->ids16 = ids16 && !wide;
-  std::vector<uint8_t> host;
-  if (!wide) {
-    h->table.shift = 32 - log2cap;
-    std::vector<uint2> s(cap, make_uint2(kEmptyKey, 0));
-    for (uint64_t k : order) {
-      uint32_t key = (uint32_t)(((k >> 32) << 16) | (k & 0xFFFF));
-      uint32_t p = hash_narrow(key, h->table.shift);
-      while (s[p].x != kEmptyKey) p = (p + 1) & h->table.mask;
-      s[p] = make_uint2(key, (uint32_t)dict[k]);
-    }
-    host.resize(cap * sizeof(uint2));
-    std::memcpy(host.data(), s.data(), host.size());
-  } else {
-    h->table.shift = 64 - log2cap;
-    std::vector<uint4> s(cap, make_uint4(kEmptyKey, 0, 0, 0));
-    for (uint64_t k : order) {
-      uint32_t a = (uint32_t)(k >> 32), b = (uint32_t)k;
-      uint32_t p = hash_wide(a, b, h->table.shift);
-      while (s[p].x != kEmptyKey) p = (p + 1) & h->table.mask;
-      s[p] = make_uint4(a, b, (uint32_t)dict[k], 0);
-    }
-    host.resize(cap * sizeof(uint4));
-    std::memcpy(host.data(), s.data(), host.size());
+  std::vector<uint4> host;
+  if (!build_cuckoo(dict, order, wide, &h->table, &host)) {
+    delete h;
+    return fail(SW_ERR_ALLOC, "sw_encoder_create: could not build the pair table");
   }
+  const size_t table_bytes = host.size() * sizeof(uint4);
   DeviceGuard g(device);
   hipError_t e = hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking);
-  if (e == hipSuccess) e = hipMalloc(&h->d_table, host.size());
-  if (e == hipSuccess) e = hipMemcpy(h->d_table, host.data(), host.size(), hipMemcpyHostToDevice);
+  if (e == hipSuccess) e = hipMalloc(&h->d_table, table_bytes);
+  if (e == hipSuccess) e = hipMemcpy(h->d_table, host.data(), table_bytes, hipMemcpyHostToDevice);
   if (e != hipSuccess) {
     sw_encoder_destroy(h);
     return fail(SW_ERR_HIP, std::string("sw_encoder_create: ") + hipGetErrorString(e));
   }
-  h->table.slots = h->d_table;
+  h->table.buckets = h->d_table;
   *out = h;
   return SW_OK;
 }

@@ -44,29 +44,27 @@ struct IdT {
   __device__ static int idx_of(Key k) { return (int)(k & 0xFF); }
 };
 
-// merges.get((a, b)): the value, or kInf.
+// merges.get((a, b)): the value, or kInf.  Two independent 16-byte loads (both cuckoo
+// candidate buckets), no loop: one memory round trip for every lane.
 template <bool kWide>
 __device__ __forceinline__ uint32_t lookup(const DevTable& t, uint32_t a, uint32_t b) {
+  const uint32_t f = mix_key(a, b);
+  const uint4* B = (const uint4*)t.buckets;
+  const uint4 q1 = B[bucket1(f, t)];
+  const uint4 q2 = B[bucket2(f, t)];
   if (!kWide) {
-    if ((a | b) > 0xFFFFu) return kInf;
-    const uint2* s = (const uint2*)t.slots;
     const uint32_t key = (a << 16) | b;
-    uint32_t h = hash_narrow(key, t.shift);
-    while (true) {
-      const uint2 e = s[h];
-      if (e.x == key) return e.y;
-      if (e.x == kEmptyKey) return kInf;
-      h = (h + 1) & t.mask;
-    }
+    uint32_t v = kInf;
+    v = (q1.x == key) ? q1.y : v;
+    v = (q1.z == key) ? q1.w : v;
+    v = (q2.x == key) ? q2.y : v;
+    v = (q2.z == key) ? q2.w : v;
+    return ((a | b) > 0xFFFFu) ? kInf : v;
   } else {
-    const uint4* s = (const uint4*)t.slots;
-    uint32_t h = hash_wide(a, b, t.shift);
-    while (true) {
-      const uint4 e = s[h];
-      if (e.x == a && e.y == b) return e.z;
-      if (e.x == kEmptyKey) return kInf;
-      h = (h + 1) & t.mask;
-    }
+    uint32_t v = kInf;
+    v = (q1.x == a && q1.y == b) ? q1.z : v;
+    v = (q2.x == a && q2.y == b) ? q2.z : v;
+    return v;
   }
 }
 
@@ -105,12 +103,23 @@ template <typename Id, bool kWide>
 __device__ int lane_merge(const DevTable& t, Id* id, Id* rk, int n) {
   using K = IdT<Id>;
   typename K::Key best = K::key_inf;
-  // initial ranks: independent lookups
-  for (int j = 0; j + 1 < n; ++j) {
-    const Id r = lookup_id<Id, kWide>(t, id[j], id[j + 1]);
-    rk[j] = r;
-    const typename K::Key k = K::key(r, j);
-    best = k < best ? k : best;
+  // initial ranks: independent lookups, four in flight per lane
+  for (int j0 = 0; j0 + 1 < n; j0 += 4) {
+    Id r[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int j = min(j0 + u, n - 2);  // clamped duplicates keep the loads unconditional
+      r[u] = lookup_id<Id, kWide>(t, id[j], id[j + 1]);
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int j = j0 + u;
+      if (j + 1 < n) {
+        rk[j] = r[u];
+        const typename K::Key k = K::key(r[u], j);
+        best = k < best ? k : best;
+      }
+    }
   }
   while (n >= 2) {
     const Id nv = K::rank_of(best);
@@ -158,13 +167,18 @@ __device__ int lane_merge(const DevTable& t, Id* id, Id* rk, int n) {
     }
     n = w;
     need &= (n >= 2) ? ((1u << (n - 1)) - 1u) : 0u;
-    while (need) {
-      const int j = __ffs(need) - 1;
+    while (need) {  // two lookups in flight per round
+      const int j1 = __ffs(need) - 1;
       need &= need - 1;
-      const Id r = lookup_id<Id, kWide>(t, id[j], id[j + 1]);
-      rk[j] = r;
-      const typename K::Key k = K::key(r, j);
-      best = k < best ? k : best;
+      const int j2 = need ? __ffs(need) - 1 : j1;
+      need &= need - 1;
+      const Id r1 = lookup_id<Id, kWide>(t, id[j1], id[j1 + 1]);
+      const Id r2 = lookup_id<Id, kWide>(t, id[j2], id[j2 + 1]);
+      rk[j1] = r1;
+      rk[j2] = r2;
+      const typename K::Key k1 = K::key(r1, j1), k2 = K::key(r2, j2);
+      best = k1 < best ? k1 : best;
+      best = k2 < best ? k2 : best;
     }
   }
   return n;
@@ -285,8 +299,8 @@ __device__ inline uint32_t block_excl_scan(uint32_t v, uint32_t* sh, uint32_t* t
 
 template <typename Id, bool kWide>
 __global__ void __launch_bounds__(kThreads) k_encode_tiles(TileArgs a) {
-  __shared__ Id s_id[kWin];
-  __shared__ Id s_rk[kWin];
+  __shared__ __attribute__((aligned(16))) Id s_id[kWin];
+  __shared__ __attribute__((aligned(16))) Id s_rk[kWin];
   __shared__ uint64_t s_bits[kTileWords];
   __shared__ uint16_t s_cstart[kTile + 1];
   __shared__ uint32_t s_cnt[kTile + 1];       // chunk length, then token count, then offset
@@ -310,8 +324,12 @@ __global__ void __launch_bounds__(kThreads) k_encode_tiles(TileArgs a) {
     if (g + 4 <= a.n_bytes && ((uintptr_t)a.bytes & 3) == 0) v = *(const uint32_t*)(a.bytes + g);
     else
       for (int k = 0; k < 4; ++k) v |= (g + k < a.n_bytes ? (uint32_t)a.bytes[g + k] : 0u) << (8 * k);
-    s_id[i] = (Id)(v & 0xFF); s_id[i + 1] = (Id)((v >> 8) & 0xFF);
-    s_id[i + 2] = (Id)((v >> 16) & 0xFF); s_id[i + 3] = (Id)(v >> 24);
+    if (sizeof(Id) == 2) {  // one 8-byte LDS store per thread
+      const uint32_t lo = (v & 0xFFu) | ((v & 0xFF00u) << 8), hi = ((v >> 16) & 0xFFu) | ((v >> 8) & 0xFF0000u);
+      *(uint2*)(s_id + i) = make_uint2(lo, hi);
+    } else {
+      *(uint4*)(s_id + i) = make_uint4(v & 0xFF, (v >> 8) & 0xFF, (v >> 16) & 0xFF, v >> 24);
+    }
   }
   if (tid < kTileWords) s_bits[tid] = (w0 + tid < a.n_words) ? a.bits[w0 + tid] : 0ULL;
   if (tid < kShort + 2) s_bin[tid] = 0;

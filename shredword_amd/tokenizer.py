@@ -105,8 +105,8 @@ class Tokenizer(BaseTokenizer):
         n = len(self._merges)
         pairs = np.array(list(self._merges.keys()), dtype=np.int64).reshape(n, 2)
         vals = np.array(list(self._merges.values()), dtype=np.int64).reshape(n)
-        if n and (pairs.min() < 0 or pairs.max() > 0x7FFFFFFF or vals.min() < 0 or vals.max() > 0x7FFFFFFD):
-            raise ValueError("merges must map non-negative int32 pairs to values in [0, 2^31-3]")
+        if n and (pairs.min() < 0 or pairs.max() > 0x7FFFFFFF or vals.min() < 0 or vals.max() > 0x7FFFFFFF):
+            raise ValueError("merges must map non-negative int32 pairs to values in [0, 2^31-1]")
         pairs = np.ascontiguousarray(pairs, dtype=np.int32)
         vals = np.ascontiguousarray(vals, dtype=np.int32)
         L = _lib.lib()

@@ -117,6 +117,12 @@ int32_t sw_encode_device(sw_encoder* h, const uint8_t* d_bytes, int64_t n_bytes,
 int32_t sw_encoder_set_timing(sw_encoder* h, int32_t on);
 double sw_encoder_last_kernel_ms(const sw_encoder* h);
 
+/* Diagnostic builds only (compiled with -DSW_STAMPS): cycles spent in each phase of the merge
+ * kernel, summed over workgroups (phases: 0 stage+enumerate, 1 lengths+sort, 2 per-lane merges,
+ * 3 long chunks, 4 scan+write, 5 string offsets).  reset != 0 zeroes the counters.  Regular
+ * builds return SW_ERR_ARG. */
+int32_t sw_encoder_phase_cycles(sw_encoder* h, double* out8, int32_t reset);
+
 /* ---- synthetic corpora (bench inputs; deterministic for any thread count) --------------
  * Fills out_off[0..n_strings] with string offsets; when out_bytes is non-NULL also writes
  * the bytes (cap >= out_off[n_strings]).  Returns the total byte count or SW_ERR_*. */

@@ -39,13 +39,16 @@ class ShredwordError(RuntimeError):
 
 def _get_lib_path():
     """Locate the built library the way cbase.py:_get_lib_path does (package dir, lib/, build/)."""
+    override = os.environ.get("SHREDWORD_HIP_LIB")  # e.g. the diagnostic (SW_STAMPS) build
+    if override:
+        return override
     pkg_dir = os.path.dirname(os.path.abspath(__file__))
     exts = (".so", sysconfig.get_config_var("EXT_SUFFIX") or ".so")
     for d in (pkg_dir, os.path.join(pkg_dir, "lib"), os.path.join(pkg_dir, "..", "build")):
         if not os.path.isdir(d):
             continue
         for f in sorted(os.listdir(d)):
-            if f.startswith(LIB_NAMES) and f.endswith(exts):
+            if f.startswith(LIB_NAMES) and f.endswith(exts) and "_stamps" not in f:
                 return os.path.join(d, f)
     raise FileNotFoundError(
         "libshredword_hip.so not found next to shredword_amd/ -- run "
@@ -70,6 +73,7 @@ _SIGNATURES = {
                                    c_void_p, c_void_p, POINTER(c_int64)]),
     "sw_encoder_set_timing": (c_int32, [c_void_p, c_int32]),
     "sw_encoder_last_kernel_ms": (c_double, [c_void_p]),
+    "sw_encoder_phase_cycles": (c_int32, [c_void_p, POINTER(c_double), c_int32]),
     "sw_synth_corpus": (c_int64, [c_uint64, c_int32, c_int64, c_int64, POINTER(c_uint8), c_int64,
                                   POINTER(c_int64), c_int32]),
 }

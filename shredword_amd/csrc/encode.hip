@@ -67,6 +67,8 @@ struct sw_encoder {
   uint32_t* d_lw_id = nullptr;
   uint32_t* d_lw_rk = nullptr;
   int64_t* d_part = nullptr;
+  int64_t* d_tile_slo = nullptr;
+  unsigned long long* d_stamps = nullptr;  // SW_STAMPS builds
   uint32_t* d_tile_cnt = nullptr;
   int64_t* d_tile_first = nullptr;
   int64_t* d_tile_base = nullptr;
@@ -100,6 +102,8 @@ struct DeviceGuard {
 
 void free_workspace(sw_encoder* h) {
   (void)hipFree(h->d_scratch); (void)hipFree(h->d_lw_id); (void)hipFree(h->d_lw_rk); (void)hipFree(h->d_part);
+  (void)hipFree(h->d_tile_slo); (void)hipFree(h->d_stamps);
+  h->d_tile_slo = nullptr; h->d_stamps = nullptr;
   (void)hipFree(h->d_tile_cnt); (void)hipFree(h->d_tile_first); (void)hipFree(h->d_tile_base);
   (void)hipFree(h->d_total);
   h->d_scratch = nullptr; h->d_lw_id = nullptr; h->d_lw_rk = nullptr; h->d_part = nullptr; h->d_tile_cnt = nullptr;
@@ -122,6 +126,9 @@ int32_t ensure_workspace(sw_encoder* h, int64_t n_bytes) {
   HIP_TRY(hipMalloc(&h->d_scratch, sizeof(int32_t) * nb));
   HIP_TRY(hipMalloc(&h->d_lw_id, sizeof(uint32_t) * nb));
   HIP_TRY(hipMalloc(&h->d_lw_rk, sizeof(uint32_t) * nb));
+  HIP_TRY(hipMalloc(&h->d_tile_slo, sizeof(int64_t) * n_tiles));
+  HIP_TRY(hipMalloc(&h->d_stamps, sizeof(unsigned long long) * 8));
+  HIP_TRY(hipMemset(h->d_stamps, 0, sizeof(unsigned long long) * 8));
   HIP_TRY(hipMalloc(&h->d_part, sizeof(int64_t) * ((n_tiles + kScanBlock - 1) / kScanBlock + 1)));
   HIP_TRY(hipMalloc(&h->d_tile_cnt, sizeof(uint32_t) * n_tiles));
   HIP_TRY(hipMalloc(&h->d_tile_first, sizeof(int64_t) * n_tiles));
@@ -282,6 +289,25 @@ extern "C" double sw_encoder_last_kernel_ms(const sw_encoder* h) {
   return sum / (double)h->ev_used;
 }
 
+// Diagnostic builds only (-DSW_STAMPS): cycles per k_encode_tiles phase summed over workgroups
+// since the workspace was allocated (or the last reset).
+extern "C" int32_t sw_encoder_phase_cycles(sw_encoder* h, double* out8, int32_t reset) {
+#ifdef SW_STAMPS
+  if (!h || !out8 || !h->d_stamps) return fail(SW_ERR_ARG, "sw_encoder_phase_cycles: no workspace");
+  DeviceGuard g(h->device);
+  unsigned long long v[8];
+  HIP_TRY(hipStreamSynchronize(h->stream));
+  HIP_TRY(hipDeviceSynchronize());
+  HIP_TRY(hipMemcpy(v, h->d_stamps, sizeof(v), hipMemcpyDeviceToHost));
+  for (int i = 0; i < 8; ++i) out8[i] = (double)v[i];
+  if (reset) HIP_TRY(hipMemset(h->d_stamps, 0, sizeof(v)));
+  return SW_OK;
+#else
+  (void)h; (void)out8; (void)reset;
+  return fail(SW_ERR_ARG, "sw_encoder_phase_cycles: not a diagnostic (SW_STAMPS) build");
+#endif
+}
+
 extern "C" int32_t sw_encode_device(sw_encoder* h, const uint8_t* d_bytes, int64_t n_bytes, const int64_t* d_str_off,
                                     int64_t n_str, const uint64_t* d_chunk_bits, int32_t* d_out_ids,
                                     int64_t* d_out_off, void* stream, int64_t* n_tokens_host) {
@@ -298,6 +324,9 @@ extern "C" int32_t sw_encode_device(sw_encoder* h, const uint8_t* d_bytes, int64
     a.str_off = d_str_off; a.n_str = n_str; a.table = h->table;
     a.scratch = h->d_scratch; a.lw_id = h->d_lw_id; a.lw_rk = h->d_lw_rk;
     a.tile_cnt = h->d_tile_cnt; a.tile_first = h->d_tile_first; a.out_off = d_out_off;
+    a.tile_slo = h->d_tile_slo; a.stamps = h->d_stamps;
+    hipLaunchKernelGGL(k_tile_strings, dim3((unsigned)((n_tiles + 255) / 256)), dim3(256), 0, st, d_str_off, n_str,
+                       n_tiles, h->d_tile_slo);
     hipEvent_t e0 = nullptr, e1 = nullptr;
     if (h->timing) {
       while (h->ev_pool.size() < 2 * (h->ev_used + 1)) {

@@ -272,7 +272,22 @@ struct TileArgs {
   uint32_t* tile_cnt;    // [n_tiles]
   int64_t* tile_first;   // [n_tiles] first chunk start in tile (or -1)
   int64_t* out_off;      // [n_str+1] tile-local offsets, rebased by k_string_offsets
+  const int64_t* tile_slo;  // [n_tiles] first string starting at or after the tile start
+  unsigned long long* stamps;  // diagnostic builds (SW_STAMPS): cycles per phase, summed
 };
+
+#ifdef SW_STAMPS
+#define SW_STAMP(k)                                                                 \
+  do {                                                                              \
+    if (threadIdx.x == 0) {                                                         \
+      const unsigned long long now_ = __builtin_readcyclecounter();                 \
+      atomicAdd(&a.stamps[k], now_ - stamp_prev_);                                  \
+      stamp_prev_ = now_;                                                           \
+    }                                                                               \
+  } while (0)
+#else
+#define SW_STAMP(k) do {} while (0)
+#endif
 
 // exclusive block scan over kThreads threads (sh: kThreads/64 words); *total = block sum
 __device__ inline uint32_t block_excl_scan(uint32_t v, uint32_t* sh, uint32_t* total) {
@@ -314,6 +329,10 @@ __global__ void __launch_bounds__(kThreads) k_encode_tiles(TileArgs a) {
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int64_t tile = blockIdx.x;
   const int64_t t0 = tile * kTile;
+#ifdef SW_STAMPS
+  unsigned long long stamp_prev_ = __builtin_readcyclecounter();
+#endif
+  if (tid == 0) s_slo = a.tile_slo[tile];
   const int64_t t1 = min(t0 + (int64_t)kTile, a.n_bytes);
   const int64_t w0 = t0 >> 6;
 
@@ -369,6 +388,7 @@ __global__ void __launch_bounds__(kThreads) k_encode_tiles(TileArgs a) {
   }
   __syncthreads();
   const int C = (int)nchunks;
+  SW_STAMP(0);
 
   // 3. lengths; histogram by length (short) / long list
   for (int k = tid; k < C; k += kThreads) {
@@ -400,14 +420,23 @@ __global__ void __launch_bounds__(kThreads) k_encode_tiles(TileArgs a) {
   }
   __syncthreads();
   const int n_short = (int)s_bin[kShort + 1];
+  SW_STAMP(1);
 
   // 4. per-lane merge loop on short chunks, in place in the LDS window
-  for (int r = tid; r < n_short; r += kThreads) {
+  // rounds alternate direction (zig-zag) so a lane with a long chunk in one round gets a short
+  // one in the next and the four waves finish together
+  for (int r0 = 0; r0 < n_short; r0 += kThreads) {
+    const int r = r0 + (((r0 / kThreads) & 1) ? (kThreads - 1 - tid) : tid);
+    if (r >= n_short) continue;
     const int k = s_order[r];
     const int ls = s_cstart[k];
     s_cnt[k] = (uint32_t)lane_merge<Id, kWide>(a.table, s_id + ls, s_rk + ls, (int)s_cnt[k]);
   }
 
+#ifdef SW_STAMPS
+  __syncthreads();
+  SW_STAMP(2);
+#endif
   // 5. long chunks: one wave per chunk (LDS window if it fits, else the global work area)
   const int nl = (int)s_nlong;
   for (int q = wid; q < nl; q += kThreads / 64) {
@@ -431,6 +460,7 @@ __global__ void __launch_bounds__(kThreads) k_encode_tiles(TileArgs a) {
   }
   __syncthreads();
 
+  SW_STAMP(3);
   // 6. tile-local exclusive offsets over chunk token counts
   const int per = (C + kThreads - 1) / kThreads;
   const int c0 = min(C, tid * per), c1 = min(C, c0 + per);
@@ -482,15 +512,10 @@ __global__ void __launch_bounds__(kThreads) k_encode_tiles(TileArgs a) {
   }
 
   // 8. strings starting in this tile: tile-local output offset (rebased later)
-  if (tid == 0) {
-    int64_t lo = 0, hi = a.n_str;  // first s with str_off[s] >= t0
-    while (lo < hi) {
-      const int64_t m = (lo + hi) >> 1;
-      if (a.str_off[m] < t0) lo = m + 1; else hi = m;
-    }
-    s_slo = lo;
-  }
+#ifdef SW_STAMPS
   __syncthreads();
+  SW_STAMP(4);
+#endif
   for (int64_t s = s_slo + tid; s < a.n_str; s += kThreads) {
     const int64_t p = a.str_off[s];
     if (p >= t1) break;
@@ -502,6 +527,23 @@ __global__ void __launch_bounds__(kThreads) k_encode_tiles(TileArgs a) {
     }
     a.out_off[s] = (int64_t)s_cnt[lo];
   }
+#ifdef SW_STAMPS
+  __syncthreads();
+  SW_STAMP(5);
+#endif
+}
+
+// first string starting at or after each tile's first byte (binary search per tile)
+__global__ void k_tile_strings(const int64_t* str_off, int64_t n_str, int64_t n_tiles, int64_t* tile_slo) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= n_tiles) return;
+  const int64_t t0 = t * kTile;
+  int64_t lo = 0, hi = n_str;
+  while (lo < hi) {
+    const int64_t m = (lo + hi) >> 1;
+    if (str_off[m] < t0) lo = m + 1; else hi = m;
+  }
+  tile_slo[t] = lo;
 }
 
 // ---------------------------------------------------------------------------------------

@@ -80,6 +80,22 @@ void sw_encoder_destroy(sw_encoder* h);
  * encode grows it on demand otherwise). */
 int32_t sw_encoder_reserve(sw_encoder* h, int64_t max_bytes, int64_t max_strings);
 
+/* Encoder options (sw_encoder_set_option).
+ *   SW_OPT_CHUNK_TABLE  1 (default): a chunk of 2..16 bytes that encodes to exactly one token is
+ *                       answered from a table built at creation (the vocabulary's byte strings
+ *                       whose own encoding is a single token); 0: every chunk runs the merge
+ *                       loop.  Results are identical either way. */
+#define SW_OPT_CHUNK_TABLE 1
+int32_t sw_encoder_set_option(sw_encoder* h, int32_t option, int64_t value);
+
+/* Encoder facts (sw_encoder_get_info): distinct merges, whole-chunk table entries, whether the
+ * pair table uses the wide (>16-bit ids) layout, whether kernels run on 16-bit ids. */
+#define SW_INFO_MERGES 1
+#define SW_INFO_CHUNK_ENTRIES 2
+#define SW_INFO_WIDE_TABLE 3
+#define SW_INFO_IDS16 4
+int64_t sw_encoder_get_info(const sw_encoder* h, int32_t what);
+
 /* ---- host pre-split (apply_regex, base.py:38-58) ---------------------------------------
  * Marks, for every string in bytes[str_off[0] .. str_off[n_str]), the first byte of each of
  * its chunks in the bitmap chunk_bits (bit i of word i/64, LSB first; offsets are relative
@@ -110,17 +126,17 @@ int32_t sw_encode_device(sw_encoder* h, const uint8_t* d_bytes, int64_t n_bytes,
                          int64_t n_str, const uint64_t* d_chunk_bits, int32_t* d_out_ids, int64_t* d_out_off,
                          void* stream, int64_t* n_tokens_host);
 
-/* Timing of the dominant kernel (the merge-loop kernel, k_encode_tiles) with HIP events on the
- * stream it is launched on.  sw_encoder_set_timing(h, 1) starts a new accumulation window (one
+/* Timing of the encode proper -- k_classify plus the merge-loop kernels (k_merge_bucket x4,
+ * k_merge_long), back to back on one stream -- with HIP events on that stream.  sw_encoder_set_timing(h, 1) starts a new accumulation window (one
  * event pair per launch, no host synchronisation per call); sw_encoder_last_kernel_ms returns the
  * average device time per launch over that window (it synchronises on the last event), or -1. */
 int32_t sw_encoder_set_timing(sw_encoder* h, int32_t on);
 double sw_encoder_last_kernel_ms(const sw_encoder* h);
 
-/* Diagnostic builds only (compiled with -DSW_STAMPS): cycles spent in each phase of the merge
- * kernel, summed over workgroups (phases: 0 stage+enumerate, 1 lengths+sort, 2 per-lane merges,
- * 3 long chunks, 4 scan+write, 5 string offsets).  reset != 0 zeroes the counters.  Regular
- * builds return SW_ERR_ARG. */
+/* Diagnostic builds only (compiled with -DSW_STAMPS): device cycles summed over workgroups,
+ * per phase: 0 k_classify stage+enumerate, 1 classify lookups, 2 slot/queue writes, 3 string
+ * offsets, 4 k_merge_bucket N<16 (per block), 5 k_merge_bucket N>=16, 6 k_merge_long.
+ * reset != 0 zeroes the counters.  Regular builds return SW_ERR_ARG. */
 int32_t sw_encoder_phase_cycles(sw_encoder* h, double* out8, int32_t reset);
 
 /* ---- synthetic corpora (bench inputs; deterministic for any thread count) --------------

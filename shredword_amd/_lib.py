@@ -21,6 +21,8 @@ SW_ERR_ARG, SW_ERR_HIP, SW_ERR_ALLOC, SW_ERR_CAP, SW_ERR_NODEV = -1, -2, -3, -4,
 
 SW_PAT_CL100K, SW_PAT_GPT2, SW_PAT_NONE = 0, 1, 2
 SW_CORPUS_ASCII, SW_CORPUS_MIXED, SW_CORPUS_STRESS = 0, 1, 2
+SW_OPT_CHUNK_TABLE = 1
+SW_INFO_MERGES, SW_INFO_CHUNK_ENTRIES, SW_INFO_WIDE_TABLE, SW_INFO_IDS16 = 1, 2, 3, 4
 
 
 class SwStats(Structure):
@@ -48,7 +50,8 @@ def _get_lib_path():
         if not os.path.isdir(d):
             continue
         for f in sorted(os.listdir(d)):
-            if f.startswith(LIB_NAMES) and f.endswith(exts) and "_stamps" not in f:
+            # variants (libshredword_hip_<name>.so: diagnostics, A/B builds) load only by override
+            if f.startswith(LIB_NAMES) and f.endswith(exts) and not f.startswith("libshredword_hip_"):
                 return os.path.join(d, f)
     raise FileNotFoundError(
         "libshredword_hip.so not found next to shredword_amd/ -- run "
@@ -71,6 +74,8 @@ _SIGNATURES = {
                                   POINTER(SwStats)]),
     "sw_encode_device": (c_int32, [c_void_p, c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_void_p,
                                    c_void_p, c_void_p, POINTER(c_int64)]),
+    "sw_encoder_set_option": (c_int32, [c_void_p, c_int32, c_int64]),
+    "sw_encoder_get_info": (c_int64, [c_void_p, c_int32]),
     "sw_encoder_set_timing": (c_int32, [c_void_p, c_int32]),
     "sw_encoder_last_kernel_ms": (c_double, [c_void_p]),
     "sw_encoder_phase_cycles": (c_int32, [c_void_p, POINTER(c_double), c_int32]),

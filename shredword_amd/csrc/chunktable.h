@@ -1,0 +1,54 @@
+// Whole-chunk table: byte strings of 2..16 bytes whose exact encoding is ONE token.
+//
+// Built once per merge table at encoder creation (host side, chunktable.cpp).  Candidates are
+// the byte strings of the vocabulary (build_vocab, shredword/base.py:60-79); each candidate B
+// is encoded with the exact merge loop and kept iff encode(B) == [T].  At encode time a chunk
+// whose bytes are in the table is answered with T directly, and every other chunk runs the
+// merge loop -- so the result is identical by construction: a chunk that encodes to a single
+// token T necessarily has bytes(T) == chunk, so the table is a perfect classifier of
+// single-token chunks.  This is the same shortcut tiktoken takes ("piece is itself a token").
+//
+// Device layout: two two-choice cuckoo tables keyed by (bytes, length):
+//   short (2..8 bytes):  16-byte entries {bytes 0-3, bytes 4-7, len << 24 | token, 0}
+//   long  (9..16 bytes): 32-byte entries {bytes 0-3, 4-7, 8-11, 12-15}{len << 24 | token, 0,0,0}
+// Unused key bytes are zero; an empty entry has len 0.  Tokens >= 2^24 are not tabled.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <unordered_map>
+#include <vector>
+
+namespace sw {
+
+struct DevChunkTable {
+  const uint4* sb;  // short buckets
+  const uint4* lb;  // long buckets (2 uint4 each)
+  uint32_t s_shift, s_m1, s_m2;
+  uint32_t l_shift, l_m1, l_m2;
+  uint32_t enabled;
+};
+
+__host__ __device__ inline uint32_t chunk_hash(uint64_t k0, uint64_t k1, uint32_t len) {
+  uint64_t x = k0 * 0x9E3779B97F4A7C15ULL ^ (k1 + 0x632BE59BD9B4E019ULL) * 0xC2B2AE3D27D4EB4FULL ^ (uint64_t)len;
+  x ^= x >> 29;
+  x *= 0xBF58476D1CE4E5B9ULL;
+  x ^= x >> 32;
+  return (uint32_t)x;
+}
+
+struct ChunkTableHost {
+  std::vector<uint4> sb, lb;
+  uint32_t s_shift = 0, s_m1 = 0, s_m2 = 0, l_shift = 0, l_m1 = 0, l_m2 = 0;
+  size_t n_short = 0, n_long = 0;
+};
+
+// dict: (a << 32 | b) -> value; order: first-insertion order of the pairs (dict order).
+bool build_chunk_table(const std::unordered_map<uint64_t, int32_t>& dict, const std::vector<uint64_t>& order,
+                       ChunkTableHost* out);
+
+// Exact encode of one chunk on the host (the semantics of shredword/base.py:10-36); used by
+// the table builder.
+std::vector<int32_t> host_encode_chunk(const std::unordered_map<uint64_t, int32_t>& dict, const uint8_t* b, int n);
+
+}  // namespace sw

@@ -8,11 +8,14 @@
 // encode abstract), merge (base.py:22-36).
 //
 // Device pipeline (all on one stream; inputs resident in HBM; kernels in kernels.h):
-//   k_encode_tiles   merge loop per 2 KiB tile (per-lane short chunks, wave-cooperative long
-//                    chunks), tile-local compaction into a position-indexed scratch
-//   k_scan_reduce / k_scan_parts / k_scan_apply   exclusive scan of per-tile id counts
-//   k_compact        tile outputs -> contiguous out_ids
-//   k_string_offsets per-string output offsets
+//   k_tile_strings   first string of each tile
+//   k_classify       per 2 KiB tile: single bytes + whole-chunk-table hits settled, the rest
+//                    queued by length bucket with reserved output slots
+//   k_merge_bucket   exact merge loop, one chunk per lane, in registers (N = 4/8/16/32)
+//   k_merge_long     wave-cooperative merge loop for chunks > 32 bytes
+//   k_scan_*         exclusive scan of per-tile id counts
+//   k_compact        sentinel-free ids, contiguous; string slot -> id offsets
+//   k_string_offsets final per-string offsets
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -61,6 +64,9 @@ struct sw_encoder {
   void* d_table = nullptr;
   int64_t n_merges = 0;
   bool ids16 = false;  // every pair member and value <= 0xFFFD: 16-bit ids in the kernels
+  DevChunkTable chunks{};
+  void* d_chunks = nullptr;
+  int64_t n_chunk_entries = 0;
   // workspace
   int64_t cap_bytes = -1, cap_str = -1;
   int32_t* d_scratch = nullptr;
@@ -68,6 +74,11 @@ struct sw_encoder {
   uint32_t* d_lw_rk = nullptr;
   int64_t* d_part = nullptr;
   int64_t* d_tile_slo = nullptr;
+  uint32_t* d_tile_slots = nullptr;
+  uint64_t* d_queue = nullptr;        // merge queue, bucket regions
+  int64_t* d_qbase = nullptr;         // [kNumBuckets] region starts
+  unsigned long long* d_qcnt = nullptr;  // [kNumBuckets] entries per bucket (zeroed per call)
+  uint64_t* d_long_slot = nullptr;
   unsigned long long* d_stamps = nullptr;  // SW_STAMPS builds
   uint32_t* d_tile_cnt = nullptr;
   int64_t* d_tile_first = nullptr;
@@ -103,7 +114,10 @@ struct DeviceGuard {
 void free_workspace(sw_encoder* h) {
   (void)hipFree(h->d_scratch); (void)hipFree(h->d_lw_id); (void)hipFree(h->d_lw_rk); (void)hipFree(h->d_part);
   (void)hipFree(h->d_tile_slo); (void)hipFree(h->d_stamps);
-  h->d_tile_slo = nullptr; h->d_stamps = nullptr;
+  (void)hipFree(h->d_tile_slots); (void)hipFree(h->d_queue); (void)hipFree(h->d_qbase); (void)hipFree(h->d_qcnt);
+  (void)hipFree(h->d_long_slot);
+  h->d_tile_slo = nullptr; h->d_stamps = nullptr; h->d_tile_slots = nullptr; h->d_queue = nullptr;
+  h->d_qbase = nullptr; h->d_qcnt = nullptr; h->d_long_slot = nullptr;
   (void)hipFree(h->d_tile_cnt); (void)hipFree(h->d_tile_first); (void)hipFree(h->d_tile_base);
   (void)hipFree(h->d_total);
   h->d_scratch = nullptr; h->d_lw_id = nullptr; h->d_lw_rk = nullptr; h->d_part = nullptr; h->d_tile_cnt = nullptr;
@@ -127,6 +141,20 @@ int32_t ensure_workspace(sw_encoder* h, int64_t n_bytes) {
   HIP_TRY(hipMalloc(&h->d_lw_id, sizeof(uint32_t) * nb));
   HIP_TRY(hipMalloc(&h->d_lw_rk, sizeof(uint32_t) * nb));
   HIP_TRY(hipMalloc(&h->d_tile_slo, sizeof(int64_t) * n_tiles));
+  HIP_TRY(hipMalloc(&h->d_tile_slots, sizeof(uint32_t) * n_tiles));
+  {
+    // bucket b holds chunks of >= bucket_min_len(b) bytes: at most nb / min_len of them
+    int64_t qb[kNumBuckets], total = 0;
+    for (int b = 0; b < kNumBuckets; ++b) {
+      qb[b] = total;
+      total += nb / bucket_min_len(b) + 64;
+    }
+    HIP_TRY(hipMalloc(&h->d_queue, sizeof(uint64_t) * total));
+    HIP_TRY(hipMalloc(&h->d_qbase, sizeof(qb)));
+    HIP_TRY(hipMemcpy(h->d_qbase, qb, sizeof(qb), hipMemcpyHostToDevice));
+    HIP_TRY(hipMalloc(&h->d_qcnt, sizeof(unsigned long long) * kNumBuckets));
+    HIP_TRY(hipMalloc(&h->d_long_slot, sizeof(uint64_t) * (nb / bucket_min_len(kLongBucket) + 64)));
+  }
   HIP_TRY(hipMalloc(&h->d_stamps, sizeof(unsigned long long) * 8));
   HIP_TRY(hipMemset(h->d_stamps, 0, sizeof(unsigned long long) * 8));
   HIP_TRY(hipMalloc(&h->d_part, sizeof(int64_t) * ((n_tiles + kScanBlock - 1) / kScanBlock + 1)));
@@ -234,6 +262,12 @@ extern "C" int32_t sw_encoder_create(const int32_t* pairs, const int32_t* vals, 
     return fail(SW_ERR_ALLOC, "sw_encoder_create: could not build the pair table");
   }
   const size_t table_bytes = host.size() * sizeof(uint4);
+  ChunkTableHost ct;
+  if (!build_chunk_table(dict, order, &ct)) {
+    delete h;
+    return fail(SW_ERR_ALLOC, "sw_encoder_create: could not build the chunk table");
+  }
+  h->n_chunk_entries = (int64_t)(ct.n_short + ct.n_long);
   DeviceGuard g(device);
   hipError_t e = hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking);
   if (e == hipSuccess) e = hipMalloc(&h->d_table, table_bytes);
@@ -243,6 +277,21 @@ extern "C" int32_t sw_encoder_create(const int32_t* pairs, const int32_t* vals, 
     return fail(SW_ERR_HIP, std::string("sw_encoder_create: ") + hipGetErrorString(e));
   }
   h->table.buckets = h->d_table;
+  {
+    const size_t sb = ct.sb.size() * sizeof(uint4), lb = ct.lb.size() * sizeof(uint4);
+    e = hipMalloc(&h->d_chunks, sb + lb);
+    if (e == hipSuccess) e = hipMemcpy(h->d_chunks, ct.sb.data(), sb, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemcpy((char*)h->d_chunks + sb, ct.lb.data(), lb, hipMemcpyHostToDevice);
+    if (e != hipSuccess) {
+      sw_encoder_destroy(h);
+      return fail(SW_ERR_HIP, std::string("sw_encoder_create: ") + hipGetErrorString(e));
+    }
+    h->chunks.sb = (const uint4*)h->d_chunks;
+    h->chunks.lb = (const uint4*)((char*)h->d_chunks + sb);
+    h->chunks.s_shift = ct.s_shift; h->chunks.s_m1 = ct.s_m1; h->chunks.s_m2 = ct.s_m2;
+    h->chunks.l_shift = ct.l_shift; h->chunks.l_m1 = ct.l_m1; h->chunks.l_m2 = ct.l_m2;
+    h->chunks.enabled = 1;
+  }
   *out = h;
   return SW_OK;
 }
@@ -255,6 +304,7 @@ extern "C" void sw_encoder_destroy(sw_encoder* h) {
     free_workspace(h);
     free_io(h);
     (void)hipFree(h->d_table);
+    (void)hipFree(h->d_chunks);
     for (hipEvent_t ev : h->ev_pool) (void)hipEventDestroy(ev);
     if (h->stream) (void)hipStreamDestroy(h->stream);
   }
@@ -267,6 +317,25 @@ extern "C" int32_t sw_encoder_reserve(sw_encoder* h, int64_t max_bytes, int64_t 
   return ensure_workspace(h, max_bytes);
 }
 
+extern "C" int32_t sw_encoder_set_option(sw_encoder* h, int32_t option, int64_t value) {
+  if (!h) return fail(SW_ERR_ARG, "sw_encoder_set_option: null handle");
+  switch (option) {
+    case SW_OPT_CHUNK_TABLE: h->chunks.enabled = value ? 1u : 0u; return SW_OK;
+    default: return fail(SW_ERR_ARG, "sw_encoder_set_option: unknown option");
+  }
+}
+
+extern "C" int64_t sw_encoder_get_info(const sw_encoder* h, int32_t what) {
+  if (!h) return SW_ERR_ARG;
+  switch (what) {
+    case SW_INFO_MERGES: return h->n_merges;
+    case SW_INFO_CHUNK_ENTRIES: return h->n_chunk_entries;
+    case SW_INFO_WIDE_TABLE: return h->table.wide;
+    case SW_INFO_IDS16: return h->ids16 ? 1 : 0;
+    default: return SW_ERR_ARG;
+  }
+}
+
 extern "C" int32_t sw_encoder_set_timing(sw_encoder* h, int32_t on) {
   if (!h) return fail(SW_ERR_ARG, "sw_encoder_set_timing: null handle");
   h->timing = on != 0;
@@ -274,7 +343,7 @@ extern "C" int32_t sw_encoder_set_timing(sw_encoder* h, int32_t on) {
   return SW_OK;
 }
 
-// Average device time of k_encode_tiles over the launches recorded since the last
+// Average device time of the encode proper (k_classify .. k_merge_long) over the launches recorded since the last
 // sw_encoder_set_timing(h, 1); synchronises on the last recorded event.
 extern "C" double sw_encoder_last_kernel_ms(const sw_encoder* h) {
   if (!h || h->ev_used == 0) return -1.0;
@@ -289,7 +358,7 @@ extern "C" double sw_encoder_last_kernel_ms(const sw_encoder* h) {
   return sum / (double)h->ev_used;
 }
 
-// Diagnostic builds only (-DSW_STAMPS): cycles per k_encode_tiles phase summed over workgroups
+// Diagnostic builds only (-DSW_STAMPS): cycles per pipeline phase summed over workgroups
 // since the workspace was allocated (or the last reset).
 extern "C" int32_t sw_encoder_phase_cycles(sw_encoder* h, double* out8, int32_t reset) {
 #ifdef SW_STAMPS
@@ -319,12 +388,15 @@ extern "C" int32_t sw_encode_device(sw_encoder* h, const uint8_t* d_bytes, int64
   if (rc) return rc;
   const int64_t n_tiles = (n_bytes + kTile - 1) / kTile;
   if (n_tiles > 0) {
-    TileArgs a;
+    EncArgs a;
     a.bytes = d_bytes; a.n_bytes = n_bytes; a.bits = d_chunk_bits; a.n_words = (n_bytes + 63) / 64;
-    a.str_off = d_str_off; a.n_str = n_str; a.table = h->table;
+    a.str_off = d_str_off; a.n_str = n_str; a.table = h->table; a.chunks = h->chunks;
     a.scratch = h->d_scratch; a.lw_id = h->d_lw_id; a.lw_rk = h->d_lw_rk;
-    a.tile_cnt = h->d_tile_cnt; a.tile_first = h->d_tile_first; a.out_off = d_out_off;
-    a.tile_slo = h->d_tile_slo; a.stamps = h->d_stamps;
+    a.tile_cnt = h->d_tile_cnt; a.tile_slots = h->d_tile_slots; a.tile_first = h->d_tile_first;
+    a.out_off = d_out_off; a.tile_slo = h->d_tile_slo;
+    a.queue = h->d_queue; a.q_base = h->d_qbase; a.q_cnt = h->d_qcnt; a.long_slot = h->d_long_slot;
+    a.stamps = h->d_stamps;
+    HIP_TRY(hipMemsetAsync(h->d_qcnt, 0, sizeof(unsigned long long) * kNumBuckets, st));
     hipLaunchKernelGGL(k_tile_strings, dim3((unsigned)((n_tiles + 255) / 256)), dim3(256), 0, st, d_str_off, n_str,
                        n_tiles, h->d_tile_slo);
     hipEvent_t e0 = nullptr, e1 = nullptr;
@@ -338,10 +410,29 @@ extern "C" int32_t sw_encode_device(sw_encoder* h, const uint8_t* d_bytes, int64
       e1 = h->ev_pool[2 * h->ev_used + 1];
       HIP_TRY(hipEventRecord(e0, st));
     }
-    const dim3 grid((unsigned)n_tiles), block(kThreads);
-    if (h->table.wide) hipLaunchKernelGGL((k_encode_tiles<uint32_t, true>), grid, block, 0, st, a);
-    else if (h->ids16) hipLaunchKernelGGL((k_encode_tiles<uint16_t, false>), grid, block, 0, st, a);
-    else hipLaunchKernelGGL((k_encode_tiles<uint32_t, false>), grid, block, 0, st, a);
+    // the encode proper: classify, then the bucketed merge loops (timed together)
+    hipLaunchKernelGGL(k_classify, dim3((unsigned)n_tiles), dim3(kThreads), 0, st, a);
+    HIP_TRY(hipGetLastError());
+    const dim3 pg(2048), pb(kThreads);  // persistent grid for the queue kernels
+    if (h->table.wide) {
+      hipLaunchKernelGGL((k_merge_bucket<true, false, 4>), pg, pb, 0, st, a, 0, 2);
+      hipLaunchKernelGGL((k_merge_bucket<true, false, 8>), pg, pb, 0, st, a, 3, 4);
+      hipLaunchKernelGGL((k_merge_bucket<true, false, 16>), pg, pb, 0, st, a, 5, 7);
+      hipLaunchKernelGGL((k_merge_bucket<true, false, 32>), pg, pb, 0, st, a, 8, 9);
+      hipLaunchKernelGGL((k_merge_long<true>), dim3(512), pb, 0, st, a);
+    } else if (h->ids16) {
+      hipLaunchKernelGGL((k_merge_bucket<false, true, 4>), pg, pb, 0, st, a, 0, 2);
+      hipLaunchKernelGGL((k_merge_bucket<false, true, 8>), pg, pb, 0, st, a, 3, 4);
+      hipLaunchKernelGGL((k_merge_bucket<false, true, 16>), pg, pb, 0, st, a, 5, 7);
+      hipLaunchKernelGGL((k_merge_bucket<false, true, 32>), pg, pb, 0, st, a, 8, 9);
+      hipLaunchKernelGGL((k_merge_long<false>), dim3(512), pb, 0, st, a);
+    } else {
+      hipLaunchKernelGGL((k_merge_bucket<false, false, 4>), pg, pb, 0, st, a, 0, 2);
+      hipLaunchKernelGGL((k_merge_bucket<false, false, 8>), pg, pb, 0, st, a, 3, 4);
+      hipLaunchKernelGGL((k_merge_bucket<false, false, 16>), pg, pb, 0, st, a, 5, 7);
+      hipLaunchKernelGGL((k_merge_bucket<false, false, 32>), pg, pb, 0, st, a, 8, 9);
+      hipLaunchKernelGGL((k_merge_long<false>), dim3(512), pb, 0, st, a);
+    }
     HIP_TRY(hipGetLastError());
     if (h->timing) {
       HIP_TRY(hipEventRecord(e1, st));
@@ -354,14 +445,13 @@ extern "C" int32_t sw_encode_device(sw_encoder* h, const uint8_t* d_bytes, int64
     hipLaunchKernelGGL(k_scan_apply, dim3((unsigned)n_parts), dim3(kThreads), 0, st, h->d_tile_cnt, n_tiles,
                        h->d_part, h->d_tile_base);
     HIP_TRY(hipGetLastError());
-    hipLaunchKernelGGL(k_compact, dim3((unsigned)n_tiles), dim3(256), 0, st, h->d_scratch, h->d_tile_cnt,
-                       h->d_tile_first, h->d_tile_base, d_out_ids);
+    hipLaunchKernelGGL(k_compact, dim3((unsigned)n_tiles), dim3(kThreads), 0, st, a, h->d_tile_base, d_out_ids);
     HIP_TRY(hipGetLastError());
   } else {
     HIP_TRY(hipMemsetAsync(h->d_total, 0, sizeof(int64_t), st));
   }
   hipLaunchKernelGGL(k_string_offsets, dim3((unsigned)((n_str + 1 + 255) / 256)), dim3(256), 0, st, d_str_off, n_str,
-                     n_bytes, h->d_tile_base, h->d_total, d_out_off);
+                     n_bytes, h->d_total, d_out_off);
   HIP_TRY(hipGetLastError());
   if (n_tokens_host) {
     HIP_TRY(hipMemcpyAsync(n_tokens_host, h->d_total, sizeof(int64_t), hipMemcpyDeviceToHost, st));

@@ -5,44 +5,56 @@
 // stop if no pair is in merges; else replace every non-overlapping occurrence of that pair,
 // left to right, by the value.
 //
-// k_encode_tiles: one 256-thread workgroup per 2 KiB tile of input bytes.
-//   LDS holds the tile (+ a 32-byte halo) as an id array in POSITION SPACE: the chunk that
-//   starts at byte p keeps its ids in id[p .. p+n) and its pair ranks in rk[p .. p+n-1), so
-//   every chunk works in place, no per-lane scratch, and the LDS footprint is ~4 B (16-bit ids)
-//   per input byte -> 6 workgroups (24 waves) per CU.
-//   Chunks <= kShort bytes: one lane each, lanes ordered by chunk length (counting sort) so a
-//   wave's lanes run loops of similar trip count.  Per merge step a single in-place pass both
-//   applies the merge and finds the next minimum; only the <= 2 pairs touching each new token
-//   are looked up again.
-//   Longer chunks: one wave each, exact wave-cooperative loop (64-bit argmin over the wave,
-//   ballot/popcount compaction, run-parity for (a,a) pairs) in LDS when the chunk lies inside
-//   the tile window, else in a position-indexed global work area.
+// Pipeline (one stream):
+//   k_classify      one 256-thread workgroup per 2 KiB tile.  Stages the tile's bytes and its
+//                   pre-split bitmap in LDS, enumerates the chunks, and settles every chunk that
+//                   is a single byte or whose bytes are in the whole-chunk table (chunktable.h)
+//                   with one lookup.  Every other chunk reserves `len` output slots (ids <=
+//                   bytes) holding a sentinel and is queued by length bucket.  Writes the tile's
+//                   slot region to a position-indexed scratch.
+//   k_merge_bucket  the exact merge loop, one chunk per lane, chunk in REGISTERS (fixed
+//                   positions + alive mask, compile-time size N); the 64 lanes of a wave come
+//                   from one length bucket so their loops have similar trip counts; persistent
+//                   grid-stride over the bucket's queue.  Writes ids into the reserved slots and
+//                   adds the count to its tile.
+//   k_merge_long    chunks > 32 bytes: one wave each, wave-cooperative loop in a position-
+//                   indexed global work area.
+//   k_scan_*        exclusive scan of per-tile id counts
+//   k_compact       per tile: drop the sentinels (block stream compaction), write the ids
+//                   contiguously, and turn each string's slot offset into its id offset.
 #pragma once
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
 #include <type_traits>
 
+#include "chunktable.h"
 #include "table.h"
 
 namespace sw {
 
-constexpr int kTile = 2048;                  // input bytes per workgroup
+constexpr int kTile = 2048;                  // input bytes per classify workgroup
 constexpr int kThreads = 256;                // 4 waves
-constexpr int kShort = 32;                   // per-lane path for chunks up to this many bytes
-constexpr int kWin = kTile + kShort;         // LDS window: tile + halo for chunks crossing the end
+constexpr int kShort = 32;                   // per-lane merge loop up to this many bytes
+constexpr int kWin = kTile + 64;             // LDS byte window (tile + halo for key reads)
 constexpr int kTileWords = kTile / 64 + 1;   // bitmap words staged (tile + 64-bit halo)
-constexpr int kMaxLong = kTile / (kShort + 1) + 1;
+constexpr int32_t kSentinel = -1;            // reserved output slot not holding an id
+constexpr int kNumBuckets = 11;              // length buckets of the merge queue
+constexpr int kLongBucket = kNumBuckets - 1;
 
-template <typename Id>
-struct IdT {
-  static constexpr Id inf = (Id)~(Id)0;
-  using Key = typename std::conditional<sizeof(Id) == 2, uint32_t, uint64_t>::type;
-  static constexpr Key key_inf = (Key)~(Key)0;
-  __device__ static Key key(Id rank, int idx) { return ((Key)rank << 8) | (Key)idx; }
-  __device__ static Id rank_of(Key k) { return (Id)(k >> 8); }
-  __device__ static int idx_of(Key k) { return (int)(k & 0xFF); }
-};
+// length -> bucket: groups of similar loop trip count
+//   [2] [3] [4] [5,6] [7,8] [9,10] [11,12] [13,16] [17,24] [25,32] long(>32)
+__host__ __device__ inline int bucket_of(int64_t len) {
+  if (len <= 4) return (int)len - 2;
+  if (len <= 12) return 3 + (int)((len - 5) >> 1);
+  if (len <= 16) return 7;
+  if (len <= 24) return 8;
+  if (len <= 32) return 9;
+  return kLongBucket;
+}
+__host__ __device__ inline int bucket_min_len(int b) {
+  return b <= 2 ? b + 2 : b <= 6 ? 5 + 2 * (b - 3) : b == 7 ? 13 : b == 8 ? 17 : b == 9 ? 25 : 33;
+}
 
 // merges.get((a, b)): the value, or kInf.  Two independent 16-byte loads (both cuckoo
 // candidate buckets), no loop: one memory round trip for every lane.
@@ -68,10 +80,43 @@ __device__ __forceinline__ uint32_t lookup(const DevTable& t, uint32_t a, uint32
   }
 }
 
-template <typename Id, bool kWide>
-__device__ __forceinline__ Id lookup_id(const DevTable& t, Id a, Id b) {
-  const uint32_t v = lookup<kWide>(t, a, b);
-  return v == kInf ? IdT<Id>::inf : (Id)v;  // narrow-16 tables hold values <= 0xFFFD
+// Whole-chunk table lookup (chunktable.h): the single token a 2..16-byte chunk encodes to, or
+// kInf if the chunk does not encode to exactly one token.  k0/k1: the chunk's bytes, LE, zero
+// padded.  Two (short) or four (long) independent 16-byte loads, one round trip.
+__device__ __forceinline__ uint32_t chunk_lookup(const DevChunkTable& c, uint64_t k0, uint64_t k1, uint32_t len) {
+  const uint32_t f = chunk_hash(k0, k1, len);
+  if (len <= 8) {
+    const uint4 q1 = c.sb[(f * c.s_m1) >> c.s_shift];
+    const uint4 q2 = c.sb[((f ^ 0xA5A5A5A5u) * c.s_m2) >> c.s_shift];
+    const uint32_t lo = (uint32_t)k0, hi = (uint32_t)(k0 >> 32);
+    uint32_t v = kInf;
+    v = (q1.x == lo && q1.y == hi && (q1.z >> 24) == len) ? (q1.z & 0xFFFFFFu) : v;
+    v = (q2.x == lo && q2.y == hi && (q2.z >> 24) == len) ? (q2.z & 0xFFFFFFu) : v;
+    return v;
+  }
+  const uint32_t b1 = (f * c.l_m1) >> c.l_shift, b2 = ((f ^ 0xA5A5A5A5u) * c.l_m2) >> c.l_shift;
+  const uint4 a1 = c.lb[2 * b1], t1 = c.lb[2 * b1 + 1];
+  const uint4 a2 = c.lb[2 * b2], t2 = c.lb[2 * b2 + 1];
+  const uint4 k = make_uint4((uint32_t)k0, (uint32_t)(k0 >> 32), (uint32_t)k1, (uint32_t)(k1 >> 32));
+  uint32_t v = kInf;
+  v = (a1.x == k.x && a1.y == k.y && a1.z == k.z && a1.w == k.w && (t1.x >> 24) == len) ? (t1.x & 0xFFFFFFu) : v;
+  v = (a2.x == k.x && a2.y == k.y && a2.z == k.z && a2.w == k.w && (t2.x >> 24) == len) ? (t2.x & 0xFFFFFFu) : v;
+  return v;
+}
+
+// bytes [ls, ls + len) of an LDS byte window as two zero-padded little-endian words (len <= 16)
+__device__ __forceinline__ void window_key(const uint32_t* w32, int ls, int len, uint64_t* k0, uint64_t* k1) {
+  const int q = ls >> 2, sh = ls & 3;
+  const uint32_t w0 = w32[q], w1 = w32[q + 1], w2 = w32[q + 2], w3 = w32[q + 3], w4 = w32[q + 4];
+  uint32_t b[4] = {__builtin_amdgcn_alignbyte(w1, w0, sh), __builtin_amdgcn_alignbyte(w2, w1, sh),
+                   __builtin_amdgcn_alignbyte(w3, w2, sh), __builtin_amdgcn_alignbyte(w4, w3, sh)};
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int keep = len - 4 * i;
+    b[i] = keep >= 4 ? b[i] : keep <= 0 ? 0u : (b[i] & ((1u << (8 * keep)) - 1u));
+  }
+  *k0 = ((uint64_t)b[1] << 32) | b[0];
+  *k1 = ((uint64_t)b[3] << 32) | b[2];
 }
 
 __device__ __forceinline__ uint64_t wave_min_u64(uint64_t v) {
@@ -96,199 +141,6 @@ __device__ inline int64_t next_set_bit(const uint64_t* bits, int64_t n_words, in
   return q < n_bits ? q : n_bits;
 }
 
-// ---------------------------------------------------------------------------------------
-// per-lane merge loop, in place on id[0..n), rk[0..n-1)   (n <= kShort)
-// ---------------------------------------------------------------------------------------
-template <typename Id, bool kWide>
-__device__ int lane_merge(const DevTable& t, Id* id, Id* rk, int n) {
-  using K = IdT<Id>;
-  typename K::Key best = K::key_inf;
-  // initial ranks: independent lookups, four in flight per lane
-  for (int j0 = 0; j0 + 1 < n; j0 += 4) {
-    Id r[4];
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const int j = min(j0 + u, n - 2);  // clamped duplicates keep the loads unconditional
-      r[u] = lookup_id<Id, kWide>(t, id[j], id[j + 1]);
-    }
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const int j = j0 + u;
-      if (j + 1 < n) {
-        rk[j] = r[u];
-        const typename K::Key k = K::key(r[u], j);
-        best = k < best ? k : best;
-      }
-    }
-  }
-  while (n >= 2) {
-    const Id nv = K::rank_of(best);
-    if (nv == K::inf) break;
-    const int bi = K::idx_of(best);
-    const Id p0 = id[bi], p1 = id[bi + 1];
-    // one pass: apply the merge (left to right, non-overlapping) and collect the minimum of the
-    // ranks that survive; positions whose pair changed are marked in `need`
-    best = K::key_inf;
-    uint32_t need = 0;
-    int w = bi;  // positions before the first occurrence are unchanged
-    bool prev_carried = false;
-    Id prev_rank = 0;
-    for (int j = 0; j < bi; ++j) {  // their ranks still count (except bi-1, re-looked up)
-      if (j + 1 < bi) {
-        const typename K::Key k = K::key(rk[j], j);
-        best = k < best ? k : best;
-      }
-    }
-    if (bi > 0) { prev_carried = true; prev_rank = rk[bi - 1]; }
-    Id x = id[bi];
-    for (int j = bi; j < n;) {
-      const Id y = (j + 1 < n) ? id[j + 1] : K::inf;
-      if (j + 1 < n && x == p0 && y == p1) {
-        id[w] = nv;
-        need |= 1u << w;
-        if (w > 0) need |= 1u << (w - 1);
-        prev_carried = false;
-        ++w;
-        j += 2;
-        x = (j < n) ? id[j] : K::inf;
-      } else {
-        if (prev_carried && !((need >> (w - 1)) & 1u)) {
-          const typename K::Key k = K::key(prev_rank, w - 1);
-          best = k < best ? k : best;
-        }
-        id[w] = x;
-        prev_rank = rk[j];
-        rk[w] = prev_rank;
-        prev_carried = true;
-        ++w;
-        ++j;
-        x = y;
-      }
-    }
-    n = w;
-    need &= (n >= 2) ? ((1u << (n - 1)) - 1u) : 0u;
-    while (need) {  // two lookups in flight per round
-      const int j1 = __ffs(need) - 1;
-      need &= need - 1;
-      const int j2 = need ? __ffs(need) - 1 : j1;
-      need &= need - 1;
-      const Id r1 = lookup_id<Id, kWide>(t, id[j1], id[j1 + 1]);
-      const Id r2 = lookup_id<Id, kWide>(t, id[j2], id[j2 + 1]);
-      rk[j1] = r1;
-      rk[j2] = r2;
-      const typename K::Key k1 = K::key(r1, j1), k2 = K::key(r2, j2);
-      best = k1 < best ? k1 : best;
-      best = k2 < best ? k2 : best;
-    }
-  }
-  return n;
-}
-
-// ---------------------------------------------------------------------------------------
-// wave-cooperative exact merge loop on id[0..n), rk[0..n-1) (any n; LDS or global memory)
-// ---------------------------------------------------------------------------------------
-template <typename Id>
-__device__ __forceinline__ void wave_sync_mem() {
-  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
-  __builtin_amdgcn_wave_barrier();
-}
-
-template <typename Id, bool kWide>
-__device__ int64_t coop_merge(const DevTable& t, Id* id, Id* rk, int64_t n, int lane) {
-  constexpr Id INF = IdT<Id>::inf;
-  constexpr Id RECOMP = (Id)(INF - 1);
-  const uint64_t lt_mask = (lane == 0) ? 0ULL : (~0ULL >> (64 - lane));
-  for (int64_t i = lane; i + 1 < n; i += 64) rk[i] = RECOMP;
-  wave_sync_mem<Id>();
-  while (n >= 2) {
-    // pass 1: resolve pending ranks; argmin over (rank, index)
-    uint64_t best = ~0ULL;
-    for (int64_t i = lane; i + 1 < n; i += 64) {
-      Id r = rk[i];
-      if (r == RECOMP) {
-        r = lookup_id<Id, kWide>(t, id[i], id[i + 1]);
-        rk[i] = r;
-      }
-      const uint64_t key = ((uint64_t)r << 32) | (uint32_t)i;
-      best = key < best ? key : best;
-    }
-    best = wave_min_u64(best);
-    const Id nv = (Id)(best >> 32);
-    if (nv == INF) break;
-    const int64_t b = (int64_t)(uint32_t)best;
-    wave_sync_mem<Id>();
-    const Id p0 = id[b], p1 = id[b + 1];
-    // pass 2: replace every non-overlapping occurrence of (p0, p1), left to right, in place
-    int64_t w = 0;
-    bool prev_taken = false;
-    for (int64_t seg = 0; seg < n; seg += 64) {
-      const int64_t i = seg + lane;
-      const bool valid = i < n;
-      const Id e = valid ? id[i] : INF;
-      const Id er = (valid && i + 1 < n) ? rk[i] : INF;
-      Id nid = (Id)__shfl_down((uint32_t)e, 1, 64);
-      if (lane == 63) nid = (i + 1 < n) ? id[i + 1] : INF;
-      const bool match = valid && (i + 1 < n) && e == p0 && nid == p1;
-      uint64_t M = __ballot(match);
-      if (prev_taken) M &= ~1ULL;  // position seg is the right half of the previous take
-      uint64_t T = M;
-      if (p0 == p1) {  // runs of (a,a): take even offsets from each run start
-        const uint64_t E = 0x5555555555555555ULL;
-        const uint64_t S = M & ~(M << 1);
-        const uint64_t runs_even = M & ~(M + (S & E));
-        T = (runs_even & E) | (M & ~runs_even & ~E);
-      }
-      const uint64_t consumed = (T << 1) | (prev_taken ? 1ULL : 0ULL);
-      const uint64_t keep = __ballot(valid) & ~consumed;
-      const bool take = (T >> lane) & 1ULL;
-      const bool next_take = lane < 63 ? ((T >> (lane + 1)) & 1ULL) : true;
-      const int64_t pos = w + __popcll(keep & lt_mask);
-      wave_sync_mem<Id>();  // all loads of this segment precede the in-place stores
-      if ((keep >> lane) & 1ULL) {
-        id[pos] = take ? nv : e;
-        rk[pos] = (take || next_take) ? RECOMP : er;
-      }
-      w += __popcll(keep);
-      prev_taken = (T >> 63) & 1ULL;
-    }
-    n = w;
-    wave_sync_mem<Id>();
-  }
-  return n;
-}
-
-// ---------------------------------------------------------------------------------------
-struct TileArgs {
-  const uint8_t* bytes;
-  int64_t n_bytes;
-  const uint64_t* bits;
-  int64_t n_words;
-  const int64_t* str_off;
-  int64_t n_str;
-  DevTable table;
-  int32_t* scratch;      // [n_bytes] tile outputs, position space (tile t at its first chunk)
-  void* lw_id;           // [n_bytes] Id: long-chunk work area, position space
-  void* lw_rk;           // [n_bytes] Id
-  uint32_t* tile_cnt;    // [n_tiles]
-  int64_t* tile_first;   // [n_tiles] first chunk start in tile (or -1)
-  int64_t* out_off;      // [n_str+1] tile-local offsets, rebased by k_string_offsets
-  const int64_t* tile_slo;  // [n_tiles] first string starting at or after the tile start
-  unsigned long long* stamps;  // diagnostic builds (SW_STAMPS): cycles per phase, summed
-};
-
-#ifdef SW_STAMPS
-#define SW_STAMP(k)                                                                 \
-  do {                                                                              \
-    if (threadIdx.x == 0) {                                                         \
-      const unsigned long long now_ = __builtin_readcyclecounter();                 \
-      atomicAdd(&a.stamps[k], now_ - stamp_prev_);                                  \
-      stamp_prev_ = now_;                                                           \
-    }                                                                               \
-  } while (0)
-#else
-#define SW_STAMP(k) do {} while (0)
-#endif
-
 // exclusive block scan over kThreads threads (sh: kThreads/64 words); *total = block sum
 __device__ inline uint32_t block_excl_scan(uint32_t v, uint32_t* sh, uint32_t* total) {
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
@@ -312,47 +164,267 @@ __device__ inline uint32_t block_excl_scan(uint32_t v, uint32_t* sh, uint32_t* t
   return base + x - v;
 }
 
-template <typename Id, bool kWide>
-__global__ void __launch_bounds__(kThreads) k_encode_tiles(TileArgs a) {
-  __shared__ __attribute__((aligned(16))) Id s_id[kWin];
-  __shared__ __attribute__((aligned(16))) Id s_rk[kWin];
+// ---------------------------------------------------------------------------------------
+// per-lane merge loop with the chunk held in REGISTERS (n <= N, N a compile-time bucket size)
+//
+// Fixed positions + an alive mask instead of compaction: a merge rewrites the left slot and
+// kills the right one, so every array index is a compile-time constant after unrolling.  Per
+// step: argmin over N keys, one left-to-right sweep applying the merge, one right-to-left sweep
+// refreshing right-neighbour ids, then the changed pairs are re-ranked two lookups at a time.
+// Returns the alive mask; the surviving ids are id[k] for the set bits, in order.
+// ---------------------------------------------------------------------------------------
+template <bool k16>
+struct RegKey {  // (rank, slot) packed so that min() picks the lowest rank, then the first slot
+  using T = typename std::conditional<k16, uint32_t, uint64_t>::type;
+  static constexpr T inf = (T)~(T)0;
+  __device__ static T make(uint32_t rank, int k) {
+    if (k16) return ((T)(rank > 0xFFFFu ? 0xFFFFu : rank) << 5) | (T)k;
+    return ((T)rank << 5) | (T)k;
+  }
+  __device__ static uint32_t rank(T key) {
+    if (k16) {
+      const uint32_t r = (uint32_t)(key >> 5);
+      return r >= 0xFFFFu ? kInf : r;
+    }
+    return (uint32_t)(key >> 5);
+  }
+};
+
+template <bool kWide, bool k16, int N>
+__device__ __forceinline__ uint32_t lane_merge_reg(const DevTable& t, uint32_t (&id)[N], int n) {
+  using RK = RegKey<k16>;
+  constexpr uint32_t NONE = 0xFFFFFFFFu;  // no right neighbour
+  uint32_t rid[N], rk[N];
+#pragma unroll
+  for (int k = 0; k < N; ++k) rid[k] = (k + 1 < n) ? id[(k + 1) % N] : NONE;
+  uint32_t alive = (n >= 32) ? 0xFFFFFFFFu : ((1u << n) - 1u);
+  // initial ranks: four lookups in flight at a time (sched barriers cap the live registers)
+#pragma unroll
+  for (int g = 0; g < N; g += 4) {
+#pragma unroll
+    for (int k = g; k < g + 4 && k < N; ++k) rk[k] = lookup<kWide>(t, id[k], rid[k]);
+#pragma unroll
+    for (int k = g; k < g + 4 && k < N; ++k) rk[k] = (rid[k] == NONE) ? kInf : rk[k];
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  while (true) {
+    typename RK::T best = RK::inf;
+#pragma unroll
+    for (int k = 0; k < N; ++k) {
+      const typename RK::T key = ((alive >> k) & 1u) ? RK::make(rk[k], k) : RK::inf;
+      best = key < best ? key : best;
+    }
+    const uint32_t nv = RK::rank(best);
+    if (nv == kInf) break;
+    const int bi = (int)(best & 31);
+    uint32_t p0 = 0, p1 = 0;
+#pragma unroll
+    for (int k = 0; k < N; ++k) {
+      p0 = (k == bi) ? id[k] : p0;
+      p1 = (k == bi) ? rid[k] : p1;
+    }
+    // left-to-right: take every non-overlapping occurrence of (p0, p1) (base.py:29-35)
+    bool took = false;
+    uint32_t changed = 0;
+#pragma unroll
+    for (int k = 0; k < N; ++k) {
+      if ((alive >> k) & 1u) {
+        if (took) {
+          alive &= ~(1u << k);
+          took = false;
+        } else if (id[k] == p0 && rid[k] == p1) {
+          id[k] = nv;
+          took = true;
+          changed |= 1u << k;
+        }
+      }
+    }
+    // right-to-left: new right neighbours; pairs touching a new token need a new rank
+    uint32_t carry = NONE, need = 0;
+    bool carry_chg = false;
+#pragma unroll
+    for (int k = N - 1; k >= 0; --k) {
+      if ((alive >> k) & 1u) {
+        const bool chg = (changed >> k) & 1u;
+        rid[k] = carry;
+        if (carry != NONE && (chg || carry_chg)) need |= 1u << k;
+        if (carry == NONE) rk[k] = kInf;
+        carry = id[k];
+        carry_chg = chg;
+      }
+    }
+    while (need) {  // two lookups in flight per round
+      const int j1 = __ffs(need) - 1;
+      need &= need - 1;
+      const int j2 = need ? __ffs(need) - 1 : j1;
+      need &= need - 1;
+      uint32_t a1 = 0, b1 = 0, a2 = 0, b2 = 0;
+#pragma unroll
+      for (int k = 0; k < N; ++k) {
+        a1 = (k == j1) ? id[k] : a1;
+        b1 = (k == j1) ? rid[k] : b1;
+        a2 = (k == j2) ? id[k] : a2;
+        b2 = (k == j2) ? rid[k] : b2;
+      }
+      const uint32_t r1 = lookup<kWide>(t, a1, b1), r2 = lookup<kWide>(t, a2, b2);
+#pragma unroll
+      for (int k = 0; k < N; ++k) {
+        rk[k] = (k == j1) ? r1 : rk[k];
+        rk[k] = (k == j2) ? r2 : rk[k];
+      }
+    }
+  }
+  return alive;
+}
+
+// ---------------------------------------------------------------------------------------
+// wave-cooperative exact merge loop on id[0..n), rk[0..n-1) (any n; global memory)
+// ---------------------------------------------------------------------------------------
+__device__ __forceinline__ void wave_sync_mem() {
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+  __builtin_amdgcn_wave_barrier();
+}
+
+template <bool kWide>
+__device__ int64_t coop_merge(const DevTable& t, uint32_t* id, uint32_t* rk, int64_t n, int lane) {
+  constexpr uint32_t INF = kInf, RECOMP = kInf - 1;
+  const uint64_t lt_mask = (lane == 0) ? 0ULL : (~0ULL >> (64 - lane));
+  for (int64_t i = lane; i + 1 < n; i += 64) rk[i] = RECOMP;
+  wave_sync_mem();
+  while (n >= 2) {
+    // pass 1: resolve pending ranks; argmin over (rank, index)
+    uint64_t best = ~0ULL;
+    for (int64_t i = lane; i + 1 < n; i += 64) {
+      uint32_t r = rk[i];
+      if (r == RECOMP) {
+        r = lookup<kWide>(t, id[i], id[i + 1]);
+        rk[i] = r;
+      }
+      const uint64_t key = ((uint64_t)r << 32) | (uint32_t)i;
+      best = key < best ? key : best;
+    }
+    best = wave_min_u64(best);
+    const uint32_t nv = (uint32_t)(best >> 32);
+    if (nv == INF) break;
+    const int64_t b = (int64_t)(uint32_t)best;
+    wave_sync_mem();
+    const uint32_t p0 = id[b], p1 = id[b + 1];
+    // pass 2: replace every non-overlapping occurrence of (p0, p1), left to right, in place
+    int64_t w = 0;
+    bool prev_taken = false;
+    for (int64_t seg = 0; seg < n; seg += 64) {
+      const int64_t i = seg + lane;
+      const bool valid = i < n;
+      const uint32_t e = valid ? id[i] : INF;
+      const uint32_t er = (valid && i + 1 < n) ? rk[i] : INF;
+      uint32_t nid = __shfl_down(e, 1, 64);
+      if (lane == 63) nid = (i + 1 < n) ? id[i + 1] : INF;
+      const bool match = valid && (i + 1 < n) && e == p0 && nid == p1;
+      uint64_t M = __ballot(match);
+      if (prev_taken) M &= ~1ULL;  // position seg is the right half of the previous take
+      uint64_t T = M;
+      if (p0 == p1) {  // runs of (a,a): take even offsets from each run start
+        const uint64_t E = 0x5555555555555555ULL;
+        const uint64_t S = M & ~(M << 1);
+        const uint64_t runs_even = M & ~(M + (S & E));
+        T = (runs_even & E) | (M & ~runs_even & ~E);
+      }
+      const uint64_t consumed = (T << 1) | (prev_taken ? 1ULL : 0ULL);
+      const uint64_t keep = __ballot(valid) & ~consumed;
+      const bool take = (T >> lane) & 1ULL;
+      const bool next_take = lane < 63 ? ((T >> (lane + 1)) & 1ULL) : true;
+      const int64_t pos = w + __popcll(keep & lt_mask);
+      wave_sync_mem();  // all loads of this segment precede the in-place stores
+      if ((keep >> lane) & 1ULL) {
+        id[pos] = take ? nv : e;
+        rk[pos] = (take || next_take) ? RECOMP : er;
+      }
+      w += __popcll(keep);
+      prev_taken = (T >> 63) & 1ULL;
+    }
+    n = w;
+    wave_sync_mem();
+  }
+  return n;
+}
+
+// ---------------------------------------------------------------------------------------
+// arguments shared by the pipeline's kernels
+// ---------------------------------------------------------------------------------------
+struct EncArgs {
+  const uint8_t* bytes;
+  int64_t n_bytes;
+  const uint64_t* bits;
+  int64_t n_words;
+  const int64_t* str_off;
+  int64_t n_str;
+  DevTable table;
+  DevChunkTable chunks;
+  int32_t* scratch;          // [n_bytes] slot regions, position space (tile t at tile_first[t])
+  uint32_t* lw_id;           // [n_bytes] long-chunk work area, position space
+  uint32_t* lw_rk;           // [n_bytes]
+  uint32_t* tile_cnt;        // [n_tiles] ids per tile (classify writes, merges add)
+  uint32_t* tile_slots;      // [n_tiles] slots per tile region
+  int64_t* tile_first;       // [n_tiles] first chunk start in tile (or -1)
+  int64_t* out_off;          // [n_str+1] string -> slot offset in its tile (k_compact converts)
+  const int64_t* tile_slo;   // [n_tiles] first string starting at or after the tile start
+  uint64_t* queue;           // merge queue: entries (start << 24 | slot offset in tile)
+  const int64_t* q_base;     // [kNumBuckets] region start of each bucket in `queue`
+  unsigned long long* q_cnt; // [kNumBuckets] entries per bucket
+  uint64_t* long_slot;       // slot offsets of long chunks (may exceed 24 bits)
+  unsigned long long* stamps;  // SW_STAMPS builds: cycles per phase, summed
+};
+
+#ifdef SW_STAMPS
+#define SW_STAMP(k)                                                                 \
+  do {                                                                              \
+    if (threadIdx.x == 0) {                                                         \
+      const unsigned long long now_ = __builtin_readcyclecounter();                 \
+      atomicAdd(&a.stamps[k], now_ - stamp_prev_);                                  \
+      stamp_prev_ = now_;                                                           \
+    }                                                                               \
+  } while (0)
+#define SW_STAMP_INIT unsigned long long stamp_prev_ = __builtin_readcyclecounter()
+#else
+#define SW_STAMP(k) do {} while (0)
+#define SW_STAMP_INIT do {} while (0)
+#endif
+
+// ---------------------------------------------------------------------------------------
+// k_classify
+// ---------------------------------------------------------------------------------------
+__global__ void __launch_bounds__(kThreads) k_classify(EncArgs a) {
+  __shared__ uint32_t s_b32[kWin / 4 + 8];    // raw bytes of the window (+ zero tail)
   __shared__ uint64_t s_bits[kTileWords];
   __shared__ uint16_t s_cstart[kTile + 1];
-  __shared__ uint32_t s_cnt[kTile + 1];       // chunk length, then token count, then offset
-  __shared__ uint16_t s_order[kTile];
-  __shared__ uint32_t s_bin[kShort + 2];
-  __shared__ uint16_t s_long[kMaxLong];
+  __shared__ uint32_t s_val[kTile];           // settled token, or kInf (queued)
+  __shared__ uint32_t s_off[kTile + 1];       // slots per chunk, then exclusive slot offsets
   __shared__ uint32_t s_wsum[kThreads / 64];
-  __shared__ uint32_t s_nlong, s_nglobal;
-  __shared__ int64_t s_last_end, s_slo;
+  __shared__ uint32_t s_bcnt[kNumBuckets];
+  __shared__ unsigned long long s_bbase[kNumBuckets];
+  __shared__ int64_t s_last_end;
+  __shared__ uint32_t s_settled;
 
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  SW_STAMP_INIT;
+  const int tid = threadIdx.x;
   const int64_t tile = blockIdx.x;
   const int64_t t0 = tile * kTile;
-#ifdef SW_STAMPS
-  unsigned long long stamp_prev_ = __builtin_readcyclecounter();
-#endif
-  if (tid == 0) s_slo = a.tile_slo[tile];
   const int64_t t1 = min(t0 + (int64_t)kTile, a.n_bytes);
   const int64_t w0 = t0 >> 6;
 
-  // 1. stage the window's bytes as ids (4 bytes per thread-load) and the bitmap words
+  // 1. stage the window's bytes (4 per thread-load) and bitmap words
   for (int i = tid * 4; i < kWin; i += kThreads * 4) {
     const int64_t g = t0 + i;
     uint32_t v = 0;
     if (g + 4 <= a.n_bytes && ((uintptr_t)a.bytes & 3) == 0) v = *(const uint32_t*)(a.bytes + g);
     else
       for (int k = 0; k < 4; ++k) v |= (g + k < a.n_bytes ? (uint32_t)a.bytes[g + k] : 0u) << (8 * k);
-    if (sizeof(Id) == 2) {  // one 8-byte LDS store per thread
-      const uint32_t lo = (v & 0xFFu) | ((v & 0xFF00u) << 8), hi = ((v >> 16) & 0xFFu) | ((v >> 8) & 0xFF0000u);
-      *(uint2*)(s_id + i) = make_uint2(lo, hi);
-    } else {
-      *(uint4*)(s_id + i) = make_uint4(v & 0xFF, (v >> 8) & 0xFF, (v >> 16) & 0xFF, v >> 24);
-    }
+    s_b32[i >> 2] = v;
   }
+  if (tid < 8) s_b32[kWin / 4 + tid] = 0;
   if (tid < kTileWords) s_bits[tid] = (w0 + tid < a.n_words) ? a.bits[w0 + tid] : 0ULL;
-  if (tid < kShort + 2) s_bin[tid] = 0;
-  if (tid == 0) { s_nlong = 0; s_nglobal = 0; }
+  if (tid < kNumBuckets) s_bcnt[tid] = 0;
+  if (tid == 0) s_settled = 0;
   __syncthreads();
 
   // 2. chunk starts in [t0, t1): one thread per bitmap word
@@ -390,133 +462,77 @@ __global__ void __launch_bounds__(kThreads) k_encode_tiles(TileArgs a) {
   const int C = (int)nchunks;
   SW_STAMP(0);
 
-  // 3. lengths; histogram by length (short) / long list
+  // 3. settle single bytes and whole-chunk-table hits; the rest reserve len slots
   for (int k = tid; k < C; k += kThreads) {
-    const int64_t start = t0 + s_cstart[k];
+    const int ls = s_cstart[k];
     const int64_t end = (k + 1 < C) ? t0 + s_cstart[k + 1] : s_last_end;
-    const int64_t len = end - start;
-    if (len > kShort) {
-      s_long[atomicAdd(&s_nlong, 1u)] = (uint16_t)k;
-      s_cnt[k] = 0;
-    } else {
-      s_cnt[k] = (uint32_t)len;
-      atomicAdd(&s_bin[len], 1u);
+    const int64_t len = end - (t0 + ls);
+    uint32_t tok = kInf;
+    if (len == 1) {
+      tok = (s_b32[ls >> 2] >> (8 * (ls & 3))) & 0xFFu;
+    } else if (len <= 16 && a.chunks.enabled) {
+      uint64_t k0, k1;
+      window_key(s_b32, ls, (int)len, &k0, &k1);
+      tok = chunk_lookup(a.chunks, k0, k1, (uint32_t)len);
     }
+    s_val[k] = tok;
+    s_off[k] = tok != kInf ? 1u : (uint32_t)min(len, (int64_t)0xFFFFFFFF);
+    if (tok != kInf) atomicAdd(&s_settled, 1u);
+    else atomicAdd(&s_bcnt[bucket_of(len)], 1u);
   }
   __syncthreads();
-  if (tid == 0) {  // bins in descending length: the longest chunks go to the first lanes
-    uint32_t acc = 0;
-    for (int L = kShort; L >= 1; --L) {
-      const uint32_t c = s_bin[L];
-      s_bin[L] = acc;
-      acc += c;
-    }
-    s_bin[kShort + 1] = acc;  // number of short chunks
-  }
-  __syncthreads();
-  for (int k = tid; k < C; k += kThreads) {
-    const uint32_t len = s_cnt[k];
-    if (len >= 1) s_order[atomicAdd(&s_bin[len], 1u)] = (uint16_t)k;
-  }
-  __syncthreads();
-  const int n_short = (int)s_bin[kShort + 1];
   SW_STAMP(1);
 
-  // 4. per-lane merge loop on short chunks, in place in the LDS window
-  // rounds alternate direction (zig-zag) so a lane with a long chunk in one round gets a short
-  // one in the next and the four waves finish together
-  for (int r0 = 0; r0 < n_short; r0 += kThreads) {
-    const int r = r0 + (((r0 / kThreads) & 1) ? (kThreads - 1 - tid) : tid);
-    if (r >= n_short) continue;
-    const int k = s_order[r];
-    const int ls = s_cstart[k];
-    s_cnt[k] = (uint32_t)lane_merge<Id, kWide>(a.table, s_id + ls, s_rk + ls, (int)s_cnt[k]);
-  }
-
-#ifdef SW_STAMPS
-  __syncthreads();
-  SW_STAMP(2);
-#endif
-  // 5. long chunks: one wave per chunk (LDS window if it fits, else the global work area)
-  const int nl = (int)s_nlong;
-  for (int q = wid; q < nl; q += kThreads / 64) {
-    const int k = s_long[q];
-    const int ls = s_cstart[k];
-    const int64_t start = t0 + ls;
-    const int64_t end = (k + 1 < C) ? t0 + s_cstart[k + 1] : s_last_end;
-    const int64_t len = end - start;
-    int64_t n;
-    if (ls + len <= kWin) {
-      n = coop_merge<Id, kWide>(a.table, s_id + ls, s_rk + ls, len, lane);
-    } else {
-      Id* gid = (Id*)a.lw_id + start;
-      Id* grk = (Id*)a.lw_rk + start;
-      for (int64_t i = lane; i < len; i += 64) gid[i] = (Id)a.bytes[start + i];
-      wave_sync_mem<Id>();
-      n = coop_merge<Id, kWide>(a.table, gid, grk, len, lane);
-      if (lane == 0) atomicAdd(&s_nglobal, 1u);
-    }
-    if (lane == 0) s_cnt[k] = (uint32_t)n;
-  }
-  __syncthreads();
-
-  SW_STAMP(3);
-  // 6. tile-local exclusive offsets over chunk token counts
+  // 4. slot offsets (exclusive scan over chunk slot counts); queue space per bucket
   const int per = (C + kThreads - 1) / kThreads;
   const int c0 = min(C, tid * per), c1 = min(C, c0 + per);
-  uint32_t local_sum = 0;
-  for (int k = c0; k < c1; ++k) local_sum += s_cnt[k];
-  uint32_t tile_total;
-  uint32_t off = block_excl_scan(local_sum, s_wsum, &tile_total);
+  uint32_t local = 0;
+  for (int k = c0; k < c1; ++k) local += s_off[k];
+  uint32_t n_slots;
+  uint32_t off = block_excl_scan(local, s_wsum, &n_slots);
   for (int k = c0; k < c1; ++k) {
-    const uint32_t c = s_cnt[k];
-    s_cnt[k] = off;
+    const uint32_t c = s_off[k];
+    s_off[k] = off;
     off += c;
   }
-  if (tid == 0) s_cnt[C] = tile_total;
+  if (tid == 0) s_off[C] = n_slots;
+  if (tid < kNumBuckets) {
+    const uint32_t c = s_bcnt[tid];
+    s_bbase[tid] = c ? atomicAdd(&a.q_cnt[tid], (unsigned long long)c) : 0ULL;
+    s_bcnt[tid] = 0;
+  }
   __syncthreads();
   const int64_t first = C > 0 ? t0 + s_cstart[0] : -1;
   if (tid == 0) {
-    a.tile_cnt[tile] = tile_total;
+    a.tile_cnt[tile] = s_settled;
+    a.tile_slots[tile] = n_slots;
     a.tile_first[tile] = first;
   }
 
-  // 7. write the tile's ids contiguously (position space at `first`)
+  // 5. write the slot region; queue the unsettled chunks
   int32_t* dst = a.scratch + first;
-  if (s_nglobal == 0) {
-    // every chunk's ids are in s_id: compact them into s_rk, then one coalesced store
-    for (int k = tid; k < C; k += kThreads) {
-      const uint32_t o = s_cnt[k], cnt = s_cnt[k + 1] - o;
-      const int ls = s_cstart[k];
-      for (uint32_t j = 0; j < cnt; ++j) s_rk[o + j] = s_id[ls + j];
+  for (int k = tid; k < C; k += kThreads) {
+    const uint32_t o = s_off[k], ns = s_off[k + 1] - o;
+    const uint32_t tok = s_val[k];
+    if (tok != kInf) {
+      dst[o] = (int32_t)tok;
+      continue;
     }
-    __syncthreads();
-    for (uint32_t j = tid; j < tile_total; j += kThreads) dst[j] = (int32_t)s_rk[j];
-  } else {
-    for (int k = tid; k < C; k += kThreads) {
-      const uint32_t o = s_cnt[k], cnt = s_cnt[k + 1] - o;
-      const int ls = s_cstart[k];
-      const int64_t len = ((k + 1 < C) ? t0 + s_cstart[k + 1] : s_last_end) - (t0 + ls);
-      if (ls + len > kWin) continue;  // global-work-area chunk: copied below
-      for (uint32_t j = 0; j < cnt; ++j) dst[o + j] = (int32_t)s_id[ls + j];
-    }
-    for (int q = wid; q < nl; q += kThreads / 64) {
-      const int k = s_long[q];
-      const int ls = s_cstart[k];
-      const int64_t len = ((k + 1 < C) ? t0 + s_cstart[k + 1] : s_last_end) - (t0 + ls);
-      if (ls + len <= kWin) continue;
-      const uint32_t o = s_cnt[k], cnt = s_cnt[k + 1] - o;
-      const Id* gid = (const Id*)a.lw_id + t0 + ls;
-      for (uint32_t j = lane; j < cnt; j += 64) dst[o + j] = (int32_t)gid[j];
+    const int64_t start = t0 + s_cstart[k];
+    const int b = bucket_of(ns);
+    const unsigned long long qi = s_bbase[b] + atomicAdd(&s_bcnt[b], 1u);
+    if (b != kLongBucket) {
+      a.queue[a.q_base[b] + qi] = ((uint64_t)start << 24) | o;
+      for (uint32_t j = 0; j < ns; ++j) dst[o + j] = kSentinel;
+    } else {
+      a.queue[a.q_base[b] + qi] = (uint64_t)start;  // k_merge_long writes all its slots
+      a.long_slot[qi] = o;
     }
   }
+  SW_STAMP(2);
 
-  // 8. strings starting in this tile: tile-local output offset (rebased later)
-#ifdef SW_STAMPS
-  __syncthreads();
-  SW_STAMP(4);
-#endif
-  for (int64_t s = s_slo + tid; s < a.n_str; s += kThreads) {
+  // 6. strings starting in this tile: slot offset within the tile (k_compact converts)
+  for (int64_t s = a.tile_slo[tile] + tid; s < a.n_str; s += kThreads) {
     const int64_t p = a.str_off[s];
     if (p >= t1) break;
     int lo = 0, hi = C;  // first chunk with start >= p
@@ -525,11 +541,77 @@ __global__ void __launch_bounds__(kThreads) k_encode_tiles(TileArgs a) {
       const int m = (lo + hi) >> 1;
       if (s_cstart[m] < lp) lo = m + 1; else hi = m;
     }
-    a.out_off[s] = (int64_t)s_cnt[lo];
+    a.out_off[s] = (int64_t)s_off[lo];
   }
 #ifdef SW_STAMPS
   __syncthreads();
-  SW_STAMP(5);
+  SW_STAMP(3);
+#endif
+}
+
+// ---------------------------------------------------------------------------------------
+// k_merge_bucket<N>: queued chunks of buckets [b_lo, b_hi] (length <= N), one per lane
+// ---------------------------------------------------------------------------------------
+template <bool kWide, bool k16, int N>
+__global__ void __launch_bounds__(kThreads) k_merge_bucket(EncArgs a, int b_lo, int b_hi) {
+  SW_STAMP_INIT;
+  const int64_t gw = ((int64_t)blockIdx.x * kThreads + threadIdx.x) >> 6;  // global wave id
+  const int64_t n_waves = ((int64_t)gridDim.x * kThreads) >> 6;
+  const int lane = threadIdx.x & 63;
+  for (int b = b_lo; b <= b_hi; ++b) {
+    const int64_t cnt = (int64_t)a.q_cnt[b];
+    const uint64_t* q = a.queue + a.q_base[b];
+    for (int64_t base = gw * 64; base < cnt; base += n_waves * 64) {
+      const int64_t i = base + lane;
+      if (i >= cnt) break;
+      const uint64_t e = q[i];
+      const int64_t start = (int64_t)(e >> 24);
+      const uint32_t o = (uint32_t)(e & 0xFFFFFFu);
+      const int64_t end = next_set_bit(a.bits, a.n_words, start + 1, a.n_bytes);
+      const int n = (int)(end - start);
+      uint32_t id[N];
+#pragma unroll
+      for (int k = 0; k < N; ++k) id[k] = (k < n) ? (uint32_t)a.bytes[start + k] : 0u;
+      const uint32_t alive = lane_merge_reg<kWide, k16, N>(a.table, id, n);
+      const int64_t tile = start / kTile;
+      int32_t* dst = a.scratch + a.tile_first[tile] + o;
+      int m = 0;
+#pragma unroll
+      for (int k = 0; k < N; ++k)
+        if ((alive >> k) & 1u) dst[m++] = (int32_t)id[k];
+      atomicAdd(&a.tile_cnt[tile], (uint32_t)m);
+    }
+  }
+#ifdef SW_STAMPS
+  SW_STAMP(N >= 16 ? 5 : 4);
+#endif
+}
+
+// long chunks (> kShort bytes): one wave each, wave-cooperative loop in the global work area
+template <bool kWide>
+__global__ void __launch_bounds__(kThreads) k_merge_long(EncArgs a) {
+  SW_STAMP_INIT;
+  const int64_t gw = ((int64_t)blockIdx.x * kThreads + threadIdx.x) >> 6;
+  const int64_t n_waves = ((int64_t)gridDim.x * kThreads) >> 6;
+  const int lane = threadIdx.x & 63;
+  const int64_t cnt = (int64_t)a.q_cnt[kLongBucket];
+  const uint64_t* q = a.queue + a.q_base[kLongBucket];
+  for (int64_t i = gw; i < cnt; i += n_waves) {
+    const int64_t start = (int64_t)q[i];
+    const int64_t end = next_set_bit(a.bits, a.n_words, start + 1, a.n_bytes);
+    const int64_t len = end - start;
+    uint32_t* gid = a.lw_id + start;
+    uint32_t* grk = a.lw_rk + start;
+    for (int64_t j = lane; j < len; j += 64) gid[j] = a.bytes[start + j];
+    wave_sync_mem();
+    const int64_t m = coop_merge<kWide>(a.table, gid, grk, len, lane);
+    const int64_t tile = start / kTile;
+    int32_t* dst = a.scratch + a.tile_first[tile] + (int64_t)a.long_slot[i];
+    for (int64_t j = lane; j < len; j += 64) dst[j] = j < m ? (int32_t)gid[j] : kSentinel;
+    if (lane == 0) atomicAdd(&a.tile_cnt[tile], (uint32_t)m);
+  }
+#ifdef SW_STAMPS
+  SW_STAMP(6);
 #endif
 }
 
@@ -547,18 +629,16 @@ __global__ void k_tile_strings(const int64_t* str_off, int64_t n_str, int64_t n_
 }
 
 // ---------------------------------------------------------------------------------------
-// tile-count scan (3 small kernels) + compaction + per-string offsets
+// tile-count scan (3 small kernels)
 // ---------------------------------------------------------------------------------------
 constexpr int kScanPer = 16;                      // tiles per thread in the scan kernels
 constexpr int kScanBlock = kThreads * kScanPer;   // tiles per scan block
 
 __global__ void __launch_bounds__(kThreads) k_scan_reduce(const uint32_t* cnt, int64_t n, int64_t* part) {
-  __shared__ uint32_t sh[kThreads / 64];
   const int64_t base = (int64_t)blockIdx.x * kScanBlock + (int64_t)threadIdx.x * kScanPer;
   uint64_t s = 0;
   for (int k = 0; k < kScanPer; ++k)
     if (base + k < n) s += cnt[base + k];
-  // wave reduce then block reduce (64-bit)
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off, 64);
   __shared__ uint64_t sw[kThreads / 64];
@@ -569,7 +649,6 @@ __global__ void __launch_bounds__(kThreads) k_scan_reduce(const uint32_t* cnt, i
     for (int k = 0; k < kThreads / 64; ++k) t += sw[k];
     part[blockIdx.x] = (int64_t)t;
   }
-  (void)sh;
 }
 
 __global__ void __launch_bounds__(1024) k_scan_parts(int64_t* part, int64_t n_parts, int64_t* total) {
@@ -595,16 +674,14 @@ __global__ void __launch_bounds__(1024) k_scan_parts(int64_t* part, int64_t n_pa
 
 __global__ void __launch_bounds__(kThreads) k_scan_apply(const uint32_t* cnt, int64_t n, const int64_t* part,
                                                          int64_t* base_out) {
-  __shared__ uint32_t sh[kThreads / 64];
   const int64_t base = (int64_t)blockIdx.x * kScanBlock + (int64_t)threadIdx.x * kScanPer;
   uint32_t v[kScanPer];
-  uint32_t s = 0;
+  uint64_t s = 0;
 #pragma unroll
   for (int k = 0; k < kScanPer; ++k) {
     v[k] = base + k < n ? cnt[base + k] : 0u;
     s += v[k];
   }
-  // a tile holds < 2^32 ids and a block < 2^32 too only if tiles are small; scan in 64-bit
   uint64_t x = s;
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
 #pragma unroll
@@ -623,28 +700,68 @@ __global__ void __launch_bounds__(kThreads) k_scan_apply(const uint32_t* cnt, in
     if (base + k < n) base_out[base + k] = run;
     run += v[k];
   }
-  (void)sh;
 }
 
-__global__ void __launch_bounds__(256) k_compact(const int32_t* scratch, const uint32_t* tile_cnt,
-                                                 const int64_t* tile_first, const int64_t* tile_base,
-                                                 int32_t* out) {
+// ---------------------------------------------------------------------------------------
+// k_compact: per tile, drop sentinels from the slot region, write the ids at the tile's base,
+// and convert the tile's string slot offsets into id offsets (stored complemented: k_string_
+// offsets restores them).
+// ---------------------------------------------------------------------------------------
+constexpr int kCompactPer = 8;                          // slots per thread per pass
+constexpr int kCompactPass = kThreads * kCompactPer;    // slots per pass
+
+__global__ void __launch_bounds__(kThreads) k_compact(EncArgs a, const int64_t* tile_base, int32_t* out) {
+  __shared__ uint32_t s_pref[kCompactPass + 1];  // ids before each slot of the pass
+  __shared__ uint32_t s_wsum[kThreads / 64];
   const int64_t t = blockIdx.x;
-  const uint32_t cnt = tile_cnt[t];
-  if (!cnt) return;
-  const int32_t* src = scratch + tile_first[t];
-  int32_t* dst = out + tile_base[t];
-  for (uint32_t j = threadIdx.x; j < cnt; j += 256) dst[j] = src[j];
+  const int tid = threadIdx.x;
+  const uint32_t n_slots = a.tile_slots[t];
+  const int64_t base = tile_base[t];
+  const int64_t t1 = min(t * kTile + (int64_t)kTile, a.n_bytes);
+  const int32_t* src = a.scratch + a.tile_first[t];
+  const int64_t s_lo = a.tile_slo[t];
+  uint32_t done = 0;  // ids written by earlier passes
+  for (uint32_t p0 = 0; p0 == 0 || p0 < n_slots; p0 += kCompactPass) {
+    int32_t v[kCompactPer];
+    uint32_t c = 0;
+#pragma unroll
+    for (int k = 0; k < kCompactPer; ++k) {
+      const uint32_t j = p0 + tid * kCompactPer + k;
+      v[k] = j < n_slots ? src[j] : kSentinel;
+      c += v[k] != kSentinel;
+    }
+    uint32_t pass_total;
+    uint32_t o = block_excl_scan(c, s_wsum, &pass_total);
+#pragma unroll
+    for (int k = 0; k < kCompactPer; ++k) {
+      s_pref[tid * kCompactPer + k] = done + o;
+      if (v[k] != kSentinel) out[base + done + o++] = v[k];
+    }
+    if (tid == 0) s_pref[kCompactPass] = done + pass_total;
+    __syncthreads();
+    // strings of this tile whose slot offset falls in this pass (or is the region's end)
+    for (int64_t s = s_lo + tid; s < a.n_str; s += kThreads) {
+      if (a.str_off[s] >= t1) break;
+      const int64_t so = a.out_off[s];
+      if (so < (int64_t)p0) continue;  // done in an earlier pass (complemented values are < 0)
+      if (so < (int64_t)p0 + kCompactPass || so == (int64_t)n_slots) a.out_off[s] = ~(base + s_pref[so - p0]);
+    }
+    done += pass_total;
+    __syncthreads();
+  }
 }
 
-__global__ void k_string_offsets(const int64_t* str_off, int64_t n_str, int64_t n_bytes, const int64_t* tile_base,
-                                 const int64_t* total, int64_t* out_off) {
+// every string offset: a complemented value is one k_compact finished; strings starting at or
+// past n_bytes (trailing empty strings) and the end sentinel get the total
+__global__ void k_string_offsets(const int64_t* str_off, int64_t n_str, int64_t n_bytes, const int64_t* total,
+                                 int64_t* out_off) {
   const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (s > n_str) return;
-  if (s == n_str) { out_off[s] = *total; return; }
-  const int64_t p = str_off[s];
-  if (p >= n_bytes) out_off[s] = *total;
-  else out_off[s] += tile_base[p / kTile];
+  if (s == n_str || str_off[s] >= n_bytes) {
+    out_off[s] = *total;
+    return;
+  }
+  out_off[s] = ~out_off[s];
 }
 
 }  // namespace sw

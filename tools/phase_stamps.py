@@ -29,8 +29,9 @@ for _ in range(reps):
     tok.encode_packed(buf, off, bits)
 _lib.check(L.sw_encoder_phase_cycles(tok._encoder(), out, 1))
 tiles = (len(buf) + 2047) // 2048
-names = ["stage+enumerate", "lengths+sort", "per-lane merges", "long chunks", "scan+write", "string offsets"]
-tot = sum(out[:6])
+names = ["classify: stage+enum", "classify: lookups", "classify: writes", "classify: strings",
+         "merge N<16 (blk)", "merge N>=16 (blk)", "merge long (blk)"]
+tot = sum(out[:7])
 print("kind=%s bytes=%d chunks=%d tiles=%d kernel_ms=%.3f" % (model, len(buf), nch, tiles, tok.last_stats.ms_kernels))
 for i, nm in enumerate(names):
-    print("%-18s %10.0f cycles/tile  %5.1f%%" % (nm, out[i] / tiles / reps, 100 * out[i] / tot))
+    print("%-22s %12.0f cycles/tile-equiv  %5.1f%%" % (nm, out[i] / tiles / reps, 100 * out[i] / tot))

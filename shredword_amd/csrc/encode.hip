@@ -75,10 +75,10 @@ struct sw_encoder {
   int64_t* d_part = nullptr;
   int64_t* d_tile_slo = nullptr;
   uint32_t* d_tile_slots = nullptr;
-  uint64_t* d_queue = nullptr;        // merge queue, bucket regions
-  int64_t* d_qbase = nullptr;         // [kNumBuckets] region starts
-  unsigned long long* d_qcnt = nullptr;  // [kNumBuckets] entries per bucket (zeroed per call)
-  uint64_t* d_long_slot = nullptr;
+  uint64_t* d_queue = nullptr;        // dense merge queue (bucket-major)
+  uint32_t* d_bcnt = nullptr;         // [kNumBuckets * n_tiles] queued chunks per (bucket, tile)
+  int64_t* d_boff = nullptr;          // its exclusive scan
+  int64_t* d_qtotal = nullptr;
   unsigned long long* d_stamps = nullptr;  // SW_STAMPS builds
   uint32_t* d_tile_cnt = nullptr;
   int64_t* d_tile_first = nullptr;
@@ -114,10 +114,10 @@ struct DeviceGuard {
 void free_workspace(sw_encoder* h) {
   (void)hipFree(h->d_scratch); (void)hipFree(h->d_lw_id); (void)hipFree(h->d_lw_rk); (void)hipFree(h->d_part);
   (void)hipFree(h->d_tile_slo); (void)hipFree(h->d_stamps);
-  (void)hipFree(h->d_tile_slots); (void)hipFree(h->d_queue); (void)hipFree(h->d_qbase); (void)hipFree(h->d_qcnt);
-  (void)hipFree(h->d_long_slot);
+  (void)hipFree(h->d_tile_slots); (void)hipFree(h->d_queue); (void)hipFree(h->d_bcnt); (void)hipFree(h->d_boff);
+  (void)hipFree(h->d_qtotal);
   h->d_tile_slo = nullptr; h->d_stamps = nullptr; h->d_tile_slots = nullptr; h->d_queue = nullptr;
-  h->d_qbase = nullptr; h->d_qcnt = nullptr; h->d_long_slot = nullptr;
+  h->d_bcnt = nullptr; h->d_boff = nullptr; h->d_qtotal = nullptr;
   (void)hipFree(h->d_tile_cnt); (void)hipFree(h->d_tile_first); (void)hipFree(h->d_tile_base);
   (void)hipFree(h->d_total);
   h->d_scratch = nullptr; h->d_lw_id = nullptr; h->d_lw_rk = nullptr; h->d_part = nullptr; h->d_tile_cnt = nullptr;
@@ -142,22 +142,12 @@ int32_t ensure_workspace(sw_encoder* h, int64_t n_bytes) {
   HIP_TRY(hipMalloc(&h->d_lw_rk, sizeof(uint32_t) * nb));
   HIP_TRY(hipMalloc(&h->d_tile_slo, sizeof(int64_t) * n_tiles));
   HIP_TRY(hipMalloc(&h->d_tile_slots, sizeof(uint32_t) * n_tiles));
-  {
-    // bucket b holds chunks of >= bucket_min_len(b) bytes: at most nb / min_len of them
-    int64_t qb[kNumBuckets], total = 0;
-    for (int b = 0; b < kNumBuckets; ++b) {
-      qb[b] = total;
-      total += nb / bucket_min_len(b) + 64;
-    }
-    HIP_TRY(hipMalloc(&h->d_queue, sizeof(uint64_t) * total));
-    HIP_TRY(hipMalloc(&h->d_qbase, sizeof(qb)));
-    HIP_TRY(hipMemcpy(h->d_qbase, qb, sizeof(qb), hipMemcpyHostToDevice));
-    HIP_TRY(hipMalloc(&h->d_qcnt, sizeof(unsigned long long) * kNumBuckets));
-    HIP_TRY(hipMalloc(&h->d_long_slot, sizeof(uint64_t) * (nb / bucket_min_len(kLongBucket) + 64)));
-  }
-  HIP_TRY(hipMalloc(&h->d_stamps, sizeof(unsigned long long) * 8));
-  HIP_TRY(hipMemset(h->d_stamps, 0, sizeof(unsigned long long) * 8));
-  HIP_TRY(hipMalloc(&h->d_part, sizeof(int64_t) * ((n_tiles + kScanBlock - 1) / kScanBlock + 1)));
+  // queued chunks have >= 2 bytes: at most nb / 2 of them
+  HIP_TRY(hipMalloc(&h->d_queue, sizeof(uint64_t) * (nb / 2 + 64)));
+  HIP_TRY(hipMalloc(&h->d_bcnt, sizeof(uint32_t) * kNumBuckets * n_tiles));
+  HIP_TRY(hipMalloc(&h->d_boff, sizeof(int64_t) * kNumBuckets * n_tiles));
+  HIP_TRY(hipMalloc(&h->d_qtotal, sizeof(int64_t)));
+  HIP_TRY(hipMalloc(&h->d_part, sizeof(int64_t) * ((kNumBuckets * n_tiles + kScanBlock - 1) / kScanBlock + 1)));
   HIP_TRY(hipMalloc(&h->d_tile_cnt, sizeof(uint32_t) * n_tiles));
   HIP_TRY(hipMalloc(&h->d_tile_first, sizeof(int64_t) * n_tiles));
   HIP_TRY(hipMalloc(&h->d_tile_base, sizeof(int64_t) * n_tiles));
@@ -222,6 +212,15 @@ bool build_cuckoo(const std::unordered_map<uint64_t, int32_t>& dict, const std::
     if (ok) { out->swap(b); return true; }
   }
   return false;
+}
+
+// exclusive scan of cnt[0..n) into base, total into *total (three small kernels)
+hipError_t launch_scan(hipStream_t st, const uint32_t* cnt, int64_t n, int64_t* part, int64_t* base, int64_t* total) {
+  const int64_t n_parts = (n + kScanBlock - 1) / kScanBlock;
+  hipLaunchKernelGGL(k_scan_reduce, dim3((unsigned)n_parts), dim3(kThreads), 0, st, cnt, n, part);
+  hipLaunchKernelGGL(k_scan_parts, dim3(1), dim3(1024), 0, st, part, n_parts, total);
+  hipLaunchKernelGGL(k_scan_apply, dim3((unsigned)n_parts), dim3(kThreads), 0, st, cnt, n, part, base);
+  return hipGetLastError();
 }
 
 }  // namespace
@@ -394,9 +393,8 @@ extern "C" int32_t sw_encode_device(sw_encoder* h, const uint8_t* d_bytes, int64
     a.scratch = h->d_scratch; a.lw_id = h->d_lw_id; a.lw_rk = h->d_lw_rk;
     a.tile_cnt = h->d_tile_cnt; a.tile_slots = h->d_tile_slots; a.tile_first = h->d_tile_first;
     a.out_off = d_out_off; a.tile_slo = h->d_tile_slo;
-    a.queue = h->d_queue; a.q_base = h->d_qbase; a.q_cnt = h->d_qcnt; a.long_slot = h->d_long_slot;
-    a.stamps = h->d_stamps;
-    HIP_TRY(hipMemsetAsync(h->d_qcnt, 0, sizeof(unsigned long long) * kNumBuckets, st));
+    a.n_tiles = n_tiles; a.qtmp = h->d_lw_id; a.bcnt = h->d_bcnt; a.boff = h->d_boff; a.q_total = h->d_qtotal;
+    a.queue = h->d_queue; a.stamps = h->d_stamps;
     hipLaunchKernelGGL(k_tile_strings, dim3((unsigned)((n_tiles + 255) / 256)), dim3(256), 0, st, d_str_off, n_str,
                        n_tiles, h->d_tile_slo);
     hipEvent_t e0 = nullptr, e1 = nullptr;
@@ -413,6 +411,8 @@ extern "C" int32_t sw_encode_device(sw_encoder* h, const uint8_t* d_bytes, int64
     // the encode proper: classify, then the bucketed merge loops (timed together)
     hipLaunchKernelGGL(k_classify, dim3((unsigned)n_tiles), dim3(kThreads), 0, st, a);
     HIP_TRY(hipGetLastError());
+    HIP_TRY(launch_scan(st, h->d_bcnt, kNumBuckets * n_tiles, h->d_part, h->d_boff, h->d_qtotal));
+    hipLaunchKernelGGL(k_scatter, dim3((unsigned)((n_tiles + 3) / 4)), dim3(kThreads), 0, st, a);
     const dim3 pg(2048), pb(kThreads);  // persistent grid for the queue kernels
     if (h->table.wide) {
       hipLaunchKernelGGL((k_merge_bucket<true, false, 4>), pg, pb, 0, st, a, 0, 2);
@@ -438,13 +438,7 @@ extern "C" int32_t sw_encode_device(sw_encoder* h, const uint8_t* d_bytes, int64
       HIP_TRY(hipEventRecord(e1, st));
       ++h->ev_used;
     }
-    const int64_t n_parts = (n_tiles + kScanBlock - 1) / kScanBlock;
-    hipLaunchKernelGGL(k_scan_reduce, dim3((unsigned)n_parts), dim3(kThreads), 0, st, h->d_tile_cnt, n_tiles,
-                       h->d_part);
-    hipLaunchKernelGGL(k_scan_parts, dim3(1), dim3(1024), 0, st, h->d_part, n_parts, h->d_total);
-    hipLaunchKernelGGL(k_scan_apply, dim3((unsigned)n_parts), dim3(kThreads), 0, st, h->d_tile_cnt, n_tiles,
-                       h->d_part, h->d_tile_base);
-    HIP_TRY(hipGetLastError());
+    HIP_TRY(launch_scan(st, h->d_tile_cnt, n_tiles, h->d_part, h->d_tile_base, h->d_total));
     hipLaunchKernelGGL(k_compact, dim3((unsigned)n_tiles), dim3(kThreads), 0, st, a, h->d_tile_base, d_out_ids);
     HIP_TRY(hipGetLastError());
   } else {

@@ -368,10 +368,12 @@ struct EncArgs {
   int64_t* tile_first;       // [n_tiles] first chunk start in tile (or -1)
   int64_t* out_off;          // [n_str+1] string -> slot offset in its tile (k_compact converts)
   const int64_t* tile_slo;   // [n_tiles] first string starting at or after the tile start
-  uint64_t* queue;           // merge queue: entries (start << 24 | slot offset in tile)
-  const int64_t* q_base;     // [kNumBuckets] region start of each bucket in `queue`
-  unsigned long long* q_cnt; // [kNumBuckets] entries per bucket
-  uint64_t* long_slot;       // slot offsets of long chunks (may exceed 24 bits)
+  int64_t n_tiles;
+  uint32_t* qtmp;            // [n_bytes] tile-local queue entries, position space (aliases lw_id)
+  uint32_t* bcnt;            // [kNumBuckets * n_tiles] queued chunks per (bucket, tile)
+  const int64_t* boff;       // [kNumBuckets * n_tiles] exclusive scan of bcnt (bucket-major)
+  const int64_t* q_total;    // queued chunks in all
+  uint64_t* queue;           // dense merge queue, bucket-major: start << 24 | len << 18 | slot
   unsigned long long* stamps;  // SW_STAMPS builds: cycles per phase, summed
 };
 
@@ -401,7 +403,7 @@ __global__ void __launch_bounds__(kThreads) k_classify(EncArgs a) {
   __shared__ uint32_t s_off[kTile + 1];       // slots per chunk, then exclusive slot offsets
   __shared__ uint32_t s_wsum[kThreads / 64];
   __shared__ uint32_t s_bcnt[kNumBuckets];
-  __shared__ unsigned long long s_bbase[kNumBuckets];
+  __shared__ uint32_t s_bbase[kNumBuckets];
   __shared__ int64_t s_last_end;
   __shared__ uint32_t s_settled;
 
@@ -477,8 +479,9 @@ __global__ void __launch_bounds__(kThreads) k_classify(EncArgs a) {
     }
     s_val[k] = tok;
     s_off[k] = tok != kInf ? 1u : (uint32_t)min(len, (int64_t)0xFFFFFFFF);
-    if (tok != kInf) atomicAdd(&s_settled, 1u);
-    else atomicAdd(&s_bcnt[bucket_of(len)], 1u);
+    if (tok == kInf) atomicAdd(&s_bcnt[bucket_of(len)], 1u);
+    const uint64_t settled = __ballot(tok != kInf);
+    if ((tid & 63) == 0) atomicAdd(&s_settled, (uint32_t)__popcll(settled));
   }
   __syncthreads();
   SW_STAMP(1);
@@ -496,9 +499,16 @@ __global__ void __launch_bounds__(kThreads) k_classify(EncArgs a) {
     off += c;
   }
   if (tid == 0) s_off[C] = n_slots;
+  if (tid == 0) {  // tile-local start of each bucket's entries
+    uint32_t acc = 0;
+    for (int b = 0; b < kNumBuckets; ++b) {
+      s_bbase[b] = acc;
+      acc += s_bcnt[b];
+    }
+  }
+  __syncthreads();
   if (tid < kNumBuckets) {
-    const uint32_t c = s_bcnt[tid];
-    s_bbase[tid] = c ? atomicAdd(&a.q_cnt[tid], (unsigned long long)c) : 0ULL;
+    a.bcnt[(int64_t)tid * a.n_tiles + tile] = s_bcnt[tid];
     s_bcnt[tid] = 0;
   }
   __syncthreads();
@@ -518,16 +528,12 @@ __global__ void __launch_bounds__(kThreads) k_classify(EncArgs a) {
       dst[o] = (int32_t)tok;
       continue;
     }
-    const int64_t start = t0 + s_cstart[k];
     const int b = bucket_of(ns);
-    const unsigned long long qi = s_bbase[b] + atomicAdd(&s_bcnt[b], 1u);
-    if (b != kLongBucket) {
-      a.queue[a.q_base[b] + qi] = ((uint64_t)start << 24) | o;
-      for (uint32_t j = 0; j < ns; ++j) dst[o + j] = kSentinel;
-    } else {
-      a.queue[a.q_base[b] + qi] = (uint64_t)start;  // k_merge_long writes all its slots
-      a.long_slot[qi] = o;
-    }
+    const uint32_t qi = s_bbase[b] + atomicAdd(&s_bcnt[b], 1u);
+    // tile-local entry: chunk start in tile (11 bits) | slot offset (13) | length (6, 0 = long)
+    a.qtmp[t0 + qi] = (uint32_t)s_cstart[k] | (o << 11) | ((b != kLongBucket ? ns : 0u) << 24);
+    if (b != kLongBucket)
+      for (uint32_t j = 0; j < ns; ++j) dst[o + j] = kSentinel;  // k_merge_long writes all its own
   }
   SW_STAMP(2);
 
@@ -550,7 +556,47 @@ __global__ void __launch_bounds__(kThreads) k_classify(EncArgs a) {
 }
 
 // ---------------------------------------------------------------------------------------
-// k_merge_bucket<N>: queued chunks of buckets [b_lo, b_hi] (length <= N), one per lane
+// k_scatter: tile-local queue entries -> the dense bucket-major queue
+// ---------------------------------------------------------------------------------------
+__global__ void __launch_bounds__(kThreads) k_scatter(EncArgs a) {
+  // one wave per tile: lane b < kNumBuckets fetches (count, destination) of bucket b at once
+  const int64_t t = ((int64_t)blockIdx.x * kThreads + threadIdx.x) >> 6;
+  const int lane = threadIdx.x & 63;
+  if (t >= a.n_tiles) return;
+  const int64_t t0 = t * kTile;
+  uint32_t c = 0;
+  int64_t dst = 0;
+  if (lane < kNumBuckets) {
+    c = a.bcnt[(int64_t)lane * a.n_tiles + t];
+    dst = a.boff[(int64_t)lane * a.n_tiles + t];
+  }
+  uint32_t local = c;  // exclusive prefix of the counts over buckets = tile-local start
+#pragma unroll
+  for (int off = 1; off < 16; off <<= 1) {
+    const uint32_t y = __shfl_up(local, off, 64);
+    if (lane >= off) local += y;
+  }
+  local -= c;
+  for (int b = 0; b < kNumBuckets; ++b) {
+    const uint32_t cb = __shfl(c, b, 64), lb = __shfl(local, b, 64);
+    const int64_t db = __shfl(dst, b, 64);
+    for (uint32_t j = lane; j < cb; j += 64) {
+      const uint32_t e = a.qtmp[t0 + lb + j];
+      const uint64_t start = (uint64_t)(t0 + (e & 0x7FFu));
+      a.queue[db + j] = (start << 24) | ((uint64_t)(e >> 24) << 18) | ((e >> 11) & 0x1FFFu);
+    }
+  }
+}
+
+// [lo, hi) of the dense queue holding buckets b_lo..b_hi
+__device__ __forceinline__ void bucket_range(const EncArgs& a, int b_lo, int b_hi, int64_t* lo, int64_t* hi) {
+  *lo = a.boff[(int64_t)b_lo * a.n_tiles];
+  *hi = (b_hi + 1 < kNumBuckets) ? a.boff[(int64_t)(b_hi + 1) * a.n_tiles] : *a.q_total;
+}
+
+// ---------------------------------------------------------------------------------------
+// k_merge_bucket<N>: queued chunks of buckets [b_lo, b_hi] (length <= N), one per lane;
+// persistent grid-stride over 64-entry batches, next batch's entry prefetched
 // ---------------------------------------------------------------------------------------
 template <bool kWide, bool k16, int N>
 __global__ void __launch_bounds__(kThreads) k_merge_bucket(EncArgs a, int b_lo, int b_hi) {
@@ -558,29 +604,43 @@ __global__ void __launch_bounds__(kThreads) k_merge_bucket(EncArgs a, int b_lo, 
   const int64_t gw = ((int64_t)blockIdx.x * kThreads + threadIdx.x) >> 6;  // global wave id
   const int64_t n_waves = ((int64_t)gridDim.x * kThreads) >> 6;
   const int lane = threadIdx.x & 63;
-  for (int b = b_lo; b <= b_hi; ++b) {
-    const int64_t cnt = (int64_t)a.q_cnt[b];
-    const uint64_t* q = a.queue + a.q_base[b];
-    for (int64_t base = gw * 64; base < cnt; base += n_waves * 64) {
-      const int64_t i = base + lane;
-      if (i >= cnt) break;
-      const uint64_t e = q[i];
-      const int64_t start = (int64_t)(e >> 24);
-      const uint32_t o = (uint32_t)(e & 0xFFFFFFu);
-      const int64_t end = next_set_bit(a.bits, a.n_words, start + 1, a.n_bytes);
-      const int n = (int)(end - start);
-      uint32_t id[N];
+  int64_t lo, hi;
+  bucket_range(a, b_lo, b_hi, &lo, &hi);
+  constexpr int W = N / 4 + 1;  // aligned words covering any N-byte span
+  const int64_t mis = (int64_t)((uintptr_t)a.bytes & 3);
+  const uint32_t* words = (const uint32_t*)((uintptr_t)a.bytes - mis);
+  const int64_t last_word = (mis + a.n_bytes - 1) >> 2;  // last word holding input bytes
+  int64_t i = lo + gw * 64 + lane;
+  uint64_t e = i < hi ? a.queue[i] : 0;
+  while (i < hi) {
+    const int64_t inext = i + n_waves * 64;
+    const uint64_t enext = inext < hi ? a.queue[inext] : 0;  // prefetch
+    const int64_t start = (int64_t)(e >> 24);
+    const int n = (int)((e >> 18) & 63u);
+    const uint32_t o = (uint32_t)(e & 0x3FFFFu);
+    // the chunk's bytes: W aligned words, realigned with v_alignbyte
+    const int64_t g = start + mis, w0 = g >> 2;
+    uint32_t w[W];
 #pragma unroll
-      for (int k = 0; k < N; ++k) id[k] = (k < n) ? (uint32_t)a.bytes[start + k] : 0u;
-      const uint32_t alive = lane_merge_reg<kWide, k16, N>(a.table, id, n);
-      const int64_t tile = start / kTile;
-      int32_t* dst = a.scratch + a.tile_first[tile] + o;
-      int m = 0;
+    for (int k = 0; k < W; ++k) w[k] = words[min(w0 + k, last_word)];
+    const uint32_t sh = (uint32_t)(g & 3);
+    uint32_t id[N];
 #pragma unroll
-      for (int k = 0; k < N; ++k)
-        if ((alive >> k) & 1u) dst[m++] = (int32_t)id[k];
-      atomicAdd(&a.tile_cnt[tile], (uint32_t)m);
+    for (int q = 0; q < N / 4; ++q) {
+      const uint32_t u = __builtin_amdgcn_alignbyte(w[q + 1], w[q], sh);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) id[4 * q + r] = (4 * q + r < n) ? ((u >> (8 * r)) & 0xFFu) : 0u;
     }
+    const uint32_t alive = lane_merge_reg<kWide, k16, N>(a.table, id, n);
+    const int64_t tile = start / kTile;
+    int32_t* dst = a.scratch + a.tile_first[tile] + o;
+    int m = 0;
+#pragma unroll
+    for (int k = 0; k < N; ++k)
+      if ((alive >> k) & 1u) dst[m++] = (int32_t)id[k];
+    atomicAdd(&a.tile_cnt[tile], (uint32_t)m);
+    i = inext;
+    e = enext;
   }
 #ifdef SW_STAMPS
   SW_STAMP(N >= 16 ? 5 : 4);
@@ -594,10 +654,11 @@ __global__ void __launch_bounds__(kThreads) k_merge_long(EncArgs a) {
   const int64_t gw = ((int64_t)blockIdx.x * kThreads + threadIdx.x) >> 6;
   const int64_t n_waves = ((int64_t)gridDim.x * kThreads) >> 6;
   const int lane = threadIdx.x & 63;
-  const int64_t cnt = (int64_t)a.q_cnt[kLongBucket];
-  const uint64_t* q = a.queue + a.q_base[kLongBucket];
-  for (int64_t i = gw; i < cnt; i += n_waves) {
-    const int64_t start = (int64_t)q[i];
+  int64_t lo, hi;
+  bucket_range(a, kLongBucket, kLongBucket, &lo, &hi);
+  for (int64_t i = lo + gw; i < hi; i += n_waves) {
+    const uint64_t e = a.queue[i];
+    const int64_t start = (int64_t)(e >> 24);
     const int64_t end = next_set_bit(a.bits, a.n_words, start + 1, a.n_bytes);
     const int64_t len = end - start;
     uint32_t* gid = a.lw_id + start;
@@ -606,7 +667,7 @@ __global__ void __launch_bounds__(kThreads) k_merge_long(EncArgs a) {
     wave_sync_mem();
     const int64_t m = coop_merge<kWide>(a.table, gid, grk, len, lane);
     const int64_t tile = start / kTile;
-    int32_t* dst = a.scratch + a.tile_first[tile] + (int64_t)a.long_slot[i];
+    int32_t* dst = a.scratch + a.tile_first[tile] + (int64_t)(e & 0x3FFFFu);
     for (int64_t j = lane; j < len; j += 64) dst[j] = j < m ? (int32_t)gid[j] : kSentinel;
     if (lane == 0) atomicAdd(&a.tile_cnt[tile], (uint32_t)m);
   }
@@ -711,6 +772,7 @@ constexpr int kCompactPer = 8;                          // slots per thread per 
 constexpr int kCompactPass = kThreads * kCompactPer;    // slots per pass
 
 __global__ void __launch_bounds__(kThreads) k_compact(EncArgs a, const int64_t* tile_base, int32_t* out) {
+  __shared__ __attribute__((aligned(16))) int32_t s_io[kCompactPass];  // slots in, ids out
   __shared__ uint32_t s_pref[kCompactPass + 1];  // ids before each slot of the pass
   __shared__ uint32_t s_wsum[kThreads / 64];
   const int64_t t = blockIdx.x;
@@ -722,23 +784,35 @@ __global__ void __launch_bounds__(kThreads) k_compact(EncArgs a, const int64_t* 
   const int64_t s_lo = a.tile_slo[t];
   uint32_t done = 0;  // ids written by earlier passes
   for (uint32_t p0 = 0; p0 == 0 || p0 < n_slots; p0 += kCompactPass) {
+    // coalesced load of the pass's slots into LDS
+#pragma unroll
+    for (int k = 0; k < kCompactPer; ++k) {
+      const uint32_t j = p0 + k * kThreads + tid;
+      s_io[k * kThreads + tid] = j < n_slots ? src[j] : kSentinel;
+    }
+    __syncthreads();
     int32_t v[kCompactPer];
     uint32_t c = 0;
 #pragma unroll
     for (int k = 0; k < kCompactPer; ++k) {
-      const uint32_t j = p0 + tid * kCompactPer + k;
-      v[k] = j < n_slots ? src[j] : kSentinel;
+      v[k] = s_io[tid * kCompactPer + k];
       c += v[k] != kSentinel;
     }
     uint32_t pass_total;
-    uint32_t o = block_excl_scan(c, s_wsum, &pass_total);
+    uint32_t o = block_excl_scan(c, s_wsum, &pass_total);  // (its barriers also fence s_io reads)
 #pragma unroll
     for (int k = 0; k < kCompactPer; ++k) {
       s_pref[tid * kCompactPer + k] = done + o;
-      if (v[k] != kSentinel) out[base + done + o++] = v[k];
+      if (v[k] != kSentinel) s_io[o++] = v[k];
     }
     if (tid == 0) s_pref[kCompactPass] = done + pass_total;
     __syncthreads();
+    // coalesced store of the pass's ids
+#pragma unroll
+    for (int k = 0; k < kCompactPer; ++k) {
+      const uint32_t j = k * kThreads + tid;
+      if (j < pass_total) out[base + done + j] = s_io[j];
+    }
     // strings of this tile whose slot offset falls in this pass (or is the region's end)
     for (int64_t s = s_lo + tid; s < a.n_str; s += kThreads) {
       if (a.str_off[s] >= t1) break;

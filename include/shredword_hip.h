@@ -135,9 +135,11 @@ double sw_encoder_last_kernel_ms(const sw_encoder* h);
 
 /* Diagnostic builds only (compiled with -DSW_STAMPS): device cycles summed over workgroups,
  * per phase: 0 k_classify stage+enumerate, 1 classify lookups, 2 slot/queue writes, 3 string
- * offsets, 4 k_merge_bucket N<16 (per block), 5 k_merge_bucket N>=16, 6 k_merge_long.
- * reset != 0 zeroes the counters.  Regular builds return SW_ERR_ARG. */
-int32_t sw_encoder_phase_cycles(sw_encoder* h, double* out8, int32_t reset);
+ * offsets, 4 k_merge_bucket N<16 (per block), 5 k_merge_bucket N>=16, 6 k_merge_long; then per
+ * merge bucket kernel g (N = 4, 8, 16, 32) at 8 + 4g: batches, merge-loop cycles, batch cycles,
+ * sum of the wave-max loop iterations.  out32 holds 32 values.  reset != 0 zeroes the
+ * counters.  Regular builds return SW_ERR_ARG. */
+int32_t sw_encoder_phase_cycles(sw_encoder* h, double* out32, int32_t reset);
 
 /* ---- synthetic corpora (bench inputs; deterministic for any thread count) --------------
  * Fills out_off[0..n_strings] with string offsets; when out_bytes is non-NULL also writes

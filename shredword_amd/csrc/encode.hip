@@ -152,6 +152,10 @@ int32_t ensure_workspace(sw_encoder* h, int64_t n_bytes) {
   HIP_TRY(hipMalloc(&h->d_tile_first, sizeof(int64_t) * n_tiles));
   HIP_TRY(hipMalloc(&h->d_tile_base, sizeof(int64_t) * n_tiles));
   HIP_TRY(hipMalloc(&h->d_total, sizeof(int64_t)));
+#ifdef SW_STAMPS
+  HIP_TRY(hipMalloc(&h->d_stamps, sizeof(unsigned long long) * 32));
+  HIP_TRY(hipMemset(h->d_stamps, 0, sizeof(unsigned long long) * 32));
+#endif
   h->cap_bytes = nb;
   return SW_OK;
 }
@@ -359,19 +363,19 @@ extern "C" double sw_encoder_last_kernel_ms(const sw_encoder* h) {
 
 // Diagnostic builds only (-DSW_STAMPS): cycles per pipeline phase summed over workgroups
 // since the workspace was allocated (or the last reset).
-extern "C" int32_t sw_encoder_phase_cycles(sw_encoder* h, double* out8, int32_t reset) {
+extern "C" int32_t sw_encoder_phase_cycles(sw_encoder* h, double* out32, int32_t reset) {
 #ifdef SW_STAMPS
-  if (!h || !out8 || !h->d_stamps) return fail(SW_ERR_ARG, "sw_encoder_phase_cycles: no workspace");
+  if (!h || !out32 || !h->d_stamps) return fail(SW_ERR_ARG, "sw_encoder_phase_cycles: no workspace");
   DeviceGuard g(h->device);
-  unsigned long long v[8];
+  unsigned long long v[32];
   HIP_TRY(hipStreamSynchronize(h->stream));
   HIP_TRY(hipDeviceSynchronize());
   HIP_TRY(hipMemcpy(v, h->d_stamps, sizeof(v), hipMemcpyDeviceToHost));
-  for (int i = 0; i < 8; ++i) out8[i] = (double)v[i];
+  for (int i = 0; i < 32; ++i) out32[i] = (double)v[i];
   if (reset) HIP_TRY(hipMemset(h->d_stamps, 0, sizeof(v)));
   return SW_OK;
 #else
-  (void)h; (void)out8; (void)reset;
+  (void)h; (void)out32; (void)reset;
   return fail(SW_ERR_ARG, "sw_encoder_phase_cycles: not a diagnostic (SW_STAMPS) build");
 #endif
 }

@@ -191,7 +191,7 @@ struct RegKey {  // (rank, slot) packed so that min() picks the lowest rank, the
 };
 
 template <bool kWide, bool k16, int N>
-__device__ __forceinline__ uint32_t lane_merge_reg(const DevTable& t, uint32_t (&id)[N], int n) {
+__device__ __forceinline__ uint32_t lane_merge_reg(const DevTable& t, uint32_t (&id)[N], int n, int* iters = nullptr) {
   using RK = RegKey<k16>;
   constexpr uint32_t NONE = 0xFFFFFFFFu;  // no right neighbour
   uint32_t rid[N], rk[N];
@@ -207,6 +207,7 @@ __device__ __forceinline__ uint32_t lane_merge_reg(const DevTable& t, uint32_t (
     for (int k = g; k < g + 4 && k < N; ++k) rk[k] = (rid[k] == NONE) ? kInf : rk[k];
     __builtin_amdgcn_sched_barrier(0);
   }
+  int it = 0;
   while (true) {
     typename RK::T best = RK::inf;
 #pragma unroll
@@ -216,6 +217,7 @@ __device__ __forceinline__ uint32_t lane_merge_reg(const DevTable& t, uint32_t (
     }
     const uint32_t nv = RK::rank(best);
     if (nv == kInf) break;
+    ++it;
     const int bi = (int)(best & 31);
     uint32_t p0 = 0, p1 = 0;
 #pragma unroll
@@ -223,35 +225,32 @@ __device__ __forceinline__ uint32_t lane_merge_reg(const DevTable& t, uint32_t (
       p0 = (k == bi) ? id[k] : p0;
       p1 = (k == bi) ? rid[k] : p1;
     }
-    // left-to-right: take every non-overlapping occurrence of (p0, p1) (base.py:29-35)
+    // left-to-right: take every non-overlapping occurrence of (p0, p1) (base.py:29-35).
+    // Branch-free: every slot is a handful of v_cndmask, no exec-mask juggling.
     bool took = false;
     uint32_t changed = 0;
 #pragma unroll
     for (int k = 0; k < N; ++k) {
-      if ((alive >> k) & 1u) {
-        if (took) {
-          alive &= ~(1u << k);
-          took = false;
-        } else if (id[k] == p0 && rid[k] == p1) {
-          id[k] = nv;
-          took = true;
-          changed |= 1u << k;
-        }
-      }
+      const bool al = (alive >> k) & 1u;
+      const bool consume = al && took;
+      const bool match = al && !took && id[k] == p0 && rid[k] == p1;
+      alive = consume ? (alive & ~(1u << k)) : alive;
+      id[k] = match ? nv : id[k];
+      changed |= match ? (1u << k) : 0u;
+      took = al ? match : took;
     }
     // right-to-left: new right neighbours; pairs touching a new token need a new rank
     uint32_t carry = NONE, need = 0;
     bool carry_chg = false;
 #pragma unroll
     for (int k = N - 1; k >= 0; --k) {
-      if ((alive >> k) & 1u) {
-        const bool chg = (changed >> k) & 1u;
-        rid[k] = carry;
-        if (carry != NONE && (chg || carry_chg)) need |= 1u << k;
-        if (carry == NONE) rk[k] = kInf;
-        carry = id[k];
-        carry_chg = chg;
-      }
+      const bool al = (alive >> k) & 1u;
+      const bool chg = (changed >> k) & 1u;
+      rid[k] = al ? carry : rid[k];
+      need |= (al && carry != NONE && (chg || carry_chg)) ? (1u << k) : 0u;
+      rk[k] = (al && carry == NONE) ? kInf : rk[k];
+      carry = al ? id[k] : carry;
+      carry_chg = al ? chg : carry_chg;
     }
     while (need) {  // two lookups in flight per round
       const int j1 = __ffs(need) - 1;
@@ -274,6 +273,7 @@ __device__ __forceinline__ uint32_t lane_merge_reg(const DevTable& t, uint32_t (
       }
     }
   }
+  if (iters) *iters = it;
   return alive;
 }
 
@@ -612,7 +612,13 @@ __global__ void __launch_bounds__(kThreads) k_merge_bucket(EncArgs a, int b_lo, 
   const int64_t last_word = (mis + a.n_bytes - 1) >> 2;  // last word holding input bytes
   int64_t i = lo + gw * 64 + lane;
   uint64_t e = i < hi ? a.queue[i] : 0;
+#ifdef SW_STAMPS
+  unsigned long long st_b = 0, st_loop = 0, st_batch = 0, st_it = 0;
+#endif
   while (i < hi) {
+#ifdef SW_STAMPS
+    const unsigned long long batch_t0 = __builtin_readcyclecounter();
+#endif
     const int64_t inext = i + n_waves * 64;
     const uint64_t enext = inext < hi ? a.queue[inext] : 0;  // prefetch
     const int64_t start = (int64_t)(e >> 24);
@@ -631,18 +637,52 @@ __global__ void __launch_bounds__(kThreads) k_merge_bucket(EncArgs a, int b_lo, 
 #pragma unroll
       for (int r = 0; r < 4; ++r) id[4 * q + r] = (4 * q + r < n) ? ((u >> (8 * r)) & 0xFFu) : 0u;
     }
-    const uint32_t alive = lane_merge_reg<kWide, k16, N>(a.table, id, n);
+#ifdef SW_STAMPS
+    const unsigned long long c0 = __builtin_readcyclecounter();
+#endif
+#ifdef SW_ABL_NOLOOP  // ablation builds only: timing experiments, results are wrong
+    const uint32_t alive = (n >= 32) ? ~0u : ((1u << n) - 1u);
+#else
+    int iters = 0;
+    const uint32_t alive = lane_merge_reg<kWide, k16, N>(a.table, id, n, &iters);
+#endif
+#ifdef SW_STAMPS
+    {
+      const unsigned long long c1 = __builtin_readcyclecounter();
+      int mx = iters;
+#pragma unroll
+      for (int off = 32; off > 0; off >>= 1) { const int o2 = __shfl_xor(mx, off, 64); mx = o2 > mx ? o2 : mx; }
+      st_b += 1; st_loop += c1 - c0; st_batch += c1 - batch_t0; st_it += (unsigned long long)mx;
+    }
+#endif
     const int64_t tile = start / kTile;
     int32_t* dst = a.scratch + a.tile_first[tile] + o;
     int m = 0;
 #pragma unroll
-    for (int k = 0; k < N; ++k)
-      if ((alive >> k) & 1u) dst[m++] = (int32_t)id[k];
+    for (int k = 0; k < N; ++k) {
+      if ((alive >> k) & 1u) {
+#ifndef SW_ABL_NOWRITE
+        dst[m] = (int32_t)id[k];
+#endif
+        ++m;
+      }
+    }
+#ifndef SW_ABL_NOATOMIC
     atomicAdd(&a.tile_cnt[tile], (uint32_t)m);
+#else
+    if (m == 99999) a.tile_cnt[0] = 0;
+#endif
     i = inext;
     e = enext;
   }
 #ifdef SW_STAMPS
+  if (lane == 0 && st_b) {
+    const int gi = 8 + 4 * (N == 4 ? 0 : N == 8 ? 1 : N == 16 ? 2 : 3);
+    atomicAdd(&a.stamps[gi + 0], st_b);
+    atomicAdd(&a.stamps[gi + 1], st_loop);
+    atomicAdd(&a.stamps[gi + 2], st_batch);
+    atomicAdd(&a.stamps[gi + 3], st_it);
+  }
   SW_STAMP(N >= 16 ? 5 : 4);
 #endif
 }

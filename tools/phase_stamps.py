@@ -22,7 +22,7 @@ tok = Tokenizer(0)
 tok.load(os.path.join(ROOT, "tests", "golden", model))
 tok.encode_packed(buf, off, bits)  # warm
 L = _lib.lib()
-out = (ctypes.c_double * 8)()
+out = (ctypes.c_double * 32)()
 _lib.check(L.sw_encoder_phase_cycles(tok._encoder(), out, 1))
 reps = 3
 for _ in range(reps):
@@ -35,3 +35,9 @@ tot = sum(out[:7])
 print("kind=%s bytes=%d chunks=%d tiles=%d kernel_ms=%.3f" % (model, len(buf), nch, tiles, tok.last_stats.ms_kernels))
 for i, nm in enumerate(names):
     print("%-22s %12.0f cycles/tile-equiv  %5.1f%%" % (nm, out[i] / tiles / reps, 100 * out[i] / tot))
+for g, N in enumerate((4, 8, 16, 32)):
+    b = out[8 + 4 * g]
+    if b:
+        print("merge N=%-2d batches %8d  loop cycles/batch %8.0f  batch cycles %8.0f  wave-max iters %5.2f  cycles/iter %6.0f"
+              % (N, b / reps, out[9 + 4 * g] / b, out[10 + 4 * g] / b, out[11 + 4 * g] / b,
+                 out[9 + 4 * g] / max(1, out[11 + 4 * g])))

@@ -43,6 +43,8 @@ def parse():
     ap.add_argument("--cpu-sample-mb", type=float, default=96.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--threads", type=int, default=16, help="host threads for corpus/pre-split")
+    ap.add_argument("--no-dedupe", action="store_true",
+                    help="A/B only: every queued chunk runs its own merge loop (same results)")
     ap.add_argument("--no-chunk-table", action="store_true",
                     help="every chunk runs the merge loop (results identical; see DESIGN.md)")
     return ap.parse_args()
@@ -86,6 +88,7 @@ def main():
     h = tok._encoder()
     _lib.check(L.sw_encoder_reserve(h, n_bytes, n_str))
     _lib.check(L.sw_encoder_set_option(h, _lib.SW_OPT_CHUNK_TABLE, 0 if args.no_chunk_table else 1))
+    _lib.check(L.sw_encoder_set_option(h, _lib.SW_OPT_DEDUPE, 0 if args.no_dedupe else 1))
 
     cap = torch.tensor([n_bytes], dtype=torch.int64, device=dev)
     if world > 1:
@@ -186,7 +189,8 @@ def main():
                                     "GPU merge loop" % args.pattern) + (" + RCCL all-gather of ids" if gather else ""),
                        "bytes_per_rank": n_bytes, "strings_per_rank": n_str, "merges": len(tok.merges),
                        "model": model, "pattern": args.pattern, "parallelism": "doc-shard x%d" % world,
-                       "gather_in_step": gather, "chunk_table": not args.no_chunk_table},
+                       "gather_in_step": gather, "chunk_table": not args.no_chunk_table,
+                       "dedupe": not args.no_dedupe},
             "mtok_per_s": round(all_tok * args.steps / sec / 1e6, 3),
             "bytes_per_token": round(all_bytes / max(all_tok, 1), 4),
             "chunks": int(all_chunks),

@@ -84,8 +84,13 @@ int32_t sw_encoder_reserve(sw_encoder* h, int64_t max_bytes, int64_t max_strings
  *   SW_OPT_CHUNK_TABLE  1 (default): a chunk of 2..16 bytes that encodes to exactly one token is
  *                       answered from a table built at creation (the vocabulary's byte strings
  *                       whose own encoding is a single token); 0: every chunk runs the merge
- *                       loop.  Results are identical either way. */
+ *                       loop.  Results are identical either way.
+ *   SW_OPT_DEDUPE       1 (default): within one launch, a multi-token chunk whose bytes already
+ *                       occurred shares the first occurrence's merge result (bytes compared, not
+ *                       just hashed); 0: every occurrence runs its own merge loop.  Results are
+ *                       identical either way. */
 #define SW_OPT_CHUNK_TABLE 1
+#define SW_OPT_DEDUPE 2
 int32_t sw_encoder_set_option(sw_encoder* h, int32_t option, int64_t value);
 
 /* Encoder facts (sw_encoder_get_info): distinct merges, whole-chunk table entries, whether the
@@ -118,7 +123,9 @@ int32_t sw_encode_batch(sw_encoder* h, const uint8_t* bytes, const int64_t* str_
 /* ---- batched encode, device-resident buffers (bench / multi-GPU driver) -----------------
  * All pointers are device pointers on the encoder's device: d_bytes[n_bytes],
  * d_str_off[n_str+1] (relative to d_bytes, d_str_off[0] == 0, d_str_off[n_str] == n_bytes),
- * d_chunk_bits[ceil(n_bytes/64)], d_out_ids[n_bytes], d_out_off[n_str+1].
+ * d_chunk_bits[ceil(n_bytes/64)], d_out_ids[n_bytes], d_out_off[n_str+1].  One launch takes
+ * n_bytes < 2^31 - 64 (SW_ERR_ARG otherwise); sw_encode_batch splits larger batches between
+ * strings by itself.
  * stream: a hipStream_t on that device, or NULL for the encoder's own stream.
  * Asynchronous: the work is enqueued on the stream.  n_tokens_host (optional) forces a
  * synchronisation and receives the total id count. */
@@ -135,10 +142,9 @@ double sw_encoder_last_kernel_ms(const sw_encoder* h);
 
 /* Diagnostic builds only (compiled with -DSW_STAMPS): device cycles summed over workgroups,
  * per phase: 0 k_classify stage+enumerate, 1 classify lookups, 2 slot/queue writes, 3 string
- * offsets, 4 k_merge_bucket N<16 (per block), 5 k_merge_bucket N>=16, 6 k_merge_long; then per
- * merge bucket kernel g (N = 4, 8, 16, 32) at 8 + 4g: batches, merge-loop cycles, batch cycles,
- * sum of the wave-max loop iterations.  out32 holds 32 values.  reset != 0 zeroes the
- * counters.  Regular builds return SW_ERR_ARG. */
+ * offsets, 4 k_merge_bucket N<16 (per block), 5 k_merge_bucket N>=16, 6 k_merge_long,
+ * 8..11 k_compact: slots + reference list, result gathers, chained scan, expansion + strings.
+ * out32 holds 32 values.  reset != 0 zeroes the counters.  Regular builds return SW_ERR_ARG. */
 int32_t sw_encoder_phase_cycles(sw_encoder* h, double* out32, int32_t reset);
 
 /* ---- synthetic corpora (bench inputs; deterministic for any thread count) --------------

@@ -9,12 +9,14 @@
 //
 // Device pipeline (all on one stream; inputs resident in HBM; kernels in kernels.h):
 //   k_tile_strings   first string of each tile
-//   k_classify       per 2 KiB tile: single bytes + whole-chunk-table hits settled, the rest
-//                    queued by length bucket with reserved output slots
-//   k_merge_bucket   exact merge loop, one chunk per lane, in registers (N = 4/8/16/32)
+//   k_classify       per 2 KiB tile: single bytes + whole-chunk-table hits settled, one slot
+//                    per chunk, the rest queued by length bucket
+//   k_scan_*/k_scatter  dense bucket-major merge queue
+//   k_merge_bucket   batch-wide chunk dedupe + exact merge loop, one chunk per lane, in
+//                    registers (N = 4/8/16/32)
 //   k_merge_long     wave-cooperative merge loop for chunks > 32 bytes
-//   k_scan_*         exclusive scan of per-tile id counts
-//   k_compact        sentinel-free ids, contiguous; string slot -> id offsets
+//   k_tile_count     ids per tile, then k_scan_* for the tile bases
+//   k_compact        slots -> contiguous ids; string chunk index -> id offset
 //   k_string_offsets final per-string offsets
 #include <hip/hip_runtime.h>
 
@@ -70,8 +72,7 @@ struct sw_encoder {
   // workspace
   int64_t cap_bytes = -1, cap_str = -1;
   int32_t* d_scratch = nullptr;
-  uint32_t* d_lw_id = nullptr;
-  uint32_t* d_lw_rk = nullptr;
+  uint32_t* d_res = nullptr;          // [2 * n_bytes] merge results, double-spaced position space
   int64_t* d_part = nullptr;
   int64_t* d_tile_slo = nullptr;
   uint32_t* d_tile_slots = nullptr;
@@ -80,8 +81,10 @@ struct sw_encoder {
   int64_t* d_boff = nullptr;          // its exclusive scan
   int64_t* d_qtotal = nullptr;
   unsigned long long* d_stamps = nullptr;  // SW_STAMPS builds
+  uint64_t* d_dtab = nullptr;         // chunk dedupe table
+  uint32_t dmask = 0;
+  bool dedupe = true;
   uint32_t* d_tile_cnt = nullptr;
-  int64_t* d_tile_first = nullptr;
   int64_t* d_tile_base = nullptr;
   int64_t* d_total = nullptr;
   // host-path staging
@@ -112,16 +115,16 @@ struct DeviceGuard {
 };
 
 void free_workspace(sw_encoder* h) {
-  (void)hipFree(h->d_scratch); (void)hipFree(h->d_lw_id); (void)hipFree(h->d_lw_rk); (void)hipFree(h->d_part);
+  (void)hipFree(h->d_scratch); (void)hipFree(h->d_res); (void)hipFree(h->d_part);
   (void)hipFree(h->d_tile_slo); (void)hipFree(h->d_stamps);
   (void)hipFree(h->d_tile_slots); (void)hipFree(h->d_queue); (void)hipFree(h->d_bcnt); (void)hipFree(h->d_boff);
   (void)hipFree(h->d_qtotal);
   h->d_tile_slo = nullptr; h->d_stamps = nullptr; h->d_tile_slots = nullptr; h->d_queue = nullptr;
   h->d_bcnt = nullptr; h->d_boff = nullptr; h->d_qtotal = nullptr;
-  (void)hipFree(h->d_tile_cnt); (void)hipFree(h->d_tile_first); (void)hipFree(h->d_tile_base);
+  (void)hipFree(h->d_dtab); (void)hipFree(h->d_tile_base); (void)hipFree(h->d_tile_cnt);
   (void)hipFree(h->d_total);
-  h->d_scratch = nullptr; h->d_lw_id = nullptr; h->d_lw_rk = nullptr; h->d_part = nullptr; h->d_tile_cnt = nullptr;
-  h->d_tile_first = nullptr; h->d_tile_base = nullptr; h->d_total = nullptr;
+  h->d_scratch = nullptr; h->d_res = nullptr; h->d_part = nullptr;
+  h->d_dtab = nullptr; h->d_tile_base = nullptr; h->d_tile_cnt = nullptr; h->d_total = nullptr;
   h->cap_bytes = -1; h->cap_str = -1;
 }
 
@@ -137,9 +140,8 @@ int32_t ensure_workspace(sw_encoder* h, int64_t n_bytes) {
   free_workspace(h);
   const int64_t nb = std::max<int64_t>(n_bytes, 1);
   const int64_t n_tiles = (nb + kTile - 1) / kTile;
-  HIP_TRY(hipMalloc(&h->d_scratch, sizeof(int32_t) * nb));
-  HIP_TRY(hipMalloc(&h->d_lw_id, sizeof(uint32_t) * nb));
-  HIP_TRY(hipMalloc(&h->d_lw_rk, sizeof(uint32_t) * nb));
+  HIP_TRY(hipMalloc(&h->d_scratch, sizeof(int32_t) * n_tiles * kTile));  // whole tiles: see k_compact
+  HIP_TRY(hipMalloc(&h->d_res, sizeof(uint32_t) * (2 * nb + 16)));  // (+ slack for k_compact's head reads)
   HIP_TRY(hipMalloc(&h->d_tile_slo, sizeof(int64_t) * n_tiles));
   HIP_TRY(hipMalloc(&h->d_tile_slots, sizeof(uint32_t) * n_tiles));
   // queued chunks have >= 2 bytes: at most nb / 2 of them
@@ -148,13 +150,18 @@ int32_t ensure_workspace(sw_encoder* h, int64_t n_bytes) {
   HIP_TRY(hipMalloc(&h->d_boff, sizeof(int64_t) * kNumBuckets * n_tiles));
   HIP_TRY(hipMalloc(&h->d_qtotal, sizeof(int64_t)));
   HIP_TRY(hipMalloc(&h->d_part, sizeof(int64_t) * ((kNumBuckets * n_tiles + kScanBlock - 1) / kScanBlock + 1)));
-  HIP_TRY(hipMalloc(&h->d_tile_cnt, sizeof(uint32_t) * n_tiles));
-  HIP_TRY(hipMalloc(&h->d_tile_first, sizeof(int64_t) * n_tiles));
+  {  // dedupe table: ~1 slot per 4 input bytes, at most 2^24 slots (128 MiB)
+    int64_t slots = 64;
+    while (slots < nb / 4 && slots < (1LL << 24)) slots <<= 1;
+    HIP_TRY(hipMalloc(&h->d_dtab, sizeof(uint64_t) * slots));
+    h->dmask = (uint32_t)(slots - 1);
+  }
   HIP_TRY(hipMalloc(&h->d_tile_base, sizeof(int64_t) * n_tiles));
+  HIP_TRY(hipMalloc(&h->d_tile_cnt, sizeof(uint32_t) * n_tiles));
   HIP_TRY(hipMalloc(&h->d_total, sizeof(int64_t)));
 #ifdef SW_STAMPS
-  HIP_TRY(hipMalloc(&h->d_stamps, sizeof(unsigned long long) * 32));
-  HIP_TRY(hipMemset(h->d_stamps, 0, sizeof(unsigned long long) * 32));
+  HIP_TRY(hipMalloc(&h->d_stamps, sizeof(unsigned long long) * 32 * 64));  // 64 copies per counter
+  HIP_TRY(hipMemset(h->d_stamps, 0, sizeof(unsigned long long) * 32 * 64));
 #endif
   h->cap_bytes = nb;
   return SW_OK;
@@ -324,6 +331,7 @@ extern "C" int32_t sw_encoder_set_option(sw_encoder* h, int32_t option, int64_t 
   if (!h) return fail(SW_ERR_ARG, "sw_encoder_set_option: null handle");
   switch (option) {
     case SW_OPT_CHUNK_TABLE: h->chunks.enabled = value ? 1u : 0u; return SW_OK;
+    case SW_OPT_DEDUPE: h->dedupe = value != 0; return SW_OK;
     default: return fail(SW_ERR_ARG, "sw_encoder_set_option: unknown option");
   }
 }
@@ -367,12 +375,16 @@ extern "C" int32_t sw_encoder_phase_cycles(sw_encoder* h, double* out32, int32_t
 #ifdef SW_STAMPS
   if (!h || !out32 || !h->d_stamps) return fail(SW_ERR_ARG, "sw_encoder_phase_cycles: no workspace");
   DeviceGuard g(h->device);
-  unsigned long long v[32];
+  std::vector<unsigned long long> v(32 * 64);
   HIP_TRY(hipStreamSynchronize(h->stream));
   HIP_TRY(hipDeviceSynchronize());
-  HIP_TRY(hipMemcpy(v, h->d_stamps, sizeof(v), hipMemcpyDeviceToHost));
-  for (int i = 0; i < 32; ++i) out32[i] = (double)v[i];
-  if (reset) HIP_TRY(hipMemset(h->d_stamps, 0, sizeof(v)));
+  HIP_TRY(hipMemcpy(v.data(), h->d_stamps, sizeof(unsigned long long) * v.size(), hipMemcpyDeviceToHost));
+  for (int i = 0; i < 32; ++i) {
+    double sum = 0;
+    for (int c = 0; c < 64; ++c) sum += (double)v[i * 64 + c];
+    out32[i] = sum;
+  }
+  if (reset) HIP_TRY(hipMemset(h->d_stamps, 0, sizeof(unsigned long long) * v.size()));
   return SW_OK;
 #else
   (void)h; (void)out32; (void)reset;
@@ -385,6 +397,7 @@ extern "C" int32_t sw_encode_device(sw_encoder* h, const uint8_t* d_bytes, int64
                                     int64_t* d_out_off, void* stream, int64_t* n_tokens_host) {
   if (!h || n_bytes < 0 || n_str < 0 || !d_str_off || !d_out_off || (n_bytes > 0 && (!d_bytes || !d_chunk_bits || !d_out_ids)))
     return fail(SW_ERR_ARG, "sw_encode_device: bad arguments");
+  if (n_bytes > kMaxLaunchBytes) return fail(SW_ERR_ARG, "sw_encode_device: n_bytes >= 2 GiB (split the batch)");
   DeviceGuard g(h->device);
   hipStream_t st = stream ? (hipStream_t)stream : h->stream;
   int32_t rc = ensure_workspace(h, n_bytes);
@@ -394,10 +407,11 @@ extern "C" int32_t sw_encode_device(sw_encoder* h, const uint8_t* d_bytes, int64
     EncArgs a;
     a.bytes = d_bytes; a.n_bytes = n_bytes; a.bits = d_chunk_bits; a.n_words = (n_bytes + 63) / 64;
     a.str_off = d_str_off; a.n_str = n_str; a.table = h->table; a.chunks = h->chunks;
-    a.scratch = h->d_scratch; a.lw_id = h->d_lw_id; a.lw_rk = h->d_lw_rk;
-    a.tile_cnt = h->d_tile_cnt; a.tile_slots = h->d_tile_slots; a.tile_first = h->d_tile_first;
+    a.scratch = h->d_scratch; a.res = h->d_res;
+    a.tile_slots = h->d_tile_slots; a.tile_cnt = h->d_tile_cnt;
+    a.dtab = h->d_dtab; a.dmask = h->dmask; a.dedupe = h->dedupe ? 1u : 0u;
     a.out_off = d_out_off; a.tile_slo = h->d_tile_slo;
-    a.n_tiles = n_tiles; a.qtmp = h->d_lw_id; a.bcnt = h->d_bcnt; a.boff = h->d_boff; a.q_total = h->d_qtotal;
+    a.n_tiles = n_tiles; a.qtmp = h->d_res; a.bcnt = h->d_bcnt; a.boff = h->d_boff; a.q_total = h->d_qtotal;
     a.queue = h->d_queue; a.stamps = h->d_stamps;
     hipLaunchKernelGGL(k_tile_strings, dim3((unsigned)((n_tiles + 255) / 256)), dim3(256), 0, st, d_str_off, n_str,
                        n_tiles, h->d_tile_slo);
@@ -416,6 +430,7 @@ extern "C" int32_t sw_encode_device(sw_encoder* h, const uint8_t* d_bytes, int64
     hipLaunchKernelGGL(k_classify, dim3((unsigned)n_tiles), dim3(kThreads), 0, st, a);
     HIP_TRY(hipGetLastError());
     HIP_TRY(launch_scan(st, h->d_bcnt, kNumBuckets * n_tiles, h->d_part, h->d_boff, h->d_qtotal));
+    if (h->dedupe) HIP_TRY(hipMemsetAsync(h->d_dtab, 0, sizeof(uint64_t) * ((size_t)h->dmask + 1), st));
     hipLaunchKernelGGL(k_scatter, dim3((unsigned)((n_tiles + 3) / 4)), dim3(kThreads), 0, st, a);
     const dim3 pg(2048), pb(kThreads);  // persistent grid for the queue kernels
     if (h->table.wide) {
@@ -442,8 +457,10 @@ extern "C" int32_t sw_encode_device(sw_encoder* h, const uint8_t* d_bytes, int64
       HIP_TRY(hipEventRecord(e1, st));
       ++h->ev_used;
     }
+    const dim3 wg((unsigned)((n_tiles + 3) / 4));  // one wave per tile
+    hipLaunchKernelGGL(k_tile_count, wg, dim3(kThreads), 0, st, a);
     HIP_TRY(launch_scan(st, h->d_tile_cnt, n_tiles, h->d_part, h->d_tile_base, h->d_total));
-    hipLaunchKernelGGL(k_compact, dim3((unsigned)n_tiles), dim3(kThreads), 0, st, a, h->d_tile_base, d_out_ids);
+    hipLaunchKernelGGL(k_compact, wg, dim3(kThreads), 0, st, a, h->d_tile_base, d_out_ids);
     HIP_TRY(hipGetLastError());
   } else {
     HIP_TRY(hipMemsetAsync(h->d_total, 0, sizeof(int64_t), st));
@@ -469,6 +486,43 @@ extern "C" int32_t sw_encode_batch(sw_encoder* h, const uint8_t* bytes, const in
   for (int64_t s = 0; s < n_str; ++s)
     if (str_off[s + 1] < str_off[s]) return fail(SW_ERR_ARG, "sw_encode_batch: string offsets not monotone");
   if (n_bytes > 0 && !out_ids) return fail(SW_ERR_ARG, "sw_encode_batch: null out_ids");
+  if (n_bytes > kMaxLaunchBytes) {
+    // one device launch addresses < 2 GiB: encode runs of whole strings separately
+    int64_t done = 0, s_lo = 0;
+    if (stats) *stats = sw_stats{};
+    while (s_lo < n_str) {
+      int64_t s_hi = s_lo + 1;
+      while (s_hi < n_str && str_off[s_hi + 1] - str_off[s_lo] <= kMaxLaunchBytes) ++s_hi;
+      if (str_off[s_hi] - str_off[s_lo] > kMaxLaunchBytes)
+        return fail(SW_ERR_ARG, "sw_encode_batch: a single string exceeds 2 GiB");
+      std::vector<uint64_t> sub;
+      if (chunk_bits) {  // the run's bits, realigned to its first byte
+        const int64_t g0 = str_off[s_lo] - b0, nb = str_off[s_hi] - str_off[s_lo];
+        sub.assign((size_t)((nb + 63) / 64 + 1), 0ULL);
+        for (int64_t w = 0; w < (nb + 63) / 64; ++w) {
+          const int64_t bit = g0 + 64 * w, q = bit >> 6, r = bit & 63;
+          uint64_t x = chunk_bits[q] >> r;
+          if (r && q + 1 <= (str_off[n_str] - b0 - 1) / 64) x |= chunk_bits[q + 1] << (64 - r);
+          sub[(size_t)w] = x;
+        }
+      }
+      sw_stats st{};
+      int32_t rc = sw_encode_batch(h, bytes, str_off + s_lo, s_hi - s_lo, pattern, chunk_bits ? sub.data() : nullptr,
+                                   out_ids + done, out_cap - done, out_off + s_lo, &st);
+      if (rc) return rc;
+      for (int64_t s = s_lo; s <= s_hi; ++s) out_off[s] += done;
+      done = out_off[s_hi];
+      if (stats) {
+        stats->n_bytes += st.n_bytes; stats->n_chunks += st.n_chunks; stats->n_tokens += st.n_tokens;
+        stats->ms_presplit += st.ms_presplit; stats->ms_h2d += st.ms_h2d; stats->ms_kernels += st.ms_kernels;
+        stats->ms_d2h += st.ms_d2h;
+      }
+      s_lo = s_hi;
+    }
+    if (stats)
+      stats->ms_total = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - T0).count();
+    return SW_OK;
+  }
   const int64_t n_words = (n_bytes + 63) / 64;
   std::vector<uint64_t> own_bits;
   double ms_pre = 0;

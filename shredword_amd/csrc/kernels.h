@@ -9,19 +9,18 @@
 //   k_classify      one 256-thread workgroup per 2 KiB tile.  Stages the tile's bytes and its
 //                   pre-split bitmap in LDS, enumerates the chunks, and settles every chunk that
 //                   is a single byte or whose bytes are in the whole-chunk table (chunktable.h)
-//                   with one lookup.  Every other chunk reserves `len` output slots (ids <=
-//                   bytes) holding a sentinel and is queued by length bucket.  Writes the tile's
-//                   slot region to a position-indexed scratch.
-//   k_merge_bucket  the exact merge loop, one chunk per lane, chunk in REGISTERS (fixed
-//                   positions + alive mask, compile-time size N); the 64 lanes of a wave come
-//                   from one length bucket so their loops have similar trip counts; persistent
-//                   grid-stride over the bucket's queue.  Writes ids into the reserved slots and
-//                   adds the count to its tile.
+//                   with one lookup.  Writes ONE slot per chunk (the token, or a reference to
+//                   the chunk's merge result) and queues the rest by length bucket (tile-local).
+//   k_scan_*, k_scatter  the tile-local queues -> one dense bucket-major queue
+//   k_merge_bucket  per queued chunk: batch-wide dedupe (repeats point their slot at the first
+//                   occurrence), then the exact merge loop, one chunk per lane, chunk in
+//                   REGISTERS (fixed positions + alive mask, compile-time size N); merge
+//                   results go to res at twice the chunk's start position.
 //   k_merge_long    chunks > 32 bytes: one wave each, wave-cooperative loop in a position-
 //                   indexed global work area.
-//   k_scan_*        exclusive scan of per-tile id counts
-//   k_compact       per tile: drop the sentinels (block stream compaction), write the ids
-//                   contiguously, and turn each string's slot offset into its id offset.
+//   k_tile_count, k_scan_*  ids per tile (one wave per tile) and their exclusive scan
+//   k_compact       one wave per tile: expand the slots into ids at the tile's base, turn each
+//                   string's chunk index into its id offset.
 #pragma once
 #include <hip/hip_runtime.h>
 
@@ -38,9 +37,15 @@ constexpr int kThreads = 256;                // 4 waves
 constexpr int kShort = 32;                   // per-lane merge loop up to this many bytes
 constexpr int kWin = kTile + 64;             // LDS byte window (tile + halo for key reads)
 constexpr int kTileWords = kTile / 64 + 1;   // bitmap words staged (tile + 64-bit halo)
-constexpr int32_t kSentinel = -1;            // reserved output slot not holding an id
 constexpr int kNumBuckets = 11;              // length buckets of the merge queue
 constexpr int kLongBucket = kNumBuckets - 1;
+constexpr int64_t kMaxLaunchBytes = (1LL << 31) - 64;  // slot references are int32 positions
+
+// A slot either holds a settled token (>= 0) or refers to the chunk starting at position p
+// whose merge result is res[2p + 1 .. 2p + 1 + res[2p]) (count, then the ids: one contiguous run,
+// and it fits, since a chunk of len bytes owns the 2 * len words from 2p).
+__host__ __device__ inline int32_t slot_ref(int64_t p) { return -(int32_t)(p + 2); }
+__host__ __device__ inline int64_t slot_pos(int32_t v) { return -(int64_t)v - 2; }
 
 // length -> bucket: groups of similar loop trip count
 //   [2] [3] [4] [5,6] [7,8] [9,10] [11,12] [13,16] [17,24] [25,32] long(>32)
@@ -360,20 +365,21 @@ struct EncArgs {
   int64_t n_str;
   DevTable table;
   DevChunkTable chunks;
-  int32_t* scratch;          // [n_bytes] slot regions, position space (tile t at tile_first[t])
-  uint32_t* lw_id;           // [n_bytes] long-chunk work area, position space
-  uint32_t* lw_rk;           // [n_bytes]
-  uint32_t* tile_cnt;        // [n_tiles] ids per tile (classify writes, merges add)
-  uint32_t* tile_slots;      // [n_tiles] slots per tile region
-  int64_t* tile_first;       // [n_tiles] first chunk start in tile (or -1)
-  int64_t* out_off;          // [n_str+1] string -> slot offset in its tile (k_compact converts)
+  int32_t* scratch;          // [n_bytes] one slot per chunk, tile t's at t * kTile (slot_ref)
+  uint32_t* res;             // [2 n_bytes] merge results (slot_ref); long chunks' work area
+  uint32_t* tile_cnt;        // [n_tiles] ids per tile (k_tile_count)
+  uint32_t* tile_slots;      // [n_tiles] chunks (= slots) per tile
+  int64_t* out_off;          // [n_str+1] string -> chunk index in its tile (k_compact converts)
   const int64_t* tile_slo;   // [n_tiles] first string starting at or after the tile start
   int64_t n_tiles;
-  uint32_t* qtmp;            // [n_bytes] tile-local queue entries, position space (aliases lw_id)
+  uint32_t* qtmp;            // [n_bytes] tile-local queue entries, position space (aliases res)
   uint32_t* bcnt;            // [kNumBuckets * n_tiles] queued chunks per (bucket, tile)
   const int64_t* boff;       // [kNumBuckets * n_tiles] exclusive scan of bcnt (bucket-major)
   const int64_t* q_total;    // queued chunks in all
   uint64_t* queue;           // dense merge queue, bucket-major: start << 24 | len << 18 | slot
+  uint64_t* dtab;            // chunk dedupe table (dedupe_claim), dmask + 1 slots
+  uint32_t dmask;
+  uint32_t dedupe;           // 0: every queued chunk runs its own merge loop
   unsigned long long* stamps;  // SW_STAMPS builds: cycles per phase, summed
 };
 
@@ -382,7 +388,7 @@ struct EncArgs {
   do {                                                                              \
     if (threadIdx.x == 0) {                                                         \
       const unsigned long long now_ = __builtin_readcyclecounter();                 \
-      atomicAdd(&a.stamps[k], now_ - stamp_prev_);                                  \
+      atomicAdd(&a.stamps[(k) * 64 + (blockIdx.x & 63)], now_ - stamp_prev_);       \
       stamp_prev_ = now_;                                                           \
     }                                                                               \
   } while (0)
@@ -400,12 +406,11 @@ __global__ void __launch_bounds__(kThreads) k_classify(EncArgs a) {
   __shared__ uint64_t s_bits[kTileWords];
   __shared__ uint16_t s_cstart[kTile + 1];
   __shared__ uint32_t s_val[kTile];           // settled token, or kInf (queued)
-  __shared__ uint32_t s_off[kTile + 1];       // slots per chunk, then exclusive slot offsets
+  __shared__ uint8_t s_len[kTile];            // chunk length if <= kShort, else 0
   __shared__ uint32_t s_wsum[kThreads / 64];
   __shared__ uint32_t s_bcnt[kNumBuckets];
   __shared__ uint32_t s_bbase[kNumBuckets];
   __shared__ int64_t s_last_end;
-  __shared__ uint32_t s_settled;
 
   SW_STAMP_INIT;
   const int tid = threadIdx.x;
@@ -426,7 +431,6 @@ __global__ void __launch_bounds__(kThreads) k_classify(EncArgs a) {
   if (tid < 8) s_b32[kWin / 4 + tid] = 0;
   if (tid < kTileWords) s_bits[tid] = (w0 + tid < a.n_words) ? a.bits[w0 + tid] : 0ULL;
   if (tid < kNumBuckets) s_bcnt[tid] = 0;
-  if (tid == 0) s_settled = 0;
   __syncthreads();
 
   // 2. chunk starts in [t0, t1): one thread per bitmap word
@@ -464,7 +468,7 @@ __global__ void __launch_bounds__(kThreads) k_classify(EncArgs a) {
   const int C = (int)nchunks;
   SW_STAMP(0);
 
-  // 3. settle single bytes and whole-chunk-table hits; the rest reserve len slots
+  // 3. settle single bytes and whole-chunk-table hits; the rest are queued
   for (int k = tid; k < C; k += kThreads) {
     const int ls = s_cstart[k];
     const int64_t end = (k + 1 < C) ? t0 + s_cstart[k + 1] : s_last_end;
@@ -478,33 +482,20 @@ __global__ void __launch_bounds__(kThreads) k_classify(EncArgs a) {
       tok = chunk_lookup(a.chunks, k0, k1, (uint32_t)len);
     }
     s_val[k] = tok;
-    s_off[k] = tok != kInf ? 1u : (uint32_t)min(len, (int64_t)0xFFFFFFFF);
+    s_len[k] = (uint8_t)(len <= kShort ? len : 0);  // 0 = long
     if (tok == kInf) atomicAdd(&s_bcnt[bucket_of(len)], 1u);
-    const uint64_t settled = __ballot(tok != kInf);
-    if ((tid & 63) == 0) atomicAdd(&s_settled, (uint32_t)__popcll(settled));
   }
   __syncthreads();
   SW_STAMP(1);
 
-  // 4. slot offsets (exclusive scan over chunk slot counts); queue space per bucket
-  const int per = (C + kThreads - 1) / kThreads;
-  const int c0 = min(C, tid * per), c1 = min(C, c0 + per);
-  uint32_t local = 0;
-  for (int k = c0; k < c1; ++k) local += s_off[k];
-  uint32_t n_slots;
-  uint32_t off = block_excl_scan(local, s_wsum, &n_slots);
-  for (int k = c0; k < c1; ++k) {
-    const uint32_t c = s_off[k];
-    s_off[k] = off;
-    off += c;
-  }
-  if (tid == 0) s_off[C] = n_slots;
-  if (tid == 0) {  // tile-local start of each bucket's entries
+  // 4. queue space per bucket (tile-local)
+  if (tid == 0) {
     uint32_t acc = 0;
     for (int b = 0; b < kNumBuckets; ++b) {
       s_bbase[b] = acc;
       acc += s_bcnt[b];
     }
+    a.tile_slots[tile] = (uint32_t)C;
   }
   __syncthreads();
   if (tid < kNumBuckets) {
@@ -512,28 +503,22 @@ __global__ void __launch_bounds__(kThreads) k_classify(EncArgs a) {
     s_bcnt[tid] = 0;
   }
   __syncthreads();
-  const int64_t first = C > 0 ? t0 + s_cstart[0] : -1;
-  if (tid == 0) {
-    a.tile_cnt[tile] = s_settled;
-    a.tile_slots[tile] = n_slots;
-    a.tile_first[tile] = first;
-  }
 
-  // 5. write the slot region; queue the unsettled chunks
-  int32_t* dst = a.scratch + first;
+  // 5. one slot per chunk (coalesced): the token, or a reference to the chunk's own merge
+  //    result; queue the unsettled chunks
+  int32_t* dst = a.scratch + t0;
   for (int k = tid; k < C; k += kThreads) {
-    const uint32_t o = s_off[k], ns = s_off[k + 1] - o;
     const uint32_t tok = s_val[k];
     if (tok != kInf) {
-      dst[o] = (int32_t)tok;
+      dst[k] = (int32_t)tok;
       continue;
     }
-    const int b = bucket_of(ns);
+    dst[k] = slot_ref(t0 + s_cstart[k]);
+    const int ns = s_len[k];
+    const int b = ns ? bucket_of(ns) : kLongBucket;
     const uint32_t qi = s_bbase[b] + atomicAdd(&s_bcnt[b], 1u);
-    // tile-local entry: chunk start in tile (11 bits) | slot offset (13) | length (6, 0 = long)
-    a.qtmp[t0 + qi] = (uint32_t)s_cstart[k] | (o << 11) | ((b != kLongBucket ? ns : 0u) << 24);
-    if (b != kLongBucket)
-      for (uint32_t j = 0; j < ns; ++j) dst[o + j] = kSentinel;  // k_merge_long writes all its own
+    // tile-local entry: chunk start in tile (11 bits) | chunk index (13) | length (6, 0 = long)
+    a.qtmp[t0 + qi] = (uint32_t)s_cstart[k] | ((uint32_t)k << 11) | ((uint32_t)ns << 24);
   }
   SW_STAMP(2);
 
@@ -547,7 +532,7 @@ __global__ void __launch_bounds__(kThreads) k_classify(EncArgs a) {
       const int m = (lo + hi) >> 1;
       if (s_cstart[m] < lp) lo = m + 1; else hi = m;
     }
-    a.out_off[s] = (int64_t)s_off[lo];
+    a.out_off[s] = (int64_t)lo;  // chunk (= slot) index; k_compact converts
   }
 #ifdef SW_STAMPS
   __syncthreads();
@@ -594,95 +579,163 @@ __device__ __forceinline__ void bucket_range(const EncArgs& a, int b_lo, int b_h
   *hi = (b_hi + 1 < kNumBuckets) ? a.boff[(int64_t)(b_hi + 1) * a.n_tiles] : *a.q_total;
 }
 
+// the chunk bytes [g, g + n) of the word-aligned input as N/4 zero-padded LE words
+template <int N>
+__device__ __forceinline__ void chunk_words(const uint32_t* words, int64_t last_word, int64_t g, int n,
+                                            uint32_t (&u)[N / 4]) {
+  constexpr int W = N / 4 + 1;  // aligned words covering any N-byte span
+  const int64_t w0 = g >> 2;
+  uint32_t w[W];
+#pragma unroll
+  for (int k = 0; k < W; ++k) w[k] = words[min(w0 + k, last_word)];
+  const uint32_t sh = (uint32_t)(g & 3);
+#pragma unroll
+  for (int q = 0; q < N / 4; ++q) {
+    const uint32_t x = __builtin_amdgcn_alignbyte(w[q + 1], w[q], sh);
+    const int keep = n - 4 * q;
+    u[q] = keep >= 4 ? x : keep <= 0 ? 0u : (x & ((1u << (8 * keep)) - 1u));
+  }
+}
+
 // ---------------------------------------------------------------------------------------
-// k_merge_bucket<N>: queued chunks of buckets [b_lo, b_hi] (length <= N), one per lane;
-// persistent grid-stride over 64-entry batches, next batch's entry prefetched
+// Batch-wide dedupe of queued chunks.  Real text repeats its multi-token words endlessly, and
+// a chunk's encoding depends on its bytes alone, so the merge loop needs to run once per
+// DISTINCT chunk of the batch.  The table (rebuilt every launch) maps a chunk's bytes to the
+// position of the first occurrence that claimed it; the slot packs a 27-bit fingerprint, the
+// length and that position.  A fingerprint match is confirmed by comparing the bytes, so a
+// hash collision can never change a result; a chunk that finds no free slot among its 8
+// candidates simply runs its own merge loop.  Returns the position whose result this chunk
+// shares, or -1 if this lane must merge the chunk itself.
+// ---------------------------------------------------------------------------------------
+#ifndef SW_DEDUPE_MIN_N
+#define SW_DEDUPE_MIN_N 8  // smallest bucket kernel that dedupes (2..4-byte chunks: not worth it)
+#endif
+template <int N>
+__device__ __forceinline__ int64_t dedupe_claim(const EncArgs& a, const uint32_t* words, int64_t last_word,
+                                                int64_t mis, int64_t start, int n, const uint32_t (&u)[N / 4]) {
+  uint64_t x = 0x9E3779B97F4A7C15ULL * (uint64_t)(n + 1);
+#pragma unroll
+  for (int q = 0; q < N / 4; q += 2) {
+    const uint64_t v = (uint64_t)u[q] | ((q + 1 < N / 4) ? ((uint64_t)u[q + 1] << 32) : 0ULL);
+    x = (x ^ v) * 0xBF58476D1CE4E5B9ULL;
+    x ^= x >> 31;
+  }
+  x *= 0x94D049BB133111EBULL;
+  const uint64_t tag = (x >> 37) << 37 | (uint64_t)n << 31;  // fingerprint | length
+  const uint64_t mine = tag | (uint64_t)start;
+  const uint32_t h = (uint32_t)(x >> 7);
+  const uint32_t grp = h & a.dmask & ~7u;
+  for (int j = 0; j < 8; ++j) {
+    uint64_t* p = a.dtab + (grp | ((h + j) & 7u));
+    // a slot changes once (0 -> final), so a cached plain load is safe: a stale 0 only sends
+    // this lane to the CAS, which returns the live value
+    uint64_t cur = *p;
+    if (cur == 0) {
+      cur = atomicCAS((unsigned long long*)p, 0ULL, (unsigned long long)mine);
+      if (cur == 0) return -1;  // claimed: this lane merges the chunk
+    }
+    if ((cur & ~0x7FFFFFFFULL) != tag) continue;
+    const int64_t other = (int64_t)(cur & 0x7FFFFFFFULL);
+    uint32_t o[N / 4];
+    chunk_words<N>(words, last_word, other + mis, n, o);
+    bool same = true;
+#pragma unroll
+    for (int q = 0; q < N / 4; ++q) same = same && (o[q] == u[q]);
+    if (same) return other;
+  }
+  return -1;
+}
+
+// merge loop for the queue entry e of this lane (act); result at res[2 * start ..)
+template <bool kWide, bool k16, int N>
+__device__ __forceinline__ void merge_entry(const EncArgs& a, const uint32_t* words, int64_t last_word, int64_t mis,
+                                            uint64_t e, bool act) {
+  const int64_t start = (int64_t)(e >> 24);
+  const int n = act ? (int)((e >> 18) & 63u) : 0;
+  uint32_t u[N / 4];
+  chunk_words<N>(words, last_word, start + mis, n, u);
+  uint32_t id[N];
+#pragma unroll
+  for (int q = 0; q < N / 4; ++q)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) id[4 * q + r] = (u[q] >> (8 * r)) & 0xFFu;
+#ifdef SW_ABL_NOLOOP  // ablation builds only: timing experiments, results are wrong
+  const uint32_t alive = (n >= 32) ? ~0u : ((1u << n) - 1u);
+#else
+  const uint32_t alive = lane_merge_reg<kWide, k16, N>(a.table, id, n);
+#endif
+  if (!act) return;
+  uint32_t* dst = a.res + 2 * start;
+  int m = 0;
+#pragma unroll
+  for (int k = 0; k < N; ++k) {
+    if ((alive >> k) & 1u) {
+#ifndef SW_ABL_NOWRITE
+      dst[1 + m] = id[k];
+#endif
+      ++m;
+    }
+  }
+  dst[0] = (uint32_t)m;
+}
+
+// ---------------------------------------------------------------------------------------
+// k_merge_bucket<N>: queued chunks of buckets [b_lo, b_hi] (length <= N).  Persistent
+// grid-stride over 64-entry batches of the bucket-major queue.  Each lane first dedupes its
+// chunk (a repeat points its slot at the first occurrence and is done); the chunks left to
+// merge collect in a per-wave LDS buffer and run the per-lane register merge loop 64 at a
+// time, so the loop always runs with a full wave however many repeats were dropped.
 // ---------------------------------------------------------------------------------------
 template <bool kWide, bool k16, int N>
 __global__ void __launch_bounds__(kThreads) k_merge_bucket(EncArgs a, int b_lo, int b_hi) {
+  __shared__ uint64_t s_own[kThreads / 64][128];
   SW_STAMP_INIT;
   const int64_t gw = ((int64_t)blockIdx.x * kThreads + threadIdx.x) >> 6;  // global wave id
   const int64_t n_waves = ((int64_t)gridDim.x * kThreads) >> 6;
   const int lane = threadIdx.x & 63;
+  const uint64_t lt_mask = (lane == 0) ? 0ULL : (~0ULL >> (64 - lane));
+  uint64_t* own = s_own[threadIdx.x >> 6];
   int64_t lo, hi;
   bucket_range(a, b_lo, b_hi, &lo, &hi);
-  constexpr int W = N / 4 + 1;  // aligned words covering any N-byte span
   const int64_t mis = (int64_t)((uintptr_t)a.bytes & 3);
   const uint32_t* words = (const uint32_t*)((uintptr_t)a.bytes - mis);
   const int64_t last_word = (mis + a.n_bytes - 1) >> 2;  // last word holding input bytes
+  int n_own = 0;  // wave-uniform
   int64_t i = lo + gw * 64 + lane;
   uint64_t e = i < hi ? a.queue[i] : 0;
-#ifdef SW_STAMPS
-  unsigned long long st_b = 0, st_loop = 0, st_batch = 0, st_it = 0;
-#endif
-  while (i < hi) {
-#ifdef SW_STAMPS
-    const unsigned long long batch_t0 = __builtin_readcyclecounter();
-#endif
+  for (int64_t base = lo + gw * 64; base < hi; base += n_waves * 64) {
     const int64_t inext = i + n_waves * 64;
     const uint64_t enext = inext < hi ? a.queue[inext] : 0;  // prefetch
-    const int64_t start = (int64_t)(e >> 24);
-    const int n = (int)((e >> 18) & 63u);
-    const uint32_t o = (uint32_t)(e & 0x3FFFFu);
-    // the chunk's bytes: W aligned words, realigned with v_alignbyte
-    const int64_t g = start + mis, w0 = g >> 2;
-    uint32_t w[W];
-#pragma unroll
-    for (int k = 0; k < W; ++k) w[k] = words[min(w0 + k, last_word)];
-    const uint32_t sh = (uint32_t)(g & 3);
-    uint32_t id[N];
-#pragma unroll
-    for (int q = 0; q < N / 4; ++q) {
-      const uint32_t u = __builtin_amdgcn_alignbyte(w[q + 1], w[q], sh);
-#pragma unroll
-      for (int r = 0; r < 4; ++r) id[4 * q + r] = (4 * q + r < n) ? ((u >> (8 * r)) & 0xFFu) : 0u;
-    }
-#ifdef SW_STAMPS
-    const unsigned long long c0 = __builtin_readcyclecounter();
-#endif
-#ifdef SW_ABL_NOLOOP  // ablation builds only: timing experiments, results are wrong
-    const uint32_t alive = (n >= 32) ? ~0u : ((1u << n) - 1u);
-#else
-    int iters = 0;
-    const uint32_t alive = lane_merge_reg<kWide, k16, N>(a.table, id, n, &iters);
-#endif
-#ifdef SW_STAMPS
-    {
-      const unsigned long long c1 = __builtin_readcyclecounter();
-      int mx = iters;
-#pragma unroll
-      for (int off = 32; off > 0; off >>= 1) { const int o2 = __shfl_xor(mx, off, 64); mx = o2 > mx ? o2 : mx; }
-      st_b += 1; st_loop += c1 - c0; st_batch += c1 - batch_t0; st_it += (unsigned long long)mx;
-    }
-#endif
-    const int64_t tile = start / kTile;
-    int32_t* dst = a.scratch + a.tile_first[tile] + o;
-    int m = 0;
-#pragma unroll
-    for (int k = 0; k < N; ++k) {
-      if ((alive >> k) & 1u) {
-#ifndef SW_ABL_NOWRITE
-        dst[m] = (int32_t)id[k];
-#endif
-        ++m;
+    bool merge_here = i < hi;
+    if (merge_here && a.dedupe && N >= SW_DEDUPE_MIN_N) {
+      const int64_t start = (int64_t)(e >> 24);
+      const int n = (int)((e >> 18) & 63u);
+      uint32_t u[N / 4];
+      chunk_words<N>(words, last_word, start + mis, n, u);
+      const int64_t other = dedupe_claim<N>(a, words, last_word, mis, start, n, u);
+      if (other >= 0) {
+        merge_here = false;
+        a.scratch[(start / kTile) * kTile + (int64_t)(e & 0x3FFFFu)] = slot_ref(other);
       }
     }
-#ifndef SW_ABL_NOATOMIC
-    atomicAdd(&a.tile_cnt[tile], (uint32_t)m);
-#else
-    if (m == 99999) a.tile_cnt[0] = 0;
-#endif
+    const uint64_t mm = __ballot(merge_here);
+    if (merge_here) own[n_own + __popcll(mm & lt_mask)] = e;
+    n_own += __popcll(mm);
+    if (n_own >= 64) {
+      wave_sync_mem();
+      const uint64_t oe = own[lane];
+      const uint64_t rest = (lane < n_own - 64) ? own[64 + lane] : 0;
+      wave_sync_mem();
+      if (lane < n_own - 64) own[lane] = rest;
+      n_own -= 64;
+      merge_entry<kWide, k16, N>(a, words, last_word, mis, oe, true);
+    }
     i = inext;
     e = enext;
   }
+  wave_sync_mem();
+  if (n_own > 0) merge_entry<kWide, k16, N>(a, words, last_word, mis, lane < n_own ? own[lane] : 0, lane < n_own);
 #ifdef SW_STAMPS
-  if (lane == 0 && st_b) {
-    const int gi = 8 + 4 * (N == 4 ? 0 : N == 8 ? 1 : N == 16 ? 2 : 3);
-    atomicAdd(&a.stamps[gi + 0], st_b);
-    atomicAdd(&a.stamps[gi + 1], st_loop);
-    atomicAdd(&a.stamps[gi + 2], st_batch);
-    atomicAdd(&a.stamps[gi + 3], st_it);
-  }
   SW_STAMP(N >= 16 ? 5 : 4);
 #endif
 }
@@ -701,15 +754,13 @@ __global__ void __launch_bounds__(kThreads) k_merge_long(EncArgs a) {
     const int64_t start = (int64_t)(e >> 24);
     const int64_t end = next_set_bit(a.bits, a.n_words, start + 1, a.n_bytes);
     const int64_t len = end - start;
-    uint32_t* gid = a.lw_id + start;
-    uint32_t* grk = a.lw_rk + start;
+    uint32_t* gid = a.res + 2 * start + 1;  // ids: len words, then ranks: len - 1 words
+    uint32_t* grk = gid + len;
     for (int64_t j = lane; j < len; j += 64) gid[j] = a.bytes[start + j];
     wave_sync_mem();
     const int64_t m = coop_merge<kWide>(a.table, gid, grk, len, lane);
-    const int64_t tile = start / kTile;
-    int32_t* dst = a.scratch + a.tile_first[tile] + (int64_t)(e & 0x3FFFFu);
-    for (int64_t j = lane; j < len; j += 64) dst[j] = j < m ? (int32_t)gid[j] : kSentinel;
-    if (lane == 0) atomicAdd(&a.tile_cnt[tile], (uint32_t)m);
+    if (lane == 0) gid[-1] = (uint32_t)m;  // (coop_merge ends wave-synchronised)
+    wave_sync_mem();
   }
 #ifdef SW_STAMPS
   SW_STAMP(6);
@@ -804,65 +855,109 @@ __global__ void __launch_bounds__(kThreads) k_scan_apply(const uint32_t* cnt, in
 }
 
 // ---------------------------------------------------------------------------------------
-// k_compact: per tile, drop sentinels from the slot region, write the ids at the tile's base,
-// and convert the tile's string slot offsets into id offsets (stored complemented: k_string_
-// offsets restores them).
+// k_tile_count / k_compact: one WAVE per tile (a tile has <= kTile chunks, ~380 on prose), the
+// tile's slots taken 64 at a time in order (slot 64r + lane in round r), so every slot load
+// is one 256-byte coalesced access and the ids of consecutive slots land at consecutive
+// output positions (near-coalesced stores without staging).  A reference costs one gather
+// from res (count + first 3 ids in one 16-byte load).
 // ---------------------------------------------------------------------------------------
-constexpr int kCompactPer = 8;                          // slots per thread per pass
-constexpr int kCompactPass = kThreads * kCompactPer;    // slots per pass
+__device__ __forceinline__ uint4 res_head(const uint32_t* res, int64_t p) {
+  // res + 2p is 8-byte aligned; a dword-aligned 16-byte global load is legal on CDNA
+  uint4 q;
+  __builtin_memcpy(&q, res + 2 * p, sizeof(q));
+  return q;
+}
+
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t x, int lane) {
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const uint32_t y = __shfl_up(x, off, 64);
+    if (lane >= off) x += y;
+  }
+  return x;
+}
+
+__global__ void __launch_bounds__(kThreads) k_tile_count(EncArgs a) {
+  const int64_t t = ((int64_t)blockIdx.x * kThreads + threadIdx.x) >> 6;
+  const int lane = threadIdx.x & 63;
+  if (t >= a.n_tiles) return;
+  const int C = (int)a.tile_slots[t];
+  const int32_t* src = a.scratch + t * kTile;
+  uint32_t c = 0;
+  for (int j = lane; j < C; j += 64) {
+    const int32_t v = src[j];
+#ifdef SW_ABL_NOGATHER
+    c += 1u;
+#else
+    c += v >= 0 ? 1u : a.res[2 * slot_pos(v)];
+#endif
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) c += __shfl_xor(c, off, 64);
+  if (lane == 0) a.tile_cnt[t] = c;
+}
 
 __global__ void __launch_bounds__(kThreads) k_compact(EncArgs a, const int64_t* tile_base, int32_t* out) {
-  __shared__ __attribute__((aligned(16))) int32_t s_io[kCompactPass];  // slots in, ids out
-  __shared__ uint32_t s_pref[kCompactPass + 1];  // ids before each slot of the pass
-  __shared__ uint32_t s_wsum[kThreads / 64];
-  const int64_t t = blockIdx.x;
-  const int tid = threadIdx.x;
-  const uint32_t n_slots = a.tile_slots[t];
-  const int64_t base = tile_base[t];
+  SW_STAMP_INIT;
+  const int64_t t = ((int64_t)blockIdx.x * kThreads + threadIdx.x) >> 6;
+  const int lane = threadIdx.x & 63;
+  if (t >= a.n_tiles) return;
+  const int C = (int)a.tile_slots[t];
+  const int32_t* src = a.scratch + t * kTile;
+  int32_t* dst = out + tile_base[t];
+  // strings starting in this tile: lane i holds string s_lo + i's chunk index (k_classify)
   const int64_t t1 = min(t * kTile + (int64_t)kTile, a.n_bytes);
-  const int32_t* src = a.scratch + a.tile_first[t];
   const int64_t s_lo = a.tile_slo[t];
-  uint32_t done = 0;  // ids written by earlier passes
-  for (uint32_t p0 = 0; p0 == 0 || p0 < n_slots; p0 += kCompactPass) {
-    // coalesced load of the pass's slots into LDS
-#pragma unroll
-    for (int k = 0; k < kCompactPer; ++k) {
-      const uint32_t j = p0 + k * kThreads + tid;
-      s_io[k * kThreads + tid] = j < n_slots ? src[j] : kSentinel;
+  const int64_t s_hi = (t + 1 < a.n_tiles) ? a.tile_slo[t + 1] : a.n_str;
+  const int64_t my_s = s_lo + lane;
+  const bool has_s = my_s < s_hi && a.str_off[my_s] < t1;
+  const int sj = has_s ? (int)a.out_off[my_s] : -1;
+  const bool many = s_hi - s_lo > 64;  // rare: slot offsets go through scratch instead
+  uint32_t s_off = 0, carry = 0;
+  const int rounds = (C + 63) >> 6;
+  for (int r = 0; r < rounds; ++r) {
+    const int j = (r << 6) + lane;
+    const bool valid = j < C;
+    const int32_t v = valid ? src[j] : 0;
+    const bool ref = valid && v < 0;
+    const int64_t p = ref ? slot_pos(v) : 0;
+#ifdef SW_ABL_NOGATHER
+    const uint4 q = make_uint4(ref ? 1u : 0u, (uint32_t)p, 0u, 0u);
+#else
+    const uint4 q = ref ? res_head(a.res, p) : make_uint4(0, 0, 0, 0);
+#endif
+    const uint32_t m = ref ? q.x : (valid ? 1u : 0u);
+    const uint32_t incl = wave_incl_scan(m, lane);
+    const uint32_t o = carry + incl - m;
+    carry += __shfl(incl, 63, 64);
+    if (valid && !ref) dst[o] = v;
+    if (ref) {
+      if (m > 0) dst[o] = (int32_t)q.y;
+      if (m > 1) dst[o + 1] = (int32_t)q.z;
+      if (m > 2) dst[o + 2] = (int32_t)q.w;
+      for (uint32_t k = 3; k < m; ++k) dst[o + k] = (int32_t)a.res[2 * p + 1 + k];
     }
-    __syncthreads();
-    int32_t v[kCompactPer];
-    uint32_t c = 0;
-#pragma unroll
-    for (int k = 0; k < kCompactPer; ++k) {
-      v[k] = s_io[tid * kCompactPer + k];
-      c += v[k] != kSentinel;
-    }
-    uint32_t pass_total;
-    uint32_t o = block_excl_scan(c, s_wsum, &pass_total);  // (its barriers also fence s_io reads)
-#pragma unroll
-    for (int k = 0; k < kCompactPer; ++k) {
-      s_pref[tid * kCompactPer + k] = done + o;
-      if (v[k] != kSentinel) s_io[o++] = v[k];
-    }
-    if (tid == 0) s_pref[kCompactPass] = done + pass_total;
-    __syncthreads();
-    // coalesced store of the pass's ids
-#pragma unroll
-    for (int k = 0; k < kCompactPer; ++k) {
-      const uint32_t j = k * kThreads + tid;
-      if (j < pass_total) out[base + done + j] = s_io[j];
-    }
-    // strings of this tile whose slot offset falls in this pass (or is the region's end)
-    for (int64_t s = s_lo + tid; s < a.n_str; s += kThreads) {
-      if (a.str_off[s] >= t1) break;
-      const int64_t so = a.out_off[s];
-      if (so < (int64_t)p0) continue;  // done in an earlier pass (complemented values are < 0)
-      if (so < (int64_t)p0 + kCompactPass || so == (int64_t)n_slots) a.out_off[s] = ~(base + s_pref[so - p0]);
-    }
-    done += pass_total;
-    __syncthreads();
+    const uint32_t got = (uint32_t)__shfl((int)o, sj & 63, 64);
+    if ((sj >> 6) == r) s_off = got;
+    if (many && valid) a.scratch[t * kTile + j] = (int32_t)o;  // (this wave's own slots)
   }
+  const int64_t base = tile_base[t];
+  if (has_s) a.out_off[my_s] = ~(base + (int64_t)(sj >= C ? carry : s_off));
+  if (many) {
+    wave_sync_mem();
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "agent");
+    for (int64_t s = s_lo + 64 + lane; s < s_hi; s += 64) {
+      if (a.str_off[s] >= t1) break;
+      const int jj = (int)a.out_off[s];
+      const uint32_t oo = jj >= C ? carry
+                                  : (uint32_t)__hip_atomic_load(&a.scratch[t * kTile + jj], __ATOMIC_RELAXED,
+                                                                __HIP_MEMORY_SCOPE_AGENT);
+      a.out_off[s] = ~(base + (int64_t)oo);
+    }
+  }
+#ifdef SW_STAMPS
+  SW_STAMP(11);
+#endif
 }
 
 // every string offset: a complemented value is one k_compact finished; strings starting at or

@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Diagnostic: per-phase cycles of k_encode_tiles from the SW_STAMPS build (GPU box).
+"""Diagnostic: per-phase cycles of the encode kernels from the SW_STAMPS build (GPU box).
 usage: SHREDWORD_HIP_LIB=shredword_amd/libshredword_hip_stamps.so python tools/phase_stamps.py [n_strings]"""
 import ctypes
 import os
@@ -29,15 +29,10 @@ for _ in range(reps):
     tok.encode_packed(buf, off, bits)
 _lib.check(L.sw_encoder_phase_cycles(tok._encoder(), out, 1))
 tiles = (len(buf) + 2047) // 2048
-names = ["classify: stage+enum", "classify: lookups", "classify: writes", "classify: strings",
-         "merge N<16 (blk)", "merge N>=16 (blk)", "merge long (blk)"]
-tot = sum(out[:7])
+names = {0: "classify: stage+enum", 1: "classify: lookups", 2: "classify: writes", 3: "classify: strings",
+         4: "merge N<16 (blk)", 5: "merge N>=16 (blk)", 6: "merge long (blk)",
+         8: "compact: slots+list", 9: "compact: gathers", 10: "compact: chained scan", 11: "compact: expand+strings"}
+tot = sum(out[i] for i in names)
 print("kind=%s bytes=%d chunks=%d tiles=%d kernel_ms=%.3f" % (model, len(buf), nch, tiles, tok.last_stats.ms_kernels))
-for i, nm in enumerate(names):
-    print("%-22s %12.0f cycles/tile-equiv  %5.1f%%" % (nm, out[i] / tiles / reps, 100 * out[i] / tot))
-for g, N in enumerate((4, 8, 16, 32)):
-    b = out[8 + 4 * g]
-    if b:
-        print("merge N=%-2d batches %8d  loop cycles/batch %8.0f  batch cycles %8.0f  wave-max iters %5.2f  cycles/iter %6.0f"
-              % (N, b / reps, out[9 + 4 * g] / b, out[10 + 4 * g] / b, out[11 + 4 * g] / b,
-                 out[9 + 4 * g] / max(1, out[11 + 4 * g])))
+for i, nm in names.items():
+    print("%-26s %12.0f cycles/tile-equiv  %5.1f%%" % (nm, out[i] / tiles / reps, 100 * out[i] / tot))

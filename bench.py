@@ -1,11 +1,12 @@
 #!/usr/bin/env python3
 """Batched BPE encode throughput on MI355X -- the BASELINE.json metric.
 
-One step = one pass of the encode hot path (merge loop + id compaction, k_encode_tiles ->
-k_scan_tiles -> k_compact -> k_string_offsets) over one batch already resident in HBM:
+One step = one pass of the encode hot path over one batch already resident in HBM: the whole
+sw_encode_device pipeline (k_tile_strings, k_classify, queue scan/scatter, k_merge_bucket x4,
+k_merge_long, k_tile_count + scan, k_compact, k_string_offsets):
   N=1  BASELINE configs[1]/[2]: 1 GiB synthetic MIXED UTF-8, 1M strings (mean 1074 B), 32k-merge
        byte-level table, cl100k pre-split on the host (the GPU pre-splitter is not built yet, so
-       this is reported as the C3 workload), GPU merge loop.
+       this is reported as the C3 workload), GPU merge loop + id compaction.
   N>1  configs[3]: every rank encodes its own 1 GiB corpus (seed + rank; doc-sharded), then the
        token-id buffers are reassembled on every rank with an RCCL all-gather (padded to the
        largest rank's count) -- weak scaling, the gather is inside the step.
@@ -145,12 +146,23 @@ def main():
     ms_step = sec / args.steps * 1e3
     value = all_bytes * args.steps / sec / 1e6
 
-    # roofline of the dominant kernel (k_encode_tiles), rank-local, per launch
+    # roofline of the encode pipeline (all sw_encode_device kernels, HIP events), rank-local, per launch
     b_algo = n_bytes + 4 * n_tok + 16 * (n_str + 1) + (n_bytes + 7) // 8
     achieved = b_algo / (k_ms * 1e-3) / 1e9 if k_ms > 0 else None
+    # traffic: HBM bytes per launch from the committed PMC profile of this same workload, if any
+    traffic, traffic_src = None, None
+    try:
+        with open(os.path.join(ROOT, "profiles", "traffic.json")) as f:
+            tj = json.load(f)
+        if (tj.get("n_bytes") == n_bytes and tj.get("merges") == len(tok.merges) and tj.get("pattern") == args.pattern
+                and tj.get("chunk_table") == (not args.no_chunk_table) and tj.get("dedupe") == (not args.no_dedupe)):
+            traffic, traffic_src = int(tj["traffic_bytes_per_launch"]), tj["source"]
+    except (OSError, ValueError, KeyError):
+        pass
     roofline = {"bound": "hbm", "achieved": round(achieved, 2) if achieved else None, "peak": HBM_PEAK_GBS,
                 "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5) if achieved else None,
-                "traffic": None, "kernel": "k_encode_tiles", "kernel_ms": round(k_ms, 4),
+                "traffic": traffic, "traffic_source": traffic_src, "kernel": "sw_encode_device pipeline (k_tile_strings..k_string_offsets)",
+                "kernel_ms": round(k_ms, 4),
                 "algo_bytes_per_launch": int(b_algo)}
 
     # parity spot-check + CPU baseline (rank 0, N=1 only): the oracle on a bounded prefix of the

@@ -133,10 +133,11 @@ int32_t sw_encode_device(sw_encoder* h, const uint8_t* d_bytes, int64_t n_bytes,
                          int64_t n_str, const uint64_t* d_chunk_bits, int32_t* d_out_ids, int64_t* d_out_off,
                          void* stream, int64_t* n_tokens_host);
 
-/* Timing of the encode proper -- k_classify plus the merge-loop kernels (k_merge_bucket x4,
- * k_merge_long), back to back on one stream -- with HIP events on that stream.  sw_encoder_set_timing(h, 1) starts a new accumulation window (one
- * event pair per launch, no host synchronisation per call); sw_encoder_last_kernel_ms returns the
- * average device time per launch over that window (it synchronises on the last event), or -1. */
+/* Device time of the whole sw_encode_device pipeline (every kernel from k_tile_strings to
+ * k_string_offsets, back to back on one stream), measured with a HIP event pair on that stream.
+ * sw_encoder_set_timing(h, 1) starts a new accumulation window (one event pair per launch, no
+ * host synchronisation per call); sw_encoder_last_kernel_ms returns the average device time per
+ * launch over that window (it synchronises on the last event), or -1. */
 int32_t sw_encoder_set_timing(sw_encoder* h, int32_t on);
 double sw_encoder_last_kernel_ms(const sw_encoder* h);
 

@@ -61,8 +61,9 @@ bool place(const std::vector<Entry>& es, bool is_long, std::vector<uint4>* out, 
       for (int kick = 0;; ++kick) {
         if (kick > 500) { ok = false; break; }
         const Entry& x = es[cur];
-        const uint32_t f = chunk_hash(x.k0, x.k1, x.len);
-        const uint32_t c1 = (f * *m1) >> *shift, c2 = ((f ^ 0xA5A5A5A5u) * *m2) >> *shift;
+        const uint32_t f = chunk_hash((uint32_t)x.k0, (uint32_t)(x.k0 >> 32), (uint32_t)x.k1, (uint32_t)(x.k1 >> 32),
+                                      x.len, *m1);
+        const uint32_t c1 = chunk_b1(f, *shift), c2 = chunk_b2(f, *m2, *shift);
         if (slot[c1] < 0) { slot[c1] = cur; break; }
         if (slot[c2] < 0) { slot[c2] = cur; break; }
         const uint32_t victim = (next() & 1) ? c1 : c2;

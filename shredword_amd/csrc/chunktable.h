@@ -24,17 +24,32 @@ namespace sw {
 struct DevChunkTable {
   const uint4* sb;  // short buckets
   const uint4* lb;  // long buckets (2 uint4 each)
-  uint32_t s_shift, s_m1, s_m2;
+  uint32_t s_shift, s_m1, s_m2;  // m1: hash seed, m2: second-candidate multiplier
   uint32_t l_shift, l_m1, l_m2;
   uint32_t enabled;
 };
 
-__host__ __device__ inline uint32_t chunk_hash(uint64_t k0, uint64_t k1, uint32_t len) {
-  uint64_t x = k0 * 0x9E3779B97F4A7C15ULL ^ (k1 + 0x632BE59BD9B4E019ULL) * 0xC2B2AE3D27D4EB4FULL ^ (uint64_t)len;
-  x ^= x >> 29;
-  x *= 0xBF58476D1CE4E5B9ULL;
-  x ^= x >> 32;
-  return (uint32_t)x;
+// 32-bit hash of a chunk key (its bytes as LE words w0..w3, zero padded): three 32-bit
+// multiplies for <= 8 bytes, five for 9..16.  `seed` is drawn per table build (m1 below).
+__host__ __device__ inline uint32_t chunk_hash(uint32_t w0, uint32_t w1, uint32_t w2, uint32_t w3, uint32_t len,
+                                               uint32_t seed) {
+  uint32_t h = seed ^ (len << 24);
+  h = (h ^ w0) * 0x85EBCA77u;
+  h ^= h >> 13;
+  h = (h ^ w1) * 0xC2B2AE3Du;
+  h ^= h >> 16;
+  if (len > 8) {
+    h = (h ^ w2) * 0x27D4EB2Fu;
+    h ^= h >> 13;
+    h = (h ^ w3) * 0x165667B1u;
+    h ^= h >> 16;
+  }
+  return h;
+}
+// the two cuckoo candidates of a hash (shift = 32 - log2(buckets); m2 odd, per build)
+__host__ __device__ inline uint32_t chunk_b1(uint32_t h, uint32_t shift) { return h >> shift; }
+__host__ __device__ inline uint32_t chunk_b2(uint32_t h, uint32_t m2, uint32_t shift) {
+  return ((h ^ (h >> 15)) * m2) >> shift;
 }
 
 struct ChunkTableHost {

@@ -354,8 +354,8 @@ extern "C" int32_t sw_encoder_set_timing(sw_encoder* h, int32_t on) {
   return SW_OK;
 }
 
-// Average device time of the encode proper (k_classify .. k_merge_long) over the launches recorded since the last
-// sw_encoder_set_timing(h, 1); synchronises on the last recorded event.
+// Average device time of the whole sw_encode_device pipeline (k_tile_strings .. k_string_offsets) over the
+// launches recorded since the last sw_encoder_set_timing(h, 1); synchronises on the last recorded event.
 extern "C" double sw_encoder_last_kernel_ms(const sw_encoder* h) {
   if (!h || h->ev_used == 0) return -1.0;
   DeviceGuard g(h->device);
@@ -403,6 +403,16 @@ extern "C" int32_t sw_encode_device(sw_encoder* h, const uint8_t* d_bytes, int64
   int32_t rc = ensure_workspace(h, n_bytes);
   if (rc) return rc;
   const int64_t n_tiles = (n_bytes + kTile - 1) / kTile;
+  hipEvent_t e1 = nullptr;
+  if (h->timing) {  // the whole device pipeline, k_tile_strings .. k_string_offsets
+    while (h->ev_pool.size() < 2 * (h->ev_used + 1)) {
+      hipEvent_t ev;
+      HIP_TRY(hipEventCreate(&ev));
+      h->ev_pool.push_back(ev);
+    }
+    e1 = h->ev_pool[2 * h->ev_used + 1];
+    HIP_TRY(hipEventRecord(h->ev_pool[2 * h->ev_used], st));
+  }
   if (n_tiles > 0) {
     EncArgs a;
     a.bytes = d_bytes; a.n_bytes = n_bytes; a.bits = d_chunk_bits; a.n_words = (n_bytes + 63) / 64;
@@ -415,19 +425,7 @@ extern "C" int32_t sw_encode_device(sw_encoder* h, const uint8_t* d_bytes, int64
     a.queue = h->d_queue; a.stamps = h->d_stamps;
     hipLaunchKernelGGL(k_tile_strings, dim3((unsigned)((n_tiles + 255) / 256)), dim3(256), 0, st, d_str_off, n_str,
                        n_tiles, h->d_tile_slo);
-    hipEvent_t e0 = nullptr, e1 = nullptr;
-    if (h->timing) {
-      while (h->ev_pool.size() < 2 * (h->ev_used + 1)) {
-        hipEvent_t ev;
-        HIP_TRY(hipEventCreate(&ev));
-        h->ev_pool.push_back(ev);
-      }
-      e0 = h->ev_pool[2 * h->ev_used];
-      e1 = h->ev_pool[2 * h->ev_used + 1];
-      HIP_TRY(hipEventRecord(e0, st));
-    }
-    // the encode proper: classify, then the bucketed merge loops (timed together)
-    hipLaunchKernelGGL(k_classify, dim3((unsigned)n_tiles), dim3(kThreads), 0, st, a);
+    hipLaunchKernelGGL(k_classify, dim3((unsigned)((n_tiles + kWaves - 1) / kWaves)), dim3(kThreads), 0, st, a);
     HIP_TRY(hipGetLastError());
     HIP_TRY(launch_scan(st, h->d_bcnt, kNumBuckets * n_tiles, h->d_part, h->d_boff, h->d_qtotal));
     if (h->dedupe) HIP_TRY(hipMemsetAsync(h->d_dtab, 0, sizeof(uint64_t) * ((size_t)h->dmask + 1), st));
@@ -453,10 +451,6 @@ extern "C" int32_t sw_encode_device(sw_encoder* h, const uint8_t* d_bytes, int64
       hipLaunchKernelGGL((k_merge_long<false>), dim3(512), pb, 0, st, a);
     }
     HIP_TRY(hipGetLastError());
-    if (h->timing) {
-      HIP_TRY(hipEventRecord(e1, st));
-      ++h->ev_used;
-    }
     const dim3 wg((unsigned)((n_tiles + 3) / 4));  // one wave per tile
     hipLaunchKernelGGL(k_tile_count, wg, dim3(kThreads), 0, st, a);
     HIP_TRY(launch_scan(st, h->d_tile_cnt, n_tiles, h->d_part, h->d_tile_base, h->d_total));
@@ -468,6 +462,10 @@ extern "C" int32_t sw_encode_device(sw_encoder* h, const uint8_t* d_bytes, int64
   hipLaunchKernelGGL(k_string_offsets, dim3((unsigned)((n_str + 1 + 255) / 256)), dim3(256), 0, st, d_str_off, n_str,
                      n_bytes, h->d_total, d_out_off);
   HIP_TRY(hipGetLastError());
+  if (h->timing) {
+    HIP_TRY(hipEventRecord(e1, st));
+    ++h->ev_used;
+  }
   if (n_tokens_host) {
     HIP_TRY(hipMemcpyAsync(n_tokens_host, h->d_total, sizeof(int64_t), hipMemcpyDeviceToHost, st));
     HIP_TRY(hipStreamSynchronize(st));

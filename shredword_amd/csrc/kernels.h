@@ -6,8 +6,8 @@
 // left to right, by the value.
 //
 // Pipeline (one stream):
-//   k_classify      one 256-thread workgroup per 2 KiB tile.  Stages the tile's bytes and its
-//                   pre-split bitmap in LDS, enumerates the chunks, and settles every chunk that
+//   k_classify      one wave per 2 KiB tile.  Stages the tile's bytes in LDS and its
+//                   pre-split bitmap in registers, enumerates the chunks, and settles every chunk that
 //                   is a single byte or whose bytes are in the whole-chunk table (chunktable.h)
 //                   with one lookup.  Writes ONE slot per chunk (the token, or a reference to
 //                   the chunk's merge result) and queues the rest by length bucket (tile-local).
@@ -32,7 +32,11 @@
 
 namespace sw {
 
-constexpr int kTile = 2048;                  // input bytes per classify workgroup
+#ifndef SW_TILE_BITS
+#define SW_TILE_BITS 11
+#endif
+constexpr int kTileBits = SW_TILE_BITS;
+constexpr int kTile = 1 << kTileBits;        // input bytes per classify workgroup
 constexpr int kThreads = 256;                // 4 waves
 constexpr int kShort = 32;                   // per-lane merge loop up to this many bytes
 constexpr int kWin = kTile + 64;             // LDS byte window (tile + halo for key reads)
@@ -86,42 +90,41 @@ __device__ __forceinline__ uint32_t lookup(const DevTable& t, uint32_t a, uint32
 }
 
 // Whole-chunk table lookup (chunktable.h): the single token a 2..16-byte chunk encodes to, or
-// kInf if the chunk does not encode to exactly one token.  k0/k1: the chunk's bytes, LE, zero
-// padded.  Two (short) or four (long) independent 16-byte loads, one round trip.
-__device__ __forceinline__ uint32_t chunk_lookup(const DevChunkTable& c, uint64_t k0, uint64_t k1, uint32_t len) {
-  const uint32_t f = chunk_hash(k0, k1, len);
-  if (len <= 8) {
-    const uint4 q1 = c.sb[(f * c.s_m1) >> c.s_shift];
-    const uint4 q2 = c.sb[((f ^ 0xA5A5A5A5u) * c.s_m2) >> c.s_shift];
-    const uint32_t lo = (uint32_t)k0, hi = (uint32_t)(k0 >> 32);
-    uint32_t v = kInf;
-    v = (q1.x == lo && q1.y == hi && (q1.z >> 24) == len) ? (q1.z & 0xFFFFFFu) : v;
-    v = (q2.x == lo && q2.y == hi && (q2.z >> 24) == len) ? (q2.z & 0xFFFFFFu) : v;
-    return v;
-  }
-  const uint32_t b1 = (f * c.l_m1) >> c.l_shift, b2 = ((f ^ 0xA5A5A5A5u) * c.l_m2) >> c.l_shift;
-  const uint4 a1 = c.lb[2 * b1], t1 = c.lb[2 * b1 + 1];
-  const uint4 a2 = c.lb[2 * b2], t2 = c.lb[2 * b2 + 1];
-  const uint4 k = make_uint4((uint32_t)k0, (uint32_t)(k0 >> 32), (uint32_t)k1, (uint32_t)(k1 >> 32));
+// kInf if the chunk does not encode to exactly one token.  w: the chunk's bytes as LE words,
+// zero padded.  Two (<= 8 bytes) or four (9..16) independent 16-byte loads, one round trip.
+__device__ __forceinline__ uint32_t chunk_lookup(const DevChunkTable& c, const uint32_t (&w)[4], uint32_t len) {
   uint32_t v = kInf;
-  v = (a1.x == k.x && a1.y == k.y && a1.z == k.z && a1.w == k.w && (t1.x >> 24) == len) ? (t1.x & 0xFFFFFFu) : v;
-  v = (a2.x == k.x && a2.y == k.y && a2.z == k.z && a2.w == k.w && (t2.x >> 24) == len) ? (t2.x & 0xFFFFFFu) : v;
+  if (len <= 8) {
+    const uint32_t f = chunk_hash(w[0], w[1], 0, 0, len, c.s_m1);
+    const uint4 q1 = c.sb[chunk_b1(f, c.s_shift)];
+    const uint4 q2 = c.sb[chunk_b2(f, c.s_m2, c.s_shift)];
+    v = (q1.x == w[0] && q1.y == w[1] && (q1.z >> 24) == len) ? (q1.z & 0xFFFFFFu) : v;
+    v = (q2.x == w[0] && q2.y == w[1] && (q2.z >> 24) == len) ? (q2.z & 0xFFFFFFu) : v;
+  } else {
+    const uint32_t f = chunk_hash(w[0], w[1], w[2], w[3], len, c.l_m1);
+    const uint32_t b1 = chunk_b1(f, c.l_shift), b2 = chunk_b2(f, c.l_m2, c.l_shift);
+    const uint4 a1 = c.lb[2 * b1], t1 = c.lb[2 * b1 + 1];
+    const uint4 a2 = c.lb[2 * b2], t2 = c.lb[2 * b2 + 1];
+    v = (a1.x == w[0] && a1.y == w[1] && a1.z == w[2] && a1.w == w[3] && (t1.x >> 24) == len) ? (t1.x & 0xFFFFFFu) : v;
+    v = (a2.x == w[0] && a2.y == w[1] && a2.z == w[2] && a2.w == w[3] && (t2.x >> 24) == len) ? (t2.x & 0xFFFFFFu) : v;
+  }
   return v;
 }
 
-// bytes [ls, ls + len) of an LDS byte window as two zero-padded little-endian words (len <= 16)
-__device__ __forceinline__ void window_key(const uint32_t* w32, int ls, int len, uint64_t* k0, uint64_t* k1) {
+// bytes [ls, ls + len) of an LDS byte window as four zero-padded little-endian words (len <= 16)
+__device__ __forceinline__ void window_words(const uint32_t* w32, int ls, int len, uint32_t (&b)[4]) {
   const int q = ls >> 2, sh = ls & 3;
   const uint32_t w0 = w32[q], w1 = w32[q + 1], w2 = w32[q + 2], w3 = w32[q + 3], w4 = w32[q + 4];
-  uint32_t b[4] = {__builtin_amdgcn_alignbyte(w1, w0, sh), __builtin_amdgcn_alignbyte(w2, w1, sh),
-                   __builtin_amdgcn_alignbyte(w3, w2, sh), __builtin_amdgcn_alignbyte(w4, w3, sh)};
+  b[0] = __builtin_amdgcn_alignbyte(w1, w0, sh);
+  b[1] = __builtin_amdgcn_alignbyte(w2, w1, sh);
+  b[2] = __builtin_amdgcn_alignbyte(w3, w2, sh);
+  b[3] = __builtin_amdgcn_alignbyte(w4, w3, sh);
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
-    const int keep = len - 4 * i;
-    b[i] = keep >= 4 ? b[i] : keep <= 0 ? 0u : (b[i] & ((1u << (8 * keep)) - 1u));
+    const int keep = len - 4 * i;  // bytes of word i inside the chunk
+    const uint32_t m = keep >= 4 ? ~0u : keep <= 0 ? 0u : ((1u << (8 * keep)) - 1u);
+    b[i] &= m;
   }
-  *k0 = ((uint64_t)b[1] << 32) | b[0];
-  *k1 = ((uint64_t)b[3] << 32) | b[2];
 }
 
 __device__ __forceinline__ uint64_t wave_min_u64(uint64_t v) {
@@ -398,132 +401,176 @@ struct EncArgs {
 #define SW_STAMP_INIT do {} while (0)
 #endif
 
-// ---------------------------------------------------------------------------------------
-// k_classify
-// ---------------------------------------------------------------------------------------
-__global__ void __launch_bounds__(kThreads) k_classify(EncArgs a) {
-  __shared__ uint32_t s_b32[kWin / 4 + 8];    // raw bytes of the window (+ zero tail)
-  __shared__ uint64_t s_bits[kTileWords];
-  __shared__ uint16_t s_cstart[kTile + 1];
-  __shared__ uint32_t s_val[kTile];           // settled token, or kInf (queued)
-  __shared__ uint8_t s_len[kTile];            // chunk length if <= kShort, else 0
-  __shared__ uint32_t s_wsum[kThreads / 64];
-  __shared__ uint32_t s_bcnt[kNumBuckets];
-  __shared__ uint32_t s_bbase[kNumBuckets];
-  __shared__ int64_t s_last_end;
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t x, int lane) {
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const uint32_t y = __shfl_up(x, off, 64);
+    if (lane >= off) x += y;
+  }
+  return x;
+}
 
+// ---------------------------------------------------------------------------------------
+// k_classify: one WAVE per 2 KiB tile (4 tiles per workgroup, no block barriers).  A prose
+// tile holds ~380 chunks, so chunks go 64 per round (chunk 64r + lane): coalesced slot stores,
+// and the per-bucket queue counts come from wave ballots (no atomics).  Two passes over the
+// rounds: (A) settle + slot + count, (B) queue entries at their bucket positions.
+static_assert(kTile <= 0x8000, "chunk starts keep a flag in bit 15");
+// ---------------------------------------------------------------------------------------
+constexpr int kWaves = kThreads / 64;
+constexpr int kWinWords = kWin / 4 + 8;
+
+__global__ void __launch_bounds__(kThreads) k_classify(EncArgs a) {
+  __shared__ uint32_t s_b32_all[kWaves][kWinWords];  // raw bytes of the window (+ zero tail)
+  __shared__ uint16_t s_cs_all[kWaves][kTile + 1];   // chunk starts (tile-relative; bit 15: queued)
   SW_STAMP_INIT;
-  const int tid = threadIdx.x;
-  const int64_t tile = blockIdx.x;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int64_t tile = (int64_t)blockIdx.x * kWaves + wv;
+  if (tile >= a.n_tiles) return;
+  uint32_t* s_b32 = s_b32_all[wv];
+  uint16_t* s_cstart = s_cs_all[wv];
+  const uint64_t lt_mask = (lane == 0) ? 0ULL : (~0ULL >> (64 - lane));
   const int64_t t0 = tile * kTile;
   const int64_t t1 = min(t0 + (int64_t)kTile, a.n_bytes);
   const int64_t w0 = t0 >> 6;
 
-  // 1. stage the window's bytes (4 per thread-load) and bitmap words
-  for (int i = tid * 4; i < kWin; i += kThreads * 4) {
-    const int64_t g = t0 + i;
-    uint32_t v = 0;
-    if (g + 4 <= a.n_bytes && ((uintptr_t)a.bytes & 3) == 0) v = *(const uint32_t*)(a.bytes + g);
-    else
-      for (int k = 0; k < 4; ++k) v |= (g + k < a.n_bytes ? (uint32_t)a.bytes[g + k] : 0u) << (8 * k);
-    s_b32[i >> 2] = v;
+  // 1. stage the window's bytes (256-byte coalesced loads) and the bitmap words (in registers)
+  const bool fast = ((uintptr_t)a.bytes & 3) == 0 && t0 + kWin <= a.n_bytes;
+#pragma unroll
+  for (int q = 0; q < (kWin / 4 + 63) / 64; ++q) {
+    const int i = lane + 64 * q;
+    if (i < kWin / 4) {
+      const int64_t g = t0 + 4 * (int64_t)i;
+      uint32_t v = 0;
+      if (fast) v = *(const uint32_t*)(a.bytes + g);
+      else
+        for (int k = 0; k < 4; ++k) v |= (g + k < a.n_bytes ? (uint32_t)a.bytes[g + k] : 0u) << (8 * k);
+      s_b32[i] = v;
+    }
   }
-  if (tid < 8) s_b32[kWin / 4 + tid] = 0;
-  if (tid < kTileWords) s_bits[tid] = (w0 + tid < a.n_words) ? a.bits[w0 + tid] : 0ULL;
-  if (tid < kNumBuckets) s_bcnt[tid] = 0;
-  __syncthreads();
+  if (lane < 8) s_b32[kWin / 4 + lane] = 0;
+  const uint64_t bw = (lane < kTileWords && w0 + lane < a.n_words) ? a.bits[w0 + lane] : 0ULL;
+  const int64_t s_first = a.tile_slo[tile];  // (prefetched: used by step 6)
 
-  // 2. chunk starts in [t0, t1): one thread per bitmap word
+  // 2. chunk starts in [t0, t1): lane w owns bitmap word w
   constexpr int nw_tile = kTile / 64;
   uint64_t myword = 0;
-  if (tid < nw_tile) {
-    myword = s_bits[tid];
-    const int64_t lim = t1 - (t0 + 64 * tid);  // bits at or beyond t1 belong to the next tile
+  if (lane < nw_tile) {
+    myword = bw;
+    const int64_t lim = t1 - (t0 + 64 * lane);  // bits at or beyond t1 belong to the next tile
     if (lim <= 0) myword = 0;
     else if (lim < 64) myword &= (1ULL << lim) - 1;
   }
-  uint32_t nchunks;
-  const uint32_t wbase = block_excl_scan((uint32_t)__popcll(myword), s_wsum, &nchunks);
-  if (tid < nw_tile) {
+  const uint32_t cnt = (uint32_t)__popcll(myword);
+  const uint32_t incl = wave_incl_scan(cnt, lane);
+  const int C = (int)__shfl(incl, 63, 64);
+  {
     uint64_t x = myword;
-    uint32_t k = wbase;
+    uint32_t k = incl - cnt;
     while (x) {
-      s_cstart[k++] = (uint16_t)(64 * tid + __ffsll((long long)x) - 1);
+      s_cstart[k++] = (uint16_t)(64 * lane + __ffsll((long long)x) - 1);
       x &= x - 1;
     }
   }
-  if (tid == 0 && nchunks > 0) {
-    // end of the last chunk: next chunk start at or after t1 (staged halo word first)
-    int64_t q = -1;
-    for (int w = (int)((t1 - t0) >> 6); w < kTileWords && q < 0; ++w) {
-      uint64_t word = s_bits[w];
-      const int64_t bit0 = t0 + 64 * w;
-      if (bit0 < t1) word &= ~0ULL << (t1 - bit0);
-      if (word) q = bit0 + __ffsll((long long)word) - 1;
+  // end of the last chunk, tile-relative: the first chunk start at or after t1 (staged halo
+  // word first; a launch is < 2^31 bytes, so tile-relative positions fit an int)
+  int64_t last_end = a.n_bytes;
+  {
+    uint64_t hw = 0;
+    const int64_t bit0 = t0 + 64 * (int64_t)lane;
+    if (lane < kTileWords && bit0 + 64 > t1) {
+      hw = bw;
+      if (bit0 < t1) hw &= ~0ULL << (t1 - bit0);
     }
-    if (q < 0) q = next_set_bit(a.bits, a.n_words, t0 + 64 * kTileWords, a.n_bytes);
-    s_last_end = min(q, a.n_bytes);
+    const uint64_t has = __ballot(hw != 0);
+    if (has) {
+      const int src = __ffsll((long long)has) - 1;
+      const int64_t q = t0 + 64 * (int64_t)src + __ffsll((long long)__shfl(hw, src, 64)) - 1;
+      last_end = min(q, a.n_bytes);
+    } else if (C > 0) {
+      last_end = min(next_set_bit(a.bits, a.n_words, t0 + 64 * kTileWords, a.n_bytes), a.n_bytes);
+    }
   }
-  __syncthreads();
-  const int C = (int)nchunks;
+  const int rel_end = (int)(last_end - t0);
+  wave_sync_mem();
   SW_STAMP(0);
 
-  // 3. settle single bytes and whole-chunk-table hits; the rest are queued
-  for (int k = tid; k < C; k += kThreads) {
-    const int ls = s_cstart[k];
-    const int64_t end = (k + 1 < C) ? t0 + s_cstart[k + 1] : s_last_end;
-    const int64_t len = end - (t0 + ls);
+  // 3. pass A: settle single bytes and whole-chunk-table hits, write every slot, count the
+  //    queued chunks per bucket (lane b holds bucket b's count).  A queued chunk's start
+  //    gets bit 15.
+  int32_t* dst = a.scratch + t0;
+  uint32_t bcount = 0;
+  const int rounds = (C + 63) >> 6;
+  const bool use_table = a.chunks.enabled != 0;
+  for (int r = 0; r < rounds; ++r) {
+    const int k = (r << 6) + lane;
+    const bool valid = k < C;
+    const int ls = valid ? s_cstart[k] : 0;
+    const int end = (k + 1 < C) ? (int)s_cstart[k + 1] : rel_end;
+    const int len = valid ? end - ls : 0;
     uint32_t tok = kInf;
     if (len == 1) {
       tok = (s_b32[ls >> 2] >> (8 * (ls & 3))) & 0xFFu;
-    } else if (len <= 16 && a.chunks.enabled) {
-      uint64_t k0, k1;
-      window_key(s_b32, ls, (int)len, &k0, &k1);
-      tok = chunk_lookup(a.chunks, k0, k1, (uint32_t)len);
+    } else if (len >= 2 && len <= 16 && use_table) {
+      uint32_t w[4];
+      window_words(s_b32, ls, len, w);
+      tok = chunk_lookup(a.chunks, w, (uint32_t)len);
     }
-    s_val[k] = tok;
-    s_len[k] = (uint8_t)(len <= kShort ? len : 0);  // 0 = long
-    if (tok == kInf) atomicAdd(&s_bcnt[bucket_of(len)], 1u);
+    const bool queued = valid && tok == kInf;
+    if (valid) {
+      dst[k] = queued ? slot_ref(t0 + ls) : (int32_t)tok;
+      if (queued) s_cstart[k] = (uint16_t)(ls | 0x8000);
+    }
+    const int b = queued ? bucket_of(len) : 15;
+    uint64_t pend = __ballot(queued);
+    while (pend) {  // one ballot per bucket present in this round
+      const int bb = __shfl(b, __ffsll((long long)pend) - 1, 64);
+      const uint64_t m = __ballot(b == bb);
+      if (lane == bb) bcount += (uint32_t)__popcll(m);
+      pend &= ~m;
+    }
   }
-  __syncthreads();
   SW_STAMP(1);
 
-  // 4. queue space per bucket (tile-local)
-  if (tid == 0) {
-    uint32_t acc = 0;
-    for (int b = 0; b < kNumBuckets; ++b) {
-      s_bbase[b] = acc;
-      acc += s_bcnt[b];
-    }
-    a.tile_slots[tile] = (uint32_t)C;
-  }
-  __syncthreads();
-  if (tid < kNumBuckets) {
-    a.bcnt[(int64_t)tid * a.n_tiles + tile] = s_bcnt[tid];
-    s_bcnt[tid] = 0;
-  }
-  __syncthreads();
+  // 4. tile-local bucket bases
+  const uint32_t binc = wave_incl_scan(lane < kNumBuckets ? bcount : 0u, lane);
+  uint32_t run = binc - bcount;  // lane b: next tile-local queue index of bucket b
+  if (lane < kNumBuckets) a.bcnt[(int64_t)lane * a.n_tiles + tile] = bcount;
+  if (lane == 0) a.tile_slots[tile] = (uint32_t)C;
+  wave_sync_mem();
 
-  // 5. one slot per chunk (coalesced): the token, or a reference to the chunk's own merge
-  //    result; queue the unsettled chunks
-  int32_t* dst = a.scratch + t0;
-  for (int k = tid; k < C; k += kThreads) {
-    const uint32_t tok = s_val[k];
-    if (tok != kInf) {
-      dst[k] = (int32_t)tok;
-      continue;
+  // 5. pass B: queue entries, in chunk order within each bucket; clears the queued bits
+  for (int r = 0; r < rounds; ++r) {
+    const int k = (r << 6) + lane;
+    const uint32_t cs = k < C ? s_cstart[k] : 0u;
+    const bool queued = (cs & 0x8000u) != 0;
+    const int ls = (int)(cs & 0x7FFFu);
+    const int end = (k + 1 < C) ? (int)(s_cstart[k + 1] & 0x7FFF) : rel_end;
+    const int len = end - ls;
+    const int ns = len <= kShort ? len : 0;
+    const int b = queued ? bucket_of(len) : 15;
+    uint32_t qi = 0;
+    uint64_t pend = __ballot(queued);
+    while (pend) {
+      const int bb = __shfl(b, __ffsll((long long)pend) - 1, 64);
+      const uint64_t m = __ballot(b == bb);
+      const uint32_t base = (uint32_t)__shfl((int)run, bb, 64);
+      if (b == bb) qi = base + (uint32_t)__popcll(m & lt_mask);
+      if (lane == bb) run += (uint32_t)__popcll(m);
+      pend &= ~m;
     }
-    dst[k] = slot_ref(t0 + s_cstart[k]);
-    const int ns = s_len[k];
-    const int b = ns ? bucket_of(ns) : kLongBucket;
-    const uint32_t qi = s_bbase[b] + atomicAdd(&s_bcnt[b], 1u);
-    // tile-local entry: chunk start in tile (11 bits) | chunk index (13) | length (6, 0 = long)
-    a.qtmp[t0 + qi] = (uint32_t)s_cstart[k] | ((uint32_t)k << 11) | ((uint32_t)ns << 24);
+    // tile-local entry: chunk start in tile (kTileBits) | chunk index (kTileBits) | length (6, 0 = long)
+    if (queued) a.qtmp[t0 + qi] = (uint32_t)ls | ((uint32_t)k << kTileBits) | ((uint32_t)ns << (2 * kTileBits));
   }
+  wave_sync_mem();
+  if (rounds > 0) {  // clear the queued bits for the string search (k and k + 1 were read above)
+    for (int k = lane; k < C; k += 64) s_cstart[k] &= 0x7FFF;
+  }
+  wave_sync_mem();
   SW_STAMP(2);
 
-  // 6. strings starting in this tile: slot offset within the tile (k_compact converts)
-  for (int64_t s = a.tile_slo[tile] + tid; s < a.n_str; s += kThreads) {
+  // 6. strings starting in this tile: chunk (= slot) index within the tile (k_compact converts)
+  for (int64_t s = s_first + lane; s < a.n_str; s += 64) {
     const int64_t p = a.str_off[s];
     if (p >= t1) break;
     int lo = 0, hi = C;  // first chunk with start >= p
@@ -532,12 +579,9 @@ __global__ void __launch_bounds__(kThreads) k_classify(EncArgs a) {
       const int m = (lo + hi) >> 1;
       if (s_cstart[m] < lp) lo = m + 1; else hi = m;
     }
-    a.out_off[s] = (int64_t)lo;  // chunk (= slot) index; k_compact converts
+    a.out_off[s] = (int64_t)lo;
   }
-#ifdef SW_STAMPS
-  __syncthreads();
   SW_STAMP(3);
-#endif
 }
 
 // ---------------------------------------------------------------------------------------
@@ -567,8 +611,8 @@ __global__ void __launch_bounds__(kThreads) k_scatter(EncArgs a) {
     const int64_t db = __shfl(dst, b, 64);
     for (uint32_t j = lane; j < cb; j += 64) {
       const uint32_t e = a.qtmp[t0 + lb + j];
-      const uint64_t start = (uint64_t)(t0 + (e & 0x7FFu));
-      a.queue[db + j] = (start << 24) | ((uint64_t)(e >> 24) << 18) | ((e >> 11) & 0x1FFFu);
+      const uint64_t start = (uint64_t)(t0 + (e & (kTile - 1)));
+      a.queue[db + j] = (start << 24) | ((uint64_t)(e >> (2 * kTileBits)) << 18) | ((e >> kTileBits) & (kTile - 1));
     }
   }
 }
@@ -866,15 +910,6 @@ __device__ __forceinline__ uint4 res_head(const uint32_t* res, int64_t p) {
   uint4 q;
   __builtin_memcpy(&q, res + 2 * p, sizeof(q));
   return q;
-}
-
-__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t x, int lane) {
-#pragma unroll
-  for (int off = 1; off < 64; off <<= 1) {
-    const uint32_t y = __shfl_up(x, off, 64);
-    if (lane >= off) x += y;
-  }
-  return x;
 }
 
 __global__ void __launch_bounds__(kThreads) k_tile_count(EncArgs a) {

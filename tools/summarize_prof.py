@@ -1,9 +1,13 @@
 #!/usr/bin/env python3
-"""Summarise a tools/profile_gpu.sh output directory into profiles/<tag>.md (+ copies of the
-rocprofv3 kernel-stats CSV).  HBM traffic per launch follows MI355X_MICROARCH.md §HBM:
-FETCH_SIZE / WRITE_SIZE are KB; FETCH_SIZE under-reports wide coalesced streaming reads by 2x on
-gfx950, so both the raw and the x2-corrected read figure are shown (the corrected one is an upper
-bound for this kernel, whose reads are not all wide streaming reads)."""
+"""Summarise a tools/profile_gpu.sh output directory into profiles/<tag>.md (+ the rocprofv3
+kernel-stats CSV and a JSON of the counters).
+
+The encode pipeline is one sw_encode_device call = several kernels; per-launch figures are the
+per-dispatch means times the dispatches per launch (launches = k_classify dispatches).  HBM
+traffic follows MI355X_MICROARCH.md §HBM: FETCH_SIZE / WRITE_SIZE are KB; FETCH_SIZE
+under-reports wide coalesced streaming reads by 2x on gfx950, so both the raw and the
+x2-corrected read figure are shown (the corrected one is an upper bound here, since much of
+this pipeline's traffic is not 16-B-per-lane streaming reads)."""
 import collections
 import csv
 import glob
@@ -12,20 +16,20 @@ import os
 import shutil
 import sys
 
-KERNEL = "k_encode_tiles"
-
 
 def pmc(dirpath):
-    vals = collections.defaultdict(list)
-    for f in sorted(glob.glob(os.path.join(dirpath, "pmc*", "run_counter_collection.csv"))):
-        per_dispatch = collections.defaultdict(lambda: collections.defaultdict(float))
+    """{kernel: {counter: mean per dispatch}}, {kernel: dispatches}"""
+    vals = collections.defaultdict(lambda: collections.defaultdict(list))
+    for f in sorted(glob.glob(os.path.join(dirpath, "pmc*", "**", "*counter_collection.csv"), recursive=True)):
+        per = collections.defaultdict(float)
+        names = {}
         for r in csv.DictReader(open(f)):
-            if KERNEL in r["Kernel_Name"]:
-                per_dispatch[r["Dispatch_Id"]][r["Counter_Name"]] += float(r["Counter_Value"])
-        for d in per_dispatch.values():
-            for c, v in d.items():
-                vals[c].append(v)
-    return {c: sum(v) / len(v) for c, v in vals.items()}
+            key = (r["Dispatch_Id"], r["Counter_Name"])
+            per[key] += float(r["Counter_Value"])
+            names[r["Dispatch_Id"]] = r["Kernel_Name"].split("(")[0].replace("void ", "")
+        for (d, c), v in per.items():
+            vals[names[d]][c].append(v)
+    return {k: {c: sum(v) / len(v) for c, v in cs.items()} for k, cs in vals.items()}
 
 
 def main():
@@ -36,34 +40,63 @@ def main():
     stats_csv = os.path.join(src, "trace", "run_kernel_stats.csv")
     shutil.copy(stats_csv, os.path.join(out, tag + "_kernel_stats.csv"))
     rows = list(csv.DictReader(open(stats_csv)))
-    c = pmc(src)
-    lines = ["# rocprofv3 summary: %s" % tag, "", "Command: `tools/profile_gpu.sh %s` (bench.py --steps 3 --warmup 1, "
-             "kernel trace + stats pass, then one pass per counter group)." % tag, "",
-             "| kernel | calls | avg ms | % |", "|---|---|---|---|"]
+    calls = {r["Name"].split("(")[0].replace("void ", ""): int(r["Calls"]) for r in rows}
+    launches = max(1, calls.get("sw::k_classify", 1))
+    per_launch_ms = sum(float(r["TotalDurationNs"]) for r in rows if r["Name"].startswith(("sw::", "void sw::")))
+    per_launch_ms = per_launch_ms / launches / 1e6
+    lines = ["# rocprofv3 summary: %s" % tag, "",
+             "Command: `tools/profile_gpu.sh %s` (bench.py --steps 3 --warmup 1 --no-cpu-baseline; kernel trace + "
+             "stats pass, then one rocprofv3 --pmc pass per counter group)." % tag, "",
+             "Encode launches traced: %d.  Sum of the pipeline's kernel time per launch: **%.3f ms**." %
+             (launches, per_launch_ms), "",
+             "| kernel | calls | avg ms | per launch ms | % |", "|---|---|---|---|---|"]
     for r in rows:
-        lines.append("| %s | %s | %.4f | %.2f |" % (r["Name"][:60], r["Calls"], float(r["AverageNs"]) / 1e6,
-                                                   float(r["Percentage"])))
-    lines += ["", "PMC, %s, mean per dispatch:" % KERNEL, "", "| counter | value |", "|---|---|"]
-    for k in sorted(c):
-        lines.append("| %s | %.4g |" % (k, c[k]))
-    derived = {}
-    if "FETCH_SIZE" in c and "WRITE_SIZE" in c:
-        derived["hbm_read_bytes_raw"] = c["FETCH_SIZE"] * 1024
-        derived["hbm_read_bytes_x2"] = c["FETCH_SIZE"] * 2048
-        derived["hbm_write_bytes"] = c["WRITE_SIZE"] * 1024
+        nm = r["Name"].split("(")[0].replace("void ", "")
+        lines.append("| %s | %s | %.4f | %.4f | %.2f |" % (
+            r["Name"][:64], r["Calls"], float(r["AverageNs"]) / 1e6,
+            float(r["TotalDurationNs"]) / launches / 1e6, float(r["Percentage"])))
+    c = pmc(src)
+    tot = collections.defaultdict(float)
+    if c:
+        cnames = sorted({n for k in c.values() for n in k})
+        lines += ["", "PMC, mean per dispatch:", "", "| kernel | " + " | ".join(cnames) + " |",
+                  "|---|" + "---|" * len(cnames)]
+        for k in sorted(c):
+            if not k.startswith("sw::"):
+                continue
+            lines.append("| %s | " % k[:48] + " | ".join("%.4g" % c[k].get(n, float("nan")) for n in cnames) + " |")
+            per = calls.get(k, launches) / launches
+            for n in cnames:
+                tot[n] += c[k].get(n, 0.0) * per
+    derived = {"pipeline_ms_per_launch": per_launch_ms}
+    if "FETCH_SIZE" in tot and "WRITE_SIZE" in tot:
+        derived["hbm_read_bytes_raw"] = tot["FETCH_SIZE"] * 1024
+        derived["hbm_read_bytes_x2"] = tot["FETCH_SIZE"] * 2048
+        derived["hbm_write_bytes"] = tot["WRITE_SIZE"] * 1024
         derived["traffic_bytes_per_launch"] = derived["hbm_read_bytes_raw"] + derived["hbm_write_bytes"]
-    if "TCC_HIT_sum" in c:
-        derived["l2_hit_rate"] = c["TCC_HIT_sum"] / max(1.0, c["TCC_HIT_sum"] + c.get("TCC_MISS_sum", 0))
-    if "SQ_WAIT_ANY" in c and "SQ_WAVE_CYCLES" in c:
-        derived["wave_wait_frac"] = c["SQ_WAIT_ANY"] / c["SQ_WAVE_CYCLES"]
-    kavg = [float(r["AverageNs"]) for r in rows if KERNEL in r["Name"]]
-    if "GRBM_GUI_ACTIVE" in c and kavg:
-        derived["effective_clock_ghz"] = c["GRBM_GUI_ACTIVE"] / 8 / kavg[0]
-    lines += ["", "Derived:", "", "```", json.dumps(derived, indent=1), "```"]
+        derived["traffic_bytes_per_launch_x2"] = derived["hbm_read_bytes_x2"] + derived["hbm_write_bytes"]
+    if tot.get("TCC_HIT_sum"):
+        derived["l2_hit_rate"] = tot["TCC_HIT_sum"] / max(1.0, tot["TCC_HIT_sum"] + tot.get("TCC_MISS_sum", 0))
+    lines += ["", "Pipeline totals per launch (sum over kernels x dispatches per launch):", "", "```",
+              json.dumps({k: v for k, v in tot.items()}, indent=1), json.dumps(derived, indent=1), "```"]
     with open(os.path.join(out, tag + ".md"), "w") as f:
         f.write("\n".join(lines) + "\n")
     with open(os.path.join(out, tag + "_pmc.json"), "w") as f:
-        json.dump({"kernel": KERNEL, "counters": c, "derived": derived}, f, indent=1)
+        json.dump({"per_kernel": c, "per_launch": tot, "derived": derived}, f, indent=1)
+    # bench.py quotes roofline.traffic from profiles/traffic.json when its workload matches
+    bench = None
+    for ln in open(os.path.join(src, "trace.log"), errors="replace"):
+        if ln.startswith("{") and '"metric"' in ln:
+            bench = json.loads(ln)
+    if bench and "traffic_bytes_per_launch" in derived:
+        with open(os.path.join(out, "traffic.json"), "w") as f:
+            json.dump({"source": "profiles/%s.md" % tag, "n_bytes": bench["config"]["bytes_per_rank"],
+                       "merges": bench["config"]["merges"], "pattern": bench["config"]["pattern"],
+                       "chunk_table": bench["config"].get("chunk_table"), "dedupe": bench["config"].get("dedupe"),
+                       "traffic_bytes_per_launch": derived["traffic_bytes_per_launch"],
+                       "traffic_bytes_per_launch_x2": derived["traffic_bytes_per_launch_x2"],
+                       "note": "FETCH_SIZE+WRITE_SIZE summed over the pipeline's kernels per launch (raw FETCH; "
+                               "_x2 doubles FETCH per the gfx950 wide-read correction)"}, f, indent=1)
     print("\n".join(lines))
 
 

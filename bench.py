@@ -41,7 +41,7 @@ def parse():
     ap.add_argument("--mean-len", type=int, default=None)
     ap.add_argument("--pattern", default="cl100k", choices=["cl100k", "gpt2"])
     ap.add_argument("--no-gather", action="store_true", help="N>1: skip the RCCL reassembly")
-    ap.add_argument("--cpu-sample-mb", type=float, default=96.0)
+    ap.add_argument("--cpu-sample-mb", type=float, default=320.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--threads", type=int, default=16, help="host threads for corpus/pre-split")
     ap.add_argument("--no-dedupe", action="store_true",
@@ -62,7 +62,7 @@ def main():
     import torch
     import torch.distributed as dist
 
-    from shredword_amd import Tokenizer, _lib, corpus
+    from shredword_amd import Tokenizer, _lib, corpus, shard
 
     if world > 1:
         dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", local))
@@ -109,17 +109,12 @@ def main():
     encode(ctypes.byref(n_tok_c))
     n_tok = int(n_tok_c.value)
     gather = world > 1 and not args.no_gather
-    if gather:
-        counts = torch.zeros(world, dtype=torch.int64, device=dev)
-        dist.all_gather_into_tensor(counts, torch.tensor([n_tok], dtype=torch.int64, device=dev))
-        max_cnt = int(counts.max().item())
-        gathered = torch.empty(world * max_cnt, dtype=torch.int32, device=dev)
-        disp = torch.cumsum(counts, 0) - counts
 
     def step():
         encode()
-        if gather:
-            dist.all_gather_into_tensor(gathered, d_out[:max_cnt])
+        if gather:  # shard.reassemble: counts, padded id buffers and string offsets, over RCCL
+            return shard.reassemble(d_out, d_oo, None, dev, concat=False)
+        return None
 
     for _ in range(args.warmup):
         step()

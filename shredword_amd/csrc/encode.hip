@@ -10,9 +10,10 @@
 // Device pipeline (all on one stream; inputs resident in HBM; kernels in kernels.h):
 //   k_tile_strings   first string of each tile
 //   k_classify       per 2 KiB tile: single bytes + whole-chunk-table hits settled, one slot
-//                    per chunk, the rest queued by length bucket
+//                    per chunk, repeats of a multi-token chunk deduped, the rest queued by
+//                    length bucket
 //   k_scan_*/k_scatter  dense bucket-major merge queue
-//   k_merge_bucket   batch-wide chunk dedupe + exact merge loop, one chunk per lane, in
+//   k_merge_bucket   exact merge loop of the distinct queued chunks, one chunk per lane, in
 //                    registers (N = 4/8/16/32)
 //   k_merge_long     wave-cooperative merge loop for chunks > 32 bytes
 //   k_tile_count     ids per tile, then k_scan_* for the tile bases
@@ -425,10 +426,10 @@ extern "C" int32_t sw_encode_device(sw_encoder* h, const uint8_t* d_bytes, int64
     a.queue = h->d_queue; a.stamps = h->d_stamps;
     hipLaunchKernelGGL(k_tile_strings, dim3((unsigned)((n_tiles + 255) / 256)), dim3(256), 0, st, d_str_off, n_str,
                        n_tiles, h->d_tile_slo);
+    if (h->dedupe) HIP_TRY(hipMemsetAsync(h->d_dtab, 0, sizeof(uint64_t) * ((size_t)h->dmask + 1), st));
     hipLaunchKernelGGL(k_classify, dim3((unsigned)((n_tiles + kWaves - 1) / kWaves)), dim3(kThreads), 0, st, a);
     HIP_TRY(hipGetLastError());
     HIP_TRY(launch_scan(st, h->d_bcnt, kNumBuckets * n_tiles, h->d_part, h->d_boff, h->d_qtotal));
-    if (h->dedupe) HIP_TRY(hipMemsetAsync(h->d_dtab, 0, sizeof(uint64_t) * ((size_t)h->dmask + 1), st));
     hipLaunchKernelGGL(k_scatter, dim3((unsigned)((n_tiles + 3) / 4)), dim3(kThreads), 0, st, a);
     const dim3 pg(2048), pb(kThreads);  // persistent grid for the queue kernels
     if (h->table.wide) {

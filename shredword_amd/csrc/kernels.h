@@ -12,10 +12,10 @@
 //                   with one lookup.  Writes ONE slot per chunk (the token, or a reference to
 //                   the chunk's merge result) and queues the rest by length bucket (tile-local).
 //   k_scan_*, k_scatter  the tile-local queues -> one dense bucket-major queue
-//   k_merge_bucket  per queued chunk: batch-wide dedupe (repeats point their slot at the first
-//                   occurrence), then the exact merge loop, one chunk per lane, chunk in
-//                   REGISTERS (fixed positions + alive mask, compile-time size N); merge
-//                   results go to res at twice the chunk's start position.
+//   k_merge_bucket  the exact merge loop, one chunk per lane, chunk in REGISTERS (fixed
+//                   positions + alive mask, compile-time size N); merge results go to res at
+//                   twice the chunk's start position.  Only distinct chunks get here: k_classify
+//                   dedupes repeats within the launch (dedupe_claim).
 //   k_merge_long    chunks > 32 bytes: one wave each, wave-cooperative loop in a position-
 //                   indexed global work area.
 //   k_tile_count, k_scan_*  ids per tile (one wave per tile) and their exclusive scan
@@ -411,6 +411,65 @@ __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t x, int lane) {
 }
 
 // ---------------------------------------------------------------------------------------
+// Batch-wide dedupe of queued chunks (in k_classify).  Real text repeats its multi-token words
+// endlessly, and a chunk's encoding depends on its bytes alone, so the merge loop needs to run
+// once per DISTINCT chunk of the launch.  The table (cleared before every launch) maps a
+// chunk's bytes to the position of the first occurrence that claimed it; a slot packs a
+// 27-bit fingerprint, the length and that position.  A fingerprint match is confirmed by
+// comparing the bytes with the claimant's bytes in the (immutable) input, so a hash collision
+// can never change a result, and nothing but the CAS needs cross-XCD coherence.  A chunk that
+// finds no free slot among its 8 candidates is merged on its own.  Returns the position whose
+// result this chunk shares, or -1 if this chunk must be merged (it claimed a slot or found
+// none).  u: the chunk's bytes as zero-padded LE words (n <= kShort).
+// ---------------------------------------------------------------------------------------
+__device__ __forceinline__ int64_t dedupe_claim(const EncArgs& a, const uint32_t* words, int64_t last_word, int64_t mis,
+                                                int64_t start, int n, const uint32_t (&u)[kShort / 4]) {
+  const int nw = (n + 3) >> 2;
+  uint32_t h = 0x9E3779B9u ^ ((uint32_t)n << 24);
+#pragma unroll
+  for (int q = 0; q < kShort / 4; ++q) {
+    if (q < nw) {
+      h = (h ^ u[q]) * 0x85EBCA77u;
+      h ^= h >> 13;
+    }
+  }
+  const uint32_t h2 = (h ^ (h >> 16)) * 0x7FEB352Du;
+  const uint64_t tag = (uint64_t)(h2 >> 5) << 37 | (uint64_t)n << 31;  // fingerprint | length
+  const uint64_t mine = tag | (uint64_t)start;
+  const uint32_t grp = h & a.dmask & ~7u;
+  for (int j = 0; j < 8; ++j) {
+    unsigned long long* p = (unsigned long long*)a.dtab + (grp | ((h2 + j) & 7u));
+    // a slot changes once (0 -> final), so a cached plain load is safe: a stale 0 only sends
+    // this lane to the CAS, which returns the live value
+    uint64_t cur = *p;
+    if (cur == 0) {
+      cur = atomicCAS(p, 0ULL, (unsigned long long)mine);
+      if (cur == 0) return -1;  // claimed: this chunk is merged and shared
+    }
+    if ((cur & ~0x7FFFFFFFULL) != tag) continue;
+    const int64_t other = (int64_t)(cur & 0x7FFFFFFFULL);
+    // compare with the claimant's bytes (aligned words of the input, realigned)
+    const int64_t g = other + mis, w0 = g >> 2;
+    const uint32_t sh = (uint32_t)(g & 3);
+    uint32_t prev = words[min(w0, last_word)];
+    bool same = true;
+#pragma unroll
+    for (int q = 0; q < kShort / 4; ++q) {
+      if (q < nw) {
+        const uint32_t next = words[min(w0 + q + 1, last_word)];
+        const int keep = n - 4 * q;
+        const uint32_t x = __builtin_amdgcn_alignbyte(next, prev, sh);
+        const uint32_t m = keep >= 4 ? ~0u : ((1u << (8 * keep)) - 1u);
+        same = same && ((x & m) == u[q]);
+        prev = next;
+      }
+    }
+    if (same) return other;
+  }
+  return -1;
+}
+
+// ---------------------------------------------------------------------------------------
 // k_classify: one WAVE per 2 KiB tile (4 tiles per workgroup, no block barriers).  A prose
 // tile holds ~380 chunks, so chunks go 64 per round (chunk 64r + lane): coalesced slot stores,
 // and the per-bucket queue counts come from wave ballots (no atomics).  Two passes over the
@@ -423,12 +482,14 @@ constexpr int kWinWords = kWin / 4 + 8;
 __global__ void __launch_bounds__(kThreads) k_classify(EncArgs a) {
   __shared__ uint32_t s_b32_all[kWaves][kWinWords];  // raw bytes of the window (+ zero tail)
   __shared__ uint16_t s_cs_all[kWaves][kTile + 1];   // chunk starts (tile-relative; bit 15: queued)
+  __shared__ uint16_t s_qb_all[kWaves][128];         // chunks not settled by pass A, to dedupe
   SW_STAMP_INIT;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int64_t tile = (int64_t)blockIdx.x * kWaves + wv;
   if (tile >= a.n_tiles) return;
   uint32_t* s_b32 = s_b32_all[wv];
   uint16_t* s_cstart = s_cs_all[wv];
+  uint16_t* s_qbuf = s_qb_all[wv];
   const uint64_t lt_mask = (lane == 0) ? 0ULL : (~0ULL >> (64 - lane));
   const int64_t t0 = tile * kTile;
   const int64_t t1 = min(t0 + (int64_t)kTile, a.n_bytes);
@@ -495,40 +556,73 @@ __global__ void __launch_bounds__(kThreads) k_classify(EncArgs a) {
   wave_sync_mem();
   SW_STAMP(0);
 
-  // 3. pass A: settle single bytes and whole-chunk-table hits, write every slot, count the
-  //    queued chunks per bucket (lane b holds bucket b's count).  A queued chunk's start
-  //    gets bit 15.
+  // 3. pass A: settle single bytes and whole-chunk-table hits (their slots written here).  The
+  //    rest collect in a small per-wave buffer and are deduped 64 at a time (full waves):
+  //    repeats point their slot at the first occurrence's result, the others are queued for
+  //    the merge kernels (bit 15 of their start) and counted per bucket (lane b: bucket b).
   int32_t* dst = a.scratch + t0;
-  uint32_t bcount = 0;
   const int rounds = (C + 63) >> 6;
   const bool use_table = a.chunks.enabled != 0;
-  for (int r = 0; r < rounds; ++r) {
-    const int k = (r << 6) + lane;
-    const bool valid = k < C;
-    const int ls = valid ? s_cstart[k] : 0;
-    const int end = (k + 1 < C) ? (int)s_cstart[k + 1] : rel_end;
-    const int len = valid ? end - ls : 0;
-    uint32_t tok = kInf;
-    if (len == 1) {
-      tok = (s_b32[ls >> 2] >> (8 * (ls & 3))) & 0xFFu;
-    } else if (len >= 2 && len <= 16 && use_table) {
-      uint32_t w[4];
-      window_words(s_b32, ls, len, w);
-      tok = chunk_lookup(a.chunks, w, (uint32_t)len);
+  const int64_t mis = (int64_t)((uintptr_t)a.bytes & 3);
+  const uint32_t* gwords = (const uint32_t*)((uintptr_t)a.bytes - mis);
+  const int64_t last_word = (mis + a.n_bytes - 1) >> 2;
+  uint32_t bcount = 0;
+  int nq = 0;  // wave-uniform: chunks waiting in s_qbuf
+  for (int r = 0; r <= rounds; ++r) {
+    if (r < rounds) {
+      const int k = (r << 6) + lane;
+      const bool valid = k < C;
+      const int ls = valid ? s_cstart[k] : 0;
+      const int end = (k + 1 < C) ? (int)s_cstart[k + 1] : rel_end;
+      const int len = valid ? end - ls : 0;
+      uint32_t tok = kInf;
+      if (len == 1) {
+        tok = (s_b32[ls >> 2] >> (8 * (ls & 3))) & 0xFFu;
+      } else if (len >= 2 && len <= 16 && use_table) {
+        uint32_t w[4];
+        window_words(s_b32, ls, len, w);
+        tok = chunk_lookup(a.chunks, w, (uint32_t)len);
+      }
+      const bool queued = valid && tok == kInf;
+      if (valid && !queued) dst[k] = (int32_t)tok;
+      const uint64_t mq = __ballot(queued);
+      if (queued) s_qbuf[nq + __popcll(mq & lt_mask)] = (uint16_t)k;
+      nq += __popcll(mq);
+      if (nq < 64) continue;
     }
-    const bool queued = valid && tok == kInf;
-    if (valid) {
-      dst[k] = queued ? slot_ref(t0 + ls) : (int32_t)tok;
-      if (queued) s_cstart[k] = (uint16_t)(ls | 0x8000);
+    if (nq == 0) break;
+    // dedupe one batch of up to 64 queued chunks
+    wave_sync_mem();
+    const bool act = lane < nq;
+    const int k = act ? s_qbuf[lane] : 0;
+    if (nq > 64 && lane < nq - 64) s_qbuf[lane] = s_qbuf[64 + lane];  // (read above, same lane)
+    nq = nq > 64 ? nq - 64 : 0;
+    const int ls = act ? (s_cstart[k] & 0x7FFF) : 0;  // (this batch may include k + 1: mask)
+    const int end = (k + 1 < C) ? (int)(s_cstart[k + 1] & 0x7FFF) : rel_end;
+    const int len = act ? end - ls : 0;
+    int64_t other = -1;
+    if (act && a.dedupe && len <= kShort) {
+      uint32_t u[kShort / 4];
+      window_words(s_b32, ls, min(len, 16), *(uint32_t(*)[4])u);
+      if (len > 16) window_words(s_b32, ls + 16, len - 16, *(uint32_t(*)[4])(u + 4));
+      else
+#pragma unroll
+        for (int q = 4; q < kShort / 4; ++q) u[q] = 0;
+      other = dedupe_claim(a, gwords, last_word, mis, t0 + ls, len, u);
     }
+    if (act) dst[k] = slot_ref(other >= 0 ? other : t0 + ls);
+    const bool queued = act && other < 0;
     const int b = queued ? bucket_of(len) : 15;
     uint64_t pend = __ballot(queued);
-    while (pend) {  // one ballot per bucket present in this round
+    while (pend) {  // one ballot per bucket present
       const int bb = __shfl(b, __ffsll((long long)pend) - 1, 64);
       const uint64_t m = __ballot(b == bb);
       if (lane == bb) bcount += (uint32_t)__popcll(m);
       pend &= ~m;
     }
+    if (queued) s_cstart[k] = (uint16_t)(ls | 0x8000);
+    wave_sync_mem();
+    if (r == rounds && nq > 0) --r;  // drain: another batch
   }
   SW_STAMP(1);
 
@@ -641,55 +735,6 @@ __device__ __forceinline__ void chunk_words(const uint32_t* words, int64_t last_
   }
 }
 
-// ---------------------------------------------------------------------------------------
-// Batch-wide dedupe of queued chunks.  Real text repeats its multi-token words endlessly, and
-// a chunk's encoding depends on its bytes alone, so the merge loop needs to run once per
-// DISTINCT chunk of the batch.  The table (rebuilt every launch) maps a chunk's bytes to the
-// position of the first occurrence that claimed it; the slot packs a 27-bit fingerprint, the
-// length and that position.  A fingerprint match is confirmed by comparing the bytes, so a
-// hash collision can never change a result; a chunk that finds no free slot among its 8
-// candidates simply runs its own merge loop.  Returns the position whose result this chunk
-// shares, or -1 if this lane must merge the chunk itself.
-// ---------------------------------------------------------------------------------------
-#ifndef SW_DEDUPE_MIN_N
-#define SW_DEDUPE_MIN_N 8  // smallest bucket kernel that dedupes (2..4-byte chunks: not worth it)
-#endif
-template <int N>
-__device__ __forceinline__ int64_t dedupe_claim(const EncArgs& a, const uint32_t* words, int64_t last_word,
-                                                int64_t mis, int64_t start, int n, const uint32_t (&u)[N / 4]) {
-  uint64_t x = 0x9E3779B97F4A7C15ULL * (uint64_t)(n + 1);
-#pragma unroll
-  for (int q = 0; q < N / 4; q += 2) {
-    const uint64_t v = (uint64_t)u[q] | ((q + 1 < N / 4) ? ((uint64_t)u[q + 1] << 32) : 0ULL);
-    x = (x ^ v) * 0xBF58476D1CE4E5B9ULL;
-    x ^= x >> 31;
-  }
-  x *= 0x94D049BB133111EBULL;
-  const uint64_t tag = (x >> 37) << 37 | (uint64_t)n << 31;  // fingerprint | length
-  const uint64_t mine = tag | (uint64_t)start;
-  const uint32_t h = (uint32_t)(x >> 7);
-  const uint32_t grp = h & a.dmask & ~7u;
-  for (int j = 0; j < 8; ++j) {
-    uint64_t* p = a.dtab + (grp | ((h + j) & 7u));
-    // a slot changes once (0 -> final), so a cached plain load is safe: a stale 0 only sends
-    // this lane to the CAS, which returns the live value
-    uint64_t cur = *p;
-    if (cur == 0) {
-      cur = atomicCAS((unsigned long long*)p, 0ULL, (unsigned long long)mine);
-      if (cur == 0) return -1;  // claimed: this lane merges the chunk
-    }
-    if ((cur & ~0x7FFFFFFFULL) != tag) continue;
-    const int64_t other = (int64_t)(cur & 0x7FFFFFFFULL);
-    uint32_t o[N / 4];
-    chunk_words<N>(words, last_word, other + mis, n, o);
-    bool same = true;
-#pragma unroll
-    for (int q = 0; q < N / 4; ++q) same = same && (o[q] == u[q]);
-    if (same) return other;
-  }
-  return -1;
-}
-
 // merge loop for the queue entry e of this lane (act); result at res[2 * start ..)
 template <bool kWide, bool k16, int N>
 __device__ __forceinline__ void merge_entry(const EncArgs& a, const uint32_t* words, int64_t last_word, int64_t mis,
@@ -724,61 +769,24 @@ __device__ __forceinline__ void merge_entry(const EncArgs& a, const uint32_t* wo
 }
 
 // ---------------------------------------------------------------------------------------
-// k_merge_bucket<N>: queued chunks of buckets [b_lo, b_hi] (length <= N).  Persistent
-// grid-stride over 64-entry batches of the bucket-major queue.  Each lane first dedupes its
-// chunk (a repeat points its slot at the first occurrence and is done); the chunks left to
-// merge collect in a per-wave LDS buffer and run the per-lane register merge loop 64 at a
-// time, so the loop always runs with a full wave however many repeats were dropped.
+// k_merge_bucket<N>: queued chunks of buckets [b_lo, b_hi] (length <= N), one per lane;
+// persistent grid-stride over 64-entry batches of the bucket-major queue
 // ---------------------------------------------------------------------------------------
 template <bool kWide, bool k16, int N>
 __global__ void __launch_bounds__(kThreads) k_merge_bucket(EncArgs a, int b_lo, int b_hi) {
-  __shared__ uint64_t s_own[kThreads / 64][128];
   SW_STAMP_INIT;
   const int64_t gw = ((int64_t)blockIdx.x * kThreads + threadIdx.x) >> 6;  // global wave id
   const int64_t n_waves = ((int64_t)gridDim.x * kThreads) >> 6;
   const int lane = threadIdx.x & 63;
-  const uint64_t lt_mask = (lane == 0) ? 0ULL : (~0ULL >> (64 - lane));
-  uint64_t* own = s_own[threadIdx.x >> 6];
   int64_t lo, hi;
   bucket_range(a, b_lo, b_hi, &lo, &hi);
   const int64_t mis = (int64_t)((uintptr_t)a.bytes & 3);
   const uint32_t* words = (const uint32_t*)((uintptr_t)a.bytes - mis);
   const int64_t last_word = (mis + a.n_bytes - 1) >> 2;  // last word holding input bytes
-  int n_own = 0;  // wave-uniform
-  int64_t i = lo + gw * 64 + lane;
-  uint64_t e = i < hi ? a.queue[i] : 0;
   for (int64_t base = lo + gw * 64; base < hi; base += n_waves * 64) {
-    const int64_t inext = i + n_waves * 64;
-    const uint64_t enext = inext < hi ? a.queue[inext] : 0;  // prefetch
-    bool merge_here = i < hi;
-    if (merge_here && a.dedupe && N >= SW_DEDUPE_MIN_N) {
-      const int64_t start = (int64_t)(e >> 24);
-      const int n = (int)((e >> 18) & 63u);
-      uint32_t u[N / 4];
-      chunk_words<N>(words, last_word, start + mis, n, u);
-      const int64_t other = dedupe_claim<N>(a, words, last_word, mis, start, n, u);
-      if (other >= 0) {
-        merge_here = false;
-        a.scratch[(start / kTile) * kTile + (int64_t)(e & 0x3FFFFu)] = slot_ref(other);
-      }
-    }
-    const uint64_t mm = __ballot(merge_here);
-    if (merge_here) own[n_own + __popcll(mm & lt_mask)] = e;
-    n_own += __popcll(mm);
-    if (n_own >= 64) {
-      wave_sync_mem();
-      const uint64_t oe = own[lane];
-      const uint64_t rest = (lane < n_own - 64) ? own[64 + lane] : 0;
-      wave_sync_mem();
-      if (lane < n_own - 64) own[lane] = rest;
-      n_own -= 64;
-      merge_entry<kWide, k16, N>(a, words, last_word, mis, oe, true);
-    }
-    i = inext;
-    e = enext;
+    const int64_t i = base + lane;
+    merge_entry<kWide, k16, N>(a, words, last_word, mis, i < hi ? a.queue[i] : 0, i < hi);
   }
-  wave_sync_mem();
-  if (n_own > 0) merge_entry<kWide, k16, N>(a, words, last_word, mis, lane < n_own ? own[lane] : 0, lane < n_own);
 #ifdef SW_STAMPS
   SW_STAMP(N >= 16 ? 5 : 4);
 #endif

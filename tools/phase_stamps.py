@@ -29,7 +29,8 @@ for _ in range(reps):
     tok.encode_packed(buf, off, bits)
 _lib.check(L.sw_encoder_phase_cycles(tok._encoder(), out, 1))
 tiles = (len(buf) + 2047) // 2048
-names = {0: "classify: stage+enum", 1: "classify: lookups", 2: "classify: writes", 3: "classify: strings",
+names = {0: "classify: stage+enum", 1: "classify: lookups+dedupe", 2: "classify: queue entries",
+         3: "classify: strings",
          4: "merge N<16 (blk)", 5: "merge N>=16 (blk)", 6: "merge long (blk)",
          8: "compact: slots+list", 9: "compact: gathers", 10: "compact: chained scan", 11: "compact: expand+strings"}
 tot = sum(out[i] for i in names)

@@ -51,6 +51,16 @@ constexpr int64_t kMaxLaunchBytes = (1LL << 31) - 64;  // slot references are in
 __host__ __device__ inline int32_t slot_ref(int64_t p) { return -(int32_t)(p + 2); }
 __host__ __device__ inline int64_t slot_pos(int32_t v) { return -(int64_t)v - 2; }
 
+// streaming accesses (read or written once per launch) carry the non-temporal hint, so the
+// caches keep the randomly gathered merge results instead
+#ifdef SW_NO_NT
+#define SW_LDNT(p) (*(p))
+#define SW_STNT(p, v) (*(p) = (v))
+#else
+#define SW_LDNT(p) __builtin_nontemporal_load(p)
+#define SW_STNT(p, v) __builtin_nontemporal_store((v), (p))
+#endif
+
 // length -> bucket: groups of similar loop trip count
 //   [2] [3] [4] [5,6] [7,8] [9,10] [11,12] [13,16] [17,24] [25,32] long(>32)
 __host__ __device__ inline int bucket_of(int64_t len) {
@@ -472,16 +482,15 @@ __device__ __forceinline__ int64_t dedupe_claim(const EncArgs& a, const uint32_t
 // ---------------------------------------------------------------------------------------
 // k_classify: one WAVE per 2 KiB tile (4 tiles per workgroup, no block barriers).  A prose
 // tile holds ~380 chunks, so chunks go 64 per round (chunk 64r + lane): coalesced slot stores,
-// and the per-bucket queue counts come from wave ballots (no atomics).  Two passes over the
-// rounds: (A) settle + slot + count, (B) queue entries at their bucket positions.
-static_assert(kTile <= 0x8000, "chunk starts keep a flag in bit 15");
+// and the per-bucket queue counts come from wave ballots (no atomics).
+static_assert(kTile <= 0x10000, "chunk starts are uint16");
 // ---------------------------------------------------------------------------------------
 constexpr int kWaves = kThreads / 64;
 constexpr int kWinWords = kWin / 4 + 8;
 
 __global__ void __launch_bounds__(kThreads) k_classify(EncArgs a) {
   __shared__ uint32_t s_b32_all[kWaves][kWinWords];  // raw bytes of the window (+ zero tail)
-  __shared__ uint16_t s_cs_all[kWaves][kTile + 1];   // chunk starts (tile-relative; bit 15: queued)
+  __shared__ uint16_t s_cs_all[kWaves][kTile + 1];   // chunk starts (tile-relative)
   __shared__ uint16_t s_qb_all[kWaves][128];         // chunks not settled by pass A, to dedupe
   SW_STAMP_INIT;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -503,7 +512,7 @@ __global__ void __launch_bounds__(kThreads) k_classify(EncArgs a) {
     if (i < kWin / 4) {
       const int64_t g = t0 + 4 * (int64_t)i;
       uint32_t v = 0;
-      if (fast) v = *(const uint32_t*)(a.bytes + g);
+      if (fast) v = SW_LDNT((const uint32_t*)(a.bytes + g));
       else
         for (int k = 0; k < 4; ++k) v |= (g + k < a.n_bytes ? (uint32_t)a.bytes[g + k] : 0u) << (8 * k);
       s_b32[i] = v;
@@ -556,10 +565,10 @@ __global__ void __launch_bounds__(kThreads) k_classify(EncArgs a) {
   wave_sync_mem();
   SW_STAMP(0);
 
-  // 3. pass A: settle single bytes and whole-chunk-table hits (their slots written here).  The
-  //    rest collect in a small per-wave buffer and are deduped 64 at a time (full waves):
-  //    repeats point their slot at the first occurrence's result, the others are queued for
-  //    the merge kernels (bit 15 of their start) and counted per bucket (lane b: bucket b).
+  // 3. settle single bytes and whole-chunk-table hits (their slots written here).  The rest
+  //    collect in a small per-wave buffer and are deduped 64 at a time (full waves): repeats
+  //    point their slot at the first occurrence's result, the others are queued for the merge
+  //    kernels and counted per length bucket (lane b: bucket b).
   int32_t* dst = a.scratch + t0;
   const int rounds = (C + 63) >> 6;
   const bool use_table = a.chunks.enabled != 0;
@@ -567,7 +576,8 @@ __global__ void __launch_bounds__(kThreads) k_classify(EncArgs a) {
   const uint32_t* gwords = (const uint32_t*)((uintptr_t)a.bytes - mis);
   const int64_t last_word = (mis + a.n_bytes - 1) >> 2;
   uint32_t bcount = 0;
-  int nq = 0;  // wave-uniform: chunks waiting in s_qbuf
+  int nq = 0;    // wave-uniform: chunks waiting in s_qbuf
+  int nown = 0;  // wave-uniform: chunks queued for the merge kernels
   for (int r = 0; r <= rounds; ++r) {
     if (r < rounds) {
       const int k = (r << 6) + lane;
@@ -584,7 +594,7 @@ __global__ void __launch_bounds__(kThreads) k_classify(EncArgs a) {
         tok = chunk_lookup(a.chunks, w, (uint32_t)len);
       }
       const bool queued = valid && tok == kInf;
-      if (valid && !queued) dst[k] = (int32_t)tok;
+      if (valid && !queued) SW_STNT(&dst[k], (int32_t)tok);
       const uint64_t mq = __ballot(queued);
       if (queued) s_qbuf[nq + __popcll(mq & lt_mask)] = (uint16_t)k;
       nq += __popcll(mq);
@@ -597,8 +607,8 @@ __global__ void __launch_bounds__(kThreads) k_classify(EncArgs a) {
     const int k = act ? s_qbuf[lane] : 0;
     if (nq > 64 && lane < nq - 64) s_qbuf[lane] = s_qbuf[64 + lane];  // (read above, same lane)
     nq = nq > 64 ? nq - 64 : 0;
-    const int ls = act ? (s_cstart[k] & 0x7FFF) : 0;  // (this batch may include k + 1: mask)
-    const int end = (k + 1 < C) ? (int)(s_cstart[k + 1] & 0x7FFF) : rel_end;
+    const int ls = act ? s_cstart[k] : 0;
+    const int end = (k + 1 < C) ? (int)s_cstart[k + 1] : rel_end;
     const int len = act ? end - ls : 0;
     int64_t other = -1;
     if (act && a.dedupe && len <= kShort) {
@@ -614,53 +624,26 @@ __global__ void __launch_bounds__(kThreads) k_classify(EncArgs a) {
     const bool queued = act && other < 0;
     const int b = queued ? bucket_of(len) : 15;
     uint64_t pend = __ballot(queued);
+    // tile-local queue entry (any order; k_scatter routes by length): chunk start in tile
+    // (kTileBits) | chunk index (kTileBits) | length (6 bits, 0 = long)
+    if (queued)
+      a.qtmp[t0 + nown + __popcll(pend & lt_mask)] =
+          (uint32_t)ls | ((uint32_t)k << kTileBits) | ((uint32_t)(len <= kShort ? len : 0) << (2 * kTileBits));
+    nown += __popcll(pend);
     while (pend) {  // one ballot per bucket present
       const int bb = __shfl(b, __ffsll((long long)pend) - 1, 64);
       const uint64_t m = __ballot(b == bb);
       if (lane == bb) bcount += (uint32_t)__popcll(m);
       pend &= ~m;
     }
-    if (queued) s_cstart[k] = (uint16_t)(ls | 0x8000);
     wave_sync_mem();
     if (r == rounds && nq > 0) --r;  // drain: another batch
   }
   SW_STAMP(1);
 
-  // 4. tile-local bucket bases
-  const uint32_t binc = wave_incl_scan(lane < kNumBuckets ? bcount : 0u, lane);
-  uint32_t run = binc - bcount;  // lane b: next tile-local queue index of bucket b
+  // 4. per-bucket counts of the queued chunks (k_scan -> k_scatter)
   if (lane < kNumBuckets) a.bcnt[(int64_t)lane * a.n_tiles + tile] = bcount;
   if (lane == 0) a.tile_slots[tile] = (uint32_t)C;
-  wave_sync_mem();
-
-  // 5. pass B: queue entries, in chunk order within each bucket; clears the queued bits
-  for (int r = 0; r < rounds; ++r) {
-    const int k = (r << 6) + lane;
-    const uint32_t cs = k < C ? s_cstart[k] : 0u;
-    const bool queued = (cs & 0x8000u) != 0;
-    const int ls = (int)(cs & 0x7FFFu);
-    const int end = (k + 1 < C) ? (int)(s_cstart[k + 1] & 0x7FFF) : rel_end;
-    const int len = end - ls;
-    const int ns = len <= kShort ? len : 0;
-    const int b = queued ? bucket_of(len) : 15;
-    uint32_t qi = 0;
-    uint64_t pend = __ballot(queued);
-    while (pend) {
-      const int bb = __shfl(b, __ffsll((long long)pend) - 1, 64);
-      const uint64_t m = __ballot(b == bb);
-      const uint32_t base = (uint32_t)__shfl((int)run, bb, 64);
-      if (b == bb) qi = base + (uint32_t)__popcll(m & lt_mask);
-      if (lane == bb) run += (uint32_t)__popcll(m);
-      pend &= ~m;
-    }
-    // tile-local entry: chunk start in tile (kTileBits) | chunk index (kTileBits) | length (6, 0 = long)
-    if (queued) a.qtmp[t0 + qi] = (uint32_t)ls | ((uint32_t)k << kTileBits) | ((uint32_t)ns << (2 * kTileBits));
-  }
-  wave_sync_mem();
-  if (rounds > 0) {  // clear the queued bits for the string search (k and k + 1 were read above)
-    for (int k = lane; k < C; k += 64) s_cstart[k] &= 0x7FFF;
-  }
-  wave_sync_mem();
   SW_STAMP(2);
 
   // 6. strings starting in this tile: chunk (= slot) index within the tile (k_compact converts)
@@ -682,10 +665,12 @@ __global__ void __launch_bounds__(kThreads) k_classify(EncArgs a) {
 // k_scatter: tile-local queue entries -> the dense bucket-major queue
 // ---------------------------------------------------------------------------------------
 __global__ void __launch_bounds__(kThreads) k_scatter(EncArgs a) {
-  // one wave per tile: lane b < kNumBuckets fetches (count, destination) of bucket b at once
+  // one wave per tile: lane b < kNumBuckets holds (count, next destination) of bucket b; the
+  // tile's entries (any order) are routed 64 at a time, one ballot per bucket present
   const int64_t t = ((int64_t)blockIdx.x * kThreads + threadIdx.x) >> 6;
   const int lane = threadIdx.x & 63;
   if (t >= a.n_tiles) return;
+  const uint64_t lt_mask = (lane == 0) ? 0ULL : (~0ULL >> (64 - lane));
   const int64_t t0 = t * kTile;
   uint32_t c = 0;
   int64_t dst = 0;
@@ -693,20 +678,29 @@ __global__ void __launch_bounds__(kThreads) k_scatter(EncArgs a) {
     c = a.bcnt[(int64_t)lane * a.n_tiles + t];
     dst = a.boff[(int64_t)lane * a.n_tiles + t];
   }
-  uint32_t local = c;  // exclusive prefix of the counts over buckets = tile-local start
+  uint32_t n = c;
 #pragma unroll
-  for (int off = 1; off < 16; off <<= 1) {
-    const uint32_t y = __shfl_up(local, off, 64);
-    if (lane >= off) local += y;
-  }
-  local -= c;
-  for (int b = 0; b < kNumBuckets; ++b) {
-    const uint32_t cb = __shfl(c, b, 64), lb = __shfl(local, b, 64);
-    const int64_t db = __shfl(dst, b, 64);
-    for (uint32_t j = lane; j < cb; j += 64) {
-      const uint32_t e = a.qtmp[t0 + lb + j];
+  for (int off = 1; off < 16; off <<= 1) n += __shfl_xor(n, off, 64);  // lanes 0..15: total
+  n = (uint32_t)__shfl((int)n, 0, 64);
+  for (uint32_t i0 = 0; i0 < n; i0 += 64) {
+    const uint32_t i = i0 + lane;
+    const bool act = i < n;
+    const uint32_t e = act ? a.qtmp[t0 + i] : 0u;
+    const uint32_t ns = e >> (2 * kTileBits);
+    const int b = act ? (ns ? bucket_of(ns) : kLongBucket) : 15;
+    int64_t d = 0;
+    uint64_t pend = __ballot(act);
+    while (pend) {
+      const int bb = __shfl(b, __ffsll((long long)pend) - 1, 64);
+      const uint64_t m = __ballot(b == bb);
+      const int64_t db = __shfl(dst, bb, 64);
+      if (b == bb) d = db + __popcll(m & lt_mask);
+      if (lane == bb) dst += __popcll(m);
+      pend &= ~m;
+    }
+    if (act) {
       const uint64_t start = (uint64_t)(t0 + (e & (kTile - 1)));
-      a.queue[db + j] = (start << 24) | ((uint64_t)(e >> (2 * kTileBits)) << 18) | ((e >> kTileBits) & (kTile - 1));
+      a.queue[d] = (start << 24) | ((uint64_t)ns << 18) | ((e >> kTileBits) & (kTile - 1));
     }
   }
 }
@@ -920,31 +914,61 @@ __device__ __forceinline__ uint4 res_head(const uint32_t* res, int64_t p) {
   return q;
 }
 
+#ifndef SW_ROUNDS_IN_FLIGHT
+#define SW_ROUNDS_IN_FLIGHT 8
+#endif
+#ifndef SW_TC_ROUNDS
+#define SW_TC_ROUNDS 8
+#endif
+constexpr int kRoundsInFlight = SW_ROUNDS_IN_FLIGHT;  // slot rounds whose loads (then gathers) issue together
+
 __global__ void __launch_bounds__(kThreads) k_tile_count(EncArgs a) {
   const int64_t t = ((int64_t)blockIdx.x * kThreads + threadIdx.x) >> 6;
   const int lane = threadIdx.x & 63;
   if (t >= a.n_tiles) return;
   const int C = (int)a.tile_slots[t];
-  const int32_t* src = a.scratch + t * kTile;
+  const int32_t* src = a.scratch + t * kTile;  // (kTile slots: loads past C are harmless)
   uint32_t c = 0;
-  for (int j = lane; j < C; j += 64) {
-    const int32_t v = src[j];
+  for (int r0 = 0; r0 * 64 < C; r0 += SW_TC_ROUNDS) {
+    int32_t v[SW_TC_ROUNDS];
+    uint32_t g[SW_TC_ROUNDS];
+#pragma unroll
+    for (int u = 0; u < SW_TC_ROUNDS; ++u) v[u] = src[min(((r0 + u) << 6) + lane, kTile - 1)];  // (re-read by k_compact)
+#pragma unroll
+    for (int u = 0; u < SW_TC_ROUNDS; ++u) g[u] = v[u] < 0 ? a.res[2 * slot_pos(v[u])] : 0u;
+#pragma unroll
+    for (int u = 0; u < SW_TC_ROUNDS; ++u) {
+      const int j = ((r0 + u) << 6) + lane;
 #ifdef SW_ABL_NOGATHER
-    c += 1u;
+      c += j < C ? 1u : 0u;
 #else
-    c += v >= 0 ? 1u : a.res[2 * slot_pos(v)];
+      c += j < C ? (v[u] >= 0 ? 1u : g[u]) : 0u;
 #endif
+    }
   }
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) c += __shfl_xor(c, off, 64);
   if (lane == 0) a.tile_cnt[t] = c;
 }
 
+constexpr int kRefCap = 128;    // references per 8-round group gathered through LDS
+constexpr int kOutCapW = 1024;  // ids per group staged in LDS (the rest are stored directly)
+
 __global__ void __launch_bounds__(kThreads) k_compact(EncArgs a, const int64_t* tile_base, int32_t* out) {
+  // per wave: the group's references, gathered with full lanes before any store (a store
+  // ahead of a load in the wave's vmcnt order would make the load wait for it)
+  __shared__ uint32_t s_rp_all[kWaves][kRefCap];
+  __shared__ uint4 s_rq_all[kWaves][kRefCap];
+  __shared__ int32_t s_out_all[kWaves][kOutCapW];  // a group's ids, staged for 256-B stores
   SW_STAMP_INIT;
+  const int wv = threadIdx.x >> 6;
   const int64_t t = ((int64_t)blockIdx.x * kThreads + threadIdx.x) >> 6;
   const int lane = threadIdx.x & 63;
   if (t >= a.n_tiles) return;
+  uint32_t* s_rp = s_rp_all[wv];
+  uint4* s_rq = s_rq_all[wv];
+  int32_t* s_out = s_out_all[wv];
+  const uint64_t lt_mask = (lane == 0) ? 0ULL : (~0ULL >> (64 - lane));
   const int C = (int)a.tile_slots[t];
   const int32_t* src = a.scratch + t * kTile;
   int32_t* dst = out + tile_base[t];
@@ -957,32 +981,80 @@ __global__ void __launch_bounds__(kThreads) k_compact(EncArgs a, const int64_t* 
   const int sj = has_s ? (int)a.out_off[my_s] : -1;
   const bool many = s_hi - s_lo > 64;  // rare: slot offsets go through scratch instead
   uint32_t s_off = 0, carry = 0;
-  const int rounds = (C + 63) >> 6;
-  for (int r = 0; r < rounds; ++r) {
-    const int j = (r << 6) + lane;
-    const bool valid = j < C;
-    const int32_t v = valid ? src[j] : 0;
-    const bool ref = valid && v < 0;
-    const int64_t p = ref ? slot_pos(v) : 0;
-#ifdef SW_ABL_NOGATHER
-    const uint4 q = make_uint4(ref ? 1u : 0u, (uint32_t)p, 0u, 0u);
-#else
-    const uint4 q = ref ? res_head(a.res, p) : make_uint4(0, 0, 0, 0);
+  constexpr int R = kRoundsInFlight;
+#ifdef SW_STAMPS
+  if (sj == -12345) s_off = 1;  // (forces the string loads to land here in stamp builds)
+  SW_STAMP(8);
 #endif
-    const uint32_t m = ref ? q.x : (valid ? 1u : 0u);
-    const uint32_t incl = wave_incl_scan(m, lane);
-    const uint32_t o = carry + incl - m;
-    carry += __shfl(incl, 63, 64);
-    if (valid && !ref) dst[o] = v;
-    if (ref) {
-      if (m > 0) dst[o] = (int32_t)q.y;
-      if (m > 1) dst[o + 1] = (int32_t)q.z;
-      if (m > 2) dst[o + 2] = (int32_t)q.w;
-      for (uint32_t k = 3; k < m; ++k) dst[o + k] = (int32_t)a.res[2 * p + 1 + k];
+  for (int r0 = 0; r0 * 64 < C; r0 += R) {
+    int32_t v[R];
+#pragma unroll
+    for (int u = 0; u < R; ++u) v[u] = SW_LDNT(&src[min(((r0 + u) << 6) + lane, kTile - 1)]);
+    // dense list of the group's references (their index in the list per round and lane)
+    uint32_t ridx[R];
+    int nref = 0;  // wave-uniform
+#pragma unroll
+    for (int u = 0; u < R; ++u) {
+      const bool ref = ((r0 + u) << 6) + lane < C && v[u] < 0;
+      const uint64_t mk = __ballot(ref);
+      ridx[u] = (uint32_t)(nref + __popcll(mk & lt_mask));
+      if (ref && ridx[u] < (uint32_t)kRefCap) s_rp[ridx[u]] = (uint32_t)slot_pos(v[u]);
+      nref += __popcll(mk);
     }
-    const uint32_t got = (uint32_t)__shfl((int)o, sj & 63, 64);
-    if ((sj >> 6) == r) s_off = got;
-    if (many && valid) a.scratch[t * kTile + j] = (int32_t)o;  // (this wave's own slots)
+    wave_sync_mem();
+#ifndef SW_ABL_NOGATHER
+    for (int i = lane; i < min(nref, kRefCap); i += 64) s_rq[i] = res_head(a.res, s_rp[i]);
+#endif
+    wave_sync_mem();
+    SW_STAMP(9);
+    const uint32_t gbase = carry;  // the group's first id, tile-relative
+#pragma unroll
+    for (int u = 0; u < R; ++u) {
+      const int r = r0 + u;
+      if ((r << 6) >= C) break;  // (wave-uniform)
+      const int j = (r << 6) + lane;
+      const bool valid = j < C;
+      const bool ref = valid && v[u] < 0;
+      uint4 q = make_uint4(0, 0, 0, 0);
+      if (ref) q = ridx[u] < (uint32_t)kRefCap ? s_rq[ridx[u]] : res_head(a.res, slot_pos(v[u]));
+#ifdef SW_ABL_NOGATHER
+      q.x = 2;
+#endif
+      const uint32_t m = ref ? q.x : (valid ? 1u : 0u);
+      const uint32_t incl = wave_incl_scan(m, lane);
+      const uint32_t o = carry + incl - m;
+      carry += __shfl(incl, 63, 64);
+      const uint32_t lo = o - gbase;
+      if (valid && !ref) {
+        if (lo < (uint32_t)kOutCapW) s_out[lo] = v[u];
+        else dst[o] = v[u];
+      }
+      if (ref) {
+        const int64_t p = slot_pos(v[u]);
+        const uint32_t hd[3] = {q.y, q.z, q.w};
+        for (uint32_t k = 0; k < m; ++k) {
+          const int32_t id = k < 3 ? (int32_t)hd[k] : (int32_t)a.res[2 * p + 1 + k];
+          if (lo + k < (uint32_t)kOutCapW) s_out[lo + k] = id;
+          else dst[o + k] = id;
+        }
+      }
+      const uint32_t got = (uint32_t)__shfl((int)o, sj & 63, 64);
+      if ((sj >> 6) == r) s_off = got;
+      if (many && valid) a.scratch[t * kTile + j] = (int32_t)o;  // (this wave's own slots)
+    }
+    wave_sync_mem();
+    // the staged ids: one contiguous 256-byte store per 64 ids
+    const uint32_t staged = min(carry - gbase, (uint32_t)kOutCapW);
+#ifndef SW_ABL_NOSTORE  // ablation builds only: timing experiments, results are wrong
+    for (uint32_t i = lane; i < staged; i += 64) SW_STNT(&dst[gbase + i], s_out[i]);
+#else
+    if (staged == 0xFFFFFFFFu) dst[0] = s_out[lane];
+#endif
+    wave_sync_mem();  // (s_rp / s_rq / s_out are rewritten by the next group)
+#ifdef SW_STAMPS
+    __builtin_amdgcn_s_waitcnt(0);
+    SW_STAMP(10);
+#endif
   }
   const int64_t base = tile_base[t];
   if (has_s) a.out_off[my_s] = ~(base + (int64_t)(sj >= C ? carry : s_off));

@@ -32,7 +32,7 @@ tiles = (len(buf) + 2047) // 2048
 names = {0: "classify: stage+enum", 1: "classify: lookups+dedupe", 2: "classify: queue entries",
          3: "classify: strings",
          4: "merge N<16 (blk)", 5: "merge N>=16 (blk)", 6: "merge long (blk)",
-         8: "compact: slots+list", 9: "compact: gathers", 10: "compact: chained scan", 11: "compact: expand+strings"}
+         8: "compact: prologue loads", 9: "compact: slots+gathers", 10: "compact: scan+stores", 11: "compact: strings"}
 tot = sum(out[i] for i in names)
 print("kind=%s bytes=%d chunks=%d tiles=%d kernel_ms=%.3f" % (model, len(buf), nch, tiles, tok.last_stats.ms_kernels))
 for i, nm in names.items():

@@ -603,6 +603,7 @@ __global__ void __launch_bounds__(kThreads) k_classify(EncArgs a) {
     if (nq == 0) break;
     // dedupe one batch of up to 64 queued chunks
     wave_sync_mem();
+    SW_STAMP(1);
     const bool act = lane < nq;
     const int k = act ? s_qbuf[lane] : 0;
     if (nq > 64 && lane < nq - 64) s_qbuf[lane] = s_qbuf[64 + lane];  // (read above, same lane)
@@ -637,6 +638,7 @@ __global__ void __launch_bounds__(kThreads) k_classify(EncArgs a) {
       pend &= ~m;
     }
     wave_sync_mem();
+    SW_STAMP(7);
     if (r == rounds && nq > 0) --r;  // drain: another batch
   }
   SW_STAMP(1);

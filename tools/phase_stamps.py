@@ -29,7 +29,7 @@ for _ in range(reps):
     tok.encode_packed(buf, off, bits)
 _lib.check(L.sw_encoder_phase_cycles(tok._encoder(), out, 1))
 tiles = (len(buf) + 2047) // 2048
-names = {0: "classify: stage+enum", 1: "classify: lookups+dedupe", 2: "classify: queue entries",
+names = {0: "classify: stage+enum", 1: "classify: lookups", 7: "classify: dedupe", 2: "classify: counts",
          3: "classify: strings",
          4: "merge N<16 (blk)", 5: "merge N>=16 (blk)", 6: "merge long (blk)",
          8: "compact: prologue loads", 9: "compact: slots+gathers", 10: "compact: scan+stores", 11: "compact: strings"}

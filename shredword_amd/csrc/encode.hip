@@ -85,7 +85,6 @@ struct sw_encoder {
   uint64_t* d_dtab = nullptr;         // chunk dedupe table
   uint32_t dmask = 0;
   bool dedupe = true;
-  int64_t classify_grid = 2048;       // resident k_classify workgroups (occupancy x CUs)
   uint32_t* d_tile_cnt = nullptr;
   int64_t* d_tile_base = nullptr;
   int64_t* d_total = nullptr;
@@ -304,13 +303,6 @@ extern "C" int32_t sw_encoder_create(const int32_t* pairs, const int32_t* vals, 
     h->chunks.l_shift = ct.l_shift; h->chunks.l_m1 = ct.l_m1; h->chunks.l_m2 = ct.l_m2;
     h->chunks.enabled = 1;
   }
-  {
-    int per_cu = 0, n_cu = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void*>(k_classify), kThreads, 0) ==
-            hipSuccess &&
-        hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess && per_cu > 0)
-      h->classify_grid = (int64_t)per_cu * n_cu;
-  }
   *out = h;
   return SW_OK;
 }
@@ -435,11 +427,7 @@ extern "C" int32_t sw_encode_device(sw_encoder* h, const uint8_t* d_bytes, int64
     hipLaunchKernelGGL(k_tile_strings, dim3((unsigned)((n_tiles + 255) / 256)), dim3(256), 0, st, d_str_off, n_str,
                        n_tiles, h->d_tile_slo);
     if (h->dedupe) HIP_TRY(hipMemsetAsync(h->d_dtab, 0, sizeof(uint64_t) * ((size_t)h->dmask + 1), st));
-    {  // persistent: as many workgroups as fit the device at once
-      const int64_t want = (n_tiles + kWaves - 1) / kWaves;
-      hipLaunchKernelGGL(k_classify, dim3((unsigned)std::min<int64_t>(want, h->classify_grid)), dim3(kThreads), 0,
-                         st, a);
-    }
+    hipLaunchKernelGGL(k_classify, dim3((unsigned)((n_tiles + kWaves - 1) / kWaves)), dim3(kThreads), 0, st, a);
     HIP_TRY(hipGetLastError());
     HIP_TRY(launch_scan(st, h->d_bcnt, kNumBuckets * n_tiles, h->d_part, h->d_boff, h->d_qtotal));
     hipLaunchKernelGGL(k_scatter, dim3((unsigned)((n_tiles + 3) / 4)), dim3(kThreads), 0, st, a);

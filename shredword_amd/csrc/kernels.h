@@ -53,6 +53,7 @@ __host__ __device__ inline int64_t slot_pos(int32_t v) { return -(int64_t)v - 2;
 
 // streaming accesses (read or written once per launch) carry the non-temporal hint, so the
 // caches keep the randomly gathered merge results instead
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 #ifdef SW_NO_NT
 #define SW_LDNT(p) (*(p))
 #define SW_STNT(p, v) (*(p) = (v))
@@ -489,56 +490,43 @@ constexpr int kWaves = kThreads / 64;
 constexpr int kWinWords = kWin / 4 + 8;
 
 __global__ void __launch_bounds__(kThreads) k_classify(EncArgs a) {
-  __shared__ uint32_t s_b32_all[kWaves][kWinWords];  // raw bytes of the window (+ zero tail)
+  __shared__ __attribute__((aligned(16))) uint32_t s_b32_all[kWaves][kWinWords];  // window bytes (+ zero tail)
   __shared__ uint16_t s_cs_all[kWaves][kTile + 1];   // chunk starts (tile-relative)
   __shared__ uint16_t s_qb_all[kWaves][128];         // chunks not settled by pass A, to dedupe
   SW_STAMP_INIT;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const int64_t gw = (int64_t)blockIdx.x * kWaves + wv;
-  const int64_t n_waves = (int64_t)gridDim.x * kWaves;
+  const int64_t tile = (int64_t)blockIdx.x * kWaves + wv;
+  if (tile >= a.n_tiles) return;
   uint32_t* s_b32 = s_b32_all[wv];
   uint16_t* s_cstart = s_cs_all[wv];
   uint16_t* s_qbuf = s_qb_all[wv];
   const uint64_t lt_mask = (lane == 0) ? 0ULL : (~0ULL >> (64 - lane));
-
-  // Persistent: each wave walks tiles gw, gw + n_waves, ...; the next tile's window, bitmap
-  // words and first string are loaded into registers while this tile is processed.
-  constexpr int kStageQ = (kWin / 4 + 63) / 64;
-  uint32_t pre[kStageQ];
-  uint64_t pre_bw = 0;
-  int64_t pre_slo = 0;
-  auto stage = [&](int64_t tt) {
-    const int64_t g0 = tt * kTile;
-    const bool fast = ((uintptr_t)a.bytes & 3) == 0 && g0 + kWin <= a.n_bytes;
-#pragma unroll
-    for (int q = 0; q < kStageQ; ++q) {
-      const int i = min(lane + 64 * q, kWin / 4 - 1);
-      const int64_t g = g0 + 4 * (int64_t)i;
-      uint32_t v = 0;
-      if (fast) v = SW_LDNT((const uint32_t*)(a.bytes + g));
-      else
-        for (int k = 0; k < 4; ++k) v |= (g + k < a.n_bytes ? (uint32_t)a.bytes[g + k] : 0u) << (8 * k);
-      pre[q] = v;
-    }
-    const int64_t w = (g0 >> 6) + lane;
-    pre_bw = (lane < kTileWords && w < a.n_words) ? a.bits[w] : 0ULL;
-    pre_slo = a.tile_slo[tt];
-  };
-  if (gw < a.n_tiles) stage(gw);
-  for (int64_t tile = gw; tile < a.n_tiles; tile += n_waves) {
   const int64_t t0 = tile * kTile;
   const int64_t t1 = min(t0 + (int64_t)kTile, a.n_bytes);
+  const int64_t w0 = t0 >> 6;
 
-  // 1. the staged window -> LDS; start loading the next tile's
+  // 1. stage the window's bytes (1-KiB coalesced 16-byte loads) and the bitmap words (in
+  //    registers)
+  if (((uintptr_t)a.bytes & 15) == 0 && t0 + kWin <= a.n_bytes) {
 #pragma unroll
-  for (int q = 0; q < kStageQ; ++q) {
-    const int i = lane + 64 * q;
-    if (i < kWin / 4) s_b32[i] = pre[q];
+    for (int q = 0; q < (kWin / 16 + 63) / 64; ++q) {
+      const int i = lane + 64 * q;
+      if (i < kWin / 16) {
+        const u32x4 x = SW_LDNT((const u32x4*)(a.bytes + t0 + 16 * (int64_t)i));
+        *(uint4*)(s_b32 + 4 * i) = make_uint4(x[0], x[1], x[2], x[3]);
+      }
+    }
+  } else {
+    for (int i = lane; i < kWin / 4; i += 64) {
+      const int64_t g = t0 + 4 * (int64_t)i;
+      uint32_t v = 0;
+      for (int k = 0; k < 4; ++k) v |= (g + k < a.n_bytes ? (uint32_t)a.bytes[g + k] : 0u) << (8 * k);
+      s_b32[i] = v;
+    }
   }
   if (lane < 8) s_b32[kWin / 4 + lane] = 0;
-  const uint64_t bw = pre_bw;
-  const int64_t s_first = pre_slo;
-  if (tile + n_waves < a.n_tiles) stage(tile + n_waves);
+  const uint64_t bw = (lane < kTileWords && w0 + lane < a.n_words) ? a.bits[w0 + lane] : 0ULL;
+  const int64_t s_first = a.tile_slo[tile];  // (prefetched: used by step 6)
 
   // 2. chunk starts in [t0, t1): lane w owns bitmap word w
   constexpr int nw_tile = kTile / 64;
@@ -679,8 +667,6 @@ __global__ void __launch_bounds__(kThreads) k_classify(EncArgs a) {
     a.out_off[s] = (int64_t)lo;
   }
   SW_STAMP(3);
-  wave_sync_mem();  // (the LDS window and chunk starts are rewritten by the next tile)
-  }
 }
 
 // ---------------------------------------------------------------------------------------

@@ -943,7 +943,8 @@ __global__ void __launch_bounds__(kThreads) k_tile_count(EncArgs a) {
 #pragma unroll
     for (int u = 0; u < SW_TC_ROUNDS; ++u) v[u] = src[min(((r0 + u) << 6) + lane, kTile - 1)];  // (re-read by k_compact)
 #pragma unroll
-    for (int u = 0; u < SW_TC_ROUNDS; ++u) g[u] = v[u] < 0 ? a.res[2 * slot_pos(v[u])] : 0u;
+    for (int u = 0; u < SW_TC_ROUNDS; ++u)  // (slots past C are stale: never dereferenced)
+      g[u] = (((r0 + u) << 6) + lane < C && v[u] < 0) ? a.res[2 * slot_pos(v[u])] : 0u;
 #pragma unroll
     for (int u = 0; u < SW_TC_ROUNDS; ++u) {
       const int j = ((r0 + u) << 6) + lane;

@@ -91,6 +91,13 @@ int32_t sw_encoder_reserve(sw_encoder* h, int64_t max_bytes, int64_t max_strings
  *                       identical either way. */
 #define SW_OPT_CHUNK_TABLE 1
 #define SW_OPT_DEDUPE 2
+/* Testing knobs of the dedupe table (results are identical for any value):
+ *   SW_OPT_DEDUPE_SLOTS    cap on the table's slots (0 = automatic, else a power of two >= 8);
+ *                          a full table makes chunks merge on their own
+ *   SW_OPT_DEDUPE_FP_BITS  fingerprint bits compared before the bytes (27 = default; 0 makes
+ *                          every probe fall through to the byte comparison) */
+#define SW_OPT_DEDUPE_SLOTS 3
+#define SW_OPT_DEDUPE_FP_BITS 4
 int32_t sw_encoder_set_option(sw_encoder* h, int32_t option, int64_t value);
 
 /* Encoder facts (sw_encoder_get_info): distinct merges, whole-chunk table entries, whether the

@@ -85,6 +85,8 @@ struct sw_encoder {
   uint64_t* d_dtab = nullptr;         // chunk dedupe table
   uint32_t dmask = 0;
   bool dedupe = true;
+  int64_t dedupe_slots = 0;           // SW_OPT_DEDUPE_SLOTS (0: automatic)
+  uint32_t dedupe_fp_mask = (1u << 27) - 1;
   uint32_t* d_tile_cnt = nullptr;
   int64_t* d_tile_base = nullptr;
   int64_t* d_total = nullptr;
@@ -333,6 +335,14 @@ extern "C" int32_t sw_encoder_set_option(sw_encoder* h, int32_t option, int64_t 
   switch (option) {
     case SW_OPT_CHUNK_TABLE: h->chunks.enabled = value ? 1u : 0u; return SW_OK;
     case SW_OPT_DEDUPE: h->dedupe = value != 0; return SW_OK;
+    case SW_OPT_DEDUPE_SLOTS:
+      if (value != 0 && (value < 8 || (value & (value - 1)))) return fail(SW_ERR_ARG, "dedupe slots: 0 or a power of two >= 8");
+      h->dedupe_slots = value;
+      return SW_OK;
+    case SW_OPT_DEDUPE_FP_BITS:
+      if (value < 0 || value > 27) return fail(SW_ERR_ARG, "dedupe fingerprint bits: 0..27");
+      h->dedupe_fp_mask = (uint32_t)((1ULL << value) - 1);
+      return SW_OK;
     default: return fail(SW_ERR_ARG, "sw_encoder_set_option: unknown option");
   }
 }
@@ -420,7 +430,8 @@ extern "C" int32_t sw_encode_device(sw_encoder* h, const uint8_t* d_bytes, int64
     a.str_off = d_str_off; a.n_str = n_str; a.table = h->table; a.chunks = h->chunks;
     a.scratch = h->d_scratch; a.res = h->d_res;
     a.tile_slots = h->d_tile_slots; a.tile_cnt = h->d_tile_cnt;
-    a.dtab = h->d_dtab; a.dmask = h->dmask; a.dedupe = h->dedupe ? 1u : 0u;
+    a.dtab = h->d_dtab; a.dedupe = h->dedupe ? 1u : 0u; a.dfp_mask = h->dedupe_fp_mask;
+    a.dmask = h->dedupe_slots ? std::min<uint32_t>(h->dmask, (uint32_t)(h->dedupe_slots - 1)) : h->dmask;
     a.out_off = d_out_off; a.tile_slo = h->d_tile_slo;
     a.n_tiles = n_tiles; a.qtmp = h->d_res; a.bcnt = h->d_bcnt; a.boff = h->d_boff; a.q_total = h->d_qtotal;
     a.queue = h->d_queue; a.stamps = h->d_stamps;

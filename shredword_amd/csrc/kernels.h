@@ -393,6 +393,7 @@ struct EncArgs {
   uint64_t* queue;           // dense merge queue, bucket-major: start << 24 | len << 18 | slot
   uint64_t* dtab;            // chunk dedupe table (dedupe_claim), dmask + 1 slots
   uint32_t dmask;
+  uint32_t dfp_mask;         // fingerprint bits in use (all 27 except in collision tests)
   uint32_t dedupe;           // 0: every queued chunk runs its own merge loop
   unsigned long long* stamps;  // SW_STAMPS builds: cycles per phase, summed
 };
@@ -445,7 +446,7 @@ __device__ __forceinline__ int64_t dedupe_claim(const EncArgs& a, const uint32_t
     }
   }
   const uint32_t h2 = (h ^ (h >> 16)) * 0x7FEB352Du;
-  const uint64_t tag = (uint64_t)(h2 >> 5) << 37 | (uint64_t)n << 31;  // fingerprint | length
+  const uint64_t tag = (uint64_t)((h2 >> 5) & a.dfp_mask) << 37 | (uint64_t)n << 31;  // fingerprint | length
   const uint64_t mine = tag | (uint64_t)start;
   const uint32_t grp = h & a.dmask & ~7u;
   for (int j = 0; j < 8; ++j) {

@@ -227,3 +227,32 @@ def test_device_api_with_torch_buffers():
     assert n_tok.value == len(exp[0])
     np.testing.assert_array_equal(d_out[:n_tok.value].cpu().numpy(), exp[0])
     np.testing.assert_array_equal(d_oo.cpu().numpy(), exp[1])
+
+
+@pytest.mark.parametrize("slots,fp_bits", [(8, 0), (8, 27), (64, 0), (1 << 12, 3), (0, 27)])
+def test_dedupe_table_pressure_and_collisions(slots, fp_bits):
+    """The batch-wide dedupe must never change a result: a table too small for the distinct
+    chunks (fallback: chunks merge on their own) and fingerprints cut to 0..3 bits (every probe
+    decided by the byte comparison alone) give the oracle's ids; so does dedupe switched off."""
+    buf, off = corpus.synth(7, corpus.MIXED, 6000, 1074)
+    t = tok_for("bl32k.model")
+    exp = oracle_encode(t.merges, buf, off, "cl100k")
+    L, h = _lib.lib(), t._encoder()
+    try:
+        _lib.check(L.sw_encoder_set_option(h, _lib.SW_OPT_DEDUPE_SLOTS, slots))
+        _lib.check(L.sw_encoder_set_option(h, _lib.SW_OPT_DEDUPE_FP_BITS, fp_bits))
+        assert_same(gpu_encode(t, buf, off), exp)
+        _lib.check(L.sw_encoder_set_option(h, _lib.SW_OPT_DEDUPE, 0))
+        assert_same(gpu_encode(t, buf, off), exp)
+    finally:
+        L.sw_encoder_set_option(h, _lib.SW_OPT_DEDUPE, 1)
+        L.sw_encoder_set_option(h, _lib.SW_OPT_DEDUPE_SLOTS, 0)
+        L.sw_encoder_set_option(h, _lib.SW_OPT_DEDUPE_FP_BITS, 27)
+
+
+def test_dedupe_options_validated():
+    t = tok_for("toy500.model")
+    L, h = _lib.lib(), t._encoder()
+    for opt, bad in ((_lib.SW_OPT_DEDUPE_SLOTS, 12), (_lib.SW_OPT_DEDUPE_SLOTS, 4), (_lib.SW_OPT_DEDUPE_FP_BITS, 28),
+                     (99, 1)):
+        assert L.sw_encoder_set_option(h, opt, bad) == _lib.SW_ERR_ARG

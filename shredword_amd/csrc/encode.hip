@@ -448,18 +448,21 @@ extern "C" int32_t sw_encode_device(sw_encoder* h, const uint8_t* d_bytes, int64
       hipLaunchKernelGGL((k_merge_bucket<true, false, 8>), pg, pb, 0, st, a, 3, 4);
       hipLaunchKernelGGL((k_merge_bucket<true, false, 16>), pg, pb, 0, st, a, 5, 7);
       hipLaunchKernelGGL((k_merge_bucket<true, false, 32>), pg, pb, 0, st, a, 8, 9);
+      hipLaunchKernelGGL((k_merge_long_lds<true>), dim3(2048), dim3(64), 0, st, a);
       hipLaunchKernelGGL((k_merge_long<true>), dim3(512), pb, 0, st, a);
     } else if (h->ids16) {
       hipLaunchKernelGGL((k_merge_bucket<false, true, 4>), pg, pb, 0, st, a, 0, 2);
       hipLaunchKernelGGL((k_merge_bucket<false, true, 8>), pg, pb, 0, st, a, 3, 4);
       hipLaunchKernelGGL((k_merge_bucket<false, true, 16>), pg, pb, 0, st, a, 5, 7);
       hipLaunchKernelGGL((k_merge_bucket<false, true, 32>), pg, pb, 0, st, a, 8, 9);
+      hipLaunchKernelGGL((k_merge_long_lds<false>), dim3(2048), dim3(64), 0, st, a);
       hipLaunchKernelGGL((k_merge_long<false>), dim3(512), pb, 0, st, a);
     } else {
       hipLaunchKernelGGL((k_merge_bucket<false, false, 4>), pg, pb, 0, st, a, 0, 2);
       hipLaunchKernelGGL((k_merge_bucket<false, false, 8>), pg, pb, 0, st, a, 3, 4);
       hipLaunchKernelGGL((k_merge_bucket<false, false, 16>), pg, pb, 0, st, a, 5, 7);
       hipLaunchKernelGGL((k_merge_bucket<false, false, 32>), pg, pb, 0, st, a, 8, 9);
+      hipLaunchKernelGGL((k_merge_long_lds<false>), dim3(2048), dim3(64), 0, st, a);
       hipLaunchKernelGGL((k_merge_long<false>), dim3(512), pb, 0, st, a);
     }
     HIP_TRY(hipGetLastError());

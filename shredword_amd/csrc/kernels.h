@@ -305,7 +305,7 @@ __device__ __forceinline__ void wave_sync_mem() {
 }
 
 template <bool kWide>
-__device__ int64_t coop_merge(const DevTable& t, uint32_t* id, uint32_t* rk, int64_t n, int lane) {
+__device__ __forceinline__ int64_t coop_merge(const DevTable& t, uint32_t* id, uint32_t* rk, int64_t n, int lane) {
   constexpr uint32_t INF = kInf, RECOMP = kInf - 1;
   const uint64_t lt_mask = (lane == 0) ? 0ULL : (~0ULL >> (64 - lane));
   for (int64_t i = lane; i + 1 < n; i += 64) rk[i] = RECOMP;
@@ -795,7 +795,33 @@ __global__ void __launch_bounds__(kThreads) k_merge_bucket(EncArgs a, int b_lo, 
 #endif
 }
 
-// long chunks (> kShort bytes): one wave each, wave-cooperative loop in the global work area
+// long chunks (> kShort bytes): one wave each, wave-cooperative loop.  Chunks up to kLongLds
+// bytes keep their ids and ranks in LDS (one 64-thread workgroup = one wave per chunk); longer
+// ones work in the global work area (res, position space).
+constexpr int kLongLds = 4096;
+
+template <bool kWide>
+__global__ void __launch_bounds__(64) k_merge_long_lds(EncArgs a) {
+  __shared__ uint32_t s_id[kLongLds];
+  __shared__ uint32_t s_rk[kLongLds];
+  const int lane = threadIdx.x;
+  int64_t lo, hi;
+  bucket_range(a, kLongBucket, kLongBucket, &lo, &hi);
+  for (int64_t i = lo + blockIdx.x; i < hi; i += gridDim.x) {
+    const uint64_t e = a.queue[i];
+    const int64_t start = (int64_t)(e >> 24);
+    const int64_t len = next_set_bit(a.bits, a.n_words, start + 1, a.n_bytes) - start;
+    if (len > kLongLds) continue;  // (k_merge_long)
+    for (int j = lane; j < len; j += 64) s_id[j] = a.bytes[start + j];
+    wave_sync_mem();
+    const int m = (int)coop_merge<kWide>(a.table, s_id, s_rk, len, lane);
+    uint32_t* gid = a.res + 2 * start + 1;
+    for (int j = lane; j < m; j += 64) gid[j] = s_id[j];
+    if (lane == 0) gid[-1] = (uint32_t)m;
+    wave_sync_mem();
+  }
+}
+
 template <bool kWide>
 __global__ void __launch_bounds__(kThreads) k_merge_long(EncArgs a) {
   SW_STAMP_INIT;
@@ -809,6 +835,7 @@ __global__ void __launch_bounds__(kThreads) k_merge_long(EncArgs a) {
     const int64_t start = (int64_t)(e >> 24);
     const int64_t end = next_set_bit(a.bits, a.n_words, start + 1, a.n_bytes);
     const int64_t len = end - start;
+    if (len <= kLongLds) continue;  // (k_merge_long_lds)
     uint32_t* gid = a.res + 2 * start + 1;  // ids: len words, then ranks: len - 1 words
     uint32_t* grk = gid + len;
     for (int64_t j = lane; j < len; j += 64) gid[j] = a.bytes[start + j];

@@ -77,6 +77,8 @@ struct sw_encoder {
   int64_t* d_part = nullptr;
   int64_t* d_tile_slo = nullptr;
   uint32_t* d_tile_slots = nullptr;
+  uint32_t* d_tile_nref = nullptr;
+  uint32_t* d_rlist = nullptr;
   uint64_t* d_queue = nullptr;        // dense merge queue (bucket-major)
   uint32_t* d_bcnt = nullptr;         // [kNumBuckets * n_tiles] queued chunks per (bucket, tile)
   int64_t* d_boff = nullptr;          // its exclusive scan
@@ -120,9 +122,9 @@ struct DeviceGuard {
 void free_workspace(sw_encoder* h) {
   (void)hipFree(h->d_scratch); (void)hipFree(h->d_res); (void)hipFree(h->d_part);
   (void)hipFree(h->d_tile_slo); (void)hipFree(h->d_stamps);
-  (void)hipFree(h->d_tile_slots); (void)hipFree(h->d_queue); (void)hipFree(h->d_bcnt); (void)hipFree(h->d_boff);
+  (void)hipFree(h->d_tile_slots); (void)hipFree(h->d_tile_nref); (void)hipFree(h->d_rlist); (void)hipFree(h->d_queue); (void)hipFree(h->d_bcnt); (void)hipFree(h->d_boff);
   (void)hipFree(h->d_qtotal);
-  h->d_tile_slo = nullptr; h->d_stamps = nullptr; h->d_tile_slots = nullptr; h->d_queue = nullptr;
+  h->d_tile_slo = nullptr; h->d_stamps = nullptr; h->d_tile_slots = nullptr; h->d_tile_nref = nullptr; h->d_rlist = nullptr; h->d_queue = nullptr;
   h->d_bcnt = nullptr; h->d_boff = nullptr; h->d_qtotal = nullptr;
   (void)hipFree(h->d_dtab); (void)hipFree(h->d_tile_base); (void)hipFree(h->d_tile_cnt);
   (void)hipFree(h->d_total);
@@ -147,6 +149,8 @@ int32_t ensure_workspace(sw_encoder* h, int64_t n_bytes) {
   HIP_TRY(hipMalloc(&h->d_res, sizeof(uint32_t) * (2 * nb + 16)));  // (+ slack for k_compact's head reads)
   HIP_TRY(hipMalloc(&h->d_tile_slo, sizeof(int64_t) * n_tiles));
   HIP_TRY(hipMalloc(&h->d_tile_slots, sizeof(uint32_t) * n_tiles));
+  HIP_TRY(hipMalloc(&h->d_tile_nref, sizeof(uint32_t) * n_tiles));
+  HIP_TRY(hipMalloc(&h->d_rlist, sizeof(uint32_t) * n_tiles * kTile));
   // queued chunks have >= 2 bytes: at most nb / 2 of them
   HIP_TRY(hipMalloc(&h->d_queue, sizeof(uint64_t) * (nb / 2 + 64)));
   HIP_TRY(hipMalloc(&h->d_bcnt, sizeof(uint32_t) * kNumBuckets * n_tiles));
@@ -429,7 +433,7 @@ extern "C" int32_t sw_encode_device(sw_encoder* h, const uint8_t* d_bytes, int64
     a.bytes = d_bytes; a.n_bytes = n_bytes; a.bits = d_chunk_bits; a.n_words = (n_bytes + 63) / 64;
     a.str_off = d_str_off; a.n_str = n_str; a.table = h->table; a.chunks = h->chunks;
     a.scratch = h->d_scratch; a.res = h->d_res;
-    a.tile_slots = h->d_tile_slots; a.tile_cnt = h->d_tile_cnt;
+    a.tile_slots = h->d_tile_slots; a.tile_nref = h->d_tile_nref; a.rlist = h->d_rlist; a.tile_cnt = h->d_tile_cnt;
     a.dtab = h->d_dtab; a.dedupe = h->dedupe ? 1u : 0u; a.dfp_mask = h->dedupe_fp_mask;
     a.dmask = h->dedupe_slots ? std::min<uint32_t>(h->dmask, (uint32_t)(h->dedupe_slots - 1)) : h->dmask;
     a.out_off = d_out_off; a.tile_slo = h->d_tile_slo;

@@ -383,6 +383,8 @@ struct EncArgs {
   uint32_t* res;             // [2 n_bytes] merge results (slot_ref); long chunks' work area
   uint32_t* tile_cnt;        // [n_tiles] ids per tile (k_tile_count)
   uint32_t* tile_slots;      // [n_tiles] chunks (= slots) per tile
+  uint32_t* tile_nref;       // [n_tiles] reference slots per tile
+  uint32_t* rlist;           // [n_tiles * kTile] per tile: the result positions its references use
   int64_t* out_off;          // [n_str+1] string -> chunk index in its tile (k_compact converts)
   const int64_t* tile_slo;   // [n_tiles] first string starting at or after the tile start
   int64_t n_tiles;
@@ -488,12 +490,17 @@ __device__ __forceinline__ int64_t dedupe_claim(const EncArgs& a, const uint32_t
 static_assert(kTile <= 0x10000, "chunk starts are uint16");
 // ---------------------------------------------------------------------------------------
 constexpr int kWaves = kThreads / 64;
+#ifndef SW_LOOK_ROUNDS
+#define SW_LOOK_ROUNDS 1
+#endif
+constexpr int kLookRounds = SW_LOOK_ROUNDS;          // lookup rounds in flight together
+constexpr int kQBuf = 64 * (kLookRounds + 1);        // dedupe buffer: one batch + a group of rounds
 constexpr int kWinWords = kWin / 4 + 8;
 
 __global__ void __launch_bounds__(kThreads) k_classify(EncArgs a) {
   __shared__ __attribute__((aligned(16))) uint32_t s_b32_all[kWaves][kWinWords];  // window bytes (+ zero tail)
   __shared__ uint16_t s_cs_all[kWaves][kTile + 1];   // chunk starts (tile-relative)
-  __shared__ uint16_t s_qb_all[kWaves][128];         // chunks not settled by pass A, to dedupe
+  __shared__ uint16_t s_qb_all[kWaves][kQBuf];       // chunks not settled by a lookup, to dedupe
   SW_STAMP_INIT;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int64_t tile = (int64_t)blockIdx.x * kWaves + wv;
@@ -585,74 +592,97 @@ __global__ void __launch_bounds__(kThreads) k_classify(EncArgs a) {
   uint32_t bcount = 0;
   int nq = 0;    // wave-uniform: chunks waiting in s_qbuf
   int nown = 0;  // wave-uniform: chunks queued for the merge kernels
-  for (int r = 0; r <= rounds; ++r) {
-    if (r < rounds) {
-      const int k = (r << 6) + lane;
-      const bool valid = k < C;
-      const int ls = valid ? s_cstart[k] : 0;
-      const int end = (k + 1 < C) ? (int)s_cstart[k + 1] : rel_end;
-      const int len = valid ? end - ls : 0;
-      uint32_t tok = kInf;
-      if (len == 1) {
-        tok = (s_b32[ls >> 2] >> (8 * (ls & 3))) & 0xFFu;
-      } else if (len >= 2 && len <= 16 && use_table) {
-        uint32_t w[4];
-        window_words(s_b32, ls, len, w);
-        tok = chunk_lookup(a.chunks, w, (uint32_t)len);
-      }
-      const bool queued = valid && tok == kInf;
-      if (valid && !queued) SW_STNT(&dst[k], (int32_t)tok);
-      const uint64_t mq = __ballot(queued);
-      if (queued) s_qbuf[nq + __popcll(mq & lt_mask)] = (uint16_t)k;
-      nq += __popcll(mq);
-      if (nq < 64) continue;
-    }
-    if (nq == 0) break;
-    // dedupe one batch of up to 64 queued chunks
-    wave_sync_mem();
-    SW_STAMP(1);
-    const bool act = lane < nq;
-    const int k = act ? s_qbuf[lane] : 0;
-    if (nq > 64 && lane < nq - 64) s_qbuf[lane] = s_qbuf[64 + lane];  // (read above, same lane)
-    nq = nq > 64 ? nq - 64 : 0;
-    const int ls = act ? s_cstart[k] : 0;
-    const int end = (k + 1 < C) ? (int)s_cstart[k + 1] : rel_end;
-    const int len = act ? end - ls : 0;
-    int64_t other = -1;
-    if (act && a.dedupe && len <= kShort) {
-      uint32_t u[kShort / 4];
-      window_words(s_b32, ls, min(len, 16), *(uint32_t(*)[4])u);
-      if (len > 16) window_words(s_b32, ls + 16, len - 16, *(uint32_t(*)[4])(u + 4));
-      else
+  int nref = 0;  // wave-uniform: slots that refer to a merge result (k_tile_count's list)
+  // kLookRounds rounds of lookups are issued together (independent chains, one wait)
+  for (int r0 = 0; r0 < rounds || nq > 0; r0 += kLookRounds) {
+    if (r0 < rounds) {
+      uint32_t tok[kLookRounds];
 #pragma unroll
-        for (int q = 4; q < kShort / 4; ++q) u[q] = 0;
-      other = dedupe_claim(a, gwords, last_word, mis, t0 + ls, len, u);
+      for (int u = 0; u < kLookRounds; ++u) {
+        const int k = ((r0 + u) << 6) + lane;
+        const bool valid = k < C;
+        const int ls = valid ? s_cstart[k] : 0;
+        const int end = (k + 1 < C) ? (int)s_cstart[k + 1] : rel_end;
+        const int len = valid ? end - ls : 0;
+        tok[u] = kInf;
+        if (len == 1) {
+          tok[u] = (s_b32[ls >> 2] >> (8 * (ls & 3))) & 0xFFu;
+        } else if (len >= 2 && len <= 16 && use_table) {
+          uint32_t w[4];
+          window_words(s_b32, ls, len, w);
+          tok[u] = chunk_lookup(a.chunks, w, (uint32_t)len);
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < kLookRounds; ++u) {
+        const int k = ((r0 + u) << 6) + lane;
+        const bool valid = k < C;
+        const bool queued = valid && tok[u] == kInf;
+        if (valid && !queued) SW_STNT(&dst[k], (int32_t)tok[u]);
+        const uint64_t mq = __ballot(queued);
+        if (queued) s_qbuf[nq + __popcll(mq & lt_mask)] = (uint16_t)k;
+        nq += __popcll(mq);
+      }
     }
-    if (act) dst[k] = slot_ref(other >= 0 ? other : t0 + ls);
-    const bool queued = act && other < 0;
-    const int b = queued ? bucket_of(len) : 15;
-    uint64_t pend = __ballot(queued);
-    // tile-local queue entry (any order; k_scatter routes by length): chunk start in tile
-    // (kTileBits) | chunk index (kTileBits) | length (6 bits, 0 = long)
-    if (queued)
-      a.qtmp[t0 + nown + __popcll(pend & lt_mask)] =
-          (uint32_t)ls | ((uint32_t)k << kTileBits) | ((uint32_t)(len <= kShort ? len : 0) << (2 * kTileBits));
-    nown += __popcll(pend);
-    while (pend) {  // one ballot per bucket present
-      const int bb = __shfl(b, __ffsll((long long)pend) - 1, 64);
-      const uint64_t m = __ballot(b == bb);
-      if (lane == bb) bcount += (uint32_t)__popcll(m);
-      pend &= ~m;
+    // dedupe full batches of 64 queued chunks (and, after the last round, the remainder)
+    while (nq >= 64 || (r0 + kLookRounds >= rounds && nq > 0)) {
+      wave_sync_mem();
+      SW_STAMP(1);
+      const bool act = lane < nq;
+      const int k = act ? s_qbuf[lane] : 0;
+      uint16_t rest[kQBuf / 64 - 1];
+#pragma unroll
+      for (int q = 1; q < kQBuf / 64; ++q) rest[q - 1] = (64 * q + lane < nq) ? s_qbuf[64 * q + lane] : 0;
+#pragma unroll
+      for (int q = 1; q < kQBuf / 64; ++q)
+        if (64 * q + lane < nq) s_qbuf[64 * (q - 1) + lane] = rest[q - 1];
+      nq = nq > 64 ? nq - 64 : 0;
+      const int ls = act ? s_cstart[k] : 0;
+      const int end = (k + 1 < C) ? (int)s_cstart[k + 1] : rel_end;
+      const int len = act ? end - ls : 0;
+      int64_t other = -1;
+      if (act && a.dedupe && len <= kShort) {
+        uint32_t u[kShort / 4];
+        window_words(s_b32, ls, min(len, 16), *(uint32_t(*)[4])u);
+        if (len > 16) window_words(s_b32, ls + 16, len - 16, *(uint32_t(*)[4])(u + 4));
+        else
+#pragma unroll
+          for (int q = 4; q < kShort / 4; ++q) u[q] = 0;
+        other = dedupe_claim(a, gwords, last_word, mis, t0 + ls, len, u);
+      }
+      if (act) {
+        const int64_t op = other >= 0 ? other : t0 + ls;
+        dst[k] = slot_ref(op);
+        a.rlist[t0 + nref + lane] = (uint32_t)op;  // (act lanes are 0 .. n-1: coalesced)
+      }
+      nref += (int)__popcll(__ballot(act));
+      const bool queued = act && other < 0;
+      const int b = queued ? bucket_of(len) : 15;
+      uint64_t pend = __ballot(queued);
+      // tile-local queue entry (any order; k_scatter routes by length): chunk start in tile
+      // (kTileBits) | chunk index (kTileBits) | length (6 bits, 0 = long)
+      if (queued)
+        a.qtmp[t0 + nown + __popcll(pend & lt_mask)] =
+            (uint32_t)ls | ((uint32_t)k << kTileBits) | ((uint32_t)(len <= kShort ? len : 0) << (2 * kTileBits));
+      nown += __popcll(pend);
+      while (pend) {  // one ballot per bucket present
+        const int bb = __shfl(b, __ffsll((long long)pend) - 1, 64);
+        const uint64_t m = __ballot(b == bb);
+        if (lane == bb) bcount += (uint32_t)__popcll(m);
+        pend &= ~m;
+      }
+      wave_sync_mem();
+      SW_STAMP(7);
     }
-    wave_sync_mem();
-    SW_STAMP(7);
-    if (r == rounds && nq > 0) --r;  // drain: another batch
   }
   SW_STAMP(1);
 
   // 4. per-bucket counts of the queued chunks (k_scan -> k_scatter)
   if (lane < kNumBuckets) a.bcnt[(int64_t)lane * a.n_tiles + tile] = bcount;
-  if (lane == 0) a.tile_slots[tile] = (uint32_t)C;
+  if (lane == 0) {
+    a.tile_slots[tile] = (uint32_t)C;
+    a.tile_nref[tile] = (uint32_t)nref;
+  }
   SW_STAMP(2);
 
   // 6. strings starting in this tile: chunk (= slot) index within the tile (k_compact converts)
@@ -954,38 +984,31 @@ __device__ __forceinline__ uint4 res_head(const uint32_t* res, int64_t p) {
 #define SW_ROUNDS_IN_FLIGHT 8
 #endif
 #ifndef SW_TC_ROUNDS
-#define SW_TC_ROUNDS 8
+#define SW_TC_ROUNDS 2
 #endif
 constexpr int kRoundsInFlight = SW_ROUNDS_IN_FLIGHT;  // slot rounds whose loads (then gathers) issue together
 
 __global__ void __launch_bounds__(kThreads) k_tile_count(EncArgs a) {
+  // ids per tile = settled slots + the id counts of the results its references use (the
+  // tile's reference list from k_classify: no pass over the slots)
   const int64_t t = ((int64_t)blockIdx.x * kThreads + threadIdx.x) >> 6;
   const int lane = threadIdx.x & 63;
   if (t >= a.n_tiles) return;
-  const int C = (int)a.tile_slots[t];
-  const int32_t* src = a.scratch + t * kTile;  // (kTile slots: loads past C are harmless)
+  const int C = (int)a.tile_slots[t], nref = (int)a.tile_nref[t];
+  const uint32_t* rl = a.rlist + t * kTile;
   uint32_t c = 0;
-  for (int r0 = 0; r0 * 64 < C; r0 += SW_TC_ROUNDS) {
-    int32_t v[SW_TC_ROUNDS];
-    uint32_t g[SW_TC_ROUNDS];
+  for (int i0 = 0; i0 < nref; i0 += 64 * SW_TC_ROUNDS) {
+    uint32_t p[SW_TC_ROUNDS], g[SW_TC_ROUNDS];
 #pragma unroll
-    for (int u = 0; u < SW_TC_ROUNDS; ++u) v[u] = src[min(((r0 + u) << 6) + lane, kTile - 1)];  // (re-read by k_compact)
+    for (int u = 0; u < SW_TC_ROUNDS; ++u) p[u] = rl[min(i0 + 64 * u + lane, kTile - 1)];
 #pragma unroll
-    for (int u = 0; u < SW_TC_ROUNDS; ++u)  // (slots past C are stale: never dereferenced)
-      g[u] = (((r0 + u) << 6) + lane < C && v[u] < 0) ? a.res[2 * slot_pos(v[u])] : 0u;
+    for (int u = 0; u < SW_TC_ROUNDS; ++u) g[u] = (i0 + 64 * u + lane < nref) ? a.res[2 * (int64_t)p[u]] : 0u;
 #pragma unroll
-    for (int u = 0; u < SW_TC_ROUNDS; ++u) {
-      const int j = ((r0 + u) << 6) + lane;
-#ifdef SW_ABL_NOGATHER
-      c += j < C ? 1u : 0u;
-#else
-      c += j < C ? (v[u] >= 0 ? 1u : g[u]) : 0u;
-#endif
-    }
+    for (int u = 0; u < SW_TC_ROUNDS; ++u) c += g[u];
   }
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) c += __shfl_xor(c, off, 64);
-  if (lane == 0) a.tile_cnt[t] = c;
+  if (lane == 0) a.tile_cnt[t] = c + (uint32_t)(C - nref);
 }
 
 constexpr int kRefCap = 128;    // references per 8-round group gathered through LDS

@@ -1,14 +1,5 @@
-// Host pre-split: apply_regex (shredword/base.py:38-58) as hand-written matchers.
-//
-// cl100k (base.py:56):
-//   '(?i:[sdmt]|ll|ve|re) | [^\r\n\p{L}\p{N}]?+\p{L}+ | \p{N}{1,3} | ?[^\s\p{L}\p{N}]++[\r\n]*
-//   | \s*[\r\n] | \s+(?!\S) | \s+
-// GPT-2 (docstring, base.py:46):
-//   '(?:[sdmt]|ll|ve|re) | ?\p{L}+ | ?\p{N}+ | ?[^\s\p{L}\p{N}]+ | \s+(?!\S) | \s+
-//
-// Leftmost-first alternation semantics of the `regex` module: at each position the first
-// alternative that matches wins; every code point is covered by some alternative, so
-// findall() never skips input and the chunks tile the string.
+// Host pre-split: apply_regex (shredword/base.py:38-58) with the matchers of
+// presplit_match.h, multithreaded over byte-balanced ranges of strings.
 #include "presplit.h"
 
 #include <algorithm>
@@ -20,134 +11,6 @@
 #include "shredword_hip.h"
 
 namespace sw {
-namespace {
-
-struct Cp {
-  uint32_t cp;
-  int cls;
-  int len;
-};
-
-inline Cp at(const uint8_t* s, int64_t n, int64_t i) {
-  Cp r;
-  uint8_t c = s[i];
-  if (c < 0x80) {
-    r.cp = c; r.len = 1;
-    // ASCII fast path of the class table
-    r.cls = (c >= 'a' && c <= 'z') || (c >= 'A' && c <= 'Z') ? kL
-          : (c >= '0' && c <= '9') ? kN
-          : (c == ' ' || (c >= 9 && c <= 13)) ? kS : kOther;
-    return r;
-  }
-  r.cp = utf8_decode(s, n, i, &r.len);
-  r.cls = r.cp == kInvalidCp ? kOther : ucd_class(r.cp);
-  return r;
-}
-
-inline int64_t run_end(const uint8_t* s, int64_t n, int64_t j, int cls) {
-  while (j < n) {
-    Cp c = at(s, n, j);
-    if (c.cls != cls) break;
-    j += c.len;
-  }
-  return j;
-}
-
-inline bool ci(uint32_t c, char lower) {  // (?i:x) per the regex module (see ucd_ranges.h)
-  if (c == (uint32_t)lower || c == (uint32_t)(lower - 32)) return true;
-  return lower == 's' && c == 0x17F;  // LATIN SMALL LETTER LONG S folds to s
-}
-
-inline bool crlf(uint32_t c) { return c == '\r' || c == '\n'; }
-
-// Whitespace-run alternatives shared by both patterns: \s+(?!\S) | \s+
-inline int64_t ws_tail(const uint8_t* s, int64_t n, int64_t i, int64_t j, int64_t last_cp_start) {
-  if (j == n) return j;                 // run reaches end of string: lookahead holds
-  if (last_cp_start > i) return last_cp_start;  // give back the last \s so (?!\S) holds
-  return j;                             // single \s before \S: plain \s+
-}
-
-}  // namespace
-
-int64_t match_cl100k(const uint8_t* s, int64_t n, int64_t i) {
-  Cp c0 = at(s, n, i);
-  int64_t i1 = i + c0.len;
-  // '(?i:[sdmt]|ll|ve|re)
-  if (c0.cp == '\'' && i1 < n) {
-    Cp c1 = at(s, n, i1);
-    if (ci(c1.cp, 's') || ci(c1.cp, 'd') || ci(c1.cp, 'm') || ci(c1.cp, 't')) return i1 + c1.len;
-    int64_t i2 = i1 + c1.len;
-    if (i2 < n) {
-      Cp c2 = at(s, n, i2);
-      if ((ci(c1.cp, 'l') && ci(c2.cp, 'l')) || (ci(c1.cp, 'v') && ci(c2.cp, 'e')) ||
-          (ci(c1.cp, 'r') && ci(c2.cp, 'e')))
-        return i2 + c2.len;
-    }
-  }
-  // [^\r\n\p{L}\p{N}]?+\p{L}+
-  if (c0.cls == kL) return run_end(s, n, i1, kL);
-  if (!crlf(c0.cp) && c0.cls != kN && i1 < n) {
-    Cp c1 = at(s, n, i1);
-    if (c1.cls == kL) return run_end(s, n, i1 + c1.len, kL);
-  }
-  // \p{N}{1,3}
-  if (c0.cls == kN) {
-    int64_t j = i1;
-    for (int k = 1; k < 3 && j < n; ++k) {
-      Cp c = at(s, n, j);
-      if (c.cls != kN) break;
-      j += c.len;
-    }
-    return j;
-  }
-  //  ?[^\s\p{L}\p{N}]++[\r\n]*
-  int64_t p = -1;
-  if (c0.cls == kOther) p = i;
-  else if (c0.cp == ' ' && i1 < n && at(s, n, i1).cls == kOther) p = i1;
-  if (p >= 0) {
-    int64_t k = run_end(s, n, p, kOther);
-    while (k < n && (s[k] == '\r' || s[k] == '\n')) ++k;
-    return k;
-  }
-  // c0 is \s here: \s*[\r\n] | \s+(?!\S) | \s+
-  int64_t j = i, last_crlf_end = -1, last_start = i;
-  while (j < n) {
-    Cp c = at(s, n, j);
-    if (c.cls != kS) break;
-    last_start = j;
-    j += c.len;
-    if (crlf(c.cp)) last_crlf_end = j;
-  }
-  if (last_crlf_end > 0) return last_crlf_end;
-  return ws_tail(s, n, i, j, last_start);
-}
-
-int64_t match_gpt2(const uint8_t* s, int64_t n, int64_t i) {
-  Cp c0 = at(s, n, i);
-  int64_t i1 = i + c0.len;
-  if (c0.cp == '\'' && i1 < n) {
-    uint8_t a = s[i1];
-    if (a == 's' || a == 'd' || a == 'm' || a == 't') return i1 + 1;
-    if (i1 + 1 < n) {
-      uint8_t b = s[i1 + 1];
-      if ((a == 'l' && b == 'l') || (a == 'v' && b == 'e') || (a == 'r' && b == 'e')) return i1 + 2;
-    }
-  }
-  //  ?\p{L}+ |  ?\p{N}+ |  ?[^\s\p{L}\p{N}]+   (the optional space backtracks)
-  if (c0.cp == ' ' && i1 < n) {
-    Cp c1 = at(s, n, i1);
-    if (c1.cls != kS) return run_end(s, n, i1 + c1.len, c1.cls);
-  }
-  if (c0.cls != kS) return run_end(s, n, i1, c0.cls);
-  int64_t j = i, last_start = i;
-  while (j < n) {
-    Cp c = at(s, n, j);
-    if (c.cls != kS) break;
-    last_start = j;
-    j += c.len;
-  }
-  return ws_tail(s, n, i, j, last_start);
-}
 
 int64_t presplit_string(const uint8_t* s, int64_t n, int pattern, uint64_t* bits, int64_t base) {
   if (n <= 0) return 0;

@@ -2,11 +2,11 @@
 """Batched BPE encode throughput on MI355X -- the BASELINE.json metric.
 
 One step = one pass of the encode hot path over one batch already resident in HBM: the whole
-sw_encode_device pipeline (k_tile_strings, k_classify, queue scan/scatter, k_merge_bucket x4,
-k_merge_long, k_tile_count + scan, k_compact, k_string_offsets):
-  N=1  BASELINE configs[1]/[2]: 1 GiB synthetic MIXED UTF-8, 1M strings (mean 1074 B), 32k-merge
-       byte-level table, cl100k pre-split on the host (the GPU pre-splitter is not built yet, so
-       this is reported as the C3 workload), GPU merge loop + id compaction.
+sw_encode_device pipeline (k_presplit, k_tile_strings, k_classify, queue scan/scatter,
+k_merge_bucket x4, k_merge_long*, k_tile_count + scan, k_compact, k_string_offsets):
+  N=1  BASELINE configs[1]: 1 GiB synthetic MIXED UTF-8, 1M strings (mean 1074 B), 32k-merge
+       byte-level table; the full path (C2): cl100k pre-split on the GPU, merge loop, id
+       compaction.  --presplit host gives configs[2] (C3: host pre-split, GPU merge loop only).
   N>1  configs[3]: every rank encodes its own 1 GiB corpus (seed + rank; doc-sharded), then the
        token-id buffers are reassembled on every rank with an RCCL all-gather (padded to the
        largest rank's count) -- weak scaling, the gather is inside the step.
@@ -40,6 +40,8 @@ def parse():
     ap.add_argument("--strings", type=int, default=None)
     ap.add_argument("--mean-len", type=int, default=None)
     ap.add_argument("--pattern", default="cl100k", choices=["cl100k", "gpt2"])
+    ap.add_argument("--presplit", default="device", choices=["device", "host"],
+                    help="device: C2 full path (pre-split inside the step); host: C3 (bitmap made on the host)")
     ap.add_argument("--no-gather", action="store_true", help="N>1: skip the RCCL reassembly")
     ap.add_argument("--cpu-sample-mb", type=float, default=320.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -79,7 +81,8 @@ def main():
 
     t = time.time()
     buf, off = corpus.synth(1_000_003 + rank, kind, n_str, mean, n_threads=args.threads)
-    bits, n_chunks = corpus.presplit(buf, off, pat, n_threads=args.threads)
+    host_ps = args.presplit == "host"
+    bits, n_chunks = corpus.presplit(buf, off, pat, n_threads=args.threads) if host_ps else (None, -1)
     t_prep = time.time() - t
     n_bytes = int(off[-1])
 
@@ -92,20 +95,30 @@ def main():
     _lib.check(L.sw_encoder_set_option(h, _lib.SW_OPT_CHUNK_TABLE, 0 if args.no_chunk_table else 1))
     _lib.check(L.sw_encoder_set_option(h, _lib.SW_OPT_DEDUPE, 0 if args.no_dedupe else 1))
     _lib.check(L.sw_encoder_set_option(h, _lib.SW_OPT_DEDUPE_SLOTS, args.dedupe_slots))
+    _lib.check(L.sw_encoder_set_option(h, _lib.SW_OPT_PATTERN, pat))
 
     cap = torch.tensor([n_bytes], dtype=torch.int64, device=dev)
     if world > 1:
         dist.all_reduce(cap, op=dist.ReduceOp.MAX)
     d_buf = torch.from_numpy(buf).to(dev)
     d_off = torch.from_numpy(off).to(dev)
-    d_bits = torch.from_numpy(bits.view(np.int64)).to(dev)
+    d_bits = torch.from_numpy(bits.view(np.int64)).to(dev) if host_ps else None
     d_out = torch.empty(int(cap.item()), dtype=torch.int32, device=dev)
     d_oo = torch.empty(n_str + 1, dtype=torch.int64, device=dev)
     stream = torch.cuda.current_stream(dev).cuda_stream
 
     def encode(n_tok_ptr=None):
-        _lib.check(L.sw_encode_device(h, d_buf.data_ptr(), n_bytes, d_off.data_ptr(), n_str, d_bits.data_ptr(),
+        _lib.check(L.sw_encode_device(h, d_buf.data_ptr(), n_bytes, d_off.data_ptr(), n_str,
+                                      d_bits.data_ptr() if host_ps else None,  # None: device pre-split (C2)
                                       d_out.data_ptr(), d_oo.data_ptr(), stream, n_tok_ptr))
+
+    if not host_ps:  # chunk count for the report (outside the timed region)
+        tmp_bits = torch.empty((n_bytes + 63) // 64, dtype=torch.int64, device=dev)
+        c = ctypes.c_int64()
+        _lib.check(L.sw_presplit_device(h, d_buf.data_ptr(), n_bytes, d_off.data_ptr(), n_str, pat,
+                                        tmp_bits.data_ptr(), stream, ctypes.byref(c)))
+        n_chunks = int(c.value)
+        del tmp_bits
 
     n_tok_c = ctypes.c_int64()
     encode(ctypes.byref(n_tok_c))
@@ -144,7 +157,8 @@ def main():
     value = all_bytes * args.steps / sec / 1e6
 
     # roofline of the encode pipeline (all sw_encode_device kernels, HIP events), rank-local, per launch
-    b_algo = n_bytes + 4 * n_tok + 16 * (n_str + 1) + (n_bytes + 7) // 8
+    # bytes in + ids out + offsets in/out (+ the bitmap when it comes from the host, C3)
+    b_algo = n_bytes + 4 * n_tok + 16 * (n_str + 1) + ((n_bytes + 7) // 8 if host_ps else 0)
     achieved = b_algo / (k_ms * 1e-3) / 1e9 if k_ms > 0 else None
     # traffic: HBM bytes per launch from the committed PMC profile of this same workload, if any
     traffic, traffic_src = None, None
@@ -152,7 +166,8 @@ def main():
         with open(os.path.join(ROOT, "profiles", "traffic.json")) as f:
             tj = json.load(f)
         if (tj.get("n_bytes") == n_bytes and tj.get("merges") == len(tok.merges) and tj.get("pattern") == args.pattern
-                and tj.get("chunk_table") == (not args.no_chunk_table) and tj.get("dedupe") == (not args.no_dedupe)):
+                and tj.get("chunk_table") == (not args.no_chunk_table) and tj.get("dedupe") == (not args.no_dedupe)
+                and tj.get("presplit", "host") == args.presplit):
             traffic, traffic_src = int(tj["traffic_bytes_per_launch"]), tj["source"]
     except (OSError, ValueError, KeyError):
         pass
@@ -194,8 +209,11 @@ def main():
             "warmup": args.warmup, "ms_per_step": round(ms_step, 4), "higher_is_better": True, "scaling": "weak",
             "vs_baseline": None, "dtype": "int32", "data": "synthetic",
             "config": {"workload": ("C5 stress, 50k merges" if c5 else
-                                    "C3: configs[1] corpus (1 GiB MIXED UTF-8, 1M strings) + host %s pre-split, "
-                                    "GPU merge loop" % args.pattern) + (" + RCCL all-gather of ids" if gather else ""),
+                                    ("C3: configs[2], host %s pre-split, GPU merge loop" % args.pattern) if host_ps else
+                                    ("C2: configs[1] full path, 1 GiB MIXED UTF-8, 1M strings, GPU %s pre-split + "
+                                     "merge loop + id compaction" % args.pattern))
+                       + (" + RCCL all-gather of ids" if gather else ""),
+                       "presplit": args.presplit,
                        "bytes_per_rank": n_bytes, "strings_per_rank": n_str, "merges": len(tok.merges),
                        "model": model, "pattern": args.pattern, "parallelism": "doc-shard x%d" % world,
                        "gather_in_step": gather, "chunk_table": not args.no_chunk_table,

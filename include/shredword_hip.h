@@ -98,6 +98,12 @@ int32_t sw_encoder_reserve(sw_encoder* h, int64_t max_bytes, int64_t max_strings
  *                          every probe fall through to the byte comparison) */
 #define SW_OPT_DEDUPE_SLOTS 3
 #define SW_OPT_DEDUPE_FP_BITS 4
+/*   SW_OPT_PATTERN         pre-split pattern (SW_PAT_*) sw_encode_device uses when it is given
+ *                          no chunk bitmap (default SW_PAT_CL100K)
+ *   SW_OPT_HOST_PRESPLIT   1: sw_encode_batch without a bitmap pre-splits on the host threads
+ *                          (sw_presplit_host) instead of on the device (default 0) */
+#define SW_OPT_PATTERN 5
+#define SW_OPT_HOST_PRESPLIT 6
 int32_t sw_encoder_set_option(sw_encoder* h, int32_t option, int64_t value);
 
 /* Encoder facts (sw_encoder_get_info): distinct merges, whole-chunk table entries, whether the
@@ -121,21 +127,33 @@ int64_t sw_presplit_host(const uint8_t* bytes, const int64_t* str_off, int64_t n
  * Encodes n_str strings (bytes[str_off[s] .. str_off[s+1])) and writes their ids
  * concatenated into out_ids, with out_off[0..n_str] the per-string offsets.
  * chunk_bits: optional pre-split bitmap as produced by sw_presplit_host; NULL => the
- * library pre-splits with `pattern`.  out_cap >= total input bytes always suffices.
+ * library pre-splits with `pattern` (on the device; on the host threads with
+ * SW_OPT_HOST_PRESPLIT).  out_cap >= total input bytes always suffices.
  * stats: optional.  Synchronous. */
 int32_t sw_encode_batch(sw_encoder* h, const uint8_t* bytes, const int64_t* str_off, int64_t n_str,
                         int32_t pattern, const uint64_t* chunk_bits, int32_t* out_ids, int64_t out_cap,
                         int64_t* out_off, sw_stats* stats);
 
+/* apply_regex (shredword/base.py:38-58) on the device: the chunk-start bitmap of the strings
+ * d_bytes[d_str_off[s] .. d_str_off[s+1]) (device pointers on the encoder's device;
+ * d_str_off[0] == 0, d_str_off[n_str] == n_bytes) into d_chunk_bits[ceil(n_bytes/64)], the
+ * layout of sw_presplit_host.  Bit-identical to sw_presplit_host.  If n_chunks_host is not
+ * NULL the call synchronises and stores the number of chunks. */
+int32_t sw_presplit_device(sw_encoder* h, const uint8_t* d_bytes, int64_t n_bytes, const int64_t* d_str_off,
+                           int64_t n_str, int32_t pattern, uint64_t* d_chunk_bits, void* stream,
+                           int64_t* n_chunks_host);
+
 /* ---- batched encode, device-resident buffers (bench / multi-GPU driver) -----------------
  * All pointers are device pointers on the encoder's device: d_bytes[n_bytes],
  * d_str_off[n_str+1] (relative to d_bytes, d_str_off[0] == 0, d_str_off[n_str] == n_bytes),
- * d_chunk_bits[ceil(n_bytes/64)], d_out_ids[n_bytes], d_out_off[n_str+1].  One launch takes
+ * d_chunk_bits[ceil(n_bytes/64)] or NULL (then the device pre-splits with the SW_OPT_PATTERN
+ * pattern first: the full path), d_out_ids[n_bytes], d_out_off[n_str+1].  One launch takes
  * n_bytes < 2^31 - 64 (SW_ERR_ARG otherwise); sw_encode_batch splits larger batches between
  * strings by itself.
  * stream: a hipStream_t on that device, or NULL for the encoder's own stream.
  * Asynchronous: the work is enqueued on the stream.  n_tokens_host (optional) forces a
  * synchronisation and receives the total id count. */
+
 int32_t sw_encode_device(sw_encoder* h, const uint8_t* d_bytes, int64_t n_bytes, const int64_t* d_str_off,
                          int64_t n_str, const uint64_t* d_chunk_bits, int32_t* d_out_ids, int64_t* d_out_off,
                          void* stream, int64_t* n_tokens_host);

@@ -22,6 +22,7 @@ SW_ERR_ARG, SW_ERR_HIP, SW_ERR_ALLOC, SW_ERR_CAP, SW_ERR_NODEV = -1, -2, -3, -4,
 SW_PAT_CL100K, SW_PAT_GPT2, SW_PAT_NONE = 0, 1, 2
 SW_CORPUS_ASCII, SW_CORPUS_MIXED, SW_CORPUS_STRESS = 0, 1, 2
 SW_OPT_CHUNK_TABLE, SW_OPT_DEDUPE, SW_OPT_DEDUPE_SLOTS, SW_OPT_DEDUPE_FP_BITS = 1, 2, 3, 4
+SW_OPT_PATTERN, SW_OPT_HOST_PRESPLIT = 5, 6
 SW_INFO_MERGES, SW_INFO_CHUNK_ENTRIES, SW_INFO_WIDE_TABLE, SW_INFO_IDS16 = 1, 2, 3, 4
 
 
@@ -72,6 +73,8 @@ _SIGNATURES = {
     "sw_encode_batch": (c_int32, [c_void_p, POINTER(c_uint8), POINTER(c_int64), c_int64, c_int32,
                                   POINTER(c_uint64), POINTER(c_int32), c_int64, POINTER(c_int64),
                                   POINTER(SwStats)]),
+    "sw_presplit_device": (c_int32, [c_void_p, c_void_p, c_int64, c_void_p, c_int64, c_int32, c_void_p, c_void_p,
+                                     POINTER(c_int64)]),
     "sw_encode_device": (c_int32, [c_void_p, c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_void_p,
                                    c_void_p, c_void_p, POINTER(c_int64)]),
     "sw_encoder_set_option": (c_int32, [c_void_p, c_int32, c_int64]),

@@ -30,6 +30,7 @@
 #include <vector>
 
 #include "kernels.h"
+#include "presplit_kernel.h"
 #include "shredword_hip.h"
 #include "table.h"
 
@@ -88,6 +89,10 @@ struct sw_encoder {
   uint32_t dmask = 0;
   bool dedupe = true;
   int64_t dedupe_slots = 0;           // SW_OPT_DEDUPE_SLOTS (0: automatic)
+  int32_t pattern = SW_PAT_CL100K;    // SW_OPT_PATTERN: device pre-split of sw_encode_device(bits = NULL)
+  bool host_presplit = false;         // SW_OPT_HOST_PRESPLIT: sw_encode_batch pre-splits on the host
+  uint64_t* d_pbits = nullptr;        // [n_bytes / 64] device pre-split bitmap
+  unsigned long long* d_pcount = nullptr;
   uint32_t dedupe_fp_mask = (1u << 27) - 1;
   uint32_t* d_tile_cnt = nullptr;
   int64_t* d_tile_base = nullptr;
@@ -120,7 +125,7 @@ struct DeviceGuard {
 };
 
 void free_workspace(sw_encoder* h) {
-  (void)hipFree(h->d_scratch); (void)hipFree(h->d_res); (void)hipFree(h->d_part);
+  (void)hipFree(h->d_scratch); (void)hipFree(h->d_res); (void)hipFree(h->d_pbits); (void)hipFree(h->d_pcount); (void)hipFree(h->d_part);
   (void)hipFree(h->d_tile_slo); (void)hipFree(h->d_stamps);
   (void)hipFree(h->d_tile_slots); (void)hipFree(h->d_tile_nref); (void)hipFree(h->d_rlist); (void)hipFree(h->d_queue); (void)hipFree(h->d_bcnt); (void)hipFree(h->d_boff);
   (void)hipFree(h->d_qtotal);
@@ -128,7 +133,7 @@ void free_workspace(sw_encoder* h) {
   h->d_bcnt = nullptr; h->d_boff = nullptr; h->d_qtotal = nullptr;
   (void)hipFree(h->d_dtab); (void)hipFree(h->d_tile_base); (void)hipFree(h->d_tile_cnt);
   (void)hipFree(h->d_total);
-  h->d_scratch = nullptr; h->d_res = nullptr; h->d_part = nullptr;
+  h->d_scratch = nullptr; h->d_res = nullptr; h->d_pbits = nullptr; h->d_pcount = nullptr; h->d_part = nullptr;
   h->d_dtab = nullptr; h->d_tile_base = nullptr; h->d_tile_cnt = nullptr; h->d_total = nullptr;
   h->cap_bytes = -1; h->cap_str = -1;
 }
@@ -166,6 +171,8 @@ int32_t ensure_workspace(sw_encoder* h, int64_t n_bytes) {
   HIP_TRY(hipMalloc(&h->d_tile_base, sizeof(int64_t) * n_tiles));
   HIP_TRY(hipMalloc(&h->d_tile_cnt, sizeof(uint32_t) * n_tiles));
   HIP_TRY(hipMalloc(&h->d_total, sizeof(int64_t)));
+  HIP_TRY(hipMalloc(&h->d_pbits, sizeof(uint64_t) * ((nb + 63) / 64)));
+  HIP_TRY(hipMalloc(&h->d_pcount, sizeof(unsigned long long)));
 #ifdef SW_STAMPS
   HIP_TRY(hipMalloc(&h->d_stamps, sizeof(unsigned long long) * 32 * 64));  // 64 copies per counter
   HIP_TRY(hipMemset(h->d_stamps, 0, sizeof(unsigned long long) * 32 * 64));
@@ -238,6 +245,17 @@ hipError_t launch_scan(hipStream_t st, const uint32_t* cnt, int64_t n, int64_t* 
   hipLaunchKernelGGL(k_scan_reduce, dim3((unsigned)n_parts), dim3(kThreads), 0, st, cnt, n, part);
   hipLaunchKernelGGL(k_scan_parts, dim3(1), dim3(1024), 0, st, part, n_parts, total);
   hipLaunchKernelGGL(k_scan_apply, dim3((unsigned)n_parts), dim3(kThreads), 0, st, cnt, n, part, base);
+  return hipGetLastError();
+}
+
+// device pre-split of [d_bytes, d_bytes + n_bytes) into d_bits (zeroed here)
+hipError_t launch_presplit(hipStream_t st, const uint8_t* d_bytes, int64_t n_bytes, const int64_t* d_str_off,
+                           int64_t n_str, int32_t pattern, uint64_t* d_bits) {
+  if (n_bytes <= 0) return hipSuccess;
+  hipError_t e = hipMemsetAsync(d_bits, 0, sizeof(uint64_t) * ((n_bytes + 63) / 64), st);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(k_presplit, dim3((unsigned)((n_bytes + kPsBlock - 1) / kPsBlock)), dim3(kPsThreads), 0, st,
+                     d_bytes, n_bytes, d_str_off, n_str, (int)pattern, d_bits);
   return hipGetLastError();
 }
 
@@ -339,6 +357,11 @@ extern "C" int32_t sw_encoder_set_option(sw_encoder* h, int32_t option, int64_t 
   switch (option) {
     case SW_OPT_CHUNK_TABLE: h->chunks.enabled = value ? 1u : 0u; return SW_OK;
     case SW_OPT_DEDUPE: h->dedupe = value != 0; return SW_OK;
+    case SW_OPT_PATTERN:
+      if (value != SW_PAT_CL100K && value != SW_PAT_GPT2 && value != SW_PAT_NONE) return fail(SW_ERR_ARG, "bad pattern");
+      h->pattern = (int32_t)value;
+      return SW_OK;
+    case SW_OPT_HOST_PRESPLIT: h->host_presplit = value != 0; return SW_OK;
     case SW_OPT_DEDUPE_SLOTS:
       if (value != 0 && (value < 8 || (value & (value - 1)))) return fail(SW_ERR_ARG, "dedupe slots: 0 or a power of two >= 8");
       h->dedupe_slots = value;
@@ -410,7 +433,7 @@ extern "C" int32_t sw_encoder_phase_cycles(sw_encoder* h, double* out32, int32_t
 extern "C" int32_t sw_encode_device(sw_encoder* h, const uint8_t* d_bytes, int64_t n_bytes, const int64_t* d_str_off,
                                     int64_t n_str, const uint64_t* d_chunk_bits, int32_t* d_out_ids,
                                     int64_t* d_out_off, void* stream, int64_t* n_tokens_host) {
-  if (!h || n_bytes < 0 || n_str < 0 || !d_str_off || !d_out_off || (n_bytes > 0 && (!d_bytes || !d_chunk_bits || !d_out_ids)))
+  if (!h || n_bytes < 0 || n_str < 0 || !d_str_off || !d_out_off || (n_bytes > 0 && (!d_bytes || !d_out_ids)))
     return fail(SW_ERR_ARG, "sw_encode_device: bad arguments");
   if (n_bytes > kMaxLaunchBytes) return fail(SW_ERR_ARG, "sw_encode_device: n_bytes >= 2 GiB (split the batch)");
   DeviceGuard g(h->device);
@@ -427,6 +450,10 @@ extern "C" int32_t sw_encode_device(sw_encoder* h, const uint8_t* d_bytes, int64
     }
     e1 = h->ev_pool[2 * h->ev_used + 1];
     HIP_TRY(hipEventRecord(h->ev_pool[2 * h->ev_used], st));
+  }
+  if (n_tiles > 0 && !d_chunk_bits) {  // the full path: device pre-split first
+    HIP_TRY(launch_presplit(st, d_bytes, n_bytes, d_str_off, n_str, h->pattern, h->d_pbits));
+    d_chunk_bits = h->d_pbits;
   }
   if (n_tiles > 0) {
     EncArgs a;
@@ -544,7 +571,8 @@ extern "C" int32_t sw_encode_batch(sw_encoder* h, const uint8_t* bytes, const in
   std::vector<uint64_t> own_bits;
   double ms_pre = 0;
   int64_t n_chunks = -1;
-  if (!chunk_bits) {
+  const bool device_presplit = !chunk_bits && !h->host_presplit;
+  if (!chunk_bits && !device_presplit) {
     own_bits.resize((size_t)std::max<int64_t>(n_words, 1));
     auto a = std::chrono::steady_clock::now();
     n_chunks = sw_presplit_host(bytes, str_off, n_str, pattern, own_bits.data(), 0);
@@ -570,7 +598,8 @@ extern "C" int32_t sw_encode_batch(sw_encoder* h, const uint8_t* bytes, const in
   hipStream_t st = h->stream;
   if (n_bytes > 0) {
     HIP_TRY(hipMemcpyAsync(h->d_bytes, bytes + b0, n_bytes, hipMemcpyHostToDevice, st));
-    HIP_TRY(hipMemcpyAsync(h->d_bits, chunk_bits, sizeof(uint64_t) * n_words, hipMemcpyHostToDevice, st));
+    if (!device_presplit)
+      HIP_TRY(hipMemcpyAsync(h->d_bits, chunk_bits, sizeof(uint64_t) * n_words, hipMemcpyHostToDevice, st));
   }
   HIP_TRY(hipMemcpyAsync(h->d_str_off, rel.data(), sizeof(int64_t) * (n_str + 1), hipMemcpyHostToDevice, st));
   HIP_TRY(hipStreamSynchronize(st));
@@ -580,8 +609,23 @@ extern "C" int32_t sw_encode_batch(sw_encoder* h, const uint8_t* bytes, const in
   const size_t was_used = h->ev_used;
   h->timing = true;
   h->ev_used = 0;
-  int32_t rc = sw_encode_device(h, h->d_bytes, n_bytes, h->d_str_off, n_str, h->d_bits, h->d_out, h->d_out_off,
-                                st, &n_tok);
+  const int32_t was_pattern = h->pattern;
+  if (device_presplit) {
+    if (pattern != SW_PAT_CL100K && pattern != SW_PAT_GPT2 && pattern != SW_PAT_NONE)
+      return fail(SW_ERR_ARG, "sw_encode_batch: bad pattern");
+    h->pattern = pattern;
+  }
+  int32_t rc = sw_encode_device(h, h->d_bytes, n_bytes, h->d_str_off, n_str, device_presplit ? nullptr : h->d_bits,
+                                h->d_out, h->d_out_off, st, &n_tok);
+  h->pattern = was_pattern;
+  if (rc == SW_OK && device_presplit && stats && n_bytes > 0) {  // chunk count for the stats
+    HIP_TRY(hipMemsetAsync(h->d_pcount, 0, sizeof(unsigned long long), st));
+    hipLaunchKernelGGL(k_popcount, dim3(1024), dim3(256), 0, st, h->d_pbits, n_words, h->d_pcount);
+    unsigned long long c = 0;
+    HIP_TRY(hipMemcpyAsync(&c, h->d_pcount, sizeof(c), hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    n_chunks = (int64_t)c;
+  }
   const double k_ms = sw_encoder_last_kernel_ms(h);
   h->timing = was_timing;
   h->ev_used = was_timing ? was_used : 0;
@@ -601,6 +645,32 @@ extern "C" int32_t sw_encode_batch(sw_encoder* h, const uint8_t* bytes, const in
     stats->ms_kernels = k_ms;
     stats->ms_d2h = ms_d2h;
     stats->ms_total = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - T0).count();
+  }
+  return SW_OK;
+}
+
+extern "C" int32_t sw_presplit_device(sw_encoder* h, const uint8_t* d_bytes, int64_t n_bytes, const int64_t* d_str_off,
+                                      int64_t n_str, int32_t pattern, uint64_t* d_chunk_bits, void* stream,
+                                      int64_t* n_chunks_host) {
+  if (!h || n_bytes < 0 || n_str < 0 || !d_str_off || (n_bytes > 0 && (!d_bytes || !d_chunk_bits)))
+    return fail(SW_ERR_ARG, "sw_presplit_device: bad arguments");
+  if (pattern != SW_PAT_CL100K && pattern != SW_PAT_GPT2 && pattern != SW_PAT_NONE)
+    return fail(SW_ERR_ARG, "sw_presplit_device: bad pattern");
+  DeviceGuard g(h->device);
+  hipStream_t st = stream ? (hipStream_t)stream : h->stream;
+  int32_t rc = ensure_workspace(h, n_bytes);
+  if (rc) return rc;
+  HIP_TRY(launch_presplit(st, d_bytes, n_bytes, d_str_off, n_str, pattern, d_chunk_bits));
+  if (n_chunks_host) {
+    *n_chunks_host = 0;
+    if (n_bytes > 0) {
+      HIP_TRY(hipMemsetAsync(h->d_pcount, 0, sizeof(unsigned long long), st));
+      hipLaunchKernelGGL(k_popcount, dim3(1024), dim3(256), 0, st, d_chunk_bits, (n_bytes + 63) / 64, h->d_pcount);
+      unsigned long long c = 0;
+      HIP_TRY(hipMemcpyAsync(&c, h->d_pcount, sizeof(c), hipMemcpyDeviceToHost, st));
+      HIP_TRY(hipStreamSynchronize(st));
+      *n_chunks_host = (int64_t)c;
+    }
   }
   return SW_OK;
 }

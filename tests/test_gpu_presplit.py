@@ -1,0 +1,113 @@
+"""Device pre-split (sw_presplit_device) against the host pre-split (sw_presplit_host, itself
+pinned to the reference's apply_regex through the `regex` module's outputs in
+tests/golden/primitives.json and test_surface.py): the bitmaps must be identical, bit for bit,
+for every pattern, on corpora and on the edge cases of the parallel parse (segments with no
+sync position, strings crossing workgroups, many tiny strings per workgroup, invalid UTF-8)."""
+import ctypes
+import random
+
+import numpy as np
+import pytest
+
+import shredword_amd as sa
+from shredword_amd import _lib, corpus
+
+pytestmark = pytest.mark.gpu
+
+PATS = [_lib.SW_PAT_CL100K, _lib.SW_PAT_GPT2, _lib.SW_PAT_NONE]
+_TOK = {}
+
+
+def _encoder():
+    if "t" not in _TOK:
+        t = sa.Tokenizer(device=0)
+        t.merges = {(104, 105): 256}
+        _TOK["t"] = t
+    return _TOK["t"]._encoder()
+
+
+def device_presplit(buf, off, pattern):
+    import torch
+    dev = torch.device("cuda", 0)
+    n = int(off[-1])
+    d_buf = torch.from_numpy(np.ascontiguousarray(buf) if len(buf) else np.zeros(1, np.uint8)).to(dev)
+    d_off = torch.from_numpy(np.ascontiguousarray(off, dtype=np.int64)).to(dev)
+    d_bits = torch.full((max((n + 63) // 64, 1),), -1, dtype=torch.int64, device=dev)  # (must be cleared)
+    cnt = ctypes.c_int64()
+    _lib.check(_lib.lib().sw_presplit_device(_encoder(), d_buf.data_ptr(), n, d_off.data_ptr(), len(off) - 1, pattern,
+                                             d_bits.data_ptr(), None, ctypes.byref(cnt)))
+    torch.cuda.synchronize()
+    return d_bits.cpu().numpy().view(np.uint64)[:max((n + 63) // 64, 1)], cnt.value
+
+
+def check(buf, off):
+    n = int(off[-1])
+    for pat in PATS:
+        exp, ecnt = corpus.presplit(buf, off, pat)
+        got, gcnt = device_presplit(buf, off, pat)
+        if n == 0:
+            assert gcnt == 0
+            continue
+        np.testing.assert_array_equal(got, exp[:len(got)], err_msg="pattern %d" % pat)
+        assert gcnt == ecnt
+
+
+def pack(datas):
+    off = np.zeros(len(datas) + 1, dtype=np.int64)
+    np.cumsum([len(d) for d in datas], out=off[1:])
+    return np.frombuffer(b"".join(datas) or b"\0", dtype=np.uint8)[:int(off[-1])].copy(), off
+
+
+@pytest.mark.parametrize("kind,n,mean", [(corpus.MIXED, 20000, 1074), (corpus.ASCII, 20000, 600),
+                                         (corpus.STRESS, 20000, 600)])
+def test_corpora(kind, n, mean):
+    buf, off = corpus.synth(11, kind, n, mean)
+    check(buf, off)
+
+
+def test_edge_strings():
+    rng = random.Random(5)
+    alphabet = ["a", "Z", " ", "  ", "\n", "\r\n", "\t", "'s", "'LL", "'ve", "1", "12345", ".", "!!", "...", " ",
+                "　", "é", "ſ", "中文", "🙂", "́", "퟿", "x\n\n", " 1", " .", "\x00", "\x7f"]
+    datas = []
+    for _ in range(3000):
+        k = rng.randint(0, 40)
+        datas.append("".join(rng.choice(alphabet) for _ in range(k)).encode("utf-8", "surrogatepass"))
+    datas += [b"", b"", b" ", b"a" * 5000, b" " * 3000, b"1" * 700, b"!" * 900, b"\n" * 600 + b"a",
+              ("word " * 4000).encode(), "中" .encode() * 3000, b"x" * 70000, b"\xff\xfe" * 500]
+    rng.shuffle(datas)
+    buf, off = pack(datas)
+    check(buf, off)
+
+
+def test_invalid_utf8_and_tiny_strings():
+    rng = np.random.default_rng(3)
+    datas = [bytes(rng.integers(0, 256, size=int(rng.integers(0, 6)), dtype=np.uint8)) for _ in range(60000)]
+    buf, off = pack(datas)  # ~150 KB, >512 strings per 16 KiB workgroup: the global-search path
+    check(buf, off)
+
+
+def test_single_huge_string_and_empty():
+    check(*pack([b""]))
+    check(*pack([]))
+    buf, off = corpus.synth(2, corpus.MIXED, 200, 1074)
+    check(buf, np.array([0, int(off[-1])], dtype=np.int64))  # one 200 KB string
+
+
+def test_encode_batch_device_vs_host_presplit():
+    """sw_encode_batch pre-splits on the device by default; SW_OPT_HOST_PRESPLIT gives the same ids."""
+    t = sa.Tokenizer(device=0)
+    from conftest import load_model_merges
+    t.merges = load_model_merges("bl32k.model")
+    buf, off = corpus.synth(21, corpus.MIXED, 4000, 1074)
+    for pat in ("", sa.GPT2_PATTERN):
+        t.pattern = pat
+        dev_ids = t.encode_packed(buf, off)
+        L, h = _lib.lib(), t._encoder()
+        _lib.check(L.sw_encoder_set_option(h, _lib.SW_OPT_HOST_PRESPLIT, 1))
+        try:
+            host_ids = t.encode_packed(buf, off)
+        finally:
+            L.sw_encoder_set_option(h, _lib.SW_OPT_HOST_PRESPLIT, 0)
+        np.testing.assert_array_equal(dev_ids[0], host_ids[0])
+        np.testing.assert_array_equal(dev_ids[1], host_ids[1])

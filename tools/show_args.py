@@ -1,7 +1,7 @@
 """Summarise gpurun_out/args_<tag>: bench value and per-kernel average ms per argument set."""
 import csv, json, os, sys
 d = 'gpurun_out/args_' + sys.argv[1]
-idx = [l.strip().split(': ', 1) for l in open(d + '/index.txt')]
+idx = [(l.split(':', 1)[0], l.split(':', 1)[1].strip()) for l in open(d + '/index.txt')]
 rows = {}
 for i, args in idx:
     try:

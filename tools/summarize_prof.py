@@ -93,6 +93,7 @@ def main():
             json.dump({"source": "profiles/%s.md" % tag, "n_bytes": bench["config"]["bytes_per_rank"],
                        "merges": bench["config"]["merges"], "pattern": bench["config"]["pattern"],
                        "chunk_table": bench["config"].get("chunk_table"), "dedupe": bench["config"].get("dedupe"),
+                       "presplit": bench["config"].get("presplit", "host"),
                        "traffic_bytes_per_launch": derived["traffic_bytes_per_launch"],
                        "traffic_bytes_per_launch_x2": derived["traffic_bytes_per_launch_x2"],
                        "note": "FETCH_SIZE+WRITE_SIZE summed over the pipeline's kernels per launch (raw FETCH; "

@@ -5,6 +5,7 @@
 #include <cstring>
 #include <vector>
 
+#include "presplit_block.h"
 #include "presplit_fsm.h"
 #include "ucd_tables.h"
 
@@ -84,12 +85,72 @@ void emul_bytes(const uint8_t* bytes, const int64_t* off, int64_t n_str, bool cl
     sw::fsm::presplit_bytes<int64_t>(x, r, s1, n, true, cl, st, last_cr, last_ws, last_sp);
   }
 }
+
+// the device kernel (k_presplit) workgroup by workgroup: presplit_block.h's phases run for
+// every thread in turn, with the kernel's window, halo and string-start bitmap
+struct HostBits {
+  uint64_t* bits;
+  int64_t widx;
+  uint64_t word;
+  void flush() { if (word) bits[widx] |= word; }
+  void set(int64_t pos) {
+    const int64_t w = pos >> 6;
+    const uint64_t bit = 1ULL << (pos & 63);
+    if (w == widx) {
+      word |= bit;
+    } else if (w > widx) {
+      flush();
+      widx = w;
+      word = bit;
+    } else {
+      bits[w] |= bit;
+    }
+  }
+};
+
+void emul_device(const uint8_t* bytes, const int64_t* off, int64_t n_str, int pattern, uint64_t* bits) {
+  const int64_t n = off[n_str];
+  const bool cl = pattern == 0, none = pattern == 2;
+  const sw::fsm::Tables* tab = pattern == 1 ? &kGpt2 : &kCl;
+  auto cls = [](uint32_t cp) { return cls_of(cp); };
+  std::vector<uint32_t> w32(sw::kPsRaw / 4), ss(sw::kPsSsWords);
+  for (int64_t blk = 0; blk * sw::kPsBlock < n; ++blk) {
+    const sw::PsGeom G = sw::ps_geom(blk, n);
+    uint8_t* buf = (uint8_t*)w32.data();
+    for (int i = 0; i < sw::kPsRaw; ++i) {
+      const int64_t g = G.wb + i;
+      buf[i] = (g >= 0 && g < G.wend) ? bytes[g] : 0;
+    }
+    std::fill(ss.begin(), ss.end(), 0u);
+    for (int64_t i = 0; i <= n_str; ++i) {
+      if (off[i] < G.wb || off[i] > G.wend) continue;
+      const int r = (int)(off[i] - G.wb);
+      ss[r >> 5] |= 1u << (r & 31);
+    }
+    if (!none) {
+      std::vector<sw::PsInfoRegs> regs(sw::kPsThreads);
+      for (int t = 0; t < sw::kPsThreads; ++t) regs[t] = sw::ps_info_load(w32.data(), t);
+      for (int t = 0; t < sw::kPsThreads; ++t)
+        sw::ps_info_convert(w32.data(), (const uint32_t*)ss.data(), tab->asc, cls, cl, G.info_hi, t, regs[t]);
+    }
+    for (int t = 0; t < sw::kPsThreads; ++t) {
+      HostBits out{bits, (G.b0 >> 6) + t, 0};
+      sw::ps_lane(G, t, (const uint8_t*)w32.data(), (const uint32_t*)ss.data(), tab, bytes, n, off, n_str, cl, none,
+                  out, cls);
+      out.flush();
+    }
+  }
+}
 }  // namespace
 
 extern "C" int fsm_emul(const uint8_t* bytes, const int64_t* off, int64_t n_str, int pattern, int seg,
                         uint64_t* bits, int byte_stepped) {
   const int64_t n = off[n_str];
   std::memset(bits, 0, sizeof(uint64_t) * (size_t)((n + 63) / 64));
+  if (byte_stepped == 2) {  // the device kernel's workgroups
+    emul_device(bytes, off, n_str, pattern, bits);
+    return 0;
+  }
   if (byte_stepped && pattern != 2) {
     emul_bytes(bytes, off, n_str, pattern == 0, seg, bits);
     return 0;

@@ -34,8 +34,10 @@ def device_presplit(buf, off, pattern):
     d_off = torch.from_numpy(np.ascontiguousarray(off, dtype=np.int64)).to(dev)
     d_bits = torch.full((max((n + 63) // 64, 1),), -1, dtype=torch.int64, device=dev)  # (must be cleared)
     cnt = ctypes.c_int64()
+    # on torch's stream: the fill above is ordered before the library's clear of the bitmap
     _lib.check(_lib.lib().sw_presplit_device(_encoder(), d_buf.data_ptr(), n, d_off.data_ptr(), len(off) - 1, pattern,
-                                             d_bits.data_ptr(), None, ctypes.byref(cnt)))
+                                             d_bits.data_ptr(), torch.cuda.current_stream(dev).cuda_stream,
+                                             ctypes.byref(cnt)))
     torch.cuda.synchronize()
     return d_bits.cpu().numpy().view(np.uint64)[:max((n + 63) // 64, 1)], cnt.value
 

@@ -4,7 +4,9 @@ pre-split (sw_presplit_host, pinned to the reference's apply_regex through the g
 primitives): identical bitmaps for every pattern, for 64-byte segments (the kernel's) and
 for small odd segment sizes that put a lane boundary at almost every position, so every
 resumption rule is exercised.  Both forms are run: the code-point-stepped one (the device's
-fallback past its staged window) and the byte-stepped one over per-byte info (its fast path)."""
+fallback past its staged window) and the byte-stepped one over per-byte info (its fast path);
+and the kernel's own workgroups (presplit_block.h: window, halo, info phase, per-lane parse
+with the fallback), thread by thread (mode 2)."""
 import ctypes
 import os
 import random
@@ -50,7 +52,7 @@ def pack(datas):
 def check(emul, buf, off, segs=(64, 1, 3, 7, 13)):
     for pat in PATS:
         exp, _ = corpus.presplit(buf, off, pat)
-        for seg, mode in [(sg, m) for sg in segs for m in (0, 1)]:
+        for seg, mode in [(sg, m) for sg in segs for m in (0, 1)] + [(64, 2)]:
             got = emul(buf, off, pat, seg, mode)
             bad = np.nonzero(got != exp[:len(got)])[0]
             if len(bad):
@@ -100,6 +102,17 @@ def test_long_runs(emul):
 @pytest.mark.parametrize("kind", [corpus.MIXED, corpus.ASCII, corpus.STRESS])
 def test_corpora(emul, kind):
     check(emul, *corpus.synth(11, kind, 1500, 700), segs=(64, 5))
+
+
+def test_device_windows(emul):
+    """Parses that run past a workgroup's 2 KiB halo (the fallback over global memory), strings
+    crossing many workgroups, and a string that starts exactly where a workgroup's info bytes
+    end (byte b0 + 18424: the fallback must settle the string before it)."""
+    tail = [b"\n x" * 10000] + fuzz_strings(9, 300)
+    for first_len in range(18420, 18429):
+        check(emul, *pack([b" " * first_len, b"ab c"] + tail), segs=(64,))
+    datas = [b"x" * 70000, "\u4e2d".encode() * 3000, b" " * 5000, b"a" * 2100, ("word " * 4000).encode()]
+    check(emul, *pack(datas + tail), segs=(64,))
 
 
 def test_empty_and_single(emul):

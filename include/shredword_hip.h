@@ -137,7 +137,8 @@ int32_t sw_encode_batch(sw_encoder* h, const uint8_t* bytes, const int64_t* str_
 /* apply_regex (shredword/base.py:38-58) on the device: the chunk-start bitmap of the strings
  * d_bytes[d_str_off[s] .. d_str_off[s+1]) (device pointers on the encoder's device;
  * d_str_off[0] == 0, d_str_off[n_str] == n_bytes) into d_chunk_bits[ceil(n_bytes/64)], the
- * layout of sw_presplit_host.  Bit-identical to sw_presplit_host.  If n_chunks_host is not
+ * layout of sw_presplit_host.  Bit-identical to sw_presplit_host.  stream: a hipStream_t on
+ * that device; NULL is the null stream (torch's default stream).  If n_chunks_host is not
  * NULL the call synchronises and stores the number of chunks. */
 int32_t sw_presplit_device(sw_encoder* h, const uint8_t* d_bytes, int64_t n_bytes, const int64_t* d_str_off,
                            int64_t n_str, int32_t pattern, uint64_t* d_chunk_bits, void* stream,
@@ -150,7 +151,8 @@ int32_t sw_presplit_device(sw_encoder* h, const uint8_t* d_bytes, int64_t n_byte
  * pattern first: the full path), d_out_ids[n_bytes], d_out_off[n_str+1].  One launch takes
  * n_bytes < 2^31 - 64 (SW_ERR_ARG otherwise); sw_encode_batch splits larger batches between
  * strings by itself.
- * stream: a hipStream_t on that device, or NULL for the encoder's own stream.
+ * stream: a hipStream_t on that device; NULL is the null stream (torch's default stream, as
+ * in every HIP library API).
  * Asynchronous: the work is enqueued on the stream.  n_tokens_host (optional) forces a
  * synchronisation and receives the total id count. */
 

@@ -437,7 +437,7 @@ extern "C" int32_t sw_encode_device(sw_encoder* h, const uint8_t* d_bytes, int64
     return fail(SW_ERR_ARG, "sw_encode_device: bad arguments");
   if (n_bytes > kMaxLaunchBytes) return fail(SW_ERR_ARG, "sw_encode_device: n_bytes >= 2 GiB (split the batch)");
   DeviceGuard g(h->device);
-  hipStream_t st = stream ? (hipStream_t)stream : h->stream;
+  hipStream_t st = (hipStream_t)stream;  // (NULL: the null stream, as torch's default stream)
   int32_t rc = ensure_workspace(h, n_bytes);
   if (rc) return rc;
   const int64_t n_tiles = (n_bytes + kTile - 1) / kTile;
@@ -657,7 +657,7 @@ extern "C" int32_t sw_presplit_device(sw_encoder* h, const uint8_t* d_bytes, int
   if (pattern != SW_PAT_CL100K && pattern != SW_PAT_GPT2 && pattern != SW_PAT_NONE)
     return fail(SW_ERR_ARG, "sw_presplit_device: bad pattern");
   DeviceGuard g(h->device);
-  hipStream_t st = stream ? (hipStream_t)stream : h->stream;
+  hipStream_t st = (hipStream_t)stream;  // (NULL: the null stream, as torch's default stream)
   int32_t rc = ensure_workspace(h, n_bytes);
   if (rc) return rc;
   HIP_TRY(launch_presplit(st, d_bytes, n_bytes, d_str_off, n_str, pattern, d_chunk_bits));

@@ -10,24 +10,84 @@
 //      (ps_info_load before the barrier: the raw words it needs from its neighbours;
 //      ps_info_convert after it);
 //   3. every lane parses from the first sync position of its segment (ps_lane): byte-stepped
-//      over the info bytes while they last, then code-point-stepped over global memory.
+//      over the info bytes while they last (one word of info per 4 steps, one step-table
+//      lookup per byte, chunk starts OR-ed into an LDS bitmap of the window), then, rarely,
+//      code-point-stepped over global memory (chunk starts OR-ed into the global bitmap);
+//   4. the window's LDS bitmap is OR-ed into the global one (the kernel does this).
 #pragma once
 #include <cstdint>
 
 #include "presplit_fsm.h"
+#include "ucd_tables.h"
 
 namespace sw {
 
-constexpr int kPsSeg = 64;                       // bytes per lane
+// ---- Unicode classes of the BMP for LDS --------------------------------------------------
+// ucd_tables.h's two-stage table restricted to U+0000..U+FFFF, its blocks renumbered densely,
+// built at compile time: 256 + 64 * nblk bytes (~3.6 KB) instead of 12.8 KB, so a workgroup
+// keeps it in LDS; code points past the BMP use the full table (global / constant memory).
+constexpr int kUcdBmpMaxBlocks = 64;
+struct UcdBmp {
+  uint8_t s1[256];
+  uint8_t s2[kUcdBmpMaxBlocks * 64];
+  int nblk;
+};
+constexpr uint8_t kUcdStage1[SW_UCD_STAGE1_SIZE] = SW_UCD_STAGE1_INIT;
+constexpr uint8_t kUcdStage2[SW_UCD_STAGE2_SIZE] = SW_UCD_STAGE2_INIT;
+constexpr UcdBmp make_ucd_bmp() {
+  UcdBmp t{};
+  int map[SW_UCD_NBLOCKS] = {};
+  for (int b = 0; b < SW_UCD_NBLOCKS; ++b) map[b] = -1;
+  for (int i = 0; i < 256; ++i) {
+    const int b = kUcdStage1[i];
+    if (map[b] < 0) {
+      map[b] = t.nblk++;
+      for (int j = 0; j < 64; ++j) t.s2[map[b] * 64 + j] = kUcdStage2[b * 64 + j];
+    }
+    t.s1[i] = (uint8_t)map[b];
+  }
+  return t;
+}
+constexpr UcdBmp kUcdBmp = make_ucd_bmp();
+static_assert(kUcdBmp.nblk <= kUcdBmpMaxBlocks, "BMP blocks");
+constexpr int kUcdBmpBytes = 256 + 64 * kUcdBmp.nblk;
+
+// class of a code point: near(cp) for the BMP from the compact table (s1, s2: its copy),
+// far(cp) past it from the full one (fn)
+template <class P, class Far>
+struct PsUcd {
+  P s1, s2;
+  Far fn;
+  SW_HD int near(uint32_t cp) const {
+    const uint32_t blk = s1[cp >> 8];
+    const uint32_t v = s2[blk * 64 + ((cp & 255) >> 2)];
+    return (int)((v >> ((cp & 3) * 2)) & 3);
+  }
+  SW_HD int far(uint32_t cp) const { return fn(cp); }
+  SW_HD int operator()(uint32_t cp) const { return cp < 0x10000u ? near(cp) : far(cp); }
+};
+
+// the same interface over one full-table function (host)
+template <class Fn>
+struct PsUcdFull {
+  Fn fn;
+  SW_HD int near(uint32_t cp) const { return fn(cp); }
+  SW_HD int far(uint32_t cp) const { return fn(cp); }
+  SW_HD int operator()(uint32_t cp) const { return fn(cp); }
+};
+
+constexpr int kPsSeg = 68;                       // bytes per lane (17 words: lanes' reads hit distinct LDS banks)
 constexpr int kPsThreads = 256;
-constexpr int kPsBlock = kPsSeg * kPsThreads;    // 16 KiB per workgroup
-constexpr int kPsHalo = 2048;                    // staged past the block for chunks that run on
+constexpr int kPsBlock = kPsSeg * kPsThreads;    // 17 KiB per workgroup (a multiple of 64)
+constexpr int kPsHalo = 1024;                    // staged past the block for chunks that run on
 constexpr int kPsPre = 16;                       // staged before it (context of the first bytes)
 constexpr int kPsWin = kPsPre + kPsBlock + kPsHalo;
 constexpr int kPsGroups = (kPsBlock + kPsHalo) / 4 / kPsThreads;  // info words per thread (18)
 constexpr int kPsRaw = kPsWin + 32;              // (zero tail: the context of the last bytes)
 constexpr int kPsSsWords = kPsWin / 32 + 2;      // string-start bitmap words of the window
+constexpr int kPsOutWords = (kPsBlock + kPsHalo) / 64;  // chunk-start bitmap of [b0, b0 + block + halo)
 static_assert(kPsGroups * 4 * kPsThreads == kPsBlock + kPsHalo, "window");
+static_assert(kPsBlock % 64 == 0 && kPsPre % 4 == 0 && kPsSeg % 4 == 0, "alignment");
 
 struct PsGeom {
   int64_t b0;      // first byte the workgroup owns
@@ -52,6 +112,12 @@ SW_HD inline PsGeom ps_geom(int64_t block, int64_t n_bytes) {
   return g;
 }
 
+// the parts of fsm::Tables the converged phases read (kept in LDS)
+struct PsStepTab {
+  uint8_t asc[128];
+  uint8_t lane[1280];
+};
+
 // ---- phase 2: info bytes in place of the staged bytes -------------------------------------
 struct PsInfoRegs {
   uint32_t prev, first, edge;  // the words before, at and after this thread's run
@@ -69,33 +135,28 @@ template <class W32, class SS, class Asc, class Cls>
 SW_HD inline void ps_info_convert(W32 w32, SS s_ss, Asc asc, const Cls& cls, bool cl, int info_hi, int tid,
                                   const PsInfoRegs& regs) {
   const int wfirst = kPsPre / 4 + tid * kPsGroups;
+  auto ss_at = [&](int r0) {  // string-start bits of bytes r0 - 4 .. r0 + 7
+    const int q = r0 - 4;
+    const uint64_t two = (uint64_t)s_ss[q >> 5] | ((uint64_t)s_ss[(q >> 5) + 1] << 32);
+    return (uint32_t)(two >> (q & 31)) & 0xFFF;
+  };
   uint32_t u[3] = {regs.prev, regs.first, 0};
-  fsm::LeadCarry carry{0, 0, 0};
+  fsm::LeadCarry carry = fsm::lead_carry(u, ss_at((wfirst - 1) * 4 + 4));
+  fsm::Ascii ap = fsm::ascii_classes(u[0]), ac = fsm::ascii_classes(u[1]), an;
   for (int i = 0; i < kPsGroups; ++i) {
     const int r0 = (wfirst + i) * 4;
     if (r0 >= info_hi) break;
     u[2] = i + 1 < kPsGroups ? w32[wfirst + i + 1] : regs.edge;
-    const int q = r0 - 4;
-    const uint64_t two = (uint64_t)s_ss[q >> 5] | ((uint64_t)s_ss[(q >> 5) + 1] << 32);
-    const uint32_t ss = (uint32_t)(two >> (q & 31)) & 0xFFF;
-    if (i == 0) carry = fsm::lead_carry(u, ss);
-    w32[wfirst + i] = fsm::info4(u, ss, asc, cls, cl, carry);
+    an = fsm::ascii_classes(u[2]);
+    w32[wfirst + i] = fsm::info4_core(u, ss_at(r0), ap, ac, an, asc, cls, cl, carry);
     u[0] = u[1];
     u[1] = u[2];
+    ap = ac;
+    ac = an;
   }
 }
 
 // ---- phase 3: one lane's segment -----------------------------------------------------------
-template <class InfoP, class TabP, class Bits>
-struct PsFast {  // presplit_bytes context: positions relative to the window start wb
-  InfoP inf;
-  TabP tab;
-  Bits* out;
-  int64_t wb;
-  SW_HD uint32_t info(int r) const { return inf[r]; }
-  SW_HD void emit(int r) { out->set(wb + r); }
-};
-
 template <class TabP, class Bits, class Cls>
 struct PsSlow {  // presplit_run context over global memory, positions relative to wb
   const uint8_t* g;  // bytes + wb
@@ -118,43 +179,152 @@ struct PsSlow {  // presplit_run context over global memory, positions relative 
   SW_HD void emit(int r) { out->set(wb + r); }
 };
 
-// Bits: set(pos) / flush(), word = the lane's own bitmap word to start with.  Returns with
-// the lane's chunk starts passed to out (not flushed).
-template <class InfoP, class SS, class TabP, class Bits, class Cls>
-SW_HD inline void ps_lane(const PsGeom& G, int tid, InfoP info, SS s_ss, TabP tab, const uint8_t* bytes,
-                          int64_t n_bytes, const int64_t* str_off, int64_t n_str, bool cl, bool none, Bits& out,
+// The settle of the open chunk at a sync position of code sc (presplit_bytes)
+template <class Emit>
+SW_HD inline void ps_settle(uint32_t sc, int pos, int st, int last_cr, int last_ws, bool cl, Emit& e) {
+  const bool wsr = st == fsm::kWsRun, lcv = cl && last_cr >= 0;
+  if (wsr && lcv) {
+    if (sc <= 2) {
+      if (last_cr < pos) e.set(last_cr);
+    } else if (sc == 3 && last_cr != pos) {
+      e.set(last_cr);
+      e.set(last_ws);
+    }
+  } else if (wsr && sc == 3) {
+    e.set(last_ws);
+  }
+  if (!cl && (st == fsm::kAL || st == fsm::kAVR)) e.set(pos - 1);
+}
+
+// The byte-stepped parse of presplit_fsm.h's presplit_bytes, restated for a converged wave:
+// every step is the same straight-line code (one lane-table lookup: the string-start settle,
+// the transition and its chunk starts), the info is read a word at a time (all lanes walk
+// word-aligned, steps before the lane's start masked), and the chunk starts of a word's steps
+// that fall at bytes 4w - 1 .. 4w + 3 gather in one mask, OR-ed into the LDS bitmap once per
+// word; only a far one (the \r\n end or last code point of a long whitespace run) goes by
+// itself.  The segment-end sync position (any sync at or past s1) is settled once, after the
+// loop.  Positions are window-relative.  Returns true when the lane is done, false when it
+// reached r_end (r == r_end) with the parse still open.
+//   Info: info word w (bytes 4w..4w+3).  LB: set(pos) / set_near(pos, mask: bit j = pos + j)
+//   on the window's bitmap (PsWinBits).
+template <class InfoW, class TabP, class LB>
+SW_HD inline bool ps_lane_steps(InfoW info, TabP tab, LB& lb, int& r, int s1, int r_end, bool at_end, bool cl,
+                                int& st, int& last_cr, int& last_ws, bool& last_sp) {
+  const int r0 = r;
+  bool done = false;
+  int fin_pos = 0;
+  uint32_t fin_v = 0;
+  for (int w = r0 >> 2; 4 * w < r_end; ++w) {
+    const uint32_t cur = info[w];
+    const int base = 4 * w - 1;
+    uint32_t near = 0;  // chunk starts at base + j (bit j)
+    int far_cr = -1, far_ws = -1;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int pos = 4 * w + k;
+      const bool act = !done && pos >= r0 && pos < r_end;
+      const uint32_t v = (cur >> (8 * k)) & 0xFFu;
+#ifdef SW_PS_NOOVERRUN  // (diagnostic timing builds only: wrong bitmaps)
+      const bool fin = act && pos >= s1;
+#else
+      const bool fin = act && pos >= s1 && (v & 0xF0u);
+#endif
+      fin_pos = fin ? pos : fin_pos;
+      fin_v = fin ? v : fin_v;
+      const bool step = act && !fin;
+      const uint32_t sym = v & 15u, ssb = (v >> 4) & 1u;
+      const uint32_t q = (last_sp ? 1u : 0u) | ((cl && last_cr == pos) ? 2u : 0u);
+      const uint32_t E = tab->lane[fsm::lane_index(st, (int)sym, (int)q, (int)ssb)];
+      near |= ((step && (E & fsm::kLRetro)) ? 1u : 0u) << k;
+      near |= ((step && (E & fsm::kLEnd)) ? 2u : 0u) << k;
+      const bool e_cr = step && (E & fsm::kLCr) && last_cr >= 0;
+      const bool e_ws = step && (E & fsm::kLWs);
+      near |= (e_cr && last_cr >= base) ? 1u << (last_cr - base) : 0u;
+      near |= (e_ws && last_ws >= base) ? 1u << (last_ws - base) : 0u;
+      far_cr = (e_cr && last_cr < base) ? last_cr : far_cr;
+      far_ws = (e_ws && last_ws < base) ? last_ws : far_ws;
+      const bool isws = step && ((0x700u >> sym) & 1u);
+      const bool in_run = st == fsm::kWsRun && !ssb;
+      last_cr = isws ? ((cl && sym == fsm::kSymCr) ? pos + 1 : (in_run ? last_cr : -1)) : last_cr;
+      last_ws = isws ? pos : last_ws;
+      last_sp = isws ? sym == fsm::kSymSp : last_sp;
+      st = step ? (int)(E & fsm::kStMask) : st;
+      done = done || fin;
+    }
+    // (a far start of this word is of a run that ended here: at most one of each kind)
+    if (far_cr >= 0) lb.set(far_cr);
+    if (far_ws >= 0) lb.set(far_ws);
+    if (near) lb.set_near(base, near);
+    if (done) break;
+  }
+  if (done) {
+    ps_settle(fsm::info_sync(fin_v), fin_pos, st, last_cr, last_ws, cl, lb);
+    return true;
+  }
+  r = r_end;
+  if (!at_end) return false;
+  if (cl && st == fsm::kWsRun && last_cr >= 0 && last_cr < r) lb.set(last_cr);
+  if (!cl && (st == fsm::kAL || st == fsm::kAVR)) lb.set(r - 1);
+  return true;
+}
+
+// The window's chunk-start bitmap (bit p - kPsPre = window position p), over any word array
+// with an OR: the kernel's is in LDS, the emulator's a plain array.
+template <class OrFn>
+struct PsWinBits {
+  OrFn orw;  // orw(word index, bits)
+  SW_HD void set(int p) {
+    const int q = p - kPsPre;
+    orw(q >> 5, 1u << (q & 31));
+  }
+  // bit 0 of m: position p, bits 1..4: the word-aligned group p + 1 .. p + 4 (one word)
+  SW_HD void set_near(int p, uint32_t m) {
+    if (m & 1u) set(p);
+    const int q = p + 1 - kPsPre;
+    if (m >> 1) orw(q >> 5, (m >> 1) << (q & 31));
+  }
+};
+
+// One lane: from the first sync position of its segment [s0, s1) to the first one at or past
+// s1.  LB: the window's LDS bitmap (ps_lane_steps); GB: the global bitmap, set(pos) / flush(),
+// for the rare parse that runs past the info bytes.  tab: asc + step (PsStepTab or Tables);
+// ftab: the full Tables (the fallback).
+template <class InfoW, class TabP, class FTabP, class LB, class GB, class Cls>
+SW_HD inline void ps_lane(const PsGeom& G, int tid, InfoW info, TabP tab, FTabP ftab, const uint8_t* bytes,
+                          int64_t n_bytes, const int64_t* str_off, int64_t n_str, bool cl, LB& lb, GB& gout,
                           const Cls& cls) {
   const int s0 = kPsPre + tid * kPsSeg;
   const int n_rel = (int)(n_bytes - G.wb);
   if (s0 >= n_rel) return;
   const int s1 = s0 + kPsSeg < n_rel ? s0 + kPsSeg : n_rel;
-  if (none) {  // the chunks are the strings: this word's string starts
-    const int q = s0;
-    const uint64_t lo = (uint64_t)s_ss[q >> 5] | ((uint64_t)s_ss[(q >> 5) + 1] << 32);
-    const uint64_t hi = s_ss[(q >> 5) + 2];
-    uint64_t w = (lo >> (q & 31)) | (hi << (64 - (q & 31)));  // (q & 31 == 16)
-    if (s1 - s0 < 64) w &= (1ULL << (s1 - s0)) - 1;
-    out.word |= w;
-    return;
+  // the first sync position in [s0, s1): a set high nibble in the info bytes
+  int r = s1;
+  for (int w = s0 >> 2; 4 * w < s1; ++w) {
+    const uint32_t m = info[w] & 0xF0F0F0F0u;
+    if (m) {
+      r = 4 * w + (__builtin_ctz(m) >> 3);
+      break;
+    }
   }
-  PsFast<InfoP, TabP, Bits> x{info, tab, &out, G.wb};
-  int r = s0;
-  while (r < s1 && !(x.info(r) >> 4)) ++r;
-  if (r == s1) return;
-  int st = fsm::sync_init_state(x.info(r) >> 4);
+  if (r >= s1) return;
+  int st = fsm::sync_init_state(fsm::info_sync((info[r >> 2] >> (8 * (r & 3))) & 0xFFu));
   int last_cr = -1, last_ws = 0;
   bool last_sp = false;
-  if (fsm::presplit_bytes<int>(x, r, s1, G.info_hi, G.at_end, cl, st, last_cr, last_ws, last_sp)) return;
-  // past the info bytes (r == info_hi): continue code point by code point over global memory.
-  // The string: the one containing position r - 1 (the last byte stepped), so that a string
-  // starting exactly at r is entered through next_string(), which settles the one before.
+  if (ps_lane_steps(info, tab, lb, r, s1, G.info_hi, G.at_end, cl, st, last_cr, last_ws, last_sp)) return;
+#ifdef SW_PS_NOFALLBACK  // (diagnostic timing builds only: wrong bitmaps)
+  return;
+#endif
+  // past the info bytes (r == info_hi): chunk starts still inside the open whitespace run go
+  // to the global bitmap like the rest.  Continue code point by code point over global memory
+  // in the string containing r - 1 (the last byte stepped), so that a string starting
+  // exactly at r is entered through next_string(), which settles the one before.
   int64_t lo = 0, hi = n_str - 1;  // last string with start < wb + r
   while (lo < hi) {
     const int64_t m = (lo + hi + 1) >> 1;
     if (str_off[m] < G.wb + r) lo = m; else hi = m - 1;
   }
-  PsSlow<TabP, Bits, Cls> y{bytes + G.wb, tab, str_off, n_str, G.wb, lo, (int)(str_off[lo] - G.wb),
-                            (int)(str_off[lo + 1] - G.wb), &out, &cls};
+  PsSlow<FTabP, GB, Cls> y{bytes + G.wb, ftab, str_off, n_str, G.wb, lo, (int)(str_off[lo] - G.wb),
+                          (int)(str_off[lo + 1] - G.wb), &gout, &cls};
   if (r < y.b) {
     for (int k = 1; k <= 3; ++k) {  // r may be inside the code point the byte steps were in
       if (r - k < y.a) break;
@@ -167,6 +337,17 @@ SW_HD inline void ps_lane(const PsGeom& G, int tid, InfoP info, SS s_ss, TabP ta
     }
   }
   fsm::presplit_run<int>(y, r, s1, cl, false, st, last_cr, last_ws, last_sp);
+  gout.flush();
+}
+
+// pattern "none": the chunks are the (non-empty) strings; bitmap word i of the block from the
+// window's string-start bits (s_ss, window-relative; the batch end is past n_bytes)
+template <class SS>
+SW_HD inline uint64_t ps_none_word(SS s_ss, int i) {
+  const int q = kPsPre + 64 * i;  // (q & 31 == 16)
+  const uint64_t lo = (uint64_t)s_ss[q >> 5] | ((uint64_t)s_ss[(q >> 5) + 1] << 32);
+  const uint64_t hi = s_ss[(q >> 5) + 2];
+  return (lo >> (q & 31)) | (hi << (64 - (q & 31)));
 }
 
 }  // namespace sw

@@ -53,7 +53,20 @@ struct Tables {
   uint8_t asc[128];      // symbol of an ASCII byte
   uint8_t t[16][16];     // [state][symbol] -> next state | flags
   uint8_t pre[2][16];    // after a whitespace run, [its last code point is ' '][symbol]
+  // one whole step (the device's lane loop): [state][symbol][q], q = last_sp | (cl && last_cr
+  // == this position) << 1 -> next state | kStepEnd (a chunk starts here) | kStepRetro (one
+  // starts at the previous byte) | kStepWsx (a whitespace run ended: its \r\n end, if any, and
+  // its last code point start chunks).  The kEnd re-dispatch from kStart is folded in.
+  uint8_t step[16][16][4];
+  // the device lane's step over an info byte (presplit_block.h): index lane_index(state, symbol,
+  // q, string start) -> next state | kLEnd (a chunk starts here) | kLRetro (one starts at the
+  // previous byte) | kLCr (one starts at the open whitespace run's \r\n end, if any) | kLWs
+  // (one starts at its last code point).  A string start first settles the open chunk.
+  uint8_t lane[1280];
 };
+constexpr uint8_t kStepEnd = 16, kStepRetro = 32, kStepWsx = 64;
+constexpr uint8_t kLEnd = 16, kLRetro = 32, kLCr = 64, kLWs = 128;
+SW_HD constexpr int lane_index(int st, int sym, int q, int ss) { return ((st * 12 + sym) * 4 + q) * 2 + ss; }
 
 constexpr bool sym_letter(int s) { return s >= kSymLs && s <= kSymL; }
 constexpr bool sym_space(int s) { return s == kSymSp || s == kSymCr || s == kSymWs; }
@@ -113,15 +126,63 @@ constexpr Tables make_tables(bool cl) {
       T.pre[1][s] = L ? kLRun : N ? kNRun : O ? kORun : kEnd;
     }
   }
+  for (int st = 0; st < 16; ++st)
+    for (int s = 0; s < 16; ++s)
+      for (int q = 0; q < 4; ++q) {
+        const bool last_sp = q & 1, crx = q & 2;
+        int t = T.t[st][s], f = 0;
+        if (t & kWsx) {
+          if (crx) {
+            t = kEnd;
+          } else {
+            f |= kStepWsx;
+            t = T.pre[last_sp][s];
+          }
+        } else if (t & kRetro) {
+          f |= kStepRetro;
+        }
+        if (t & kEnd) {
+          f |= kStepEnd;
+          t = T.t[kStart][s];
+        }
+        T.step[st][s][q] = (uint8_t)((t & kStMask) | f);
+      }
+  for (int st = 0; st <= kNRun; ++st)
+    for (int s = 0; s <= kSymCont; ++s)
+      for (int q = 0; q < 4; ++q)
+        for (int ss = 0; ss < 2; ++ss) {
+          const bool last_sp = q & 1, crx = q & 2;
+          int cur = st, f = 0;
+          if (ss) {  // a string start settles the open chunk (presplit_bytes, sync code 1)
+            if (cur == kWsRun && cl && !crx) f |= kLCr;
+            if (!cl && (cur == kAL || cur == kAVR)) f |= kLRetro;
+            cur = kStart;
+          }
+          int t = T.t[cur][s];
+          if (t & kWsx) {
+            if (crx) {
+              t = kEnd;
+            } else {
+              f |= kLWs | (cl ? kLCr : 0);
+              t = T.pre[last_sp][s];
+            }
+          } else if (t & kRetro) {
+            f |= kLRetro;
+          }
+          if (t & kEnd) {
+            f |= kLEnd;
+            t = T.t[kStart][s];
+          }
+          T.lane[lane_index(st, s, q, ss)] = (uint8_t)((t & kStMask) | f);
+        }
   return T;
 }
 
 // Symbol of a decoded non-ASCII code point (class from the UCD table; U+017F folds to 's')
 SW_HD inline int nonascii_sym(uint32_t cp, int cls, bool cl) {
-  if (cls == kL) return (cl && cp == 0x17F) ? kSymLs : kSymL;
-  if (cls == kN) return kSymN;
-  if (cls == kS) return kSymWs;
-  return kSymO;
+  static_assert(kSymO == 0 && kSymL == 6 && kSymN == 7 && kSymWs == 10, "symbol numbering");
+  const int s = (int)((0x0A070600u >> (8 * cls)) & 0xFFu);  // class other, L, N, S -> symbol
+  return (cl && cp == 0x17F) ? (int)kSymLs : s;              // (U+017F is a letter)
 }
 
 // The state a sync position starts in, or -1.  `Ctx`: byte(p), string bounds a, b (p in [a, b)).
@@ -255,13 +316,17 @@ SW_HD inline void presplit_segment(Ctx& x, I s0, I s1, bool cl, bool none) {
 }
 
 // ---- byte-stepped form (the device's fast path) -------------------------------------------
-// A workgroup first computes, for every byte of its window, one INFO byte: the symbol of the
-// code point starting there (kSymCont for a continuation byte) and its sync code
+// A workgroup first computes, for every byte of its window, one INFO byte: bits 0-3 the symbol
+// of the code point starting there (kSymCont for a continuation byte), bit 4 "a string starts
+// here", bits 5-7 the sync code less one (info_sync):
 //   0 none, 1 string start, 2 ' ' + ASCII letter, 3 ASCII letter after '\n',
 //   4 fourth ASCII letter in a row, 5 ASCII punctuation pair, 6 (GPT-2) ASCII digit pair;
-// the lanes then step one byte at a time through the info bytes.
+// the lanes then step one byte at a time through the info bytes.  Any sync: info & 0xF0.
 
-constexpr int sync_init_state(uint32_t sc) { return sc <= 3 ? kStart : sc == 4 ? kLRun : sc == 5 ? kORun : kNRun; }
+constexpr int sync_init_state(uint32_t sc) {
+  return sc <= 3 ? kStart : sc == 4 ? kLRun : sc == 5 ? kORun : kNRun;
+}
+SW_HD constexpr uint32_t info_sync(uint32_t v) { return (v & 16u) ? 1u : (v >> 5) ? (v >> 5) + 1u : 0u; }
 
 // Info bytes are computed four at a time with SWAR masks: a 32-bit word holds 4 bytes, and a
 // mask has bit 7 of a byte lane set where that byte has the property.  A group's context is
@@ -334,21 +399,24 @@ SW_HD inline LeadCarry lead_carry(const uint32_t* u, uint32_t ss) {
   return LeadCarry{l.v2, l.v3, l.v4};
 }
 
+// The info word of u[1] given the ASCII classes of u[0], u[1], u[2] (p, c, n; a run of groups
+// passes them on, so each word is classified once).
 template <class Asc, class Cls>
-SW_HD inline uint32_t info4(const uint32_t* u, uint32_t ss, const Asc* asc, const Cls& cls, bool cl, LeadCarry& carry) {
+SW_HD inline uint32_t info4_core(const uint32_t* u, uint32_t ss, const Ascii& p, const Ascii& c, const Ascii& n,
+                                 Asc asc, const Cls& cls, bool cl, LeadCarry& carry) {
   const uint32_t ssp = spread4(ss), ssc = spread4(ss >> 4), ssn = spread4(ss >> 8);
   // sync codes (ASCII lanes only)
-  const Ascii p = ascii_classes(u[0]), c = ascii_classes(u[1]), n = ascii_classes(u[2]);
   const uint32_t sc2 = c.spc & after(c.let, n.let, 1) & ~after(ssc, ssn, 1);
   const uint32_t sc3 = c.let & before(p.nl, c.nl, 1);
   const uint32_t sc4 = c.let & before(p.let, c.let, 1) & before(p.let, c.let, 2) & before(p.let, c.let, 3) &
                        ~before(ssp, ssc, 1) & ~before(ssp, ssc, 2) & ~sc3;
   const uint32_t sc5 = c.oth & before(p.oth, c.oth, 1);
   const uint32_t sc6 = cl ? 0u : c.dig & before(p.dig, c.dig, 1);
-  uint32_t code = (sc2 >> 7) * 2 + (sc3 >> 7) * 3 + (sc4 >> 7) * 4 + (sc5 >> 7) * 5 + (sc6 >> 7) * 6;
-  code = (code & ~((ssc >> 7) * 0xFF)) | (ssc >> 7);  // a string start is sync code 1
+  // (bits 5-7: the code less one; bit 4: a string start, which takes precedence)
+  const uint32_t code = (sc2 >> 7) * 2 + (sc3 >> 7) * 4 + (sc4 >> 7) * 6 + (sc5 >> 7) * 8 + (sc6 >> 7) * 10 + (ssc >> 7);
   // symbols: ASCII from the table; continuation bytes of a valid sequence; decoded leads
   uint32_t sym = 0;
+#pragma unroll
   for (int k = 0; k < 4; ++k) {
     const uint32_t b = (u[1] >> (8 * k)) & 0xFF;
     sym |= (uint32_t)asc[b & 0x7F] << (8 * k);
@@ -361,20 +429,30 @@ SW_HD inline uint32_t info4(const uint32_t* u, uint32_t ss, const Asc* asc, cons
     const uint32_t high = u[1] & kLane7;
     // high lanes: kSymO, unless a continuation (kSymCont) or a lead (its code point's symbol)
     sym = (sym & ~((high >> 7) * 0xFF)) | ((contv >> 7) * kSymCont);
+    // the leads, one at a time (a word holds one or two on non-ASCII text)
+    const uint64_t w64 = ((uint64_t)u[2] << 32) | u[1];
     uint32_t leads = any_lead(l);
     while (leads) {
       const int k = __builtin_ctz(leads) >> 3;
       leads &= leads - 1;
       const int L = ((l.v2 >> (8 * k + 7)) & 1) ? 2 : ((l.v3 >> (8 * k + 7)) & 1) ? 3 : 4;
-      const uint64_t w = (((uint64_t)u[2] << 32) | u[1]) >> (8 * k);
+      const uint64_t w = w64 >> (8 * k);
       uint32_t v = (uint32_t)w & (L == 2 ? 0x1F : L == 3 ? 0x0F : 0x07);
       for (int q = 1; q < L; ++q) v = (v << 6) | (uint32_t)((w >> (8 * q)) & 0x3F);
-      sym |= (uint32_t)nonascii_sym(v, cls(v), cl) << (8 * k);
+      // Cls: near(cp) for the BMP (no branch), far(cp) past it
+      int c = cls.near(v < 0x10000u ? v : 0x80u);
+      if (v >= 0x10000u) c = cls.far(v);
+      sym |= (uint32_t)nonascii_sym(v, c, cl) << (8 * k);
     }
   } else {
     carry = LeadCarry{0, 0, 0};
   }
   return sym | (code << 4);
+}
+
+template <class Asc, class Cls>
+SW_HD inline uint32_t info4(const uint32_t* u, uint32_t ss, Asc asc, const Cls& cls, bool cl, LeadCarry& carry) {
+  return info4_core(u, ss, ascii_classes(u[0]), ascii_classes(u[1]), ascii_classes(u[2]), asc, cls, cl, carry);
 }
 
 // The byte-stepped parse from r (state and whitespace-run registers in/out) while r < r_end:
@@ -386,7 +464,7 @@ SW_HD inline bool presplit_bytes(Ctx& x, I& r, I s1, I r_end, bool at_end, bool 
                                  bool& last_sp) {
   for (; r < r_end; ++r) {
     const uint32_t v = x.info(r);
-    const uint32_t sc = v >> 4;
+    const uint32_t sc = info_sync(v);
     if (sc != 0 && (sc == 1 || r >= s1)) {  // settle the open chunk
       if (st == kWsRun && cl && last_cr >= 0) {
         if (sc == 1 || sc == 2) {

@@ -26,11 +26,14 @@ namespace sw {
 __constant__ uint8_t c_ucd1[SW_UCD_STAGE1_SIZE] = SW_UCD_STAGE1_INIT;
 __constant__ uint8_t c_ucd2[SW_UCD_STAGE2_SIZE] = SW_UCD_STAGE2_INIT;
 
-__constant__ fsm::Tables c_fsm[2] = {fsm::make_tables(true), fsm::make_tables(false)};
+__constant__ __attribute__((aligned(16))) fsm::Tables c_fsm[2] = {fsm::make_tables(true), fsm::make_tables(false)};
 
 #define SW_LDS __attribute__((address_space(3)))  // (explicit, so reads are ds_read, not flat)
 
 __device__ inline int ucd_class(uint32_t cp) {
+#ifdef SW_PS_NOUCD  // (diagnostic timing builds only)
+  return (int)(cp & 1);
+#endif
   if (cp > 0x10FFFF) return kOther;
   const uint32_t blk = c_ucd1[cp >> 8];
   const uint32_t v = c_ucd2[blk * 64 + ((cp & 255) >> 2)];
@@ -41,7 +44,11 @@ struct UcdClass {
   __device__ int operator()(uint32_t cp) const { return ucd_class(cp); }
 };
 
-struct PsBits {  // one lane's chunk starts, gathered one 64-bit word at a time
+#ifndef SW_PS_ABL
+#define SW_PS_ABL 0  // diagnostic ablations (timing only, wrong bitmaps): 1 staging, 2 + info, 3 + lanes
+#endif
+
+struct PsBits {  // a lane's chunk starts past the info bytes, gathered one 64-bit word at a time
   uint64_t* bits;
   int64_t widx;
   uint64_t word;
@@ -63,17 +70,31 @@ struct PsBits {  // one lane's chunk starts, gathered one 64-bit word at a time
   }
 };
 
+struct LdsOr {
+  uint32_t* b;  // (a __shared__ array)
+  __device__ void operator()(int w, uint32_t v) const {
+    __hip_atomic_fetch_or(&b[w], v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  }
+};
+
+__constant__ __attribute__((aligned(16))) UcdBmp c_ucd_bmp = make_ucd_bmp();
+
 __global__ void __launch_bounds__(kPsThreads) k_presplit(const uint8_t* bytes, int64_t n_bytes, const int64_t* str_off,
                                                          int64_t n_str, int pattern, uint64_t* bits) {
   __shared__ __attribute__((aligned(16))) uint8_t s_buf[kPsRaw];  // bytes, then info bytes
-  __shared__ uint32_t s_ss[kPsSsWords];  // string starts (and the batch end) in the window
-  __shared__ fsm::Tables s_tab;
+  // string starts (and the batch end) in the window; after the info phase, the chunk starts
+  // of [b0, b0 + block + halo)
+  __shared__ __attribute__((aligned(8))) uint32_t s_ss[kPsSsWords];
+  __shared__ __attribute__((aligned(16))) uint8_t s_step[sizeof(PsStepTab)];
+  __shared__ __attribute__((aligned(16))) uint8_t s_ucd[(kUcdBmpBytes + 15) & ~15];
   __shared__ int64_t s_first;
+  static_assert(kPsSsWords >= 2 * kPsOutWords, "the chunk-start bitmap reuses s_ss");
   const int tid = threadIdx.x;
   const PsGeom G = ps_geom(blockIdx.x, n_bytes);
   const bool cl = pattern == 0, none = pattern == 2;
+  const fsm::Tables* ftab = &c_fsm[pattern == 1 ? 1 : 0];
 
-  // 1. stage [wb, wend) (zeros outside the batch and in the tail) and the pattern's tables
+  // 1. stage [wb, wend) (zeros outside the batch and in the tail) and the tables
   {
     const bool aligned = ((uintptr_t)bytes & 15) == 0;
     for (int i = tid * 16; i < kPsRaw; i += kPsThreads * 16) {
@@ -85,8 +106,17 @@ __global__ void __launch_bounds__(kPsThreads) k_presplit(const uint8_t* bytes, i
       }
     }
     for (int i = tid; i < kPsSsWords; i += kPsThreads) s_ss[i] = 0;
-    const uint8_t* src = (const uint8_t*)&c_fsm[pattern == 1 ? 1 : 0];
-    for (int i = tid; i < (int)sizeof(fsm::Tables); i += kPsThreads) ((uint8_t*)&s_tab)[i] = src[i];
+    {  // asc and step of the pattern, the compact BMP class table
+      const uint32_t* a = (const uint32_t*)ftab->asc;
+      const uint32_t* ln = (const uint32_t*)ftab->lane;
+      static_assert(offsetof(PsStepTab, lane) == 128 && sizeof(ftab->lane) % 4 == 0, "PsStepTab layout");
+      for (int i = tid; i < 32; i += kPsThreads) ((uint32_t*)s_step)[i] = a[i];
+      for (int i = tid; i < (int)sizeof(ftab->lane) / 4; i += kPsThreads) ((uint32_t*)s_step)[32 + i] = ln[i];
+      const uint32_t* u = (const uint32_t*)&c_ucd_bmp;
+      for (int i = tid; i < 64; i += kPsThreads) ((uint32_t*)s_ucd)[i] = u[i];
+      const uint32_t* u2 = (const uint32_t*)c_ucd_bmp.s2;
+      for (int i = tid; i < 16 * kUcdBmp.nblk; i += kPsThreads) ((uint32_t*)s_ucd)[64 + i] = u2[i];
+    }
     if (tid == 0) {  // first string starting at or after wb
       int64_t lo = 0, hi = n_str;
       while (lo < hi) {
@@ -106,21 +136,54 @@ __global__ void __launch_bounds__(kPsThreads) k_presplit(const uint8_t* bytes, i
   }
   __syncthreads();
 
-  // 2. info bytes, in place of the staged bytes
-  if (!none) {
-    SW_LDS uint32_t* w32 = (SW_LDS uint32_t*)s_buf;
-    const PsInfoRegs regs = ps_info_load(w32, tid);
-    __syncthreads();
-    ps_info_convert(w32, (const SW_LDS uint32_t*)s_ss, ((const SW_LDS fsm::Tables*)&s_tab)->asc, UcdClass{}, cl,
-                    G.info_hi, tid, regs);
-    __syncthreads();
+  if (none) {  // the chunks are the strings: the block's words straight from the string starts
+    for (int i = tid; i < kPsBlock / 64; i += kPsThreads) {
+      const int64_t gw = (G.b0 >> 6) + i;
+      if (64 * gw >= n_bytes) break;
+      uint64_t v = ps_none_word((const uint32_t*)s_ss, i);
+      if (64 * gw + 64 > n_bytes) v &= (1ULL << (n_bytes - 64 * gw)) - 1;
+      bits[gw] = v;
+    }
+    return;
   }
+#if SW_PS_ABL == 1
+  return;
+#endif
+
+  // 2. info bytes, in place of the staged bytes
+  SW_LDS uint32_t* w32 = (SW_LDS uint32_t*)s_buf;
+  const PsInfoRegs regs = ps_info_load(w32, tid);
+  __syncthreads();
+  {
+    const PsUcd<const SW_LDS uint8_t*, UcdClass> cls{(const SW_LDS uint8_t*)s_ucd, (const SW_LDS uint8_t*)s_ucd + 256,
+                                                     UcdClass{}};
+    ps_info_convert(w32, (const SW_LDS uint32_t*)s_ss, (const SW_LDS uint8_t*)s_step, cls, cl, G.info_hi, tid, regs);
+  }
+  __syncthreads();
+  for (int i = tid; i < 2 * kPsOutWords; i += kPsThreads) s_ss[i] = 0;  // (now the chunk-start bitmap)
+  __syncthreads();
+#if SW_PS_ABL == 2
+  return;
+#endif
 
   // 3. this lane's segment
-  PsBits out{bits, (G.b0 >> 6) + tid, 0};
-  ps_lane(G, tid, (const SW_LDS uint8_t*)s_buf, (const SW_LDS uint32_t*)s_ss, (const SW_LDS fsm::Tables*)&s_tab,
-          bytes, n_bytes, str_off, n_str, cl, none, out, UcdClass{});
-  out.flush();
+  PsWinBits<LdsOr> lb{LdsOr{s_ss}};
+  PsBits gout{bits, -1, 0};
+  ps_lane(G, tid, (const SW_LDS uint32_t*)s_buf, (const SW_LDS PsStepTab*)s_step, ftab, bytes, n_bytes, str_off,
+          n_str, cl, lb, gout, UcdClass{});
+  __syncthreads();
+#if SW_PS_ABL == 3
+  return;
+#endif
+
+  // 4. the window's chunk starts into the global bitmap (OR: the previous workgroup's lanes
+  //    may have run into this block, and this one's into the next)
+  for (int i = tid; i < kPsOutWords; i += kPsThreads) {
+    const int64_t gw = (G.b0 >> 6) + i;
+    if (64 * gw >= n_bytes) break;
+    const uint64_t v = (uint64_t)s_ss[2 * i] | ((uint64_t)s_ss[2 * i + 1] << 32);
+    if (v) atomicOr((unsigned long long*)&bits[gw], (unsigned long long)v);
+  }
 }
 
 // number of set bits (chunks) in the bitmap

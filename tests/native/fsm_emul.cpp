@@ -70,7 +70,7 @@ void emul_bytes(const uint8_t* bytes, const int64_t* off, int64_t n_str, bool cl
       sb |= S(r0 - 4 + j) << j;
     }
     if (r0 % 72 == 0) carry = sw::fsm::lead_carry(u, sb);  // (the device: a run of 18 groups per thread)
-    const uint32_t w = sw::fsm::info4(u, sb, tab->asc, cls, cl, carry);
+    const uint32_t w = sw::fsm::info4(u, sb, tab->asc, sw::PsUcdFull<decltype(cls)>{cls}, cl, carry);
     for (int k = 0; k < 4; ++k) inf[r0 + k] = (uint8_t)(w >> (8 * k));
   }
   ByteCtx x{inf.data(), tab, bits};
@@ -79,7 +79,7 @@ void emul_bytes(const uint8_t* bytes, const int64_t* off, int64_t n_str, bool cl
     int64_t r = s0;
     while (r < s1 && !(inf[r] >> 4)) ++r;
     if (r == s1) continue;
-    int st = sw::fsm::sync_init_state(inf[r] >> 4);
+    int st = sw::fsm::sync_init_state(sw::fsm::info_sync(inf[r]));
     int64_t last_cr = -1, last_ws = 0;
     bool last_sp = false;
     sw::fsm::presplit_bytes<int64_t>(x, r, s1, n, true, cl, st, last_cr, last_ws, last_sp);
@@ -113,7 +113,7 @@ void emul_device(const uint8_t* bytes, const int64_t* off, int64_t n_str, int pa
   const bool cl = pattern == 0, none = pattern == 2;
   const sw::fsm::Tables* tab = pattern == 1 ? &kGpt2 : &kCl;
   auto cls = [](uint32_t cp) { return cls_of(cp); };
-  std::vector<uint32_t> w32(sw::kPsRaw / 4), ss(sw::kPsSsWords);
+  std::vector<uint32_t> w32(sw::kPsRaw / 4), ss(sw::kPsSsWords), wb(2 * sw::kPsOutWords);
   for (int64_t blk = 0; blk * sw::kPsBlock < n; ++blk) {
     const sw::PsGeom G = sw::ps_geom(blk, n);
     uint8_t* buf = (uint8_t*)w32.data();
@@ -122,22 +122,39 @@ void emul_device(const uint8_t* bytes, const int64_t* off, int64_t n_str, int pa
       buf[i] = (g >= 0 && g < G.wend) ? bytes[g] : 0;
     }
     std::fill(ss.begin(), ss.end(), 0u);
+    std::fill(wb.begin(), wb.end(), 0u);
     for (int64_t i = 0; i <= n_str; ++i) {
       if (off[i] < G.wb || off[i] > G.wend) continue;
       const int r = (int)(off[i] - G.wb);
       ss[r >> 5] |= 1u << (r & 31);
     }
-    if (!none) {
-      std::vector<sw::PsInfoRegs> regs(sw::kPsThreads);
-      for (int t = 0; t < sw::kPsThreads; ++t) regs[t] = sw::ps_info_load(w32.data(), t);
-      for (int t = 0; t < sw::kPsThreads; ++t)
-        sw::ps_info_convert(w32.data(), (const uint32_t*)ss.data(), tab->asc, cls, cl, G.info_hi, t, regs[t]);
+    if (none) {
+      for (int i = 0; i < sw::kPsBlock / 64; ++i) {
+        const int64_t gw = (G.b0 >> 6) + i;
+        if (64 * gw >= n) break;
+        uint64_t v = sw::ps_none_word((const uint32_t*)ss.data(), i);
+        if (64 * gw + 64 > n) v &= (1ULL << (n - 64 * gw)) - 1;
+        bits[gw] = v;
+      }
+      continue;
     }
+    std::vector<sw::PsInfoRegs> regs(sw::kPsThreads);
+    for (int t = 0; t < sw::kPsThreads; ++t) regs[t] = sw::ps_info_load(w32.data(), t);
+    // the kernel's class lookup: the compact BMP table, the full table past it
+    const sw::PsUcd<const uint8_t*, decltype(cls)> ucd{sw::kUcdBmp.s1, sw::kUcdBmp.s2, cls};
+    for (int t = 0; t < sw::kPsThreads; ++t)
+      sw::ps_info_convert(w32.data(), (const uint32_t*)ss.data(), tab->asc, ucd, cl, G.info_hi, t, regs[t]);
+    uint32_t* wbp = wb.data();
+    auto orw = [wbp](int w, uint32_t v) { wbp[w] |= v; };
     for (int t = 0; t < sw::kPsThreads; ++t) {
-      HostBits out{bits, (G.b0 >> 6) + t, 0};
-      sw::ps_lane(G, t, (const uint8_t*)w32.data(), (const uint32_t*)ss.data(), tab, bytes, n, off, n_str, cl, none,
-                  out, cls);
-      out.flush();
+      sw::PsWinBits<decltype(orw)> lb{orw};
+      HostBits gout{bits, -1, 0};
+      sw::ps_lane(G, t, (const uint32_t*)w32.data(), tab, tab, bytes, n, off, n_str, cl, lb, gout, cls);
+    }
+    for (int i = 0; i < sw::kPsOutWords; ++i) {
+      const int64_t gw = (G.b0 >> 6) + i;
+      if (64 * gw >= n) break;
+      bits[gw] |= (uint64_t)wb[2 * i] | ((uint64_t)wb[2 * i + 1] << 32);
     }
   }
 }

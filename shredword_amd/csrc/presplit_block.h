@@ -18,56 +18,12 @@
 #include <cstdint>
 
 #include "presplit_fsm.h"
-#include "ucd_tables.h"
 
 namespace sw {
 
-// ---- Unicode classes of the BMP for LDS --------------------------------------------------
-// ucd_tables.h's two-stage table restricted to U+0000..U+FFFF, its blocks renumbered densely,
-// built at compile time: 256 + 64 * nblk bytes (~3.6 KB) instead of 12.8 KB, so a workgroup
-// keeps it in LDS; code points past the BMP use the full table (global / constant memory).
-constexpr int kUcdBmpMaxBlocks = 64;
-struct UcdBmp {
-  uint8_t s1[256];
-  uint8_t s2[kUcdBmpMaxBlocks * 64];
-  int nblk;
-};
-constexpr uint8_t kUcdStage1[SW_UCD_STAGE1_SIZE] = SW_UCD_STAGE1_INIT;
-constexpr uint8_t kUcdStage2[SW_UCD_STAGE2_SIZE] = SW_UCD_STAGE2_INIT;
-constexpr UcdBmp make_ucd_bmp() {
-  UcdBmp t{};
-  int map[SW_UCD_NBLOCKS] = {};
-  for (int b = 0; b < SW_UCD_NBLOCKS; ++b) map[b] = -1;
-  for (int i = 0; i < 256; ++i) {
-    const int b = kUcdStage1[i];
-    if (map[b] < 0) {
-      map[b] = t.nblk++;
-      for (int j = 0; j < 64; ++j) t.s2[map[b] * 64 + j] = kUcdStage2[b * 64 + j];
-    }
-    t.s1[i] = (uint8_t)map[b];
-  }
-  return t;
-}
-constexpr UcdBmp kUcdBmp = make_ucd_bmp();
-static_assert(kUcdBmp.nblk <= kUcdBmpMaxBlocks, "BMP blocks");
-constexpr int kUcdBmpBytes = 256 + 64 * kUcdBmp.nblk;
-
-// class of a code point: near(cp) for the BMP from the compact table (s1, s2: its copy),
-// far(cp) past it from the full one (fn)
-template <class P, class Far>
-struct PsUcd {
-  P s1, s2;
-  Far fn;
-  SW_HD int near(uint32_t cp) const {
-    const uint32_t blk = s1[cp >> 8];
-    const uint32_t v = s2[blk * 64 + ((cp & 255) >> 2)];
-    return (int)((v >> ((cp & 3) * 2)) & 3);
-  }
-  SW_HD int far(uint32_t cp) const { return fn(cp); }
-  SW_HD int operator()(uint32_t cp) const { return cp < 0x10000u ? near(cp) : far(cp); }
-};
-
-// the same interface over one full-table function (host)
+// ---- Unicode classes ----------------------------------------------------------------------
+// Cls interface of fsm::info4_high: near(cp) for the BMP, far(cp) past it, operator() for any.
+// one full-table function (ucd_tables.h) behind that interface
 template <class Fn>
 struct PsUcdFull {
   Fn fn;
@@ -115,10 +71,13 @@ SW_HD inline PsGeom ps_geom(int64_t block, int64_t n_bytes) {
 // the parts of fsm::Tables the converged phases read (kept in LDS)
 struct PsStepTab {
   uint8_t asc[128];
-  uint8_t lane[1280];
+  uint16_t lane[32 * 4 * 13];
 };
 
 // ---- phase 2: info bytes in place of the staged bytes -------------------------------------
+// Pass 1 (every group, ps_info_convert) and pass 2 (groups holding a byte >= 0x80, spread
+// densely over the threads: ps_high_select, ps_high_group); see presplit_fsm.h info4_ascii /
+// info4_high.
 struct PsInfoRegs {
   uint32_t prev, first, edge;  // the words before, at and after this thread's run
 };
@@ -129,31 +88,81 @@ SW_HD inline PsInfoRegs ps_info_load(W32 w32, int tid) {
   return PsInfoRegs{w32[wfirst - 1], w32[wfirst], w32[wfirst + kPsGroups]};
 }
 
-// converts this thread's kPsGroups words in order, holding the raw words it still needs in
-// registers (its neighbours' edge words came from ps_info_load, before anyone wrote)
-template <class W32, class SS, class Asc, class Cls>
-SW_HD inline void ps_info_convert(W32 w32, SS s_ss, Asc asc, const Cls& cls, bool cl, int info_hi, int tid,
-                                  const PsInfoRegs& regs) {
+constexpr int kPsHiWords = kPsGroups * kPsThreads / 32;  // bitmask of the groups with a byte >= 0x80
+
+// string-start bits of window bytes r0 - 4 .. r0 + 7
+template <class SS>
+SW_HD inline uint32_t ps_ss_at(SS s_ss, int r0) {
+  const int q = r0 - 4;
+  const uint64_t two = (uint64_t)s_ss[q >> 5] | ((uint64_t)s_ss[(q >> 5) + 1] << 32);
+  return (uint32_t)(two >> (q & 31)) & 0xFFF;
+}
+
+// pass 1: converts this thread's kPsGroups words in order (info4_ascii), holding the raw words
+// it still needs in registers (its neighbours' edge words came from ps_info_load, before
+// anyone wrote); marks the words with a byte >= 0x80 for pass 2 (mark(j), j = group index in
+// the window's info)
+template <class W32, class SS, class Asc, class Mark>
+SW_HD inline void ps_info_convert(W32 w32, SS s_ss, Asc asc, bool cl, int info_hi, int tid, const PsInfoRegs& regs,
+                                  const Mark& mark) {
   const int wfirst = kPsPre / 4 + tid * kPsGroups;
-  auto ss_at = [&](int r0) {  // string-start bits of bytes r0 - 4 .. r0 + 7
-    const int q = r0 - 4;
-    const uint64_t two = (uint64_t)s_ss[q >> 5] | ((uint64_t)s_ss[(q >> 5) + 1] << 32);
-    return (uint32_t)(two >> (q & 31)) & 0xFFF;
-  };
   uint32_t u[3] = {regs.prev, regs.first, 0};
-  fsm::LeadCarry carry = fsm::lead_carry(u, ss_at((wfirst - 1) * 4 + 4));
   fsm::Ascii ap = fsm::ascii_classes(u[0]), ac = fsm::ascii_classes(u[1]), an;
   for (int i = 0; i < kPsGroups; ++i) {
     const int r0 = (wfirst + i) * 4;
     if (r0 >= info_hi) break;
     u[2] = i + 1 < kPsGroups ? w32[wfirst + i + 1] : regs.edge;
     an = fsm::ascii_classes(u[2]);
-    w32[wfirst + i] = fsm::info4_core(u, ss_at(r0), ap, ac, an, asc, cls, cl, carry);
+    w32[wfirst + i] = fsm::info4_ascii(u, ps_ss_at(s_ss, r0), ap, ac, an, asc, cl);
+    if (u[1] & fsm::kLane7) mark(tid * kPsGroups + i);
     u[0] = u[1];
     u[1] = u[2];
     ap = ac;
     ac = an;
   }
+}
+
+// window word o / 4 of the staged bytes, re-read from global memory (zeros outside [0, wend),
+// as staged)
+SW_HD inline uint32_t ps_raw_word(const uint8_t* bytes, const PsGeom& G, int o) {
+  const int64_t g = G.wb + o;
+  if (g >= 0 && g + 4 <= G.wend && (((uintptr_t)bytes & 3) == 0)) return *(const uint32_t*)(bytes + g);
+  uint32_t v = 0;
+  for (int k = 0; k < 4; ++k) v |= (g + k >= 0 && g + k < G.wend) ? (uint32_t)bytes[g + k] << (8 * k) : 0u;
+  return v;
+}
+
+// pass 2, for the j-th group of the window's info (one marked by pass 1): its high bytes'
+// symbols, from the raw bytes around it (global memory: pass 1 overwrote the staged copy)
+template <class W32, class SS, class Cls>
+SW_HD inline void ps_high_group(W32 w32, SS s_ss, const Cls& cls, bool cl, const PsGeom& G, const uint8_t* bytes,
+                                int j) {
+  const int wi = kPsPre / 4 + j;
+  const uint32_t u[3] = {ps_raw_word(bytes, G, 4 * wi - 4), ps_raw_word(bytes, G, 4 * wi),
+                         ps_raw_word(bytes, G, 4 * wi + 4)};
+  w32[wi] = fsm::info4_high(w32[wi], u, ps_ss_at(s_ss, 4 * wi), cls, cl);
+}
+
+// the k-th set bit of the marks (pre: exclusive prefix counts of the mark words, kPsHiWords + 1)
+template <class HP, class HM>
+SW_HD inline int ps_high_select(HP pre, HM marks, int k) {
+  int lo = 0, hi = kPsHiWords - 1;  // last word with pre <= k
+  while (lo < hi) {
+    const int m = (lo + hi + 1) >> 1;
+    if ((int)pre[m] <= k) lo = m; else hi = m - 1;
+  }
+  uint32_t x = marks[lo];
+  int r = k - (int)pre[lo], pos = 0;
+#pragma unroll
+  for (int sh = 16; sh >= 1; sh >>= 1) {
+    const int c = __builtin_popcount(x & ((1u << sh) - 1u));
+    if (r >= c) {
+      r -= c;
+      x >>= sh;
+      pos += sh;
+    }
+  }
+  return 32 * lo + pos;
 }
 
 // ---- phase 3: one lane's segment -----------------------------------------------------------
@@ -224,30 +233,27 @@ SW_HD inline bool ps_lane_steps(InfoW info, TabP tab, LB& lb, int& r, int s1, in
       const int pos = 4 * w + k;
       const bool act = !done && pos >= r0 && pos < r_end;
       const uint32_t v = (cur >> (8 * k)) & 0xFFu;
-#ifdef SW_PS_NOOVERRUN  // (diagnostic timing builds only: wrong bitmaps)
-      const bool fin = act && pos >= s1;
-#else
       const bool fin = act && pos >= s1 && (v & 0xF0u);
-#endif
       fin_pos = fin ? pos : fin_pos;
       fin_v = fin ? v : fin_v;
       const bool step = act && !fin;
-      const uint32_t sym = v & 15u, ssb = (v >> 4) & 1u;
-      const uint32_t q = (last_sp ? 1u : 0u) | ((cl && last_cr == pos) ? 2u : 0u);
-      const uint32_t E = tab->lane[fsm::lane_index(st, (int)sym, (int)q, (int)ssb)];
-      near |= ((step && (E & fsm::kLRetro)) ? 1u : 0u) << k;
-      near |= ((step && (E & fsm::kLEnd)) ? 2u : 0u) << k;
-      const bool e_cr = step && (E & fsm::kLCr) && last_cr >= 0;
-      const bool e_ws = step && (E & fsm::kLWs);
+      const uint32_t q = (last_sp ? 1u : 0u) | (last_cr == pos ? 2u : 0u);  // (last_cr is -1 for GPT-2)
+#ifdef SW_PS_NOCHAIN  // (diagnostic timing builds only: wrong bitmaps)
+      const uint32_t E = step ? (uint32_t)tab->lane[fsm::lane_index(v & 31u, q, k)] : 0u;
+#else
+      const uint32_t E = step ? (uint32_t)tab->lane[fsm::lane_index(v & 31u, q, st)] : 0u;
+#endif
+      near |= ((E & fsm::kLRetro) ? 1u : 0u) << k;
+      near |= ((E & fsm::kLEnd) ? 2u : 0u) << k;
+      const bool e_cr = (E & fsm::kLCr) && last_cr >= 0;
+      const bool e_ws = E & fsm::kLWs;
       near |= (e_cr && last_cr >= base) ? 1u << (last_cr - base) : 0u;
       near |= (e_ws && last_ws >= base) ? 1u << (last_ws - base) : 0u;
       far_cr = (e_cr && last_cr < base) ? last_cr : far_cr;
       far_ws = (e_ws && last_ws < base) ? last_ws : far_ws;
-      const bool isws = step && ((0x700u >> sym) & 1u);
-      const bool in_run = st == fsm::kWsRun && !ssb;
-      last_cr = isws ? ((cl && sym == fsm::kSymCr) ? pos + 1 : (in_run ? last_cr : -1)) : last_cr;
-      last_ws = isws ? pos : last_ws;
-      last_sp = isws ? sym == fsm::kSymSp : last_sp;
+      last_ws = (E & fsm::kLWsSet) ? pos : last_ws;
+      last_sp = (E & fsm::kLWsSet) ? (E & fsm::kLSp) != 0 : last_sp;
+      last_cr = (E & fsm::kLCrSet) ? pos + 1 : (E & fsm::kLCrClear) ? -1 : last_cr;
       st = step ? (int)(E & fsm::kStMask) : st;
       done = done || fin;
     }

@@ -53,20 +53,17 @@ struct Tables {
   uint8_t asc[128];      // symbol of an ASCII byte
   uint8_t t[16][16];     // [state][symbol] -> next state | flags
   uint8_t pre[2][16];    // after a whitespace run, [its last code point is ' '][symbol]
-  // one whole step (the device's lane loop): [state][symbol][q], q = last_sp | (cl && last_cr
-  // == this position) << 1 -> next state | kStepEnd (a chunk starts here) | kStepRetro (one
-  // starts at the previous byte) | kStepWsx (a whitespace run ended: its \r\n end, if any, and
-  // its last code point start chunks).  The kEnd re-dispatch from kStart is folded in.
-  uint8_t step[16][16][4];
-  // the device lane's step over an info byte (presplit_block.h): index lane_index(state, symbol,
-  // q, string start) -> next state | kLEnd (a chunk starts here) | kLRetro (one starts at the
-  // previous byte) | kLCr (one starts at the open whitespace run's \r\n end, if any) | kLWs
-  // (one starts at its last code point).  A string start first settles the open chunk.
-  uint8_t lane[1280];
+  // the device lane's step over an info byte (presplit_block.h): lane[lane_index(low 5 bits of
+  // the info byte = symbol | string start << 4, q, state)] -> next state | kLEnd (a chunk starts
+  // here) | kLRetro (one starts at the previous byte) | kLCr (one starts at the open whitespace
+  // run's \r\n end, if any) | kLWs (one starts at its last code point) | the whitespace-run
+  // registers' update: kLWsSet (last_ws = here, last_sp = kLSp), kLCrSet / kLCrClear (last_cr =
+  // here + 1 / none).  A string start first settles the open chunk.
+  uint16_t lane[32 * 4 * 13];
 };
-constexpr uint8_t kStepEnd = 16, kStepRetro = 32, kStepWsx = 64;
-constexpr uint8_t kLEnd = 16, kLRetro = 32, kLCr = 64, kLWs = 128;
-SW_HD constexpr int lane_index(int st, int sym, int q, int ss) { return ((st * 12 + sym) * 4 + q) * 2 + ss; }
+constexpr uint16_t kLEnd = 16, kLRetro = 32, kLCr = 64, kLWs = 128, kLWsSet = 256, kLSp = 512, kLCrSet = 1024,
+                   kLCrClear = 2048;
+SW_HD constexpr int lane_index(uint32_t sym_ss, uint32_t q, int st) { return (int)(sym_ss * 52 + q * 13) + st; }
 
 constexpr bool sym_letter(int s) { return s >= kSymLs && s <= kSymL; }
 constexpr bool sym_space(int s) { return s == kSymSp || s == kSymCr || s == kSymWs; }
@@ -126,32 +123,15 @@ constexpr Tables make_tables(bool cl) {
       T.pre[1][s] = L ? kLRun : N ? kNRun : O ? kORun : kEnd;
     }
   }
-  for (int st = 0; st < 16; ++st)
-    for (int s = 0; s < 16; ++s)
-      for (int q = 0; q < 4; ++q) {
-        const bool last_sp = q & 1, crx = q & 2;
-        int t = T.t[st][s], f = 0;
-        if (t & kWsx) {
-          if (crx) {
-            t = kEnd;
-          } else {
-            f |= kStepWsx;
-            t = T.pre[last_sp][s];
-          }
-        } else if (t & kRetro) {
-          f |= kStepRetro;
-        }
-        if (t & kEnd) {
-          f |= kStepEnd;
-          t = T.t[kStart][s];
-        }
-        T.step[st][s][q] = (uint8_t)((t & kStMask) | f);
-      }
   for (int st = 0; st <= kNRun; ++st)
-    for (int s = 0; s <= kSymCont; ++s)
+    for (int s = 0; s < 16; ++s)
       for (int q = 0; q < 4; ++q)
         for (int ss = 0; ss < 2; ++ss) {
-          const bool last_sp = q & 1, crx = q & 2;
+          if (s > kSymCont) {  // (no such symbol: a byte past the info, never stepped)
+            T.lane[lane_index((uint32_t)(s | ss << 4), (uint32_t)q, st)] = (uint16_t)st;
+            continue;
+          }
+          const bool last_sp = q & 1, crx = cl && (q & 2);
           int cur = st, f = 0;
           if (ss) {  // a string start settles the open chunk (presplit_bytes, sync code 1)
             if (cur == kWsRun && cl && !crx) f |= kLCr;
@@ -173,7 +153,12 @@ constexpr Tables make_tables(bool cl) {
             f |= kLEnd;
             t = T.t[kStart][s];
           }
-          T.lane[lane_index(st, s, q, ss)] = (uint8_t)((t & kStMask) | f);
+          if (s == kSymSp || s == kSymCr || s == kSymWs) {  // the whitespace-run registers
+            f |= kLWsSet | (s == kSymSp ? kLSp : 0);
+            if (cl && s == kSymCr) f |= kLCrSet;
+            else if (cur != kWsRun) f |= kLCrClear;
+          }
+          T.lane[lane_index((uint32_t)(s | ss << 4), (uint32_t)q, st)] = (uint16_t)((t & kStMask) | f);
         }
   return T;
 }
@@ -388,8 +373,7 @@ SW_HD inline Leads valid_leads(uint32_t cur, uint32_t next, uint32_t ss_cur, uin
 }
 SW_HD inline uint32_t any_lead(const Leads& l) { return l.v2 | l.v3 | l.v4; }
 
-// Info bytes of the group u[1] (u[0] before it, u[2] after it; ss as above).  `carry`: in,
-// the valid-lead lanes of u[0] (lead_carry for the first group of a run); out, those of u[1].
+// The valid-lead lanes of u[0] (u[1] after it; ss as for info)
 struct LeadCarry {
   uint32_t v2, v3, v4;
 };
@@ -399,11 +383,15 @@ SW_HD inline LeadCarry lead_carry(const uint32_t* u, uint32_t ss) {
   return LeadCarry{l.v2, l.v3, l.v4};
 }
 
-// The info word of u[1] given the ASCII classes of u[0], u[1], u[2] (p, c, n; a run of groups
-// passes them on, so each word is classified once).
-template <class Asc, class Cls>
-SW_HD inline uint32_t info4_core(const uint32_t* u, uint32_t ss, const Ascii& p, const Ascii& c, const Ascii& n,
-                                 Asc asc, const Cls& cls, bool cl, LeadCarry& carry) {
+// Info is computed in two passes over a group u[1] (u[0] before it, u[2] after it; ss as above):
+//   info4_ascii  every group: sync codes, the symbols of ASCII bytes, kSymO (0) for the rest;
+//   info4_high   only groups with a byte >= 0x80: the symbols of those bytes (a continuation of
+//                a valid sequence kSymCont, a valid lead its code point's symbol, else kSymO),
+//                OR-ed into the first pass's word.  Independent of every other group, so the
+//                device runs it over the (few) such groups densely.
+template <class Asc>
+SW_HD inline uint32_t info4_ascii(const uint32_t* u, uint32_t ss, const Ascii& p, const Ascii& c, const Ascii& n,
+                                  Asc asc, bool cl) {
   const uint32_t ssp = spread4(ss), ssc = spread4(ss >> 4), ssn = spread4(ss >> 8);
   // sync codes (ASCII lanes only)
   const uint32_t sc2 = c.spc & after(c.let, n.let, 1) & ~after(ssc, ssn, 1);
@@ -413,46 +401,49 @@ SW_HD inline uint32_t info4_core(const uint32_t* u, uint32_t ss, const Ascii& p,
   const uint32_t sc5 = c.oth & before(p.oth, c.oth, 1);
   const uint32_t sc6 = cl ? 0u : c.dig & before(p.dig, c.dig, 1);
   // (bits 5-7: the code less one; bit 4: a string start, which takes precedence)
-  const uint32_t code = (sc2 >> 7) * 2 + (sc3 >> 7) * 4 + (sc4 >> 7) * 6 + (sc5 >> 7) * 8 + (sc6 >> 7) * 10 + (ssc >> 7);
-  // symbols: ASCII from the table; continuation bytes of a valid sequence; decoded leads
+  const uint32_t code = (sc2 >> 7) * 2 + (sc3 >> 7) * 4 + (sc4 >> 7) * 6 + (sc5 >> 7) * 8 + (sc6 >> 7) * 10 +
+                        (ssc >> 7);
   uint32_t sym = 0;
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
     const uint32_t b = (u[1] >> (8 * k)) & 0xFF;
     sym |= (uint32_t)asc[b & 0x7F] << (8 * k);
   }
-  if (((u[1] | u[2]) & kLane7) | carry.v2 | carry.v3 | carry.v4) {
-    const Leads l = valid_leads(u[1], u[2], ssc, ssn);
-    const uint32_t contv = before(carry.v2, l.v2, 1) | before(carry.v3, l.v3, 1) | before(carry.v3, l.v3, 2) |
-                           before(carry.v4, l.v4, 1) | before(carry.v4, l.v4, 2) | before(carry.v4, l.v4, 3);
-    carry = LeadCarry{l.v2, l.v3, l.v4};
-    const uint32_t high = u[1] & kLane7;
-    // high lanes: kSymO, unless a continuation (kSymCont) or a lead (its code point's symbol)
-    sym = (sym & ~((high >> 7) * 0xFF)) | ((contv >> 7) * kSymCont);
-    // the leads, one at a time (a word holds one or two on non-ASCII text)
-    const uint64_t w64 = ((uint64_t)u[2] << 32) | u[1];
-    uint32_t leads = any_lead(l);
-    while (leads) {
-      const int k = __builtin_ctz(leads) >> 3;
-      leads &= leads - 1;
-      const int L = ((l.v2 >> (8 * k + 7)) & 1) ? 2 : ((l.v3 >> (8 * k + 7)) & 1) ? 3 : 4;
-      const uint64_t w = w64 >> (8 * k);
-      uint32_t v = (uint32_t)w & (L == 2 ? 0x1F : L == 3 ? 0x0F : 0x07);
-      for (int q = 1; q < L; ++q) v = (v << 6) | (uint32_t)((w >> (8 * q)) & 0x3F);
-      // Cls: near(cp) for the BMP (no branch), far(cp) past it
-      int c = cls.near(v < 0x10000u ? v : 0x80u);
-      if (v >= 0x10000u) c = cls.far(v);
-      sym |= (uint32_t)nonascii_sym(v, c, cl) << (8 * k);
-    }
-  } else {
-    carry = LeadCarry{0, 0, 0};
-  }
+  sym &= ~(((u[1] & kLane7) >> 7) * 0xFF);  // high bytes: kSymO until info4_high
   return sym | (code << 4);
 }
 
+template <class Cls>
+SW_HD inline uint32_t info4_high(uint32_t info, const uint32_t* u, uint32_t ss, const Cls& cls, bool cl) {
+  const uint32_t ssc = spread4(ss >> 4), ssn = spread4(ss >> 8);
+  const LeadCarry carry = lead_carry(u, ss);  // leads of u[0]
+  const Leads l = valid_leads(u[1], u[2], ssc, ssn);
+  const uint32_t contv = before(carry.v2, l.v2, 1) | before(carry.v3, l.v3, 1) | before(carry.v3, l.v3, 2) |
+                         before(carry.v4, l.v4, 1) | before(carry.v4, l.v4, 2) | before(carry.v4, l.v4, 3);
+  uint32_t sym = (contv >> 7) * kSymCont;
+  // the leads, one at a time (a group holds one or two on non-ASCII text)
+  const uint64_t w64 = ((uint64_t)u[2] << 32) | u[1];
+  uint32_t leads = any_lead(l);
+  while (leads) {
+    const int k = __builtin_ctz(leads) >> 3;
+    leads &= leads - 1;
+    const int L = ((l.v2 >> (8 * k + 7)) & 1) ? 2 : ((l.v3 >> (8 * k + 7)) & 1) ? 3 : 4;
+    const uint64_t w = w64 >> (8 * k);
+    uint32_t v = (uint32_t)w & (L == 2 ? 0x1F : L == 3 ? 0x0F : 0x07);
+    for (int q = 1; q < L; ++q) v = (v << 6) | (uint32_t)((w >> (8 * q)) & 0x3F);
+    // Cls: near(cp) for the BMP (no branch), far(cp) past it
+    int c = cls.near(v < 0x10000u ? v : 0x80u);
+    if (v >= 0x10000u) c = cls.far(v);
+    sym |= (uint32_t)nonascii_sym(v, c, cl) << (8 * k);
+  }
+  return info | sym;
+}
+
+// both passes for one group (the CPU emulator's byte-stepped form)
 template <class Asc, class Cls>
-SW_HD inline uint32_t info4(const uint32_t* u, uint32_t ss, Asc asc, const Cls& cls, bool cl, LeadCarry& carry) {
-  return info4_core(u, ss, ascii_classes(u[0]), ascii_classes(u[1]), ascii_classes(u[2]), asc, cls, cl, carry);
+SW_HD inline uint32_t info4(const uint32_t* u, uint32_t ss, Asc asc, const Cls& cls, bool cl) {
+  const uint32_t a = info4_ascii(u, ss, ascii_classes(u[0]), ascii_classes(u[1]), ascii_classes(u[2]), asc, cl);
+  return (u[1] & kLane7) ? info4_high(a, u, ss, cls, cl) : a;
 }
 
 // The byte-stepped parse from r (state and whitespace-run registers in/out) while r < r_end:

@@ -77,7 +77,6 @@ struct LdsOr {
   }
 };
 
-__constant__ __attribute__((aligned(16))) UcdBmp c_ucd_bmp = make_ucd_bmp();
 
 __global__ void __launch_bounds__(kPsThreads) k_presplit(const uint8_t* bytes, int64_t n_bytes, const int64_t* str_off,
                                                          int64_t n_str, int pattern, uint64_t* bits) {
@@ -86,7 +85,8 @@ __global__ void __launch_bounds__(kPsThreads) k_presplit(const uint8_t* bytes, i
   // of [b0, b0 + block + halo)
   __shared__ __attribute__((aligned(8))) uint32_t s_ss[kPsSsWords];
   __shared__ __attribute__((aligned(16))) uint8_t s_step[sizeof(PsStepTab)];
-  __shared__ __attribute__((aligned(16))) uint8_t s_ucd[(kUcdBmpBytes + 15) & ~15];
+  __shared__ uint32_t s_hi[kPsHiWords];         // groups with a byte >= 0x80 (info pass 2)
+  __shared__ uint16_t s_hpre[kPsHiWords + 1];    // exclusive prefix counts of s_hi
   __shared__ int64_t s_first;
   static_assert(kPsSsWords >= 2 * kPsOutWords, "the chunk-start bitmap reuses s_ss");
   const int tid = threadIdx.x;
@@ -106,16 +106,13 @@ __global__ void __launch_bounds__(kPsThreads) k_presplit(const uint8_t* bytes, i
       }
     }
     for (int i = tid; i < kPsSsWords; i += kPsThreads) s_ss[i] = 0;
-    {  // asc and step of the pattern, the compact BMP class table
+    for (int i = tid; i < kPsHiWords; i += kPsThreads) s_hi[i] = 0;
+    {  // asc and lane table of the pattern
       const uint32_t* a = (const uint32_t*)ftab->asc;
       const uint32_t* ln = (const uint32_t*)ftab->lane;
       static_assert(offsetof(PsStepTab, lane) == 128 && sizeof(ftab->lane) % 4 == 0, "PsStepTab layout");
       for (int i = tid; i < 32; i += kPsThreads) ((uint32_t*)s_step)[i] = a[i];
       for (int i = tid; i < (int)sizeof(ftab->lane) / 4; i += kPsThreads) ((uint32_t*)s_step)[32 + i] = ln[i];
-      const uint32_t* u = (const uint32_t*)&c_ucd_bmp;
-      for (int i = tid; i < 64; i += kPsThreads) ((uint32_t*)s_ucd)[i] = u[i];
-      const uint32_t* u2 = (const uint32_t*)c_ucd_bmp.s2;
-      for (int i = tid; i < 16 * kUcdBmp.nblk; i += kPsThreads) ((uint32_t*)s_ucd)[64 + i] = u2[i];
     }
     if (tid == 0) {  // first string starting at or after wb
       int64_t lo = 0, hi = n_str;
@@ -150,19 +147,49 @@ __global__ void __launch_bounds__(kPsThreads) k_presplit(const uint8_t* bytes, i
   return;
 #endif
 
-  // 2. info bytes, in place of the staged bytes
+  // 2. info bytes, in place of the staged bytes: pass 1 over every group
   SW_LDS uint32_t* w32 = (SW_LDS uint32_t*)s_buf;
   const PsInfoRegs regs = ps_info_load(w32, tid);
   __syncthreads();
-  {
-    const PsUcd<const SW_LDS uint8_t*, UcdClass> cls{(const SW_LDS uint8_t*)s_ucd, (const SW_LDS uint8_t*)s_ucd + 256,
-                                                     UcdClass{}};
-    ps_info_convert(w32, (const SW_LDS uint32_t*)s_ss, (const SW_LDS uint8_t*)s_step, cls, cl, G.info_hi, tid, regs);
+  ps_info_convert(w32, (const SW_LDS uint32_t*)s_ss, (const SW_LDS uint8_t*)s_step, cl, G.info_hi, tid, regs,
+                  [&](int j) { atomicOr(&s_hi[j >> 5], 1u << (j & 31)); });
+  __syncthreads();
+  if (tid < 64) {  // prefix counts of the marks (wave 0; 3 words per lane)
+    static_assert(kPsHiWords <= 3 * 64, "marks");
+    uint32_t c[3], t = 0;
+#pragma unroll
+    for (int q = 0; q < 3; ++q) {
+      const int j = 3 * tid + q;
+      c[q] = j < kPsHiWords ? (uint32_t)__popc(s_hi[j]) : 0u;
+      t += c[q];
+    }
+    uint32_t x = t;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+      const uint32_t y = __shfl_up(x, off, 64);
+      if (tid >= off) x += y;
+    }
+    uint32_t run = x - t;
+#pragma unroll
+    for (int q = 0; q < 3; ++q) {
+      const int j = 3 * tid + q;
+      if (j <= kPsHiWords) s_hpre[j] = (uint16_t)run;
+      run += c[q];
+    }
+  }
+  __syncthreads();
+  {  // pass 2 over the marked groups, spread densely over the threads
+    const PsUcdFull<UcdClass> cls{UcdClass{}};  // (the full table in constant memory: pass 2 is sparse)
+    const int total = s_hpre[kPsHiWords];
+    for (int k = tid; k < total; k += kPsThreads)
+      ps_high_group(w32, (const SW_LDS uint32_t*)s_ss, cls, cl, G, bytes,
+                    ps_high_select((const SW_LDS uint16_t*)s_hpre, (const SW_LDS uint32_t*)s_hi, k));
   }
   __syncthreads();
   for (int i = tid; i < 2 * kPsOutWords; i += kPsThreads) s_ss[i] = 0;  // (now the chunk-start bitmap)
   __syncthreads();
 #if SW_PS_ABL == 2
+  if (n_bytes == 12345) bits[tid] = w32[4 + tid * kPsGroups] + w32[5 + tid * kPsGroups];  // (keeps the info live)
   return;
 #endif
 

@@ -62,15 +62,13 @@ void emul_bytes(const uint8_t* bytes, const int64_t* off, int64_t n_str, bool cl
   auto B = [&](int64_t i) -> uint32_t { return i >= 0 && i < n ? bytes[i] : 0; };
   auto S = [&](int64_t i) -> uint32_t { return i >= 0 && i <= n ? ss[i] : 0; };
   auto cls = [](uint32_t cp) { return cls_of(cp); };
-  sw::fsm::LeadCarry carry{0, 0, 0};
   for (int64_t r0 = 0; r0 < n; r0 += 4) {
     uint32_t u[3] = {0, 0, 0}, sb = 0;
     for (int j = 0; j < 12; ++j) {
       u[j >> 2] |= B(r0 - 4 + j) << ((j & 3) * 8);
       sb |= S(r0 - 4 + j) << j;
     }
-    if (r0 % 72 == 0) carry = sw::fsm::lead_carry(u, sb);  // (the device: a run of 18 groups per thread)
-    const uint32_t w = sw::fsm::info4(u, sb, tab->asc, sw::PsUcdFull<decltype(cls)>{cls}, cl, carry);
+    const uint32_t w = sw::fsm::info4(u, sb, tab->asc, sw::PsUcdFull<decltype(cls)>{cls}, cl);
     for (int k = 0; k < 4; ++k) inf[r0 + k] = (uint8_t)(w >> (8 * k));
   }
   ByteCtx x{inf.data(), tab, bits};
@@ -140,10 +138,16 @@ void emul_device(const uint8_t* bytes, const int64_t* off, int64_t n_str, int pa
     }
     std::vector<sw::PsInfoRegs> regs(sw::kPsThreads);
     for (int t = 0; t < sw::kPsThreads; ++t) regs[t] = sw::ps_info_load(w32.data(), t);
-    // the kernel's class lookup: the compact BMP table, the full table past it
-    const sw::PsUcd<const uint8_t*, decltype(cls)> ucd{sw::kUcdBmp.s1, sw::kUcdBmp.s2, cls};
+    const sw::PsUcdFull<decltype(cls)> ucd{cls};
+    std::vector<uint32_t> hi(sw::kPsHiWords, 0u);
     for (int t = 0; t < sw::kPsThreads; ++t)
-      sw::ps_info_convert(w32.data(), (const uint32_t*)ss.data(), tab->asc, ucd, cl, G.info_hi, t, regs[t]);
+      sw::ps_info_convert(w32.data(), (const uint32_t*)ss.data(), tab->asc, cl, G.info_hi, t, regs[t],
+                          [&](int j) { hi[j >> 5] |= 1u << (j & 31); });
+    std::vector<uint16_t> pre(sw::kPsHiWords + 1, 0);
+    for (int j = 0; j < sw::kPsHiWords; ++j) pre[j + 1] = (uint16_t)(pre[j] + __builtin_popcount(hi[j]));
+    for (int k = 0; k < pre[sw::kPsHiWords]; ++k)
+      sw::ps_high_group(w32.data(), (const uint32_t*)ss.data(), ucd, cl, G, bytes,
+                        sw::ps_high_select(pre.data(), hi.data(), k));
     uint32_t* wbp = wb.data();
     auto orw = [wbp](int w, uint32_t v) { wbp[w] |= v; };
     for (int t = 0; t < sw::kPsThreads; ++t) {

@@ -173,7 +173,7 @@ def main():
         pass
     roofline = {"bound": "hbm", "achieved": round(achieved, 2) if achieved else None, "peak": HBM_PEAK_GBS,
                 "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5) if achieved else None,
-                "traffic": traffic, "traffic_source": traffic_src, "kernel": "sw_encode_device pipeline (k_tile_strings..k_string_offsets)",
+                "traffic": traffic, "traffic_source": traffic_src, "kernel": ("sw_encode_device pipeline (k_presplit..k_string_offsets)" if not host_ps else "sw_encode_device pipeline (k_tile_strings..k_string_offsets)"),
                 "kernel_ms": round(k_ms, 4),
                 "algo_bytes_per_launch": int(b_algo)}
 

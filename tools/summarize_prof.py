@@ -42,19 +42,25 @@ def main():
     rows = list(csv.DictReader(open(stats_csv)))
     calls = {r["Name"].split("(")[0].replace("void ", ""): int(r["Calls"]) for r in rows}
     launches = max(1, calls.get("sw::k_classify", 1))
-    per_launch_ms = sum(float(r["TotalDurationNs"]) for r in rows if r["Name"].startswith(("sw::", "void sw::")))
-    per_launch_ms = per_launch_ms / launches / 1e6
+
+    def per_launch(name):  # dispatches of a kernel per encode launch (bench.py's one extra
+        # k_presplit + k_popcount outside the timed steps, for the chunk count, is not one)
+        return max(1, int(round(calls.get(name, launches) / launches))) if calls.get(name, 0) >= launches else 0
+
+    per_launch_ms = sum(float(r["AverageNs"]) * per_launch(r["Name"].split("(")[0].replace("void ", ""))
+                        for r in rows if r["Name"].startswith(("sw::", "void sw::"))) / 1e6
     lines = ["# rocprofv3 summary: %s" % tag, "",
              "Command: `tools/profile_gpu.sh %s` (bench.py --steps 3 --warmup 1 --no-cpu-baseline; kernel trace + "
              "stats pass, then one rocprofv3 --pmc pass per counter group)." % tag, "",
-             "Encode launches traced: %d.  Sum of the pipeline's kernel time per launch: **%.3f ms**." %
-             (launches, per_launch_ms), "",
+             "Encode launches traced: %d.  Sum of the pipeline's kernel time per launch: **%.3f ms** "
+             "(per launch = average x dispatches per launch; bench.py's one extra pre-split for the "
+             "chunk count, outside the timed steps, is not counted)." % (launches, per_launch_ms), "",
              "| kernel | calls | avg ms | per launch ms | % |", "|---|---|---|---|---|"]
     for r in rows:
         nm = r["Name"].split("(")[0].replace("void ", "")
         lines.append("| %s | %s | %.4f | %.4f | %.2f |" % (
             r["Name"][:64], r["Calls"], float(r["AverageNs"]) / 1e6,
-            float(r["TotalDurationNs"]) / launches / 1e6, float(r["Percentage"])))
+            float(r["AverageNs"]) * per_launch(nm) / 1e6, float(r["Percentage"])))
     c = pmc(src)
     tot = collections.defaultdict(float)
     if c:
@@ -65,7 +71,7 @@ def main():
             if not k.startswith("sw::"):
                 continue
             lines.append("| %s | " % k[:48] + " | ".join("%.4g" % c[k].get(n, float("nan")) for n in cnames) + " |")
-            per = calls.get(k, launches) / launches
+            per = per_launch(k)
             for n in cnames:
                 tot[n] += c[k].get(n, 0.0) * per
     derived = {"pipeline_ms_per_launch": per_launch_ms}

@@ -29,6 +29,7 @@
 #include <unordered_map>
 #include <vector>
 
+#include "capi.h"
 #include "kernels.h"
 #include "presplit_kernel.h"
 #include "shredword_hip.h"
@@ -40,10 +41,11 @@ using namespace sw;
 // errors
 // ------------------------------------------------------------------------------------------
 static thread_local std::string g_err;
-static int32_t fail(int32_t code, const std::string& msg) {
+int32_t sw::set_error(int32_t code, const std::string& msg) {
   g_err = msg;
   return code;
 }
+static int32_t fail(int32_t code, const std::string& msg) { return sw::set_error(code, msg); }
 #define HIP_TRY(expr)                                                                       \
   do {                                                                                      \
     hipError_t e_ = (expr);                                                                 \
@@ -239,14 +241,6 @@ bool build_cuckoo(const std::unordered_map<uint64_t, int32_t>& dict, const std::
   return false;
 }
 
-// exclusive scan of cnt[0..n) into base, total into *total (three small kernels)
-hipError_t launch_scan(hipStream_t st, const uint32_t* cnt, int64_t n, int64_t* part, int64_t* base, int64_t* total) {
-  const int64_t n_parts = (n + kScanBlock - 1) / kScanBlock;
-  hipLaunchKernelGGL(k_scan_reduce, dim3((unsigned)n_parts), dim3(kThreads), 0, st, cnt, n, part);
-  hipLaunchKernelGGL(k_scan_parts, dim3(1), dim3(1024), 0, st, part, n_parts, total);
-  hipLaunchKernelGGL(k_scan_apply, dim3((unsigned)n_parts), dim3(kThreads), 0, st, cnt, n, part, base);
-  return hipGetLastError();
-}
 
 // device pre-split of [d_bytes, d_bytes + n_bytes) into d_bits (zeroed here)
 hipError_t launch_presplit(hipStream_t st, const uint8_t* d_bytes, int64_t n_bytes, const int64_t* d_str_off,
@@ -260,6 +254,17 @@ hipError_t launch_presplit(hipStream_t st, const uint8_t* d_bytes, int64_t n_byt
 }
 
 }  // namespace
+
+// exclusive scan of cnt[0..n) into base, total into *total (three small kernels)
+hipError_t sw::launch_scan(hipStream_t st, const uint32_t* cnt, int64_t n, int64_t* part, int64_t* base,
+                           int64_t* total) {
+  const int64_t n_parts = (n + kScanBlock - 1) / kScanBlock;
+  hipLaunchKernelGGL(k_scan_reduce, dim3((unsigned)n_parts), dim3(kThreads), 0, st, cnt, n, part);
+  hipLaunchKernelGGL(k_scan_parts, dim3(1), dim3(1024), 0, st, part, n_parts, total);
+  hipLaunchKernelGGL(k_scan_apply, dim3((unsigned)n_parts), dim3(kThreads), 0, st, cnt, n, part, base);
+  return hipGetLastError();
+}
+int64_t sw::scan_block() { return kScanBlock; }
 
 extern "C" int32_t sw_encoder_create(const int32_t* pairs, const int32_t* vals, int64_t n, int32_t device,
                                      sw_encoder** out) {

@@ -160,6 +160,28 @@ int32_t sw_encode_device(sw_encoder* h, const uint8_t* d_bytes, int64_t n_bytes,
                          int64_t n_str, const uint64_t* d_chunk_bits, int32_t* d_out_ids, int64_t* d_out_off,
                          void* stream, int64_t* n_tokens_host);
 
+/* ---- decode (build_vocab, shredword/base.py:60-79, and the byte join of a decode) --------
+ * A decoder holds a vocabulary: token t's bytes are vocab_bytes[vocab_off[t] .. vocab_off[t+1])
+ * for every t < n_vocab with defined[t] != 0; the other ids are not tokens, and decoding one is
+ * an error (the reference's vocab[idx] raises KeyError).  The UTF-8 decoding of the bytes
+ * (errors="replace") is the caller's: it is per string. */
+typedef struct sw_decoder sw_decoder;
+int32_t sw_decoder_create(const uint8_t* vocab_bytes, const int64_t* vocab_off, const uint8_t* defined,
+                          int64_t n_vocab, int32_t device, sw_decoder** out);
+void sw_decoder_destroy(sw_decoder* d);
+
+/* The ids ids[id_off[s] .. id_off[s+1]) of n_str strings -> their bytes, concatenated into
+ * out[out_cap], with out_off[0..n_str] the per-string offsets.  Host buffers; synchronous.
+ * SW_ERR_ARG if an id is not in the vocabulary, SW_ERR_CAP if out_cap is too small. */
+int32_t sw_decode_batch(sw_decoder* d, const int32_t* ids, const int64_t* id_off, int64_t n_str, uint8_t* out,
+                        int64_t out_cap, int64_t* out_off);
+
+/* The same on device buffers (d_id_off[0] == 0, d_id_off[n_str] == n_ids) on a stream (NULL:
+ * the null stream).  Asynchronous unless n_bytes_host is given: then the call synchronises,
+ * stores the byte count and reports the errors above. */
+int32_t sw_decode_device(sw_decoder* d, const int32_t* d_ids, int64_t n_ids, const int64_t* d_id_off, int64_t n_str,
+                         uint8_t* d_out, int64_t out_cap, int64_t* d_out_off, void* stream, int64_t* n_bytes_host);
+
 /* Device time of the whole sw_encode_device pipeline (every kernel from k_tile_strings to
  * k_string_offsets, back to back on one stream), measured with a HIP event pair on that stream.
  * sw_encoder_set_timing(h, 1) starts a new accumulation window (one event pair per launch, no

@@ -82,6 +82,13 @@ _SIGNATURES = {
     "sw_encoder_set_timing": (c_int32, [c_void_p, c_int32]),
     "sw_encoder_last_kernel_ms": (c_double, [c_void_p]),
     "sw_encoder_phase_cycles": (c_int32, [c_void_p, POINTER(c_double), c_int32]),
+    "sw_decoder_create": (c_int32, [POINTER(c_uint8), POINTER(c_int64), POINTER(c_uint8), c_int64, c_int32,
+                                    POINTER(c_void_p)]),
+    "sw_decoder_destroy": (None, [c_void_p]),
+    "sw_decode_batch": (c_int32, [c_void_p, POINTER(c_int32), POINTER(c_int64), c_int64, POINTER(c_uint8), c_int64,
+                                  POINTER(c_int64)]),
+    "sw_decode_device": (c_int32, [c_void_p, c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_int64, c_void_p,
+                                   c_void_p, POINTER(c_int64)]),
     "sw_synth_corpus": (c_int64, [c_uint64, c_int32, c_int64, c_int64, POINTER(c_uint8), c_int64,
                                   POINTER(c_int64), c_int32]),
 }

@@ -75,6 +75,9 @@ class Tokenizer(BaseTokenizer):
         self.device = device
         self._handle = None
         self._handle_key = None
+        self._dec = None
+        self._dec_key = None
+        self._dec_len = None
         self.last_stats = None
 
     # merges is tracked so that edits (README-style `tok.merges[(a, b)] = id`) reach the device
@@ -95,6 +98,9 @@ class Tokenizer(BaseTokenizer):
         h, self._handle = getattr(self, "_handle", None), None
         if h:
             _lib.lib().sw_encoder_destroy(h)
+        d, self._dec = getattr(self, "_dec", None), None
+        if d:
+            _lib.lib().sw_decoder_destroy(d)
 
     # ---------------------------------------------------------------- device table
     def _encoder(self):
@@ -199,11 +205,75 @@ class Tokenizer(BaseTokenizer):
         return self.encode_batch([text], "none")[0]
 
     # ---------------------------------------------------------------- decode
-    def decode(self, ids):
-        """ids -> str via vocab bytes, undecodable bytes replaced (conventional minbpe decode)."""
+    def _vocab_now(self):
         if len(self.vocab) != 256 + len(self._merges) + len(self.special_tokens):
             self.vocab = build_vocab(self._merges, self.special_tokens)
-        return b"".join(self.vocab[int(i)] for i in ids).decode("utf-8", errors="replace")
+        return self.vocab
+
+    def _decoder(self):
+        """Device copy of the vocabulary (build_vocab, base.py:60-79), rebuilt when it changes."""
+        vocab = self._vocab_now()
+        key = (id(vocab), len(vocab), self.device)
+        if self._dec is not None and self._dec_key == key:
+            return self._dec
+        d, self._dec = self._dec, None
+        if d:
+            _lib.lib().sw_decoder_destroy(d)
+        n = max(vocab) + 1 if vocab else 0
+        lens = np.zeros(n, dtype=np.int64)
+        defined = np.zeros(max(n, 1), dtype=np.uint8)
+        for i, b in vocab.items():
+            lens[i] = len(b)
+            defined[i] = 1
+        off = np.zeros(n + 1, dtype=np.int64)
+        np.cumsum(lens, out=off[1:])
+        flat = b"".join(vocab[i] for i in sorted(vocab))  # (ascending ids: the offsets' order)
+        vb = np.frombuffer(flat or b"\0", dtype=np.uint8)
+        h = ctypes.c_void_p()
+        _lib.check(_lib.lib().sw_decoder_create(_lib.ptr(vb, ctypes.c_uint8), _lib.ptr(off, ctypes.c_int64),
+                                                _lib.ptr(defined, ctypes.c_uint8), n, int(self.device),
+                                                ctypes.byref(h)))
+        self._dec, self._dec_key, self._dec_len = h, key, (lens, defined[:n].astype(bool))
+        return h
+
+    def decode_packed(self, ids, id_off):
+        """Bytes of the id strings ids[id_off[s]:id_off[s+1]] (int32 ids, int64 offsets), decoded on
+        the device in one batch.  Returns (uint8 bytes, int64 byte offsets[n+1]).  An id that is
+        not in the vocabulary raises KeyError, as vocab[idx] does in the reference."""
+        ids = np.ascontiguousarray(ids, dtype=np.int32)
+        id_off = np.ascontiguousarray(id_off, dtype=np.int64)
+        h = self._decoder()
+        lens, defined = self._dec_len
+        sel = ids[int(id_off[0]):int(id_off[-1])] if len(id_off) else ids[:0]
+        bad = (sel < 0) | (sel >= len(lens))
+        if not bad.any():
+            bad = ~defined[sel]
+        if bad.any():
+            raise KeyError(int(sel[np.flatnonzero(bad)[0]]))
+        total = int(lens[sel].sum())
+        out = np.empty(max(total, 1), dtype=np.uint8)
+        n = len(id_off) - 1
+        out_off = np.empty(n + 1, dtype=np.int64)
+        _lib.check(_lib.lib().sw_decode_batch(h, _lib.ptr(ids if ids.size else np.zeros(1, np.int32), ctypes.c_int32),
+                                              _lib.ptr(id_off, ctypes.c_int64), n, _lib.ptr(out, ctypes.c_uint8),
+                                              total, _lib.ptr(out_off, ctypes.c_int64)))
+        return out[:total], out_off
+
+    def decode_batch(self, id_lists):
+        """Many id lists -> strings (one device batch; UTF-8 errors replaced, per string)."""
+        off = np.zeros(len(id_lists) + 1, dtype=np.int64)
+        np.cumsum([len(x) for x in id_lists], out=off[1:])
+        flat = np.fromiter((i for x in id_lists for i in x), dtype=np.int64, count=int(off[-1]))
+        if flat.size and (flat.min() < -2 ** 31 or flat.max() >= 2 ** 31):
+            raise KeyError(int(flat[(flat < -2 ** 31) | (flat >= 2 ** 31)][0]))
+        buf, boff = self.decode_packed(flat.astype(np.int32), off)
+        data = buf.tobytes()
+        return [data[boff[k]:boff[k + 1]].decode("utf-8", errors="replace") for k in range(len(id_lists))]
+
+    def decode(self, ids):
+        """ids -> str: vocab bytes joined (on the device), undecodable bytes replaced (the
+        conventional decode over build_vocab, base.py:60-79)."""
+        return self.decode_batch([list(ids)])[0]
 
     def load(self, model_file):
         super().load(model_file)

@@ -39,6 +39,8 @@ def test_errors_are_status_codes_not_exit():
     assert L.sw_last_error()
     assert L.sw_presplit_host(None, None, -1, 0, None, 1) == _lib.SW_ERR_ARG
     assert L.sw_synth_corpus(1, 99, 10, 10, None, 0, None, 1) == _lib.SW_ERR_ARG
+    assert L.sw_decoder_create(None, None, None, -1, 0, ctypes.byref(h)) == _lib.SW_ERR_ARG
+    assert L.sw_decode_batch(None, None, None, 0, None, 0, None) == _lib.SW_ERR_ARG
 
 
 def test_no_device_fails_loudly():

@@ -45,6 +45,8 @@ def parse():
     ap.add_argument("--no-gather", action="store_true", help="N>1: skip the RCCL reassembly")
     ap.add_argument("--cpu-sample-mb", type=float, default=320.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--e2e-steps", type=int, default=2,
+                    help="N=1: also time host buffers -> host buffers (PCIe-inclusive, reported beside value)")
     ap.add_argument("--threads", type=int, default=16, help="host threads for corpus/pre-split")
     ap.add_argument("--no-dedupe", action="store_true",
                     help="A/B only: every queued chunk runs its own merge loop (same results)")
@@ -177,6 +179,22 @@ def main():
                 "kernel_ms": round(k_ms, 4),
                 "algo_bytes_per_launch": int(b_algo)}
 
+    # PCIe-inclusive rate (rank 0, N=1): the same batch from pageable host buffers to host
+    # buffers through sw_encode_batch (Tokenizer.encode_packed).  Reported beside, never `value`.
+    e2e = None
+    if rank == 0 and world == 1 and args.e2e_steps > 0:
+        tok.encode_packed(buf, off, bits)  # (its own device workspace, grown once)
+        te = time.perf_counter()
+        for _ in range(args.e2e_steps):
+            ids_e, off_e = tok.encode_packed(buf, off, bits)
+        dte = (time.perf_counter() - te) / args.e2e_steps
+        st = tok.last_stats
+        e2e = {"mb_s": round(n_bytes / dte / 1e6, 1), "ms": round(dte * 1e3, 2), "ms_h2d": round(st.ms_h2d, 2),
+               "ms_kernels": round(st.ms_kernels, 2), "ms_d2h": round(st.ms_d2h, 2),
+               "same_token_count": int(off_e[-1]) == n_tok, "steps": args.e2e_steps,
+               "host_buffers": "pageable numpy, sw_encode_batch"}
+        del ids_e, off_e
+
     # parity spot-check + CPU baseline (rank 0, N=1 only): the oracle on a bounded prefix of the
     # same corpus; the GPU ids for that prefix must be bit-identical
     cpu = None
@@ -224,6 +242,7 @@ def main():
             "roofline": roofline,
             "cpu_baseline": cpu,
             "parity_vs_oracle_sample": parity,
+            "e2e_pcie": e2e,
             "host_prep_s": round(t_prep, 2),
         }
         print(json.dumps(line), flush=True)

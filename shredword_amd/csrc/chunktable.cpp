@@ -1,6 +1,7 @@
 // Host builder of the whole-chunk table (see chunktable.h).
 #include "chunktable.h"
 
+#include <algorithm>
 #include <string>
 #include <unordered_set>
 
@@ -56,6 +57,9 @@ bool place(const std::vector<Entry>& es, bool is_long, std::vector<uint4>* out, 
     *m2 = (uint32_t)next() | 1u;
     std::vector<int64_t> slot(nb, -1);  // entry index per bucket
     bool ok = true;
+    // entries come in token order (lower token = earlier merge = more frequent in the table's
+    // training text), each to its first candidate when free: the frequent chunks are answered
+    // by the first probe
     for (size_t e = 0; e < es.size() && ok; ++e) {
       int64_t cur = (int64_t)e;
       for (int kick = 0;; ++kick) {
@@ -72,15 +76,25 @@ bool place(const std::vector<Entry>& es, bool is_long, std::vector<uint4>* out, 
     }
     if (!ok) continue;
     out->assign(nb * w, make_uint4(0, 0, 0, 0));
+    std::vector<uint32_t> spill(nb, 0);  // 1: some entry whose first candidate is this bucket sits in its second
     for (size_t bk = 0; bk < nb; ++bk) {
+      if (slot[bk] < 0) continue;
+      const Entry& x = es[slot[bk]];
+      const uint32_t f = chunk_hash((uint32_t)x.k0, (uint32_t)(x.k0 >> 32), (uint32_t)x.k1, (uint32_t)(x.k1 >> 32),
+                                    x.len, *m1);
+      if (chunk_b1(f, *shift) != bk) spill[chunk_b1(f, *shift)] = 1;
+    }
+    for (size_t bk = 0; bk < nb; ++bk) {
+      if (!is_long) (*out)[bk].w = spill[bk];
+      else (*out)[2 * bk + 1].y = spill[bk];
       if (slot[bk] < 0) continue;
       const Entry& x = es[slot[bk]];
       const uint32_t tag = (x.len << 24) | x.token;
       if (!is_long) {
-        (*out)[bk] = make_uint4((uint32_t)x.k0, (uint32_t)(x.k0 >> 32), tag, 0);
+        (*out)[bk] = make_uint4((uint32_t)x.k0, (uint32_t)(x.k0 >> 32), tag, spill[bk]);
       } else {
         (*out)[2 * bk] = make_uint4((uint32_t)x.k0, (uint32_t)(x.k0 >> 32), (uint32_t)x.k1, (uint32_t)(x.k1 >> 32));
-        (*out)[2 * bk + 1] = make_uint4(tag, 0, 0, 0);
+        (*out)[2 * bk + 1] = make_uint4(tag, spill[bk], 0, 0);
       }
     }
     return true;
@@ -112,6 +126,9 @@ bool build_chunk_table(const std::unordered_map<uint64_t, int32_t>& dict, const 
     Entry x{le64(s, 0), le64(s, 8), (uint32_t)s.size(), (uint32_t)e[0]};
     (s.size() <= 8 ? es_short : es_long).push_back(x);
   }
+  auto by_token = [](const Entry& x, const Entry& y) { return x.token < y.token; };
+  std::stable_sort(es_short.begin(), es_short.end(), by_token);
+  std::stable_sort(es_long.begin(), es_long.end(), by_token);
   out->n_short = es_short.size();
   out->n_long = es_long.size();
   return place(es_short, false, &out->sb, &out->s_shift, &out->s_m1, &out->s_m2) &&

@@ -9,9 +9,13 @@
 // single-token chunks.  This is the same shortcut tiktoken takes ("piece is itself a token").
 //
 // Device layout: two two-choice cuckoo tables keyed by (bytes, length):
-//   short (2..8 bytes):  16-byte entries {bytes 0-3, bytes 4-7, len << 24 | token, 0}
-//   long  (9..16 bytes): 32-byte entries {bytes 0-3, 4-7, 8-11, 12-15}{len << 24 | token, 0,0,0}
+//   short (2..8 bytes):  16-byte entries {bytes 0-3, bytes 4-7, len << 24 | token, spill}
+//   long  (9..16 bytes): 32-byte entries {bytes 0-3, 4-7, 8-11, 12-15}{len << 24 | token, spill, 0,0}
 // Unused key bytes are zero; an empty entry has len 0.  Tokens >= 2^24 are not tabled.
+// spill = 1 marks a bucket that is the FIRST candidate of some key stored in its second: a
+// lookup whose first probe neither matches nor sees spill is a certain miss, so most lookups
+// cost one memory request instead of two (entries are placed in token order, first candidate
+// preferred, so the frequent chunks sit in their first bucket).
 #pragma once
 #include <hip/hip_runtime.h>
 

@@ -102,22 +102,41 @@ __device__ __forceinline__ uint32_t lookup(const DevTable& t, uint32_t a, uint32
 
 // Whole-chunk table lookup (chunktable.h): the single token a 2..16-byte chunk encodes to, or
 // kInf if the chunk does not encode to exactly one token.  w: the chunk's bytes as LE words,
-// zero padded.  Two (<= 8 bytes) or four (9..16) independent 16-byte loads, one round trip.
+// zero padded.  The first candidate bucket, then the second only when the first neither matches
+// nor carries the spill bit (chunktable.h): one 16-byte request (two for 9..16 bytes) for most
+// chunks.  k_classify is bound by the L2 request rate, not by latency, so fewer requests win
+// over the rare second round trip.
 __device__ __forceinline__ uint32_t chunk_lookup(const DevChunkTable& c, const uint32_t (&w)[4], uint32_t len) {
   uint32_t v = kInf;
   if (len <= 8) {
     const uint32_t f = chunk_hash(w[0], w[1], 0, 0, len, c.s_m1);
     const uint4 q1 = c.sb[chunk_b1(f, c.s_shift)];
-    const uint4 q2 = c.sb[chunk_b2(f, c.s_m2, c.s_shift)];
-    v = (q1.x == w[0] && q1.y == w[1] && (q1.z >> 24) == len) ? (q1.z & 0xFFFFFFu) : v;
-    v = (q2.x == w[0] && q2.y == w[1] && (q2.z >> 24) == len) ? (q2.z & 0xFFFFFFu) : v;
+    const bool hit = q1.x == w[0] && q1.y == w[1] && (q1.z >> 24) == len;
+    v = hit ? (q1.z & 0xFFFFFFu) : v;
+#ifdef SW_CT_TWO_PROBES  // (A/B builds: always probe both candidates)
+    if (!hit) {
+#else
+    if (!hit && (q1.w & 1u)) {
+#endif
+      const uint4 q2 = c.sb[chunk_b2(f, c.s_m2, c.s_shift)];
+      v = (q2.x == w[0] && q2.y == w[1] && (q2.z >> 24) == len) ? (q2.z & 0xFFFFFFu) : v;
+    }
   } else {
     const uint32_t f = chunk_hash(w[0], w[1], w[2], w[3], len, c.l_m1);
-    const uint32_t b1 = chunk_b1(f, c.l_shift), b2 = chunk_b2(f, c.l_m2, c.l_shift);
+    const uint32_t b1 = chunk_b1(f, c.l_shift);
     const uint4 a1 = c.lb[2 * b1], t1 = c.lb[2 * b1 + 1];
-    const uint4 a2 = c.lb[2 * b2], t2 = c.lb[2 * b2 + 1];
-    v = (a1.x == w[0] && a1.y == w[1] && a1.z == w[2] && a1.w == w[3] && (t1.x >> 24) == len) ? (t1.x & 0xFFFFFFu) : v;
-    v = (a2.x == w[0] && a2.y == w[1] && a2.z == w[2] && a2.w == w[3] && (t2.x >> 24) == len) ? (t2.x & 0xFFFFFFu) : v;
+    const bool hit = a1.x == w[0] && a1.y == w[1] && a1.z == w[2] && a1.w == w[3] && (t1.x >> 24) == len;
+    v = hit ? (t1.x & 0xFFFFFFu) : v;
+#ifdef SW_CT_TWO_PROBES
+    if (!hit) {
+#else
+    if (!hit && (t1.y & 1u)) {
+#endif
+      const uint32_t b2 = chunk_b2(f, c.l_m2, c.l_shift);
+      const uint4 a2 = c.lb[2 * b2], t2 = c.lb[2 * b2 + 1];
+      v = (a2.x == w[0] && a2.y == w[1] && a2.z == w[2] && a2.w == w[3] && (t2.x >> 24) == len) ? (t2.x & 0xFFFFFFu)
+                                                                                                 : v;
+    }
   }
   return v;
 }
@@ -462,20 +481,50 @@ __device__ __forceinline__ int64_t dedupe_claim(const EncArgs& a, const uint32_t
     }
     if ((cur & ~0x7FFFFFFFULL) != tag) continue;
     const int64_t other = (int64_t)(cur & 0x7FFFFFFFULL);
-    // compare with the claimant's bytes (aligned words of the input, realigned)
+    // compare with the claimant's bytes in the input, realigned
     const int64_t g = other + mis, w0 = g >> 2;
     const uint32_t sh = (uint32_t)(g & 3);
-    uint32_t prev = words[min(w0, last_word)];
     bool same = true;
+#ifdef SW_DD_WORDS  // (A/B builds: word-by-word verification only)
+    if (false) {
+#else
+    if ((((uintptr_t)words & 15) == 0) && ((g + n - 1) >> 4) <= ((last_word + 1) >> 2) - 1) {
+#endif
+      // 16-byte aligned loads: one memory request per 16-byte block the chunk touches (1-3),
+      // not one per word; then the words from the chunk's first word on (selects, no
+      // dynamically indexed registers)
+      const uint4* q16 = (const uint4*)words;
+      const int64_t b0 = g >> 4;
+      const int span = (int)(g & 15) + n;
+      const uint4 x0 = q16[b0];
+      const uint4 x1 = span > 16 ? q16[b0 + 1] : make_uint4(0, 0, 0, 0);
+      const uint4 x2 = span > 32 ? q16[b0 + 2] : make_uint4(0, 0, 0, 0);
+      const uint32_t W[12] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w, x2.x, x2.y, x2.z, x2.w};
+      const int k = (int)(w0 & 3);
+      uint32_t R[kShort / 4 + 1];
 #pragma unroll
-    for (int q = 0; q < kShort / 4; ++q) {
-      if (q < nw) {
-        const uint32_t next = words[min(w0 + q + 1, last_word)];
-        const int keep = n - 4 * q;
-        const uint32_t x = __builtin_amdgcn_alignbyte(next, prev, sh);
-        const uint32_t m = keep >= 4 ? ~0u : ((1u << (8 * keep)) - 1u);
-        same = same && ((x & m) == u[q]);
-        prev = next;
+      for (int i = 0; i <= kShort / 4; ++i) R[i] = k == 0 ? W[i] : k == 1 ? W[i + 1] : k == 2 ? W[i + 2] : W[i + 3];
+#pragma unroll
+      for (int q = 0; q < kShort / 4; ++q) {
+        if (q < nw) {
+          const int keep = n - 4 * q;
+          const uint32_t x = __builtin_amdgcn_alignbyte(R[q + 1], R[q], sh);
+          const uint32_t m = keep >= 4 ? ~0u : ((1u << (8 * keep)) - 1u);
+          same = same && ((x & m) == u[q]);
+        }
+      }
+    } else {  // (unaligned input, or the batch's last bytes): word by word
+      uint32_t prev = words[min(w0, last_word)];
+#pragma unroll
+      for (int q = 0; q < kShort / 4; ++q) {
+        if (q < nw) {
+          const uint32_t next = words[min(w0 + q + 1, last_word)];
+          const int keep = n - 4 * q;
+          const uint32_t x = __builtin_amdgcn_alignbyte(next, prev, sh);
+          const uint32_t m = keep >= 4 ? ~0u : ((1u << (8 * keep)) - 1u);
+          same = same && ((x & m) == u[q]);
+          prev = next;
+        }
       }
     }
     if (same) return other;
@@ -497,7 +546,12 @@ constexpr int kLookRounds = SW_LOOK_ROUNDS;          // lookup rounds in flight 
 constexpr int kQBuf = 64 * (kLookRounds + 1);        // dedupe buffer: one batch + a group of rounds
 constexpr int kWinWords = kWin / 4 + 8;
 
-__global__ void __launch_bounds__(kThreads) k_classify(EncArgs a) {
+#ifdef SW_CLS_WAVES_PER_EU  // (A/B builds: cap the VGPRs for this many waves per SIMD)
+#define SW_CLS_ATTR __attribute__((amdgpu_waves_per_eu(SW_CLS_WAVES_PER_EU, SW_CLS_WAVES_PER_EU)))
+#else
+#define SW_CLS_ATTR
+#endif
+__global__ void __launch_bounds__(kThreads) SW_CLS_ATTR k_classify(EncArgs a) {
   __shared__ __attribute__((aligned(16))) uint32_t s_b32_all[kWaves][kWinWords];  // window bytes (+ zero tail)
   __shared__ uint16_t s_cs_all[kWaves][kTile + 1];   // chunk starts (tile-relative)
   __shared__ uint16_t s_qb_all[kWaves][kQBuf];       // chunks not settled by a lookup, to dedupe
@@ -1014,7 +1068,7 @@ __global__ void __launch_bounds__(kThreads) k_tile_count(EncArgs a) {
 constexpr int kRefCap = 128;    // references per 8-round group gathered through LDS
 constexpr int kOutCapW = 1024;  // ids per group staged in LDS (the rest are stored directly)
 
-__global__ void __launch_bounds__(kThreads) k_compact(EncArgs a, const int64_t* tile_base, int32_t* out) {
+__global__ void __launch_bounds__(kThreads) SW_CLS_ATTR k_compact(EncArgs a, const int64_t* tile_base, int32_t* out) {
   // per wave: the group's references, gathered with full lanes before any store (a store
   // ahead of a load in the wave's vmcnt order would make the load wait for it)
   __shared__ uint32_t s_rp_all[kWaves][kRefCap];

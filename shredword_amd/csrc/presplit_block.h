@@ -32,7 +32,10 @@ struct PsUcdFull {
   SW_HD int operator()(uint32_t cp) const { return fn(cp); }
 };
 
-constexpr int kPsSeg = 68;                       // bytes per lane (17 words: lanes' reads hit distinct LDS banks)
+#ifndef SW_PS_SEG
+#define SW_PS_SEG 68
+#endif
+constexpr int kPsSeg = SW_PS_SEG;                // bytes per lane (17 words: lanes' reads hit distinct LDS banks)
 constexpr int kPsThreads = 256;
 constexpr int kPsBlock = kPsSeg * kPsThreads;    // 17 KiB per workgroup (a multiple of 64)
 constexpr int kPsHalo = 1024;                    // staged past the block for chunks that run on

@@ -1048,10 +1048,20 @@ __global__ void __launch_bounds__(kThreads) k_tile_count(EncArgs a) {
   const int64_t t = ((int64_t)blockIdx.x * kThreads + threadIdx.x) >> 6;
   const int lane = threadIdx.x & 63;
   if (t >= a.n_tiles) return;
-  const int C = (int)a.tile_slots[t], nref = (int)a.tile_nref[t];
   const uint32_t* rl = a.rlist + t * kTile;
+#ifndef SW_NO_PREFETCH
+  // the first round's list entries load with the counts, not after them: one dependent memory
+  // round trip less per tile (most tiles have < 64 references)
+  const uint32_t p0 = rl[lane];
+#endif
+  const int C = (int)a.tile_slots[t], nref = (int)a.tile_nref[t];
   uint32_t c = 0;
+#ifndef SW_NO_PREFETCH
+  c = lane < nref ? a.res[2 * (int64_t)p0] : 0u;
+  for (int i0 = 64; i0 < nref; i0 += 64 * SW_TC_ROUNDS) {
+#else
   for (int i0 = 0; i0 < nref; i0 += 64 * SW_TC_ROUNDS) {
+#endif
     uint32_t p[SW_TC_ROUNDS], g[SW_TC_ROUNDS];
 #pragma unroll
     for (int u = 0; u < SW_TC_ROUNDS; ++u) p[u] = rl[min(i0 + 64 * u + lane, kTile - 1)];
@@ -1083,27 +1093,52 @@ __global__ void __launch_bounds__(kThreads) SW_CLS_ATTR k_compact(EncArgs a, con
   uint4* s_rq = s_rq_all[wv];
   int32_t* s_out = s_out_all[wv];
   const uint64_t lt_mask = (lane == 0) ? 0ULL : (~0ULL >> (64 - lane));
-  const int C = (int)a.tile_slots[t];
+  constexpr int R = kRoundsInFlight;
   const int32_t* src = a.scratch + t * kTile;
+#ifdef SW_CP_V0  // (A/B builds: the first group's slots before the slot count is known)
+  int32_t v0[R];
+#pragma unroll
+  for (int u = 0; u < R; ++u) v0[u] = SW_LDNT(&src[min((u << 6) + lane, kTile - 1)]);
+#endif
+  const int C = (int)a.tile_slots[t];
   int32_t* dst = out + tile_base[t];
   // strings starting in this tile: lane i holds string s_lo + i's chunk index (k_classify)
   const int64_t t1 = min(t * kTile + (int64_t)kTile, a.n_bytes);
   const int64_t s_lo = a.tile_slo[t];
   const int64_t s_hi = (t + 1 < a.n_tiles) ? a.tile_slo[t + 1] : a.n_str;
   const int64_t my_s = s_lo + lane;
+#ifndef SW_NO_PREFETCH
+  // a string's chunk index loads with its offset, not after it (one dependent round trip
+  // less); the out_off of a string past this tile may be being rewritten by its own tile's
+  // wave: the value is read but not used then
+  const int64_t ms = min(my_s, a.n_str);
+  const int64_t s_at = a.str_off[ms], s_cj = a.out_off[ms];
+  const bool has_s = my_s < s_hi && s_at < t1;
+  const int sj = has_s ? (int)s_cj : -1;
+#else
   const bool has_s = my_s < s_hi && a.str_off[my_s] < t1;
   const int sj = has_s ? (int)a.out_off[my_s] : -1;
+#endif
   const bool many = s_hi - s_lo > 64;  // rare: slot offsets go through scratch instead
   uint32_t s_off = 0, carry = 0;
-  constexpr int R = kRoundsInFlight;
 #ifdef SW_STAMPS
   if (sj == -12345) s_off = 1;  // (forces the string loads to land here in stamp builds)
   SW_STAMP(8);
 #endif
   for (int r0 = 0; r0 * 64 < C; r0 += R) {
     int32_t v[R];
+#ifdef SW_CP_V0
+    if (r0 == 0) {
+#pragma unroll
+      for (int u = 0; u < R; ++u) v[u] = v0[u];
+    } else {
+#pragma unroll
+      for (int u = 0; u < R; ++u) v[u] = SW_LDNT(&src[min(((r0 + u) << 6) + lane, kTile - 1)]);
+    }
+#else
 #pragma unroll
     for (int u = 0; u < R; ++u) v[u] = SW_LDNT(&src[min(((r0 + u) << 6) + lane, kTile - 1)]);
+#endif
     // dense list of the group's references (their index in the list per round and lane)
     uint32_t ridx[R];
     int nref = 0;  // wave-uniform

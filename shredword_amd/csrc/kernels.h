@@ -884,10 +884,186 @@ __global__ void __launch_bounds__(kThreads) k_merge_bucket(EncArgs a, int b_lo, 
 // ones work in the global work area (res, position space).
 constexpr int kLongLds = 4096;
 
+// ---------------------------------------------------------------------------------------
+// Exact merge loop for one chunk of 33..kLongLds bytes, one wave, without compaction: lane j
+// owns positions [64j, 64j + 64) and keeps in registers their ALIVE mask (merged-away
+// positions die; "adjacent" means the next alive position), the smallest (rank, position) key
+// of its pairs and the mask of the positions holding that rank.  Per step of the reference
+// loop (base.py:10-36):
+//   - the global minimum key is one wave min: the lowest rank, first occurrence (the pair of
+//     the earliest position with that rank, as min() over the first-occurrence-ordered stats);
+//   - its occurrences can only sit at positions of lanes whose minimum rank is that rank, in
+//     their min-rank masks (a pair's rank is its value; ill-formed tables may give two pairs
+//     one value, so the ids are compared too);
+//   - all occurrences are replaced, left to right, non-overlapping: for (a, b) with a != b
+//     occurrences cannot overlap; for (a, a) the runs are resolved in position order, lane
+//     after lane;
+//   - the right partners die, and only the ranks of the new tokens and of their alive
+//     predecessors are looked up again; only the lanes whose positions changed recompute
+//     their minimum.
+// So a step costs a few wave-wide operations plus the changed segments, not two passes over
+// the whole chunk.  id / rk live in LDS at lds_pos(p): a wave's reads of "position k of every
+// lane" hit 64 distinct banks.  Returns the surviving count; their ids are written to out.
+// ---------------------------------------------------------------------------------------
+__device__ __forceinline__ int lds_pos(int p) { return ((p & 63) << 6) | (p >> 6); }
+
+template <bool kWide>
+__device__ int seg_merge(const DevTable& t, uint32_t* id, uint32_t* rk, uint64_t* s_kill, uint64_t* s_dirty, int n,
+                         int lane, uint32_t* out) {
+  const int base = lane << 6;
+  uint64_t am;
+  {
+    const int c = n - base;
+    am = c >= 64 ? ~0ULL : c <= 0 ? 0ULL : ((1ULL << c) - 1ULL);
+  }
+  s_kill[lane] = 0;
+  s_dirty[lane] = 0;
+  // exclusive scans over the lanes: first alive position after my segment (n: none), last
+  // alive position before it (-1: none)
+  int nxt_after = n, prv_before = -1;
+  auto scans = [&]() {
+    int f = am ? base + __builtin_ctzll(am) : n;
+    int l = am ? base + 63 - __builtin_clzll(am) : -1;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+      const int fy = __shfl_down(f, off, 64);
+      const int ly = __shfl_up(l, off, 64);
+      if (lane + off < 64) f = min(f, fy);
+      if (lane >= off) l = max(l, ly);
+    }
+    nxt_after = __shfl_down(f, 1, 64);
+    if (lane == 63) nxt_after = n;
+    prv_before = __shfl_up(l, 1, 64);
+    if (lane == 0) prv_before = -1;
+  };
+  auto next_of = [&](int k) -> int {  // next alive position after base + k (mine)
+    const uint64_t m = k == 63 ? 0ULL : (am & (~0ULL << (k + 1)));
+    return m ? base + __builtin_ctzll(m) : nxt_after;
+  };
+  auto prev_of = [&](int k) -> int {  // last alive position before base + k (mine)
+    const uint64_t m = am & ((1ULL << k) - 1ULL);
+    return m ? base + 63 - __builtin_clzll(m) : prv_before;
+  };
+  uint64_t smin = ~0ULL, mmask = 0;  // my minimum key (rank << 32 | position), its positions
+  auto seg_min = [&]() {
+    smin = ~0ULL;
+    mmask = 0;
+    for (uint64_t m = am; m; m &= m - 1) {
+      const int k = __builtin_ctzll(m);
+      const uint32_t r = rk[lds_pos(base + k)];
+      const uint32_t cur = (uint32_t)(smin >> 32);
+      if (r < cur) {
+        smin = ((uint64_t)r << 32) | (uint32_t)(base + k);
+        mmask = 1ULL << k;
+      } else if (r == cur) {
+        mmask |= 1ULL << k;
+      }
+    }
+    if ((uint32_t)(smin >> 32) == kInf) mmask = 0;
+  };
+  scans();
+  // initial ranks: every pair (p, p + 1), eight lookups in flight per lane
+  for (int k0 = 0; k0 < 64; k0 += 8) {
+    uint32_t r[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int p = base + k0 + u;
+      r[u] = p + 1 < n ? lookup<kWide>(t, id[lds_pos(p)], id[lds_pos(p + 1)]) : kInf;
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u)
+      if (base + k0 + u < n) rk[lds_pos(base + k0 + u)] = r[u];
+  }
+  seg_min();
+  wave_sync_mem();
+  while (true) {
+    const uint64_t key = wave_min_u64(smin);
+    const uint32_t r = (uint32_t)(key >> 32);
+    if (r == kInf) break;
+    const int pm = (int)(uint32_t)key;
+    // the pair at pm (lane pm >> 6 owns it)
+    const int lm = pm >> 6, km = pm & 63;
+    const uint64_t am_m = __shfl(am, lm, 64);
+    const int na_m = __shfl(nxt_after, lm, 64);
+    const uint64_t mq = km == 63 ? 0ULL : (am_m & (~0ULL << (km + 1)));
+    const int qm = mq ? (lm << 6) + __builtin_ctzll(mq) : na_m;
+    const uint32_t p0 = id[lds_pos(pm)], p1 = id[lds_pos(qm)];
+    // my occurrences of (p0, p1): among my min-rank positions
+    uint64_t take = 0;
+    if ((uint32_t)(smin >> 32) == r) {
+      for (uint64_t m = mmask; m; m &= m - 1) {
+        const int k = __builtin_ctzll(m);
+        if (id[lds_pos(base + k)] == p0 && id[lds_pos(next_of(k))] == p1) take |= 1ULL << k;
+      }
+    }
+    if (p0 == p1) {  // runs of (a, a): left to right, a taken position consumes its next
+      uint64_t lanes = __ballot(take != 0);
+      int consumed = -1;
+      uint64_t tk = 0;
+      while (lanes) {
+        const int L = __builtin_ctzll(lanes);
+        lanes &= lanes - 1;
+        if (lane == L) {
+          for (uint64_t m = take; m; m &= m - 1) {
+            const int k = __builtin_ctzll(m);
+            if (base + k != consumed) {
+              tk |= 1ULL << k;
+              consumed = next_of(k);
+            }
+          }
+        }
+        consumed = __shfl(consumed, L, 64);
+      }
+      take = tk;
+    }
+    // new ids; the right partners die (a partner in a later segment is that segment's first
+    // alive position: its bit goes through LDS)
+    uint64_t kill = 0;
+    for (uint64_t m = take; m; m &= m - 1) {
+      const int k = __builtin_ctzll(m);
+      id[lds_pos(base + k)] = r;
+      const int nc = next_of(k);
+      if (nc < base + 64) kill |= 1ULL << (nc - base);
+      else __hip_atomic_fetch_or(&s_kill[nc >> 6], 1ULL << (nc & 63), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+    wave_sync_mem();
+    kill |= s_kill[lane];
+    am &= ~kill;
+    s_kill[lane] = 0;
+    scans();
+    // ranks to look up again: every new token and its alive predecessor
+    uint64_t dirty = take;
+    for (uint64_t m = take; m; m &= m - 1) {
+      const int pv = prev_of(__builtin_ctzll(m));
+      if (pv < 0) continue;
+      if (pv >= base) dirty |= 1ULL << (pv - base);
+      else __hip_atomic_fetch_or(&s_dirty[pv >> 6], 1ULL << (pv & 63), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+    wave_sync_mem();
+    dirty |= s_dirty[lane];
+    s_dirty[lane] = 0;
+    dirty &= am;
+    for (uint64_t m = dirty; m; m &= m - 1) {
+      const int k = __builtin_ctzll(m);
+      const int nx = next_of(k);
+      rk[lds_pos(base + k)] = nx < n ? lookup<kWide>(t, id[lds_pos(base + k)], id[lds_pos(nx)]) : kInf;
+    }
+    if (dirty | kill) seg_min();
+    wave_sync_mem();
+  }
+  // the surviving ids, in order
+  const uint32_t cnt = (uint32_t)__popcll(am);
+  const uint32_t incl = wave_incl_scan(cnt, lane);
+  uint32_t o = incl - cnt;
+  for (uint64_t m = am; m; m &= m - 1) out[o++] = id[lds_pos(base + __builtin_ctzll(m))];
+  return (int)__shfl(incl, 63, 64);
+}
+
 template <bool kWide>
 __global__ void __launch_bounds__(64) k_merge_long_lds(EncArgs a) {
   __shared__ uint32_t s_id[kLongLds];
   __shared__ uint32_t s_rk[kLongLds];
+  __shared__ uint64_t s_kill[64], s_dirty[64];
   const int lane = threadIdx.x;
   int64_t lo, hi;
   bucket_range(a, kLongBucket, kLongBucket, &lo, &hi);
@@ -896,11 +1072,10 @@ __global__ void __launch_bounds__(64) k_merge_long_lds(EncArgs a) {
     const int64_t start = (int64_t)(e >> 24);
     const int64_t len = next_set_bit(a.bits, a.n_words, start + 1, a.n_bytes) - start;
     if (len > kLongLds) continue;  // (k_merge_long)
-    for (int j = lane; j < len; j += 64) s_id[j] = a.bytes[start + j];
+    for (int j = lane; j < len; j += 64) s_id[lds_pos(j)] = a.bytes[start + j];
     wave_sync_mem();
-    const int m = (int)coop_merge<kWide>(a.table, s_id, s_rk, len, lane);
     uint32_t* gid = a.res + 2 * start + 1;
-    for (int j = lane; j < m; j += 64) gid[j] = s_id[j];
+    const int m = seg_merge<kWide>(a.table, s_id, s_rk, s_kill, s_dirty, (int)len, lane, gid);
     if (lane == 0) gid[-1] = (uint32_t)m;
     wave_sync_mem();
   }

@@ -479,26 +479,27 @@ extern "C" int32_t sw_encode_device(sw_encoder* h, const uint8_t* d_bytes, int64
     HIP_TRY(launch_scan(st, h->d_bcnt, kNumBuckets * n_tiles, h->d_part, h->d_boff, h->d_qtotal));
     hipLaunchKernelGGL(k_scatter, dim3((unsigned)((n_tiles + 3) / 4)), dim3(kThreads), 0, st, a);
     const dim3 pg(2048), pb(kThreads);  // persistent grid for the queue kernels
+    constexpr unsigned kLongGrid = 32768;  // k_merge_long_lds: a workgroup per long chunk (grid-stride past that)
     if (h->table.wide) {
       hipLaunchKernelGGL((k_merge_bucket<true, false, 4>), pg, pb, 0, st, a, 0, 2);
       hipLaunchKernelGGL((k_merge_bucket<true, false, 8>), pg, pb, 0, st, a, 3, 4);
       hipLaunchKernelGGL((k_merge_bucket<true, false, 16>), pg, pb, 0, st, a, 5, 7);
       hipLaunchKernelGGL((k_merge_bucket<true, false, 32>), pg, pb, 0, st, a, 8, 9);
-      hipLaunchKernelGGL((k_merge_long_lds<true>), dim3(2048), dim3(64), 0, st, a);
+      hipLaunchKernelGGL((k_merge_long_lds<true, false>), dim3(kLongGrid), dim3(64), 0, st, a);
       hipLaunchKernelGGL((k_merge_long<true>), dim3(512), pb, 0, st, a);
     } else if (h->ids16) {
       hipLaunchKernelGGL((k_merge_bucket<false, true, 4>), pg, pb, 0, st, a, 0, 2);
       hipLaunchKernelGGL((k_merge_bucket<false, true, 8>), pg, pb, 0, st, a, 3, 4);
       hipLaunchKernelGGL((k_merge_bucket<false, true, 16>), pg, pb, 0, st, a, 5, 7);
       hipLaunchKernelGGL((k_merge_bucket<false, true, 32>), pg, pb, 0, st, a, 8, 9);
-      hipLaunchKernelGGL((k_merge_long_lds<false>), dim3(2048), dim3(64), 0, st, a);
+      hipLaunchKernelGGL((k_merge_long_lds<false, true>), dim3(kLongGrid), dim3(64), 0, st, a);
       hipLaunchKernelGGL((k_merge_long<false>), dim3(512), pb, 0, st, a);
     } else {
       hipLaunchKernelGGL((k_merge_bucket<false, false, 4>), pg, pb, 0, st, a, 0, 2);
       hipLaunchKernelGGL((k_merge_bucket<false, false, 8>), pg, pb, 0, st, a, 3, 4);
       hipLaunchKernelGGL((k_merge_bucket<false, false, 16>), pg, pb, 0, st, a, 5, 7);
       hipLaunchKernelGGL((k_merge_bucket<false, false, 32>), pg, pb, 0, st, a, 8, 9);
-      hipLaunchKernelGGL((k_merge_long_lds<false>), dim3(2048), dim3(64), 0, st, a);
+      hipLaunchKernelGGL((k_merge_long_lds<false, false>), dim3(kLongGrid), dim3(64), 0, st, a);
       hipLaunchKernelGGL((k_merge_long<false>), dim3(512), pb, 0, st, a);
     }
     HIP_TRY(hipGetLastError());

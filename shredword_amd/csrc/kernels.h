@@ -907,9 +907,13 @@ constexpr int kLongLds = 4096;
 // ---------------------------------------------------------------------------------------
 __device__ __forceinline__ int lds_pos(int p) { return ((p & 63) << 6) | (p >> 6); }
 
-template <bool kWide>
-__device__ int seg_merge(const DevTable& t, uint32_t* id, uint32_t* rk, uint64_t* s_kill, uint64_t* s_dirty, int n,
-                         int lane, uint32_t* out) {
+template <bool kWide, typename T>  // T: uint16_t when every id and value fits 16 bits (half the LDS)
+__device__ int seg_merge(const DevTable& t, T* id, T* rk, uint64_t* s_kill, uint64_t* s_dirty, int n, int lane,
+                         uint32_t* out) {
+  auto rank_at = [&](int p) -> uint32_t {  // (16-bit storage: 0xFFFF is +inf)
+    const uint32_t r = rk[lds_pos(p)];
+    return (sizeof(T) == 2 && r == 0xFFFFu) ? kInf : r;
+  };
   const int base = lane << 6;
   uint64_t am;
   {
@@ -950,7 +954,7 @@ __device__ int seg_merge(const DevTable& t, uint32_t* id, uint32_t* rk, uint64_t
     mmask = 0;
     for (uint64_t m = am; m; m &= m - 1) {
       const int k = __builtin_ctzll(m);
-      const uint32_t r = rk[lds_pos(base + k)];
+      const uint32_t r = rank_at(base + k);
       const uint32_t cur = (uint32_t)(smin >> 32);
       if (r < cur) {
         smin = ((uint64_t)r << 32) | (uint32_t)(base + k);
@@ -972,7 +976,7 @@ __device__ int seg_merge(const DevTable& t, uint32_t* id, uint32_t* rk, uint64_t
     }
 #pragma unroll
     for (int u = 0; u < 8; ++u)
-      if (base + k0 + u < n) rk[lds_pos(base + k0 + u)] = r[u];
+      if (base + k0 + u < n) rk[lds_pos(base + k0 + u)] = (T)r[u];
   }
   seg_min();
   wave_sync_mem();
@@ -993,7 +997,7 @@ __device__ int seg_merge(const DevTable& t, uint32_t* id, uint32_t* rk, uint64_t
     if ((uint32_t)(smin >> 32) == r) {
       for (uint64_t m = mmask; m; m &= m - 1) {
         const int k = __builtin_ctzll(m);
-        if (id[lds_pos(base + k)] == p0 && id[lds_pos(next_of(k))] == p1) take |= 1ULL << k;
+        if ((uint32_t)id[lds_pos(base + k)] == p0 && (uint32_t)id[lds_pos(next_of(k))] == p1) take |= 1ULL << k;
       }
     }
     if (p0 == p1) {  // runs of (a, a): left to right, a taken position consumes its next
@@ -1021,7 +1025,7 @@ __device__ int seg_merge(const DevTable& t, uint32_t* id, uint32_t* rk, uint64_t
     uint64_t kill = 0;
     for (uint64_t m = take; m; m &= m - 1) {
       const int k = __builtin_ctzll(m);
-      id[lds_pos(base + k)] = r;
+      id[lds_pos(base + k)] = (T)r;
       const int nc = next_of(k);
       if (nc < base + 64) kill |= 1ULL << (nc - base);
       else __hip_atomic_fetch_or(&s_kill[nc >> 6], 1ULL << (nc & 63), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -1046,7 +1050,7 @@ __device__ int seg_merge(const DevTable& t, uint32_t* id, uint32_t* rk, uint64_t
     for (uint64_t m = dirty; m; m &= m - 1) {
       const int k = __builtin_ctzll(m);
       const int nx = next_of(k);
-      rk[lds_pos(base + k)] = nx < n ? lookup<kWide>(t, id[lds_pos(base + k)], id[lds_pos(nx)]) : kInf;
+      rk[lds_pos(base + k)] = (T)(nx < n ? lookup<kWide>(t, id[lds_pos(base + k)], id[lds_pos(nx)]) : kInf);
     }
     if (dirty | kill) seg_min();
     wave_sync_mem();
@@ -1059,10 +1063,13 @@ __device__ int seg_merge(const DevTable& t, uint32_t* id, uint32_t* rk, uint64_t
   return (int)__shfl(incl, 63, 64);
 }
 
-template <bool kWide>
+// one 64-thread workgroup (one wave) per chunk; launched with a grid far larger than the
+// usual long-chunk count, so the dispatcher hands chunks to free CUs as others finish
+template <bool kWide, bool k16>
 __global__ void __launch_bounds__(64) k_merge_long_lds(EncArgs a) {
-  __shared__ uint32_t s_id[kLongLds];
-  __shared__ uint32_t s_rk[kLongLds];
+  typedef typename std::conditional<k16, uint16_t, uint32_t>::type T;
+  __shared__ T s_id[kLongLds];
+  __shared__ T s_rk[kLongLds];
   __shared__ uint64_t s_kill[64], s_dirty[64];
   const int lane = threadIdx.x;
   int64_t lo, hi;
@@ -1072,10 +1079,10 @@ __global__ void __launch_bounds__(64) k_merge_long_lds(EncArgs a) {
     const int64_t start = (int64_t)(e >> 24);
     const int64_t len = next_set_bit(a.bits, a.n_words, start + 1, a.n_bytes) - start;
     if (len > kLongLds) continue;  // (k_merge_long)
-    for (int j = lane; j < len; j += 64) s_id[lds_pos(j)] = a.bytes[start + j];
+    for (int j = lane; j < len; j += 64) s_id[lds_pos(j)] = (T)a.bytes[start + j];
     wave_sync_mem();
     uint32_t* gid = a.res + 2 * start + 1;
-    const int m = seg_merge<kWide>(a.table, s_id, s_rk, s_kill, s_dirty, (int)len, lane, gid);
+    const int m = seg_merge<kWide, T>(a.table, s_id, s_rk, s_kill, s_dirty, (int)len, lane, gid);
     if (lane == 0) gid[-1] = (uint32_t)m;
     wave_sync_mem();
   }

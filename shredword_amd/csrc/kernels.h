@@ -949,18 +949,25 @@ __device__ int seg_merge(const DevTable& t, T* id, T* rk, uint64_t* s_kill, uint
     return m ? base + 63 - __builtin_clzll(m) : prv_before;
   };
   uint64_t smin = ~0ULL, mmask = 0;  // my minimum key (rank << 32 | position), its positions
-  auto seg_min = [&]() {
+  auto seg_min = [&]() {  // (all 64 entries read 16 at a time, independent loads: one LDS wait per 16)
     smin = ~0ULL;
     mmask = 0;
-    for (uint64_t m = am; m; m &= m - 1) {
-      const int k = __builtin_ctzll(m);
-      const uint32_t r = rank_at(base + k);
-      const uint32_t cur = (uint32_t)(smin >> 32);
-      if (r < cur) {
-        smin = ((uint64_t)r << 32) | (uint32_t)(base + k);
-        mmask = 1ULL << k;
-      } else if (r == cur) {
-        mmask |= 1ULL << k;
+#pragma unroll 1
+    for (int k0 = 0; k0 < 64; k0 += 16) {
+      uint32_t rr[16];
+#pragma unroll
+      for (int u = 0; u < 16; ++u) rr[u] = rank_at(base + k0 + u);
+#pragma unroll
+      for (int u = 0; u < 16; ++u) {
+        const int k = k0 + u;
+        const uint32_t r = ((am >> k) & 1ULL) ? rr[u] : kInf;
+        const uint32_t cur = (uint32_t)(smin >> 32);
+        if (r < cur) {
+          smin = ((uint64_t)r << 32) | (uint32_t)(base + k);
+          mmask = 1ULL << k;
+        } else if (r == cur) {
+          mmask |= 1ULL << k;
+        }
       }
     }
     if ((uint32_t)(smin >> 32) == kInf) mmask = 0;

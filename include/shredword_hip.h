@@ -15,7 +15,9 @@
  *     by status codes plus sw_last_error() (thread-local message).
  *   - The caller owns every buffer it passes.  The encoder handle owns its device copy of the
  *     merge table, its workspace and its stream.
- *   - One handle per host thread (a handle is not internally locked).
+ *   - One handle per host thread (a handle is not internally locked).  The device workspace
+ *     belongs to the handle: a launch on a stream other than the previous launch's waits for
+ *     that launch (a HIP event), so calls on one handle are ordered whatever their streams.
  *   - Ids are int32.  Vocab ids 0..255 are raw bytes (base.py:74); a merge value is both the
  *     pair's rank and the new token id (base.py:137,147).
  */
@@ -104,6 +106,14 @@ int32_t sw_encoder_reserve(sw_encoder* h, int64_t max_bytes, int64_t max_strings
  *                          (sw_presplit_host) instead of on the device (default 0) */
 #define SW_OPT_PATTERN 5
 #define SW_OPT_HOST_PRESPLIT 6
+/*   SW_OPT_LONG_SPLIT      1 (default): chunks of 33..4096 bytes are cut into pieces that are
+ *                          encoded on their own, then every junction is verified exactly and
+ *                          conflicting pieces are joined and encoded again (well-formed tables
+ *                          only, SW_INFO_SPLIT); 0: one wave loop per chunk.  Results identical.
+ *   SW_OPT_MAX_LAUNCH_BYTES  sw_encode_batch encodes larger batches as several launches of
+ *                          whole strings (0 = the 2 GiB device limit; testing: any value >= 64) */
+#define SW_OPT_LONG_SPLIT 7
+#define SW_OPT_MAX_LAUNCH_BYTES 8
 int32_t sw_encoder_set_option(sw_encoder* h, int32_t option, int64_t value);
 
 /* Encoder facts (sw_encoder_get_info): distinct merges, whole-chunk table entries, whether the
@@ -112,6 +122,7 @@ int32_t sw_encoder_set_option(sw_encoder* h, int32_t option, int64_t value);
 #define SW_INFO_CHUNK_ENTRIES 2
 #define SW_INFO_WIDE_TABLE 3
 #define SW_INFO_IDS16 4
+#define SW_INFO_SPLIT 5     /* the table is well-formed: long chunks may take the split path */
 int64_t sw_encoder_get_info(const sw_encoder* h, int32_t what);
 
 /* ---- host pre-split (apply_regex, base.py:38-58) ---------------------------------------

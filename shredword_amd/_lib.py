@@ -22,8 +22,8 @@ SW_ERR_ARG, SW_ERR_HIP, SW_ERR_ALLOC, SW_ERR_CAP, SW_ERR_NODEV = -1, -2, -3, -4,
 SW_PAT_CL100K, SW_PAT_GPT2, SW_PAT_NONE = 0, 1, 2
 SW_CORPUS_ASCII, SW_CORPUS_MIXED, SW_CORPUS_STRESS = 0, 1, 2
 SW_OPT_CHUNK_TABLE, SW_OPT_DEDUPE, SW_OPT_DEDUPE_SLOTS, SW_OPT_DEDUPE_FP_BITS = 1, 2, 3, 4
-SW_OPT_PATTERN, SW_OPT_HOST_PRESPLIT = 5, 6
-SW_INFO_MERGES, SW_INFO_CHUNK_ENTRIES, SW_INFO_WIDE_TABLE, SW_INFO_IDS16 = 1, 2, 3, 4
+SW_OPT_PATTERN, SW_OPT_HOST_PRESPLIT, SW_OPT_LONG_SPLIT, SW_OPT_MAX_LAUNCH_BYTES = 5, 6, 7, 8
+SW_INFO_MERGES, SW_INFO_CHUNK_ENTRIES, SW_INFO_WIDE_TABLE, SW_INFO_IDS16, SW_INFO_SPLIT = 1, 2, 3, 4, 5
 
 
 class SwStats(Structure):

@@ -5,6 +5,7 @@ values and error behaviour.  Encode/decode live in `tokenizer.Tokenizer`; the ho
 (pre-split + merge loop) runs natively, never through these Python helpers.
 """
 import unicodedata
+import warnings
 from collections import Counter
 
 import numpy as np
@@ -28,16 +29,32 @@ pattern = ""
 special_tokens = {}
 
 
+_warned_patterns = set()
+
+
 def pattern_id(pat):
-    """Native pre-split id for a pattern string ("" = the reference's apply_regex default)."""
-    if isinstance(pat, int):
-        return pat
-    try:
-        return _PATTERN_IDS[pat]
-    except KeyError:
-        raise NotImplementedError(
-            "no native pre-splitter for pattern %r (supported: the cl100k pattern of "
-            "shredword/base.py:56 and the GPT-2 pattern of base.py:46)" % (pat,)) from None
+    """Native pre-split id for a tokenizer's `pattern`.
+
+    Policy: "" and the cl100k pattern -> SW_PAT_CL100K, what apply_regex runs
+    (base.py:56); the GPT-2 pattern of base.py:46 -> SW_PAT_GPT2; the ints SW_PAT_* as they are.
+    Any other pattern string (e.g. the docstring's pattern3/pattern4, base.py:50,54) falls back
+    to cl100k with a one-time warning -- the reference's apply_regex ignores the tokenizer's
+    pattern and always splits with cl100k, so this keeps its results."""
+    if isinstance(pat, (int, np.integer)) and not isinstance(pat, bool):
+        if int(pat) not in (_lib.SW_PAT_CL100K, _lib.SW_PAT_GPT2, _lib.SW_PAT_NONE):
+            raise ValueError("unknown pre-split id %r (SW_PAT_CL100K, SW_PAT_GPT2 or SW_PAT_NONE)" % (pat,))
+        return int(pat)
+    if not isinstance(pat, str):
+        raise TypeError("pattern must be a str or an SW_PAT_* int, not %s" % type(pat).__name__)
+    pid = _PATTERN_IDS.get(pat)
+    if pid is None:
+        if pat not in _warned_patterns:
+            _warned_patterns.add(pat)
+            warnings.warn("no native pre-splitter for pattern %r: splitting with the cl100k pattern, as "
+                          "shredword's apply_regex does for every tokenizer (base.py:56)" % (pat,),
+                          stacklevel=3)
+        pid = _lib.SW_PAT_CL100K
+    return pid
 
 
 def get_stats(ids, counts=None):

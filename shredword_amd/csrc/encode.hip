@@ -27,6 +27,7 @@
 #include <cstring>
 #include <string>
 #include <unordered_map>
+#include <unordered_set>
 #include <vector>
 
 #include "capi.h"
@@ -73,6 +74,16 @@ struct sw_encoder {
   DevChunkTable chunks{};
   void* d_chunks = nullptr;
   int64_t n_chunk_entries = 0;
+  // split + verify for long chunks (k_merge_long_split): well-formed tables only
+  bool split_ok = false;              // values >= 256, unique, larger than both pair members
+  bool long_split = true;             // SW_OPT_LONG_SPLIT
+  uint2* d_inv = nullptr;             // merge value -> pair
+  uint32_t n_inv = 0;
+  int64_t max_launch = kMaxLaunchBytes;  // SW_OPT_MAX_LAUNCH_BYTES (sw_encode_batch splits above it)
+  // the workspace is reused by every call: a call on another stream waits for the last one
+  hipEvent_t ws_done = nullptr;
+  hipStream_t ws_stream = nullptr;
+  bool ws_pending = false;
   // workspace
   int64_t cap_bytes = -1, cap_str = -1;
   int32_t* d_scratch = nullptr;
@@ -291,9 +302,24 @@ extern "C" int32_t sw_encoder_create(const int32_t* pairs, const int32_t* vals, 
     if (a > 0xFFFF || b > 0xFFFF || (a == 0xFFFF && b == 0xFFFF)) wide = true;
     if (a > 0xFFFD || b > 0xFFFD || v > 0xFFFD) ids16 = false;
   }
+  // well-formed (the split path's precondition, kernels.h): every value >= 256, unique, and
+  // larger than both members of its pair
+  bool split_ok = true;
+  uint32_t max_v = 0;
+  {
+    std::unordered_set<int32_t> vals;
+    vals.reserve(order.size() * 2);
+    for (uint64_t k : order) {
+      const int32_t v = dict.at(k), a = (int32_t)(k >> 32), b = (int32_t)(uint32_t)k;
+      if (v < 256 || v <= a || v <= b || !vals.insert(v).second) split_ok = false;
+      max_v = std::max<uint32_t>(max_v, (uint32_t)v);
+    }
+    if (max_v >= (1u << 26)) split_ok = false;  // (inverse table bounded to 512 MiB)
+  }
   sw_encoder* h = new sw_encoder();
   h->device = device;
   h->n_merges = (int64_t)order.size();
+  h->split_ok = split_ok && !order.empty();
   h->table.wide = wide ? 1u : 0u;
   h->ids16 = ids16 && !wide;
   std::vector<uint4> host;
@@ -332,6 +358,22 @@ extern "C" int32_t sw_encoder_create(const int32_t* pairs, const int32_t* vals, 
     h->chunks.l_shift = ct.l_shift; h->chunks.l_m1 = ct.l_m1; h->chunks.l_m2 = ct.l_m2;
     h->chunks.enabled = 1;
   }
+  if (h->split_ok) {
+    std::vector<uint2> inv((size_t)max_v + 1, make_uint2(kInf, kInf));
+    for (uint64_t k : order) inv[(size_t)dict.at(k)] = make_uint2((uint32_t)(k >> 32), (uint32_t)k);
+    e = hipMalloc(&h->d_inv, inv.size() * sizeof(uint2));
+    if (e == hipSuccess) e = hipMemcpy(h->d_inv, inv.data(), inv.size() * sizeof(uint2), hipMemcpyHostToDevice);
+    if (e != hipSuccess) {
+      sw_encoder_destroy(h);
+      return fail(SW_ERR_HIP, std::string("sw_encoder_create: ") + hipGetErrorString(e));
+    }
+    h->n_inv = (uint32_t)inv.size();
+  }
+  e = hipEventCreateWithFlags(&h->ws_done, hipEventDisableTiming);
+  if (e != hipSuccess) {
+    sw_encoder_destroy(h);
+    return fail(SW_ERR_HIP, std::string("sw_encoder_create: ") + hipGetErrorString(e));
+  }
   *out = h;
   return SW_OK;
 }
@@ -343,8 +385,11 @@ extern "C" void sw_encoder_destroy(sw_encoder* h) {
     if (h->stream) (void)hipStreamSynchronize(h->stream);
     free_workspace(h);
     free_io(h);
+    if (h->ws_done) (void)hipEventSynchronize(h->ws_done);
     (void)hipFree(h->d_table);
     (void)hipFree(h->d_chunks);
+    (void)hipFree(h->d_inv);
+    if (h->ws_done) (void)hipEventDestroy(h->ws_done);
     for (hipEvent_t ev : h->ev_pool) (void)hipEventDestroy(ev);
     if (h->stream) (void)hipStreamDestroy(h->stream);
   }
@@ -375,6 +420,12 @@ extern "C" int32_t sw_encoder_set_option(sw_encoder* h, int32_t option, int64_t 
       if (value < 0 || value > 27) return fail(SW_ERR_ARG, "dedupe fingerprint bits: 0..27");
       h->dedupe_fp_mask = (uint32_t)((1ULL << value) - 1);
       return SW_OK;
+    case SW_OPT_LONG_SPLIT: h->long_split = value != 0; return SW_OK;
+    case SW_OPT_MAX_LAUNCH_BYTES:
+      if (value != 0 && (value < 64 || value > kMaxLaunchBytes))
+        return fail(SW_ERR_ARG, "max launch bytes: 0 (default) or 64 .. 2^31 - 128");
+      h->max_launch = value ? value : kMaxLaunchBytes;
+      return SW_OK;
     default: return fail(SW_ERR_ARG, "sw_encoder_set_option: unknown option");
   }
 }
@@ -386,6 +437,7 @@ extern "C" int64_t sw_encoder_get_info(const sw_encoder* h, int32_t what) {
     case SW_INFO_CHUNK_ENTRIES: return h->n_chunk_entries;
     case SW_INFO_WIDE_TABLE: return h->table.wide;
     case SW_INFO_IDS16: return h->ids16 ? 1 : 0;
+    case SW_INFO_SPLIT: return h->split_ok ? 1 : 0;
     default: return SW_ERR_ARG;
   }
 }
@@ -443,6 +495,8 @@ extern "C" int32_t sw_encode_device(sw_encoder* h, const uint8_t* d_bytes, int64
   if (n_bytes > kMaxLaunchBytes) return fail(SW_ERR_ARG, "sw_encode_device: n_bytes >= 2 GiB (split the batch)");
   DeviceGuard g(h->device);
   hipStream_t st = (hipStream_t)stream;  // (NULL: the null stream, as torch's default stream)
+  // the workspace belongs to the handle: order this launch after the previous one on any stream
+  if (h->ws_pending && h->ws_stream != st) HIP_TRY(hipStreamWaitEvent(st, h->ws_done, 0));
   int32_t rc = ensure_workspace(h, n_bytes);
   if (rc) return rc;
   const int64_t n_tiles = (n_bytes + kTile - 1) / kTile;
@@ -471,6 +525,8 @@ extern "C" int32_t sw_encode_device(sw_encoder* h, const uint8_t* d_bytes, int64
     a.out_off = d_out_off; a.tile_slo = h->d_tile_slo;
     a.n_tiles = n_tiles; a.qtmp = h->d_res; a.bcnt = h->d_bcnt; a.boff = h->d_boff; a.q_total = h->d_qtotal;
     a.queue = h->d_queue; a.stamps = h->d_stamps;
+    a.inv = h->d_inv; a.n_inv = h->n_inv;
+    const bool split = h->split_ok && h->long_split;
     hipLaunchKernelGGL(k_tile_strings, dim3((unsigned)((n_tiles + 255) / 256)), dim3(256), 0, st, d_str_off, n_str,
                        n_tiles, h->d_tile_slo);
     if (h->dedupe) HIP_TRY(hipMemsetAsync(h->d_dtab, 0, sizeof(uint64_t) * ((size_t)h->dmask + 1), st));
@@ -485,21 +541,24 @@ extern "C" int32_t sw_encode_device(sw_encoder* h, const uint8_t* d_bytes, int64
       hipLaunchKernelGGL((k_merge_bucket<true, false, 8>), pg, pb, 0, st, a, 3, 4);
       hipLaunchKernelGGL((k_merge_bucket<true, false, 16>), pg, pb, 0, st, a, 5, 7);
       hipLaunchKernelGGL((k_merge_bucket<true, false, 32>), pg, pb, 0, st, a, 8, 9);
-      hipLaunchKernelGGL((k_merge_long_lds<true, false>), dim3(kLongGrid), dim3(64), 0, st, a);
+      if (split) hipLaunchKernelGGL((k_merge_long_split<true, false>), dim3(kLongGrid), dim3(64), 0, st, a);
+      else hipLaunchKernelGGL((k_merge_long_lds<true, false>), dim3(kLongGrid), dim3(64), 0, st, a);
       hipLaunchKernelGGL((k_merge_long<true>), dim3(512), pb, 0, st, a);
     } else if (h->ids16) {
       hipLaunchKernelGGL((k_merge_bucket<false, true, 4>), pg, pb, 0, st, a, 0, 2);
       hipLaunchKernelGGL((k_merge_bucket<false, true, 8>), pg, pb, 0, st, a, 3, 4);
       hipLaunchKernelGGL((k_merge_bucket<false, true, 16>), pg, pb, 0, st, a, 5, 7);
       hipLaunchKernelGGL((k_merge_bucket<false, true, 32>), pg, pb, 0, st, a, 8, 9);
-      hipLaunchKernelGGL((k_merge_long_lds<false, true>), dim3(kLongGrid), dim3(64), 0, st, a);
+      if (split) hipLaunchKernelGGL((k_merge_long_split<false, true>), dim3(kLongGrid), dim3(64), 0, st, a);
+      else hipLaunchKernelGGL((k_merge_long_lds<false, true>), dim3(kLongGrid), dim3(64), 0, st, a);
       hipLaunchKernelGGL((k_merge_long<false>), dim3(512), pb, 0, st, a);
     } else {
       hipLaunchKernelGGL((k_merge_bucket<false, false, 4>), pg, pb, 0, st, a, 0, 2);
       hipLaunchKernelGGL((k_merge_bucket<false, false, 8>), pg, pb, 0, st, a, 3, 4);
       hipLaunchKernelGGL((k_merge_bucket<false, false, 16>), pg, pb, 0, st, a, 5, 7);
       hipLaunchKernelGGL((k_merge_bucket<false, false, 32>), pg, pb, 0, st, a, 8, 9);
-      hipLaunchKernelGGL((k_merge_long_lds<false, false>), dim3(kLongGrid), dim3(64), 0, st, a);
+      if (split) hipLaunchKernelGGL((k_merge_long_split<false, false>), dim3(kLongGrid), dim3(64), 0, st, a);
+      else hipLaunchKernelGGL((k_merge_long_lds<false, false>), dim3(kLongGrid), dim3(64), 0, st, a);
       hipLaunchKernelGGL((k_merge_long<false>), dim3(512), pb, 0, st, a);
     }
     HIP_TRY(hipGetLastError());
@@ -518,6 +577,9 @@ extern "C" int32_t sw_encode_device(sw_encoder* h, const uint8_t* d_bytes, int64
     HIP_TRY(hipEventRecord(e1, st));
     ++h->ev_used;
   }
+  HIP_TRY(hipEventRecord(h->ws_done, st));
+  h->ws_stream = st;
+  h->ws_pending = true;
   if (n_tokens_host) {
     HIP_TRY(hipMemcpyAsync(n_tokens_host, h->d_total, sizeof(int64_t), hipMemcpyDeviceToHost, st));
     HIP_TRY(hipStreamSynchronize(st));
@@ -536,15 +598,17 @@ extern "C" int32_t sw_encode_batch(sw_encoder* h, const uint8_t* bytes, const in
   for (int64_t s = 0; s < n_str; ++s)
     if (str_off[s + 1] < str_off[s]) return fail(SW_ERR_ARG, "sw_encode_batch: string offsets not monotone");
   if (n_bytes > 0 && !out_ids) return fail(SW_ERR_ARG, "sw_encode_batch: null out_ids");
-  if (n_bytes > kMaxLaunchBytes) {
+  if (!chunk_bits && pattern != SW_PAT_CL100K && pattern != SW_PAT_GPT2 && pattern != SW_PAT_NONE)
+    return fail(SW_ERR_ARG, "sw_encode_batch: bad pattern");
+  if (n_bytes > h->max_launch) {
     // one device launch addresses < 2 GiB: encode runs of whole strings separately
     int64_t done = 0, s_lo = 0;
     if (stats) *stats = sw_stats{};
     while (s_lo < n_str) {
       int64_t s_hi = s_lo + 1;
-      while (s_hi < n_str && str_off[s_hi + 1] - str_off[s_lo] <= kMaxLaunchBytes) ++s_hi;
-      if (str_off[s_hi] - str_off[s_lo] > kMaxLaunchBytes)
-        return fail(SW_ERR_ARG, "sw_encode_batch: a single string exceeds 2 GiB");
+      while (s_hi < n_str && str_off[s_hi + 1] - str_off[s_lo] <= h->max_launch) ++s_hi;
+      if (str_off[s_hi] - str_off[s_lo] > h->max_launch)
+        return fail(SW_ERR_ARG, "sw_encode_batch: a single string exceeds the launch limit (2 GiB)");
       std::vector<uint64_t> sub;
       if (chunk_bits) {  // the run's bits, realigned to its first byte
         const int64_t g0 = str_off[s_lo] - b0, nb = str_off[s_hi] - str_off[s_lo];
@@ -563,7 +627,9 @@ extern "C" int32_t sw_encode_batch(sw_encoder* h, const uint8_t* bytes, const in
       for (int64_t s = s_lo; s <= s_hi; ++s) out_off[s] += done;
       done = out_off[s_hi];
       if (stats) {
-        stats->n_bytes += st.n_bytes; stats->n_chunks += st.n_chunks; stats->n_tokens += st.n_tokens;
+        // (a run without a chunk count -- caller bits -- makes the total unknown: -1)
+        stats->n_chunks = (stats->n_chunks < 0 || st.n_chunks < 0) ? -1 : stats->n_chunks + st.n_chunks;
+        stats->n_bytes += st.n_bytes; stats->n_tokens += st.n_tokens;
         stats->ms_presplit += st.ms_presplit; stats->ms_h2d += st.ms_h2d; stats->ms_kernels += st.ms_kernels;
         stats->ms_d2h += st.ms_d2h;
       }
@@ -616,11 +682,7 @@ extern "C" int32_t sw_encode_batch(sw_encoder* h, const uint8_t* bytes, const in
   h->timing = true;
   h->ev_used = 0;
   const int32_t was_pattern = h->pattern;
-  if (device_presplit) {
-    if (pattern != SW_PAT_CL100K && pattern != SW_PAT_GPT2 && pattern != SW_PAT_NONE)
-      return fail(SW_ERR_ARG, "sw_encode_batch: bad pattern");
-    h->pattern = pattern;
-  }
+  if (device_presplit) h->pattern = pattern;
   int32_t rc = sw_encode_device(h, h->d_bytes, n_bytes, h->d_str_off, n_str, device_presplit ? nullptr : h->d_bits,
                                 h->d_out, h->d_out_off, st, &n_tok);
   h->pattern = was_pattern;

@@ -417,6 +417,8 @@ struct EncArgs {
   uint32_t dfp_mask;         // fingerprint bits in use (all 27 except in collision tests)
   uint32_t dedupe;           // 0: every queued chunk runs its own merge loop
   unsigned long long* stamps;  // SW_STAMPS builds: cycles per phase, summed
+  const uint2* inv;          // [n_inv] merge value -> its pair (a, b); well-formed tables only
+  uint32_t n_inv;
 };
 
 #ifdef SW_STAMPS
@@ -1091,6 +1093,248 @@ __global__ void __launch_bounds__(64) k_merge_long_lds(EncArgs a) {
     uint32_t* gid = a.res + 2 * start + 1;
     const int m = seg_merge<kWide, T>(a.table, s_id, s_rk, s_kill, s_dirty, (int)len, lane, gid);
     if (lane == 0) gid[-1] = (uint32_t)m;
+    wave_sync_mem();
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+// Long chunks by exact SPLIT + VERIFY (well-formed tables; DESIGN.md §4.2 has the proof).
+//
+// A table is well-formed when every value is >= 256, unique, and larger than both ids of its
+// pair.  Then the reference loop (base.py:10-36) applies ranks in strictly increasing order,
+// and a token's id is the step that created it.  Cut a chunk into pieces A | B and encode them
+// on their own: until a merge joins the last token of A with the first token of B, the joint
+// state is the concatenation of the two states.  The last token of A over time is the RIGHT
+// spine of A's final last token in the merge tree (a_0 < a_1 < ... ids = creation steps), the
+// first token of B the LEFT spine of B's final first token.  The pair (a_i, b_j) exists from
+// max(a_i, b_j) until min(a_{i+1}, b_{j+1}); the joint loop merges it iff its rank R comes
+// before either token is replaced: R < a_{i+1} and R <= b_{j+1} (R == a_{i+1} means the same
+// (x, x) pair also ends A, and left to right takes A's occurrence first).  If no coexisting pair
+// of the two spines satisfies that, the joint encoding IS the concatenation; otherwise the two
+// pieces are joined into one window and encoded again, and its new neighbours are checked.
+// After kSplitRounds rounds (long (a,a) runs cascade) or for a window over kMaxWindow bytes the
+// whole chunk runs the wave loop (seg_merge).  Cut points are chosen where the byte pair ranks
+// highest (ideally not a merge at all), which leaves ~1% of the junctions in conflict.
+// ---------------------------------------------------------------------------------------
+constexpr int kPieceW = 24;                                      // cut spacing (pieces 17..31 B)
+constexpr int kMaxPieces = (kLongLds + kPieceW - 1) / kPieceW;   // 171
+constexpr int kJWords = (kMaxPieces + 63) / 64;                  // junction bitmask words
+constexpr int kSplitRounds = 3;
+constexpr int kMaxWindow = 512;
+static_assert(kJWords == 3, "cbit() selects among three words");
+
+// May the joint encoding of two adjacent segments differ from their separate encodings?  a: the
+// left segment's last token, b: the right segment's first token (both encoded on their own).
+// Walks the coexisting pairs of the two spines from the final state backwards: one pair lookup
+// and one inverse-table load (issued together) per step.
+template <bool kWide>
+__device__ __forceinline__ bool junction_conflict(const DevTable& t, const uint2* inv, uint32_t n_inv, uint32_t a,
+                                                  uint32_t b) {
+  uint32_t na = kInf, nb = kInf;  // the ids (= creation steps) of the tokens that replace a / b
+  for (int it = 0; it < 128; ++it) {
+    const bool ra = a >= 256 && (b < 256 || a > b);  // the later-created one is reverted next
+    const uint32_t x = ra ? a : b;
+    if (x >= 256 && x >= n_inv) return true;  // (not a merge value: cannot happen; be conservative)
+    const uint2 pr = x >= 256 ? inv[x] : make_uint2(0u, 0u);
+    const uint32_t R = lookup<kWide>(t, a, b);
+    if (R != kInf && R < na && R <= nb) return true;
+    if (a < 256 && b < 256) return false;
+    if (ra) { na = a; a = pr.y; } else { nb = b; b = pr.x; }
+  }
+  return true;
+}
+
+// The exact loop (any table) on id[0..n) in LDS, run by ONE lane: ranks in rk[0..n-1), merges
+// compacted in place.  For the rare re-encoded windows of the split path.  Returns the count.
+template <bool kWide, typename T>
+__device__ int lane_merge_lds(const DevTable& t, T* id, T* rk, int n) {
+  constexpr uint32_t TINF = sizeof(T) == 2 ? 0xFFFFu : kInf;  // (16-bit storage: values <= 0xFFFD)
+  constexpr uint32_t TREC = TINF - 1;                          // "look up again"
+  auto st = [](uint32_t r) -> T { return (T)(r == kInf ? TINF : r); };
+  for (int i0 = 0; i0 + 1 < n; i0 += 8) {  // initial ranks, eight lookups in flight
+    uint32_t r[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) r[u] = (i0 + u + 1 < n) ? lookup<kWide>(t, id[i0 + u], id[i0 + u + 1]) : kInf;
+#pragma unroll
+    for (int u = 0; u < 8; ++u)
+      if (i0 + u + 1 < n) rk[i0 + u] = st(r[u]);
+  }
+  while (n >= 2) {
+    uint32_t best = TINF;
+    int bp = -1;
+    for (int i = 0; i + 1 < n; ++i) {
+      const uint32_t r = rk[i];
+      if (r < best) { best = r; bp = i; }
+    }
+    if (bp < 0) break;
+    // every non-overlapping occurrence, left to right (none before bp: it is the first with
+    // the minimum rank)
+    const uint32_t p0 = id[bp], p1 = id[bp + 1];
+    int w = bp;
+    for (int i = bp; i < n;) {
+      if (i + 1 < n && id[i] == p0 && id[i + 1] == p1) {
+        id[w] = (T)best;
+        rk[w] = (T)TREC;
+        if (w > 0) rk[w - 1] = (T)TREC;
+        ++w;
+        i += 2;
+      } else {
+        id[w] = id[i];
+        rk[w] = rk[i];
+        ++w;
+        ++i;
+      }
+    }
+    n = w;
+    for (int i = bp > 0 ? bp - 1 : 0; i + 1 < n; ++i)
+      if (rk[i] == TREC) rk[i] = st(lookup<kWide>(t, id[i], id[i + 1]));
+  }
+  return n;
+}
+
+template <bool kWide, bool k16>
+__global__ void __launch_bounds__(64) k_merge_long_split(EncArgs a) {
+  typedef typename std::conditional<k16, uint16_t, uint32_t>::type T;
+  __shared__ T s_id[kLongLds];
+  __shared__ T s_rk[kLongLds];
+  __shared__ uint64_t s_kill[64], s_dirty[64];
+  __shared__ uint16_t s_cut[2][kMaxPieces + 1];  // piece k = [cut[k], cut[k + 1]) (double-buffered)
+  __shared__ uint16_t s_cnt[2][kMaxPieces];      // its ids, at s_id[cut[k] ..)
+  __shared__ uint8_t s_win[kMaxPieces];          // piece k is a window to encode again
+  const int lane = threadIdx.x;
+  const uint64_t lt_mask = (lane == 0) ? 0ULL : (~0ULL >> (64 - lane));
+  const DevTable& tb = a.table;
+  int64_t lo, hi;
+  bucket_range(a, kLongBucket, kLongBucket, &lo, &hi);
+  for (int64_t i = lo + blockIdx.x; i < hi; i += gridDim.x) {
+    const uint64_t e = a.queue[i];
+    const int64_t start = (int64_t)(e >> 24);
+    const int len = (int)(next_set_bit(a.bits, a.n_words, start + 1, a.n_bytes) - start);
+    if (len > kLongLds) continue;  // (k_merge_long)
+    const uint8_t* src = a.bytes + start;
+    uint32_t* gid = a.res + 2 * start + 1;
+    for (int j = lane; j < len; j += 64) s_id[j] = (T)src[j];
+    int cur = 0;
+    int P = (len + kPieceW - 1) / kPieceW;
+    if (lane == 0) { s_cut[0][0] = 0; s_cut[0][P] = (uint16_t)len; }
+    wave_sync_mem();
+    // cut k (1 <= k < P) at the position in [24k - 4, 24k + 4) whose byte pair ranks highest
+    for (int k = 1 + lane; k < P; k += 64) {
+      const int c0 = k * kPieceW - 4;
+      uint32_t r[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) r[u] = (c0 + u < len) ? lookup<kWide>(tb, s_id[c0 + u - 1], s_id[c0 + u]) : 0u;
+      int best = c0;
+      uint32_t br = r[0];
+#pragma unroll
+      for (int u = 1; u < 8; ++u)
+        if (r[u] > br) { br = r[u]; best = c0 + u; }
+      s_cut[0][k] = (uint16_t)best;
+    }
+    wave_sync_mem();
+    // every piece on its own (one lane each, in registers)
+    for (int k = lane; k < P; k += 64) {
+      const int c = s_cut[0][k], n = s_cut[0][k + 1] - c;
+      uint32_t id[kShort];
+#pragma unroll
+      for (int j = 0; j < kShort; ++j) id[j] = j < n ? (uint32_t)s_id[c + j] : 0u;
+      const uint32_t alive = lane_merge_reg<kWide, k16, kShort>(tb, id, n);
+      int m = 0;
+#pragma unroll
+      for (int j = 0; j < kShort; ++j)
+        if ((alive >> j) & 1u) s_id[c + m++] = (T)id[j];
+      s_cnt[0][k] = (uint16_t)m;
+    }
+    wave_sync_mem();
+    // junction k (between pieces k - 1 and k) is bit k - 1
+    uint64_t conf[kJWords];
+#pragma unroll
+    for (int g = 0; g < kJWords; ++g) {
+      const int k = 1 + 64 * g + lane;
+      bool c = false;
+      if (k < P) c = junction_conflict<kWide>(tb, a.inv, a.n_inv, s_id[s_cut[0][k - 1] + s_cnt[0][k - 1] - 1],
+                                              s_id[s_cut[0][k]]);
+      conf[g] = __ballot(c);
+    }
+    auto cbit = [&](int j) -> bool {  // (selects: no dynamically indexed registers)
+      const uint64_t w = j < 64 ? conf[0] : j < 128 ? conf[1] : conf[2];
+      return (w >> (j & 63)) & 1ULL;
+    };
+    bool fall = false;
+    for (int round = 0; (conf[0] | conf[1] | conf[2]) != 0ULL; ++round) {
+      if (round == kSplitRounds) { fall = true; break; }
+      // join the pieces across conflicting junctions; a joined piece is a window to encode again
+      const uint16_t* cut = s_cut[cur];
+      const uint16_t* cnt = s_cnt[cur];
+      uint16_t* ncut = s_cut[cur ^ 1];
+      uint16_t* ncnt = s_cnt[cur ^ 1];
+      int np = 0;
+#pragma unroll
+      for (int g = 0; g < kJWords; ++g) {
+        const int k = 64 * g + lane;
+        const bool keep = k < P && (k == 0 || !cbit(k - 1));
+        const bool win = keep && k + 1 < P && cbit(k);
+        const uint64_t km = __ballot(keep);
+        const int idx = np + __popcll(km & lt_mask);
+        if (keep) {
+          ncut[idx] = cut[k];
+          ncnt[idx] = cnt[k];
+          s_win[idx] = win ? 1 : 0;
+        }
+        np += __popcll(km);
+      }
+      if (lane == 0) ncut[np] = (uint16_t)len;
+      cur ^= 1;
+      P = np;
+      wave_sync_mem();
+      bool over = false;
+      for (int j = lane; j < P; j += 64) {
+        if (!s_win[j]) continue;
+        const int c = ncut[j], n = ncut[j + 1] - c;
+        if (n > kMaxWindow) { over = true; continue; }
+        for (int q = 0; q < n; ++q) s_id[c + q] = (T)src[c + q];
+        ncnt[j] = (uint16_t)lane_merge_lds<kWide, T>(tb, s_id + c, s_rk + c, n);
+      }
+      if (__ballot(over)) { fall = true; break; }
+      wave_sync_mem();
+      // only the junctions next to a window can have changed
+#pragma unroll
+      for (int g = 0; g < kJWords; ++g) {
+        const int k = 1 + 64 * g + lane;
+        bool c = false;
+        if (k < P && (s_win[k - 1] || s_win[k]))
+          c = junction_conflict<kWide>(tb, a.inv, a.n_inv, s_id[ncut[k - 1] + ncnt[k - 1] - 1], s_id[ncut[k]]);
+        conf[g] = __ballot(c);
+      }
+    }
+    if (fall) {  // the whole chunk in the wave loop
+      wave_sync_mem();
+      for (int j = lane; j < len; j += 64) s_id[lds_pos(j)] = (T)src[j];
+      wave_sync_mem();
+      const int m = seg_merge<kWide, T>(tb, s_id, s_rk, s_kill, s_dirty, len, lane, gid);
+      if (lane == 0) gid[-1] = (uint32_t)m;
+      wave_sync_mem();
+      continue;
+    }
+    // the pieces' ids in order: gathered into s_rk, then stored coalesced
+    const uint16_t* cut = s_cut[cur];
+    const uint16_t* cnt = s_cnt[cur];
+    int total = 0;
+#pragma unroll
+    for (int g = 0; g < kJWords; ++g) {
+      const int k = 64 * g + lane;
+      const uint32_t c = k < P ? cnt[k] : 0u;
+      const uint32_t incl = wave_incl_scan(c, lane);
+      const int o = total + (int)(incl - c);
+      if (k < P) {
+        const int b = cut[k];
+        for (uint32_t q = 0; q < c; ++q) s_rk[o + q] = s_id[b + q];
+      }
+      total += (int)__shfl(incl, 63, 64);
+    }
+    wave_sync_mem();
+    for (int q = lane; q < total; q += 64) gid[q] = (uint32_t)s_rk[q];
+    if (lane == 0) gid[-1] = (uint32_t)total;
     wave_sync_mem();
   }
 }

@@ -7,6 +7,7 @@ base.py:22-36).  Pre-split runs in native host code, the merge loop in HIP kerne
 device.  There is no CPU fallback: without the library or a device, encode raises.
 """
 import ctypes
+import re
 
 import numpy as np
 
@@ -52,6 +53,10 @@ class _TrackedDict(dict):
         self._bump()
         return r
 
+    def __ior__(self, other):
+        self.update(other)
+        return self
+
 
 def _pack_strings(datas):
     """list of bytes -> (uint8 buffer, int64 offsets[n+1])."""
@@ -65,12 +70,17 @@ class Tokenizer(BaseTokenizer):
     """shredword tokenizer whose encode runs on an MI355X.
 
     Attributes are those of BaseTokenizer (merges, pattern, special_tokens, vocab).  `pattern`
-    selects the pre-split: "" (default) or the cl100k pattern = what apply_regex does; the GPT-2
-    pattern; anything else raises NotImplementedError at encode time.
+    selects the pre-split (base.pattern_id): "" (default) or the cl100k pattern = what
+    apply_regex does; the GPT-2 pattern of base.py:46; any other pattern string falls back to
+    cl100k, because the reference's apply_regex ignores the tokenizer's pattern (base.py:56).
+    Edits to `merges` (item assignment, update, |=, reassignment) reach the device table on the
+    next encode; `vocab` is rebuilt from merges and special_tokens whenever either changed.
     """
 
     def __init__(self, device=0):
         self._merges = _TrackedDict()
+        self._vocab = _TrackedDict()
+        self._vocab_key = None
         super().__init__()
         self.device = device
         self._handle = None
@@ -78,6 +88,8 @@ class Tokenizer(BaseTokenizer):
         self._dec = None
         self._dec_key = None
         self._dec_len = None
+        self._sp_key = None
+        self._sp_re = None
         self.last_stats = None
 
     # merges is tracked so that edits (README-style `tok.merges[(a, b)] = id`) reach the device
@@ -90,6 +102,21 @@ class Tokenizer(BaseTokenizer):
         d = _TrackedDict(value)
         d.version = self._merges.version + 1
         self._merges = d
+
+    # vocab is tracked too, so in-place edits reach the device decoder
+    @property
+    def vocab(self):
+        return self._vocab
+
+    @vocab.setter
+    def vocab(self, value):
+        d = _TrackedDict(value)
+        d.version = self._vocab.version + 1
+        self._vocab = d
+        self._vocab_key = self._vocab_source_key()
+
+    def _vocab_source_key(self):
+        return (id(self._merges), self._merges.version, tuple(getattr(self, "special_tokens", {}).items()))
 
     def __del__(self):
         self.close()
@@ -153,20 +180,21 @@ class Tokenizer(BaseTokenizer):
 
     def _split_specials(self, text):
         """Split on special tokens: leftmost occurrence first, dictionary order breaking ties
-        (the reference stores special_tokens at base.py:103 but defines no split)."""
-        specials = [s for s in self.special_tokens if s]
-        if not specials:
+        (the reference stores special_tokens at base.py:103 but defines no split).  One regex
+        alternation of the escaped specials in dict order: `re` takes the leftmost match and,
+        at one position, the first alternative that matches -- exactly that rule."""
+        key = tuple(self.special_tokens.items())
+        if key != self._sp_key:
+            specials = [s for s in self.special_tokens if s]
+            self._sp_re = re.compile("|".join(map(re.escape, specials))) if specials else None
+            self._sp_key = key
+        if self._sp_re is None:
             return [text]
-        parts, seg, i, n = [], 0, 0, len(text)
-        while i < n:
-            hit = next((s for s in specials if text.startswith(s, i)), None)
-            if hit is None:
-                i += 1
-                continue
-            parts.append(text[seg:i])
-            parts.append(self.special_tokens[hit])
-            i += len(hit)
-            seg = i
+        parts, seg = [], 0
+        for m in self._sp_re.finditer(text):
+            parts.append(text[seg:m.start()])
+            parts.append(self.special_tokens[m.group()])
+            seg = m.end()
         parts.append(text[seg:])
         return parts
 
@@ -174,11 +202,16 @@ class Tokenizer(BaseTokenizer):
         """Encode many strings in one device batch; returns a list of id lists."""
         if allowed_special not in ("all", "none"):
             raise ValueError("allowed_special must be 'all' or 'none'")
+        texts = list(texts)
+        split = allowed_special == "all" and any(self.special_tokens)
+        if not split:  # one piece per text: one device batch, one list conversion
+            ids, off = self.encode_ordinary_batch_np([t.encode("utf-8") for t in texts])
+            flat, o = ids.tolist(), off.tolist()
+            return [flat[o[k]:o[k + 1]] for k in range(len(texts))]
         pieces, layout = [], []
         for t in texts:
-            parts = self._split_specials(t) if allowed_special == "all" else [t]
             lay = []
-            for p in parts:
+            for p in self._split_specials(t):
                 if isinstance(p, int):
                     lay.append(p)
                 else:
@@ -186,6 +219,7 @@ class Tokenizer(BaseTokenizer):
                     pieces.append(p.encode("utf-8"))
             layout.append(lay)
         ids, off = self.encode_ordinary_batch_np(pieces)
+        flat, o = ids.tolist(), off.tolist()
         out = []
         for lay in layout:
             r = []
@@ -193,8 +227,7 @@ class Tokenizer(BaseTokenizer):
                 if x >= 0:
                     r.append(x)
                 else:
-                    k = -1 - x
-                    r.extend(ids[off[k]:off[k + 1]].tolist())
+                    r.extend(flat[o[-1 - x]:o[-x]])
             out.append(r)
         return out
 
@@ -206,14 +239,16 @@ class Tokenizer(BaseTokenizer):
 
     # ---------------------------------------------------------------- decode
     def _vocab_now(self):
-        if len(self.vocab) != 256 + len(self._merges) + len(self.special_tokens):
+        """self.vocab, rebuilt by build_vocab (base.py:60-79) when merges or special_tokens have
+        changed since it was last set; a vocab assigned directly is used as it is."""
+        if self._vocab_key != self._vocab_source_key():
             self.vocab = build_vocab(self._merges, self.special_tokens)
-        return self.vocab
+        return self._vocab
 
     def _decoder(self):
         """Device copy of the vocabulary (build_vocab, base.py:60-79), rebuilt when it changes."""
         vocab = self._vocab_now()
-        key = (id(vocab), len(vocab), self.device)
+        key = (id(vocab), vocab.version, self.device)
         if self._dec is not None and self._dec_key == key:
             return self._dec
         d, self._dec = self._dec, None
@@ -274,9 +309,3 @@ class Tokenizer(BaseTokenizer):
         """ids -> str: vocab bytes joined (on the device), undecodable bytes replaced (the
         conventional decode over build_vocab, base.py:60-79)."""
         return self.decode_batch([list(ids)])[0]
-
-    def load(self, model_file):
-        super().load(model_file)
-
-    def load_binary(self, model_file):
-        super().load_binary(model_file)

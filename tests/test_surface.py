@@ -123,8 +123,59 @@ def test_pattern_selection():
     assert sb.pattern_id(sb.CL100K_PATTERN) == 0
     assert sb.pattern_id(sb.GPT2_PATTERN) == 1
     assert sb.pattern_id(sb.GPT2_PATTERN_ALT) == 1
-    with pytest.raises(NotImplementedError):
-        sb.pattern_id(r"\w+")
+    assert sb.pattern_id(2) == 2
+    # any other pattern string: cl100k, as the reference's apply_regex (base.py:56) does
+    pattern3 = r"""'s|'t|'re|'ve|'m|'ll|'d|[\w']+|[^\s\w\d]+|\s+(?!\S)|\s+"""
+    with pytest.warns(UserWarning, match="cl100k"):
+        assert sb.pattern_id(pattern3) == 0
+    for bad in (7, -1):
+        with pytest.raises(ValueError):
+            sb.pattern_id(bad)
+    with pytest.raises(TypeError):
+        sb.pattern_id(None)
+
+
+def test_tracked_merges_and_vocab():
+    # edits of every kind bump the version the device table is keyed on (ADVICE r1)
+    t = sa.Tokenizer(device=0)
+    seen = [t.merges.version]
+    t.merges[(97, 98)] = 256
+    seen.append(t.merges.version)
+    t.merges |= {(99, 100): 257}  # (__ior__, then the property setter)
+    seen.append(t.merges.version)
+    d = t.merges
+    d |= {(1, 2): 259}  # __ior__ alone
+    seen.append(t.merges.version)
+    t.merges.update({(256, 257): 258})
+    seen.append(t.merges.version)
+    assert all(a < b for a, b in zip(seen, seen[1:])), seen
+    assert isinstance(t.merges, type(t.merges)) and t.merges[(99, 100)] == 257
+    # a same-size replacement rebuilds the vocabulary decode uses
+    t.merges = {(97, 98): 256}
+    assert t._vocab_now()[256] == b"ab"
+    t.merges = {(99, 100): 256}
+    assert t._vocab_now()[256] == b"cd"
+    t.merges[(99, 100)] = 300  # in-place value change
+    assert t._vocab_now()[300] == b"cd"
+    t.special_tokens["<|x|>"] = 400
+    assert t._vocab_now()[400] == b"<|x|>"
+    # a vocab assigned directly is used as given until merges/specials change
+    ver = t.vocab.version
+    t.vocab = dict(t.vocab, **{})
+    assert t.vocab.version == ver + 1
+    t.vocab[5] = b"zz"
+    assert t._vocab_now()[5] == b"zz" and t.vocab.version == ver + 2
+
+
+def test_special_split_rule():
+    t = sa.Tokenizer(device=0)
+    t.special_tokens = {"<a>": 300, "<a><b>": 301, "<b>": 302}
+    # leftmost first; at one position the first special in dict order wins
+    assert t._split_specials("x<a><b>y<b>") == ["x", 300, "", 302, "y", 302, ""]
+    t.special_tokens = {"<a><b>": 301, "<a>": 300}
+    assert t._split_specials("x<a><b>y<a>") == ["x", 301, "y", 300, ""]
+    t.special_tokens = {}
+    assert t._split_specials("x<a>") == ["x<a>"]
 
 
 def test_corpus_deterministic_across_threads():

@@ -228,23 +228,16 @@ struct RegKey {  // (rank, slot) packed so that min() picks the lowest rank, the
   }
 };
 
+// the loop itself: id[k] / rk[k] = the ids and the ranks of the pairs (k, k + 1) (kInf past n - 1)
 template <bool kWide, bool k16, int N>
-__device__ __forceinline__ uint32_t lane_merge_reg(const DevTable& t, uint32_t (&id)[N], int n, int* iters = nullptr) {
+__device__ __forceinline__ uint32_t lane_merge_reg_loop(const DevTable& t, uint32_t (&id)[N], uint32_t (&rk)[N], int n,
+                                                        int* iters = nullptr) {
   using RK = RegKey<k16>;
   constexpr uint32_t NONE = 0xFFFFFFFFu;  // no right neighbour
-  uint32_t rid[N], rk[N];
+  uint32_t rid[N];
 #pragma unroll
   for (int k = 0; k < N; ++k) rid[k] = (k + 1 < n) ? id[(k + 1) % N] : NONE;
   uint32_t alive = (n >= 32) ? 0xFFFFFFFFu : ((1u << n) - 1u);
-  // initial ranks: four lookups in flight at a time (sched barriers cap the live registers)
-#pragma unroll
-  for (int g = 0; g < N; g += 4) {
-#pragma unroll
-    for (int k = g; k < g + 4 && k < N; ++k) rk[k] = lookup<kWide>(t, id[k], rid[k]);
-#pragma unroll
-    for (int k = g; k < g + 4 && k < N; ++k) rk[k] = (rid[k] == NONE) ? kInf : rk[k];
-    __builtin_amdgcn_sched_barrier(0);
-  }
   int it = 0;
   while (true) {
     typename RK::T best = RK::inf;
@@ -313,6 +306,21 @@ __device__ __forceinline__ uint32_t lane_merge_reg(const DevTable& t, uint32_t (
   }
   if (iters) *iters = it;
   return alive;
+}
+
+template <bool kWide, bool k16, int N>
+__device__ __forceinline__ uint32_t lane_merge_reg(const DevTable& t, uint32_t (&id)[N], int n, int* iters = nullptr) {
+  uint32_t rk[N];
+  // initial ranks: four lookups in flight at a time (sched barriers cap the live registers)
+#pragma unroll
+  for (int g = 0; g < N; g += 4) {
+#pragma unroll
+    for (int k = g; k < g + 4 && k < N; ++k) rk[k] = lookup<kWide>(t, id[k], id[(k + 1) % N]);
+#pragma unroll
+    for (int k = g; k < g + 4 && k < N; ++k) rk[k] = (k + 1 < n) ? rk[k] : kInf;
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  return lane_merge_reg_loop<kWide, k16, N>(t, id, rk, n, iters);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -431,7 +439,12 @@ struct EncArgs {
     }                                                                               \
   } while (0)
 #define SW_STAMP_INIT unsigned long long stamp_prev_ = __builtin_readcyclecounter()
+#define SW_COUNT(k, v)                                                              \
+  do {                                                                              \
+    if (threadIdx.x == 0) atomicAdd(&a.stamps[(k) * 64 + (blockIdx.x & 63)], (unsigned long long)(v)); \
+  } while (0)
 #else
+#define SW_COUNT(k, v) do {} while (0)
 #define SW_STAMP(k) do {} while (0)
 #define SW_STAMP_INIT do {} while (0)
 #endif
@@ -1116,12 +1129,21 @@ __global__ void __launch_bounds__(64) k_merge_long_lds(EncArgs a) {
 // whole chunk runs the wave loop (seg_merge).  Cut points are chosen where the byte pair ranks
 // highest (ideally not a merge at all), which leaves ~1% of the junctions in conflict.
 // ---------------------------------------------------------------------------------------
-constexpr int kPieceW = 24;                                      // cut spacing (pieces 17..31 B)
-constexpr int kMaxPieces = (kLongLds + kPieceW - 1) / kPieceW;   // 171
+#ifndef SW_PIECE_N
+#define SW_PIECE_N 16
+#endif
+constexpr int kPieceN = SW_PIECE_N;                              // per-lane register loop size
+constexpr int kPieceW = kPieceN == 32 ? 24 : 12;                 // cut spacing
+constexpr int kCutHalf = kPieceN == 32 ? 4 : 2;                  // cuts in [W k - H, W k + H)
+constexpr int kMaxPieces = (kLongLds + kPieceW - 1) / kPieceW;   // 171 (342)
 constexpr int kJWords = (kMaxPieces + 63) / 64;                  // junction bitmask words
-constexpr int kSplitRounds = 3;
+static_assert(kPieceW + 2 * kCutHalf - 1 <= kPieceN && kPieceW + kCutHalf <= kPieceN, "pieces fit the loop");
+constexpr int kSplitRounds = 6;
+#ifndef SW_BRK_BATCH
+#define SW_BRK_BATCH 8
+#endif
+constexpr int kBrkBatch = SW_BRK_BATCH;                          // byte-pair lookups in flight per lane
 constexpr int kMaxWindow = 512;
-static_assert(kJWords == 3, "cbit() selects among three words");
 
 // May the joint encoding of two adjacent segments differ from their separate encodings?  a: the
 // left segment's last token, b: the right segment's first token (both encoded on their own).
@@ -1144,21 +1166,13 @@ __device__ __forceinline__ bool junction_conflict(const DevTable& t, const uint2
   return true;
 }
 
-// The exact loop (any table) on id[0..n) in LDS, run by ONE lane: ranks in rk[0..n-1), merges
-// compacted in place.  For the rare re-encoded windows of the split path.  Returns the count.
+// The exact loop (any table) on id[0..n) in LDS run by ONE lane, for the rare windows over 64
+// bytes: rk[0..n-1) holds the ranks of the pairs (i, i + 1) on entry (TINF = not a merge) and is
+// scratch after; merges are compacted in place.  Returns the count.
 template <bool kWide, typename T>
 __device__ int lane_merge_lds(const DevTable& t, T* id, T* rk, int n) {
   constexpr uint32_t TINF = sizeof(T) == 2 ? 0xFFFFu : kInf;  // (16-bit storage: values <= 0xFFFD)
   constexpr uint32_t TREC = TINF - 1;                          // "look up again"
-  auto st = [](uint32_t r) -> T { return (T)(r == kInf ? TINF : r); };
-  for (int i0 = 0; i0 + 1 < n; i0 += 8) {  // initial ranks, eight lookups in flight
-    uint32_t r[8];
-#pragma unroll
-    for (int u = 0; u < 8; ++u) r[u] = (i0 + u + 1 < n) ? lookup<kWide>(t, id[i0 + u], id[i0 + u + 1]) : kInf;
-#pragma unroll
-    for (int u = 0; u < 8; ++u)
-      if (i0 + u + 1 < n) rk[i0 + u] = st(r[u]);
-  }
   while (n >= 2) {
     uint32_t best = TINF;
     int bp = -1;
@@ -1186,17 +1200,74 @@ __device__ int lane_merge_lds(const DevTable& t, T* id, T* rk, int n) {
       }
     }
     n = w;
-    for (int i = bp > 0 ? bp - 1 : 0; i + 1 < n; ++i)
-      if (rk[i] == TREC) rk[i] = st(lookup<kWide>(t, id[i], id[i + 1]));
+    for (int i = bp > 0 ? bp - 1 : 0; i + 1 < n; ++i) {
+      if (rk[i] == TREC) {
+        const uint32_t r = lookup<kWide>(t, id[i], id[i + 1]);
+        rk[i] = (T)(r == kInf ? TINF : r);
+      }
+    }
   }
   return n;
+}
+
+// The exact loop (any table) on a window of n <= 64 ids held one per lane (lane = position):
+// rk = the rank of the pair (lane, lane + 1), kInf for the last.  Per step one wave min of
+// (rank, position), the occurrences of that pair by ballot ((a, a) runs resolved left to right in
+// alive order), the right partners die, and only the pairs touching a new token are looked up
+// again -- all lanes at once.  Returns the alive mask; the survivors' ids stay in `id`.
+template <bool kWide>
+__device__ uint64_t wave_merge64(const DevTable& t, uint32_t& id, uint32_t& rk, int n, int lane) {
+  uint64_t alive = n >= 64 ? ~0ULL : ((1ULL << n) - 1ULL);
+  auto next_alive = [&](int j) -> int {
+    const uint64_t m = j >= 63 ? 0ULL : (alive & (~0ULL << (j + 1)));
+    return m ? __builtin_ctzll(m) : 64;
+  };
+  while (true) {
+    const bool al = (alive >> lane) & 1ULL;
+    const uint64_t key = (al && rk != kInf) ? (((uint64_t)rk << 6) | (uint64_t)lane) : ~0ULL;
+    const uint64_t kmin = wave_min_u64(key);
+    if (kmin == ~0ULL) break;
+    const uint32_t r = (uint32_t)(kmin >> 6);
+    const int pm = (int)(kmin & 63);
+    const int nx = next_alive(lane);
+    const uint32_t nid = (uint32_t)__shfl((int)id, nx & 63, 64);
+    const uint32_t p0 = (uint32_t)__shfl((int)id, pm, 64), p1 = (uint32_t)__shfl((int)nid, pm, 64);
+    const uint64_t M = __ballot(al && nx < 64 && id == p0 && nid == p1);
+    uint64_t T = M;
+    if (p0 == p1) {  // (a, a): a taken position consumes its next alive one
+      T = 0;
+      int consumed = -1;
+      for (uint64_t m = M; m; m &= m - 1) {
+        const int q = __builtin_ctzll(m);
+        if (q != consumed) {
+          T |= 1ULL << q;
+          consumed = next_alive(q);
+        }
+      }
+    }
+    const uint64_t below = alive & ((1ULL << lane) - 1ULL);
+    const int pv = below ? 63 - __builtin_clzll(below) : -1;
+    const bool dies = al && pv >= 0 && ((T >> pv) & 1ULL);
+    const bool took = (T >> lane) & 1ULL;
+    if (took) id = r;
+    alive &= ~__ballot(dies);
+    const bool al2 = (alive >> lane) & 1ULL;
+    const int nx2 = next_alive(lane);
+    const uint32_t nid2 = (uint32_t)__shfl((int)id, nx2 & 63, 64);
+    if (al2) {
+      if (nx2 >= 64) rk = kInf;
+      else if (took || ((T >> nx2) & 1ULL)) rk = lookup<kWide>(t, id, nid2);
+    }
+  }
+  return alive;
 }
 
 template <bool kWide, bool k16>
 __global__ void __launch_bounds__(64) k_merge_long_split(EncArgs a) {
   typedef typename std::conditional<k16, uint16_t, uint32_t>::type T;
-  __shared__ T s_id[kLongLds];
-  __shared__ T s_rk[kLongLds];
+  constexpr uint32_t TINF = k16 ? 0xFFFFu : kInf;  // (16-bit storage: values <= 0xFFFD)
+  __shared__ T s_id[kLongLds];    // bytes, then each piece's ids from its first position
+  __shared__ T s_brk[kLongLds];   // rank of the byte pair (p, p + 1); output staging at the end
   __shared__ uint64_t s_kill[64], s_dirty[64];
   __shared__ uint16_t s_cut[2][kMaxPieces + 1];  // piece k = [cut[k], cut[k + 1]) (double-buffered)
   __shared__ uint16_t s_cnt[2][kMaxPieces];      // its ids, at s_id[cut[k] ..)
@@ -1204,48 +1275,79 @@ __global__ void __launch_bounds__(64) k_merge_long_split(EncArgs a) {
   const int lane = threadIdx.x;
   const uint64_t lt_mask = (lane == 0) ? 0ULL : (~0ULL >> (64 - lane));
   const DevTable& tb = a.table;
+  auto brk = [&](int p) -> uint32_t {
+    const uint32_t r = s_brk[p];
+    return r == TINF ? kInf : r;
+  };
   int64_t lo, hi;
+  SW_STAMP_INIT;
   bucket_range(a, kLongBucket, kLongBucket, &lo, &hi);
   for (int64_t i = lo + blockIdx.x; i < hi; i += gridDim.x) {
     const uint64_t e = a.queue[i];
     const int64_t start = (int64_t)(e >> 24);
     const int len = (int)(next_set_bit(a.bits, a.n_words, start + 1, a.n_bytes) - start);
     if (len > kLongLds) continue;  // (k_merge_long)
+    SW_STAMP(18);
+    SW_COUNT(20, 1);
+    SW_COUNT(21, len);
+#ifdef SW_STAMPS
+    const unsigned long long t_chunk0 = __builtin_readcyclecounter();
+    bool big_win = false;
+#endif
     const uint8_t* src = a.bytes + start;
     uint32_t* gid = a.res + 2 * start + 1;
     for (int j = lane; j < len; j += 64) s_id[j] = (T)src[j];
+    wave_sync_mem();
+    // the rank of every byte pair, all lanes, kBrkBatch lookups in flight per lane
+    for (int p0 = 0; p0 < len - 1; p0 += 64 * kBrkBatch) {
+      uint32_t r[kBrkBatch];
+#pragma unroll
+      for (int u = 0; u < kBrkBatch; ++u) {
+        const int p = p0 + 64 * u + lane;
+        r[u] = p < len - 1 ? lookup<kWide>(tb, s_id[p], s_id[p + 1]) : kInf;
+      }
+#pragma unroll
+      for (int u = 0; u < kBrkBatch; ++u) {
+        const int p = p0 + 64 * u + lane;
+        if (p < len - 1) s_brk[p] = (T)(r[u] == kInf ? TINF : r[u]);
+      }
+    }
     int cur = 0;
     int P = (len + kPieceW - 1) / kPieceW;
     if (lane == 0) { s_cut[0][0] = 0; s_cut[0][P] = (uint16_t)len; }
     wave_sync_mem();
-    // cut k (1 <= k < P) at the position in [24k - 4, 24k + 4) whose byte pair ranks highest
+    // cut k (1 <= k < P) at the position in [W k - H, W k + H) whose byte pair ranks highest
     for (int k = 1 + lane; k < P; k += 64) {
-      const int c0 = k * kPieceW - 4;
-      uint32_t r[8];
-#pragma unroll
-      for (int u = 0; u < 8; ++u) r[u] = (c0 + u < len) ? lookup<kWide>(tb, s_id[c0 + u - 1], s_id[c0 + u]) : 0u;
+      const int c0 = k * kPieceW - kCutHalf;
       int best = c0;
-      uint32_t br = r[0];
+      uint32_t br = brk(c0 - 1);
 #pragma unroll
-      for (int u = 1; u < 8; ++u)
-        if (r[u] > br) { br = r[u]; best = c0 + u; }
+      for (int u = 1; u < 2 * kCutHalf; ++u) {
+        const uint32_t r = c0 + u < len ? brk(c0 + u - 1) : 0u;
+        if (r > br) { br = r; best = c0 + u; }
+      }
       s_cut[0][k] = (uint16_t)best;
     }
     wave_sync_mem();
-    // every piece on its own (one lane each, in registers)
+    SW_STAMP(12);
+    // every piece on its own (one lane each, in registers; initial ranks from s_brk)
     for (int k = lane; k < P; k += 64) {
       const int c = s_cut[0][k], n = s_cut[0][k + 1] - c;
-      uint32_t id[kShort];
+      uint32_t id[kPieceN], rk[kPieceN];
 #pragma unroll
-      for (int j = 0; j < kShort; ++j) id[j] = j < n ? (uint32_t)s_id[c + j] : 0u;
-      const uint32_t alive = lane_merge_reg<kWide, k16, kShort>(tb, id, n);
+      for (int j = 0; j < kPieceN; ++j) {
+        id[j] = j < n ? (uint32_t)s_id[c + j] : 0u;
+        rk[j] = j + 1 < n ? brk(c + j) : kInf;
+      }
+      const uint32_t alive = lane_merge_reg_loop<kWide, k16, kPieceN>(tb, id, rk, n);
       int m = 0;
 #pragma unroll
-      for (int j = 0; j < kShort; ++j)
+      for (int j = 0; j < kPieceN; ++j)
         if ((alive >> j) & 1u) s_id[c + m++] = (T)id[j];
       s_cnt[0][k] = (uint16_t)m;
     }
     wave_sync_mem();
+    SW_STAMP(13);
     // junction k (between pieces k - 1 and k) is bit k - 1
     uint64_t conf[kJWords];
 #pragma unroll
@@ -1257,18 +1359,36 @@ __global__ void __launch_bounds__(64) k_merge_long_split(EncArgs a) {
       conf[g] = __ballot(c);
     }
     auto cbit = [&](int j) -> bool {  // (selects: no dynamically indexed registers)
-      const uint64_t w = j < 64 ? conf[0] : j < 128 ? conf[1] : conf[2];
+      uint64_t w = conf[0];
+#pragma unroll
+      for (int g = 1; g < kJWords; ++g) w = (j >> 6) == g ? conf[g] : w;
       return (w >> (j & 63)) & 1ULL;
     };
+    auto any_conf = [&]() -> bool {
+      uint64_t o = 0;
+#pragma unroll
+      for (int g = 0; g < kJWords; ++g) o |= conf[g];
+      return o != 0ULL;
+    };
     bool fall = false;
-    for (int round = 0; (conf[0] | conf[1] | conf[2]) != 0ULL; ++round) {
+    SW_STAMP(14);
+#ifdef SW_STAMPS
+    {
+      int nc = 0;
+      for (int g = 0; g < kJWords; ++g) nc += __popcll(conf[g]);
+      SW_COUNT(22, nc);
+    }
+#endif
+    for (int round = 0; any_conf(); ++round) {
       if (round == kSplitRounds) { fall = true; break; }
+      SW_COUNT(23, 1);
       // join the pieces across conflicting junctions; a joined piece is a window to encode again
       const uint16_t* cut = s_cut[cur];
       const uint16_t* cnt = s_cnt[cur];
       uint16_t* ncut = s_cut[cur ^ 1];
       uint16_t* ncnt = s_cnt[cur ^ 1];
       int np = 0;
+      uint64_t wins[kJWords];
 #pragma unroll
       for (int g = 0; g < kJWords; ++g) {
         const int k = 64 * g + lane;
@@ -1287,15 +1407,45 @@ __global__ void __launch_bounds__(64) k_merge_long_split(EncArgs a) {
       cur ^= 1;
       P = np;
       wave_sync_mem();
-      bool over = false;
-      for (int j = lane; j < P; j += 64) {
-        if (!s_win[j]) continue;
-        const int c = ncut[j], n = ncut[j + 1] - c;
-        if (n > kMaxWindow) { over = true; continue; }
-        for (int q = 0; q < n; ++q) s_id[c + q] = (T)src[c + q];
-        ncnt[j] = (uint16_t)lane_merge_lds<kWide, T>(tb, s_id + c, s_rk + c, n);
+      // the windows, one after the other, each by the whole wave (bytes again, ranks from s_brk)
+#pragma unroll
+      for (int g = 0; g < kJWords; ++g) {
+        const int j = 64 * g + lane;
+        wins[g] = __ballot(j < P && s_win[j]);
       }
-      if (__ballot(over)) { fall = true; break; }
+#pragma unroll
+      for (int g = 0; g < kJWords; ++g) {
+        for (uint64_t wm = wins[g]; wm; wm &= wm - 1) {
+          const int j = 64 * g + __builtin_ctzll(wm);
+          const int c = ncut[j], n = ncut[j + 1] - c;
+          if (n > kMaxWindow) { fall = true; break; }
+          if (n > 64) {  // (rare) one lane, in LDS; the window's byte-pair ranks are restored after
+            SW_COUNT(27, 1);
+#ifdef SW_STAMPS
+            big_win = true;
+#endif
+            if (lane == 0) {
+              for (int q = 0; q < n; ++q) s_id[c + q] = (T)src[c + q];
+              ncnt[j] = (uint16_t)lane_merge_lds<kWide, T>(tb, s_id + c, s_brk + c, n);
+            }
+            wave_sync_mem();
+            for (int q = lane; q < n - 1; q += 64) {
+              const uint32_t r = lookup<kWide>(tb, src[c + q], src[c + q + 1]);
+              s_brk[c + q] = (T)(r == kInf ? TINF : r);
+            }
+            wave_sync_mem();
+            continue;
+          }
+          uint32_t id = lane < n ? (uint32_t)src[c + lane] : 0u;
+          uint32_t rk = lane + 1 < n ? brk(c + lane) : kInf;
+          const uint64_t al = wave_merge64<kWide>(tb, id, rk, n, lane);
+          wave_sync_mem();  // (every lane's reads of the window's old ids precede the stores)
+          if ((al >> lane) & 1ULL) s_id[c + __popcll(al & lt_mask)] = (T)id;
+          if (lane == 0) ncnt[j] = (uint16_t)__popcll(al);
+        }
+        if (fall) break;
+      }
+      if (fall) break;
       wave_sync_mem();
       // only the junctions next to a window can have changed
 #pragma unroll
@@ -1307,19 +1457,25 @@ __global__ void __launch_bounds__(64) k_merge_long_split(EncArgs a) {
         conf[g] = __ballot(c);
       }
     }
+    SW_STAMP(15);
     if (fall) {  // the whole chunk in the wave loop
+      SW_COUNT(24, 1);
+      SW_COUNT(25, len);
+      SW_COUNT(26, len > 1024 ? 1 : 0);
       wave_sync_mem();
       for (int j = lane; j < len; j += 64) s_id[lds_pos(j)] = (T)src[j];
       wave_sync_mem();
-      const int m = seg_merge<kWide, T>(tb, s_id, s_rk, s_kill, s_dirty, len, lane, gid);
+      const int m = seg_merge<kWide, T>(tb, s_id, s_brk, s_kill, s_dirty, len, lane, gid);
       if (lane == 0) gid[-1] = (uint32_t)m;
       wave_sync_mem();
+      SW_STAMP(16);
       continue;
     }
-    // the pieces' ids in order: gathered into s_rk, then stored coalesced
+    // the pieces' ids in order: gathered into s_brk, then stored coalesced
     const uint16_t* cut = s_cut[cur];
     const uint16_t* cnt = s_cnt[cur];
     int total = 0;
+    wave_sync_mem();
 #pragma unroll
     for (int g = 0; g < kJWords; ++g) {
       const int k = 64 * g + lane;
@@ -1328,14 +1484,23 @@ __global__ void __launch_bounds__(64) k_merge_long_split(EncArgs a) {
       const int o = total + (int)(incl - c);
       if (k < P) {
         const int b = cut[k];
-        for (uint32_t q = 0; q < c; ++q) s_rk[o + q] = s_id[b + q];
+        for (uint32_t q = 0; q < c; ++q) s_brk[o + q] = s_id[b + q];
       }
       total += (int)__shfl(incl, 63, 64);
     }
     wave_sync_mem();
-    for (int q = lane; q < total; q += 64) gid[q] = (uint32_t)s_rk[q];
+    for (int q = lane; q < total; q += 64) gid[q] = (uint32_t)s_brk[q];
     if (lane == 0) gid[-1] = (uint32_t)total;
     wave_sync_mem();
+    SW_STAMP(17);
+#ifdef SW_STAMPS
+    if (threadIdx.x == 0) {
+      const unsigned long long dt = __builtin_readcyclecounter() - t_chunk0;
+      atomicMax(&a.stamps[19 * 64], dt);
+      if (len > 1024) { atomicAdd(&a.stamps[28 * 64], dt); atomicAdd(&a.stamps[29 * 64], 1ULL); }
+      if (big_win) { atomicAdd(&a.stamps[30 * 64], dt); atomicAdd(&a.stamps[31 * 64], 1ULL); }
+    }
+#endif
   }
 }
 
@@ -1510,6 +1675,7 @@ __global__ void __launch_bounds__(kThreads) k_tile_count(EncArgs a) {
 
 constexpr int kRefCap = 128;    // references per 8-round group gathered through LDS
 constexpr int kOutCapW = 1024;  // ids per group staged in LDS (the rest are stored directly)
+constexpr uint32_t kLaneCopy = 64;  // results longer than this are copied by the whole wave
 
 __global__ void __launch_bounds__(kThreads) SW_CLS_ATTR k_compact(EncArgs a, const int64_t* tile_base, int32_t* out) {
   // per wave: the group's references, gathered with full lanes before any store (a store
@@ -1611,13 +1777,26 @@ __global__ void __launch_bounds__(kThreads) SW_CLS_ATTR k_compact(EncArgs a, con
         if (lo < (uint32_t)kOutCapW) s_out[lo] = v[u];
         else dst[o] = v[u];
       }
+      const int64_t p = ref ? slot_pos(v[u]) : 0;
       if (ref) {
-        const int64_t p = slot_pos(v[u]);
         const uint32_t hd[3] = {q.y, q.z, q.w};
-        for (uint32_t k = 0; k < m; ++k) {
+        const uint32_t mm = m > kLaneCopy ? 3u : m;  // (long results: the head here, the rest below)
+        for (uint32_t k = 0; k < mm; ++k) {
           const int32_t id = k < 3 ? (int32_t)hd[k] : (int32_t)a.res[2 * p + 1 + k];
           if (lo + k < (uint32_t)kOutCapW) s_out[lo + k] = id;
           else dst[o + k] = id;
+        }
+      }
+      // long results (C5: whole 4 KiB chunks): one coalesced copy by the whole wave each
+      for (uint64_t lm = __ballot(ref && m > kLaneCopy); lm; lm &= lm - 1) {
+        const int L = __ffsll((long long)lm) - 1;
+        const int64_t pL = (int64_t)__shfl((long long)p, L, 64);
+        const uint32_t oL = (uint32_t)__shfl((int)o, L, 64), mL = (uint32_t)__shfl((int)m, L, 64);
+        const uint32_t loL = oL - gbase;
+        for (uint32_t k = 3 + lane; k < mL; k += 64) {
+          const int32_t id = (int32_t)a.res[2 * pL + 1 + k];
+          if (loL + k < (uint32_t)kOutCapW) s_out[loL + k] = id;
+          else dst[oL + k] = id;
         }
       }
       const uint32_t got = (uint32_t)__shfl((int)o, sj & 63, 64);

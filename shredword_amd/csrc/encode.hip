@@ -255,12 +255,20 @@ bool build_cuckoo(const std::unordered_map<uint64_t, int32_t>& dict, const std::
 
 // device pre-split of [d_bytes, d_bytes + n_bytes) into d_bits (zeroed here)
 hipError_t launch_presplit(hipStream_t st, const uint8_t* d_bytes, int64_t n_bytes, const int64_t* d_str_off,
-                           int64_t n_str, int32_t pattern, uint64_t* d_bits) {
+                           int64_t n_str, int32_t pattern, uint64_t* d_bits, const int64_t* d_tile_slo) {
   if (n_bytes <= 0) return hipSuccess;
+#ifdef SW_PS_FSM  // (A/B builds: the byte-stepped transducer of round 1)
+  (void)d_tile_slo;
   hipError_t e = hipMemsetAsync(d_bits, 0, sizeof(uint64_t) * ((n_bytes + 63) / 64), st);
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(k_presplit, dim3((unsigned)((n_bytes + kPsBlock - 1) / kPsBlock)), dim3(kPsThreads), 0, st,
                      d_bytes, n_bytes, d_str_off, n_str, (int)pattern, d_bits);
+#else
+  // every dword of the bitmap is stored (no clearing)
+  PbArgs g{d_bytes, n_bytes, d_str_off, n_str, d_tile_slo};
+  hipLaunchKernelGGL(k_presplit_bits, dim3((unsigned)((n_bytes + kPbBlock - 1) / kPbBlock)), dim3(kPbThreads), 0, st, g,
+                     (int)pattern, (uint32_t*)d_bits);
+#endif
   return hipGetLastError();
 }
 
@@ -510,8 +518,11 @@ extern "C" int32_t sw_encode_device(sw_encoder* h, const uint8_t* d_bytes, int64
     e1 = h->ev_pool[2 * h->ev_used + 1];
     HIP_TRY(hipEventRecord(h->ev_pool[2 * h->ev_used], st));
   }
+  if (n_tiles > 0)  // (the pre-split and k_classify start from each tile's first string)
+    hipLaunchKernelGGL(k_tile_strings, dim3((unsigned)((n_tiles + 255) / 256)), dim3(256), 0, st, d_str_off, n_str,
+                       n_tiles, h->d_tile_slo);
   if (n_tiles > 0 && !d_chunk_bits) {  // the full path: device pre-split first
-    HIP_TRY(launch_presplit(st, d_bytes, n_bytes, d_str_off, n_str, h->pattern, h->d_pbits));
+    HIP_TRY(launch_presplit(st, d_bytes, n_bytes, d_str_off, n_str, h->pattern, h->d_pbits, h->d_tile_slo));
     d_chunk_bits = h->d_pbits;
   }
   if (n_tiles > 0) {
@@ -527,8 +538,6 @@ extern "C" int32_t sw_encode_device(sw_encoder* h, const uint8_t* d_bytes, int64
     a.queue = h->d_queue; a.stamps = h->d_stamps;
     a.inv = h->d_inv; a.n_inv = h->n_inv;
     const bool split = h->split_ok && h->long_split;
-    hipLaunchKernelGGL(k_tile_strings, dim3((unsigned)((n_tiles + 255) / 256)), dim3(256), 0, st, d_str_off, n_str,
-                       n_tiles, h->d_tile_slo);
     if (h->dedupe) HIP_TRY(hipMemsetAsync(h->d_dtab, 0, sizeof(uint64_t) * ((size_t)h->dmask + 1), st));
     hipLaunchKernelGGL(k_classify, dim3((unsigned)((n_tiles + kWaves - 1) / kWaves)), dim3(kThreads), 0, st, a);
     HIP_TRY(hipGetLastError());
@@ -728,7 +737,10 @@ extern "C" int32_t sw_presplit_device(sw_encoder* h, const uint8_t* d_bytes, int
   hipStream_t st = (hipStream_t)stream;  // (NULL: the null stream, as torch's default stream)
   int32_t rc = ensure_workspace(h, n_bytes);
   if (rc) return rc;
-  HIP_TRY(launch_presplit(st, d_bytes, n_bytes, d_str_off, n_str, pattern, d_chunk_bits));
+  if (n_bytes > 0)
+    hipLaunchKernelGGL(k_tile_strings, dim3((unsigned)(((n_bytes + kTile - 1) / kTile + 255) / 256)), dim3(256), 0, st,
+                       d_str_off, n_str, (n_bytes + kTile - 1) / kTile, h->d_tile_slo);
+  HIP_TRY(launch_presplit(st, d_bytes, n_bytes, d_str_off, n_str, pattern, d_chunk_bits, h->d_tile_slo));
   if (n_chunks_host) {
     *n_chunks_host = 0;
     if (n_bytes > 0) {

@@ -1,0 +1,315 @@
+// Bit-parallel pre-split (apply_regex, shredword/base.py:38-58): the chunk starts of the cl100k
+// pattern (base.py:56) and the GPT-2 pattern (base.py:46) as a handful of 64-bit mask
+// operations per 32 bytes, for k_presplit_bits (presplit_bits_kernel.h) and its CPU harness
+// (tests/native/psb_emul.cpp).  Written once for the device and the host (SW_HD).
+//
+// The regex alternation, applied leftmost-first from every chunk start, reduces to LOCAL rules
+// over the code-point classes L (\p{L}), N (\p{N}), C (\r \n), P (' '), H (other \s), O (the
+// rest; invalid UTF-8 bytes are one-byte O code points) -- checked against the `regex` module on
+// random strings before this was written, and against the host pre-split by the tests.  With
+// prev(i) / next(i) the neighbouring code points in the same string, a string start is a chunk
+// start, and so is code point i when:
+//   cl100k  (ost(p): p is O, prev(p) neither O nor P -- an O that starts a chunk)
+//     L: prev L and i is the first letter after a contraction chunk ('s 't 'd 'm, 'll 've 're,
+//        case-insensitive, at an apostrophe with ost); prev O and not ost(prev); prev N or C
+//        (a prev P / H, or an ost O, is the optional prefix of [^\r\n\p{L}\p{N}]?+\p{L}+)
+//     N: the first of a digit run, then every third one (\p{N}{1,3})
+//     O: ost(i)                                  ( ?[^\s\p{L}\p{N}]++[\r\n]*)
+//     ws: prev not ws, unless i is C and prev O  (the O run's [\r\n]* took it);
+//         i in P|H after C: the C run before it follows an O (its leading C's were taken), or no
+//         C follows i in its whitespace run      (\s*[\r\n] ends at the run's last C);
+//         i in P|H after P|H: next exists and is not ws   (\s+(?!\S) gives the last one back)
+//   GPT-2  (contractions case-sensitive, at an apostrophe with prev neither O nor P)
+//     non-ws after P: never (` ?` prefixes of the three alternatives); L: prev L and the first
+//     letter after a contraction, or prev not L and not the first contraction letter; N: prev not
+//     N; O: prev not O; ws: prev not ws, or prev ws and next exists and is not ws.
+//
+// Two things are not local: a digit run's phase (every third from its start), and whether a C
+// run follows an O / a whitespace run holds a later C.  Inside the 64-bit window they are mask
+// fills; a run that crosses the window edge is reported (`need`) and resolved by the caller's
+// walk over the neighbouring chunks (Carry).
+#pragma once
+#include <cstdint>
+
+#include "presplit_fsm.h"
+#include "presplit_match.h"
+
+namespace sw {
+namespace psb {
+
+#define SW_PSB_FI __attribute__((always_inline))  // (the walks take the source by reference: keep it in registers)
+
+constexpr int kChunk = 32;  // payload bytes per lane
+
+// Class masks of a 32-byte chunk: bit k = byte pos + k.  Classes are set at code-point leads;
+// X marks the continuation bytes of valid UTF-8 sequences.  K1 / K2: an apostrophe followed by a
+// one- / two-letter contraction of the pattern (not crossing a string start).
+struct Masks {
+  uint32_t L, N, C, P, H, A, X, K1, K2;
+};
+
+// bit 7 of each byte lane of x -> 4 bits
+SW_HD inline uint32_t mm4(uint32_t x) { return ((x & 0x80808080u) * 0x00204081u) >> 28; }
+
+SW_HD inline uint64_t rev64(uint64_t x) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __builtin_bitreverse64(x);
+#else
+  x = ((x >> 1) & 0x5555555555555555ULL) | ((x & 0x5555555555555555ULL) << 1);
+  x = ((x >> 2) & 0x3333333333333333ULL) | ((x & 0x3333333333333333ULL) << 2);
+  x = ((x >> 4) & 0x0F0F0F0F0F0F0F0FULL) | ((x & 0x0F0F0F0F0F0F0F0FULL) << 4);
+  x = ((x >> 8) & 0x00FF00FF00FF00FFULL) | ((x & 0x00FF00FF00FF00FFULL) << 8);
+  x = ((x >> 16) & 0x0000FFFF0000FFFFULL) | ((x & 0x0000FFFF0000FFFFULL) << 16);
+  return (x >> 32) | (x << 32);
+#endif
+}
+
+// the run of R (contiguous set bits) from each bit of Y upwards (Y's bits outside R: nothing)
+SW_HD inline uint64_t fill_up(uint64_t Y, uint64_t R) { return ((R + (Y & R)) ^ R) & R; }
+SW_HD inline uint64_t fill_down(uint64_t Y, uint64_t R) { return rev64(fill_up(rev64(Y), rev64(R))); }
+
+// The class masks of the chunk at pos.  w: the bytes [pos - 4, pos + 36) as little-endian words
+// (zeros outside the batch); ss: string-start bits of those 40 bytes (bit k = byte pos - 4 + k;
+// the batch end counts as one).  Cls: cls(cp) -> kOther / kL / kN / kS (ucd_tables.h).
+template <class Cls>
+SW_HD inline Masks classify(const uint32_t (&w)[10], uint64_t ss, const Cls& cls, bool cl) {
+  using fsm::in7;
+  using fsm::kLane7;
+  using fsm::kLow7;
+  // ASCII classes of the chunk's bytes (words 1..8)
+  uint32_t L = 0, N = 0, C = 0, P = 0, H = 0, A = 0;
+#pragma unroll
+  for (int i = 1; i < 9; ++i) {
+    const uint32_t x = w[i], asc = ~x & kLane7, x7 = x & kLow7;
+    const int s = 4 * (i - 1);
+    const uint32_t ws = in7(x7, 9, 13) & asc, cr = (in7(x7, '\n', '\n') | in7(x7, '\r', '\r')) & asc;
+    L |= mm4(in7(x7 | 0x20202020u, 'a', 'z') & asc) << s;
+    N |= mm4(in7(x7, '0', '9') & asc) << s;
+    C |= mm4(cr) << s;
+    H |= mm4(ws & ~cr) << s;
+    P |= mm4(in7(x7, ' ', ' ') & asc) << s;
+    A |= mm4(in7(x7, '\'', '\'') & asc) << s;
+  }
+  // the words' bytes k .. k + 3 of the 40 (zeros past them; selects: no dynamically indexed
+  // registers)
+  auto bytes4 = [&](int k) -> uint32_t {
+    uint32_t lo_w = w[0], hi_w = w[1];
+#pragma unroll
+    for (int q = 1; q < 10; ++q) {
+      lo_w = (k >> 2) == q ? w[q] : lo_w;
+      hi_w = (k >> 2) == q ? (q + 1 < 10 ? w[q + 1] : 0u) : hi_w;
+    }
+    return (uint32_t)((((uint64_t)hi_w << 32) | lo_w) >> (8 * (k & 3)));
+  };
+  // UTF-8: every lead byte of [pos - 4, pos + 32) checked on its own (strict: no overlongs,
+  // surrogates or code points past U+10FFFF, not crossing a string start); the continuation
+  // bytes of the valid ones make X, and the chunk's non-ASCII code points get their class
+  uint64_t X = 0;
+  uint64_t hi40 = 0, ct40 = 0;
+#pragma unroll
+  for (int i = 0; i < 10; ++i) hi40 |= (uint64_t)mm4(w[i]) << (4 * i);
+  if (hi40) {
+#pragma unroll
+    for (int i = 0; i < 10; ++i) {
+      const uint32_t h7 = (w[i] ^ kLane7) & kLow7;  // (bytes >= 0x80, less 0x80)
+      ct40 |= (uint64_t)mm4(in7(h7, 0x00, 0x3F) & w[i] & kLane7) << (4 * i);
+    }
+    for (uint64_t m = hi40 & ~ct40 & 0xFFFFFFFFFULL; m; m &= m - 1) {
+      const int k = __builtin_ctzll(m);
+      const uint32_t b4 = bytes4(k), c0 = b4 & 0xFFu, c1 = (b4 >> 8) & 0xFFu;
+      const int n = c0 >= 0xF0 ? 4 : c0 >= 0xE0 ? 3 : 2;
+      const uint64_t tail = ((1ULL << (n - 1)) - 1ULL) << (k + 1);
+      bool ok = (ct40 & tail) == tail && (ss & tail) == 0 && c0 >= 0xC2 && c0 <= 0xF4;
+      ok = ok && !(c0 == 0xE0 && c1 < 0xA0) && !(c0 == 0xED && c1 > 0x9F) && !(c0 == 0xF0 && c1 < 0x90) &&
+           !(c0 == 0xF4 && c1 > 0x8F);
+      if (!ok) continue;
+      X |= tail;
+      if (k < 4) continue;
+      uint32_t v = c0 & (n == 2 ? 0x1Fu : n == 3 ? 0x0Fu : 0x07u);
+      for (int q = 1; q < n; ++q) v = (v << 6) | ((b4 >> (8 * q)) & 0x3Fu);
+      const int c = cls(v);
+      const uint32_t bit = 1u << (k - 4);
+      if (c == kL) L |= bit;
+      else if (c == kN) N |= bit;
+      else if (c == kS) H |= bit;
+    }
+  }
+  // contractions after each apostrophe of the chunk (the next one or two code points, ASCII or
+  // U+017F LONG S = C5 BF for cl100k's case-insensitive 's')
+  uint32_t K1 = 0, K2 = 0;
+  for (uint32_t m = A; m; m &= m - 1) {
+    const int a = __builtin_ctz(m), k = a + 5;  // (the byte after it, in the 40)
+    if ((ss >> k) & 1) continue;
+    const uint32_t b4 = bytes4(k), c1 = b4 & 0xFFu, c2 = (b4 >> 8) & 0xFFu;
+    const uint32_t l1 = cl && c1 >= 'A' && c1 <= 'Z' ? c1 | 0x20u : c1, l2 = cl && c2 >= 'A' && c2 <= 'Z' ? c2 | 0x20u : c2;
+    const bool two_ok = !((ss >> (k + 1)) & 1);
+    if (l1 == 's' || l1 == 'd' || l1 == 'm' || l1 == 't' || (cl && c1 == 0xC5 && c2 == 0xBF && two_ok)) {
+      K1 |= 1u << a;
+    } else if (two_ok && ((l1 == 'l' && l2 == 'l') || (l1 == 'v' && l2 == 'e') || (l1 == 'r' && l2 == 'e'))) {
+      K2 |= 1u << a;
+    }
+  }
+  Masks r;
+  r.L = L; r.N = N; r.C = C; r.P = P; r.H = H; r.A = A; r.X = (uint32_t)(X >> 4); r.K1 = K1; r.K2 = K2;
+  return r;
+}
+
+// Facts about runs crossing the window's edges (-1: unknown), found by the caller's walk:
+struct Carry {
+  int digit = -1;  // the digit run holding the window's first code point: its members before the window, mod 3
+  int cro = -1;    // the C run holding the window's first code point follows an O
+  int hasc = -1;   // the whitespace run holding the window's last byte has a C past the window
+};
+enum : uint32_t { kNeedDigit = 1, kNeedCro = 2, kNeedHasc = 4 };
+
+SW_HD inline uint64_t window(uint32_t before, uint32_t mine, uint32_t after) {
+  return (uint64_t)(before >> 16) | ((uint64_t)mine << 16) | ((uint64_t)after << 48);
+}
+
+// The chunk starts of the 32 bytes of chunk m1 (m0 before it, m2 after it).  ssw: string-start
+// bits of the window [pos - 16, pos + 48) (bit j = byte pos - 16 + j).  *need: the carries the
+// result depends on but cy does not give (then the result is not final).
+SW_HD inline uint32_t rules(const Masks& m0, const Masks& m1, const Masks& m2, uint64_t ssw, bool cl, const Carry& cy,
+                            uint32_t* need) {
+  const uint64_t X = window(m0.X, m1.X, m2.X);
+  const uint64_t L = window(m0.L, m1.L, m2.L), N = window(m0.N, m1.N, m2.N), C = window(m0.C, m1.C, m2.C);
+  const uint64_t P = window(m0.P, m1.P, m2.P), H = window(m0.H, m1.H, m2.H), A = window(m0.A, m1.A, m2.A);
+  const uint64_t K1 = window(m0.K1, m1.K1, m2.K1), K2 = window(m0.K2, m1.K2, m2.K2);
+  const uint64_t LEAD = ~X, WS = C | P | H, O = LEAD & ~(L | N | WS), PH_ = P | H;
+  constexpr uint64_t kPay = 0x0000FFFFFFFF0000ULL;  // the payload bytes
+  // prev(i) in M, at every lead i (nothing at a string start): M one code point up
+  auto F = [&](uint64_t M) -> uint64_t { return ((X + (M << 1)) & ~X) & ~ssw; };
+  // next(i) in M (M's string starts excluded: the next code point is in another string)
+  auto B = [&](uint64_t M) -> uint64_t {
+    const uint64_t y = rev64(((M & LEAD & ~ssw) >> 1)), rx = rev64(X);
+    return rev64((rx + y) & ~rx);
+  };
+  const uint64_t PL = F(L), PN = F(N), PO = F(O), PP = F(P), PC = F(C), PWS = F(WS);
+  const uint64_t first = LEAD & (~LEAD + 1);  // the window's first code point (its prev is unknown)
+  *need = 0;
+  uint64_t st;
+  const uint64_t NNW = B(LEAD & ~WS);  // next exists and is not ws
+  if (cl) {
+    const uint64_t OST = O & ~PO & ~PP;
+    const uint64_t SLc = PL & (F(F(OST & K1)) | F(F(F(OST & K2))));
+    const uint64_t STL = L & (SLc | (PO & ~F(OST)) | PN | PC);
+    // digit runs: the first, then every third member (the window-edge run from its carry)
+    const uint64_t NB = N | fill_up((N << 1) & X, X);  // digits with their continuation bytes
+    const uint64_t edge = (first & N) ? fill_up(first, NB & ~ssw) & N : 0;  // (a run ends at a string start)
+    uint64_t seed = N & ~PN & ~edge;
+    if (edge) {
+      if (cy.digit < 0) {
+        if (edge & kPay) *need |= kNeedDigit;
+      } else {
+        uint64_t s = first;
+        for (int k = (3 - cy.digit) % 3; k > 0; --k) s = F(s) & N;
+        seed |= s;
+      }
+    }
+    uint64_t STN = seed;
+    for (uint64_t t = seed; t;) {
+      t = F(F(F(t) & N) & N) & N;
+      STN |= t;
+    }
+    // whitespace: C runs that follow an O, whitespace runs with a later C
+    const uint64_t Rc = C & ~ssw;
+    const uint64_t cedge = (first & C) ? fill_up(first, Rc) : 0;
+    uint64_t CRO = fill_up(C & PO, Rc);
+    if (cedge) {
+      if (cy.cro < 0) {
+        if (F(cedge) & PH_ & kPay) *need |= kNeedCro;
+      } else if (cy.cro) {
+        CRO |= cedge;
+      }
+    }
+    const uint64_t WSB = WS | fill_up((WS << 1) & X, X), Rw = WSB & ~ssw;
+    uint64_t HASC = fill_down(C, Rw);
+    const uint64_t wedge = fill_down((Rw >> 63) << 63, Rw);
+    const uint64_t after_c = PH_ & PC;
+    if (wedge) {
+      if (cy.hasc < 0) {
+        if (after_c & kPay & wedge & ~HASC) *need |= kNeedHasc;
+      } else if (cy.hasc) {
+        HASC |= wedge;
+      }
+    }
+    const uint64_t STW = (WS & ~PWS & ~(C & PO)) | (after_c & (F(CRO) | ~HASC)) | (PH_ & (PP | F(H)) & NNW);
+    st = STL | STN | OST | STW;
+  } else {
+    const uint64_t OSG = A & ~PO & ~PP;
+    const uint64_t SLc = PL & (F(F(OSG & K1)) | F(F(F(OSG & K2))));
+    const uint64_t STL = L & ~PP & (SLc | (~PL & ~F(OSG & (K1 | K2))));
+    const uint64_t STN = N & ~PP & ~PN;
+    const uint64_t STO = O & ~PP & ~PO;
+    const uint64_t STW = (WS & ~PWS) | (WS & PWS & NNW);
+    st = STL | STN | STO | STW;
+  }
+  return (uint32_t)(((st & LEAD) | ssw) >> 16);
+}
+
+// ---- carries: walks over the chunk masks on either side of the window ----------------------
+// Src: get(chunk index) -> Masks (zero masks past the batch), ss(chunk index) -> its string-start
+// bits (the batch end included), n_chunks.  Chunk c covers bytes [32c, 32c + 32).
+enum Field { kFX, kFN, kFC };
+template <Field F, class Src>
+SW_HD SW_PSB_FI inline bool bit_at(const Src& src, int64_t pos) {
+  const Masks m = src.get(pos >> 5);
+  const uint32_t v = F == kFX ? m.X : F == kFN ? m.N : m.C;
+  return (v >> (pos & 31)) & 1u;
+}
+
+// The carries of the window of chunk c (bytes [32c - 16, 32c + 48)) that `need` asks for.
+template <class Src>
+SW_HD SW_PSB_FI inline Carry carries(const Src& src, int64_t c, uint32_t need) {
+  Carry cy;
+  const int64_t w0 = 32 * c - 16, w1 = 32 * c + 48;
+  if (need & (kNeedDigit | kNeedCro)) {
+    // the window's first code point (the first lead at or after w0)
+    int64_t f = w0;
+    while (f < 32 * c + 16 && bit_at<kFX>(src, f)) ++f;
+    auto is_ss = [&](int64_t p) -> bool { return p <= 0 || ((src.ss(p >> 5) >> (p & 31)) & 1u); };
+    auto lead_before = [&](int64_t p) -> int64_t {  // the lead of the code point ending at p - 1
+      int64_t q = p - 1;
+      while (q > 0 && bit_at<kFX>(src, q)) --q;
+      return q;
+    };
+    if (need & kNeedDigit) {  // members of its digit run before f, mod 3
+      int cnt = 0;
+      for (int64_t p = f; !is_ss(p);) {
+        const int64_t q = lead_before(p);
+        if (!bit_at<kFN>(src, q)) break;
+        cnt = (cnt + 1) % 3;
+        p = q;
+      }
+      cy.digit = cnt;
+    }
+    if (need & kNeedCro) {  // the start of f's C run follows an O
+      int64_t p = f;
+      while (!is_ss(p) && bit_at<kFC>(src, p - 1)) --p;
+      if (is_ss(p)) {
+        cy.cro = 0;
+      } else {
+        const int64_t q = lead_before(p);
+        const Masks m = src.get(q >> 5);
+        const uint32_t b = 1u << (q & 31);
+        cy.cro = ((m.L | m.N | m.C | m.P | m.H) & b) ? 0 : 1;
+      }
+    }
+  }
+  if (need & kNeedHasc) {  // a C in the whitespace run that goes on past the window
+    cy.hasc = 0;
+    for (int64_t p = w1;; ++p) {
+      const int64_t ch = p >> 5;
+      if (ch >= src.n_chunks) break;
+      const Masks m = src.get(ch);
+      const uint32_t b = 1u << (p & 31);
+      if ((src.ss(ch) & b)) break;
+      if (m.C & b) { cy.hasc = 1; break; }
+      if (!((m.P | m.H | m.X) & b)) break;  // (X: a multi-byte whitespace code point's tail)
+    }
+  }
+  return cy;
+}
+
+}  // namespace psb
+}  // namespace sw

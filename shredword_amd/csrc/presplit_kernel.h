@@ -16,6 +16,7 @@
 
 #include <cstdint>
 
+#include "presplit_bits.h"
 #include "presplit_block.h"
 #include "presplit_fsm.h"
 #include "presplit_match.h"
@@ -211,6 +212,168 @@ __global__ void __launch_bounds__(kPsThreads) k_presplit(const uint8_t* bytes, i
     const uint64_t v = (uint64_t)s_ss[2 * i] | ((uint64_t)s_ss[2 * i + 1] << 32);
     if (v) atomicOr((unsigned long long*)&bits[gw], (unsigned long long)v);
   }
+}
+
+// ---------------------------------------------------------------------------------------------
+// k_presplit_bits: the bit-parallel pre-split (presplit_bits.h).  A workgroup owns kPbBlock
+// bytes, one 32-byte chunk per thread:
+//   0. the string starts of [b0 - 64, b0 + kPbBlock + 64) into an LDS bitmap;
+//   1. every chunk's class masks (classify) for chunks -1 .. 256 of the block, into LDS;
+//   2. every thread's window rules over chunks t - 1, t, t + 1, with the run carries walked over
+//      the LDS masks (and, for runs past the block, over chunks classified from global memory);
+//      the 32 chunk-start bits are stored as one dword of the bitmap (no atomics, no clearing).
+// ---------------------------------------------------------------------------------------------
+constexpr int kPbThreads = 256;
+constexpr int kPbBlock = kPbThreads * psb::kChunk;      // 8 KiB
+constexpr int kPbPre = 64;                               // string starts staged before b0 ...
+constexpr int kPbSsWords = (kPbPre + kPbBlock + 128) / 32;  // ... and after the block
+constexpr int kPbChunks = kPbThreads + 2;                // chunks -1 .. 256
+
+struct PbArgs {
+  const uint8_t* bytes;
+  int64_t n_bytes;
+  const int64_t* str_off;
+  int64_t n_str;
+  const int64_t* tile_slo;  // first string starting at or after each 2 KiB tile (k_tile_strings)
+};
+
+// string-start bits of bytes [p, p + 32) from str_off (batch end included): global fallback
+__device__ inline uint32_t pb_ss_global(const PbArgs& g, int64_t p) {
+  int64_t lo = 0, hi = g.n_str;  // first string start >= p
+  while (lo < hi) {
+    const int64_t m = (lo + hi) >> 1;
+    if (g.str_off[m] < p) lo = m + 1; else hi = m;
+  }
+  uint32_t v = 0;
+  for (int64_t i = lo; i <= g.n_str; ++i) {
+    const int64_t o = g.str_off[i];
+    if (o >= p + 32) break;
+    v |= 1u << (o - p);
+  }
+  return v;
+}
+
+// the 40 bytes [p - 4, p + 36) as words (zeros outside the batch); vector loads when in range
+__device__ inline void pb_load40(const PbArgs& g, int64_t p, uint32_t (&w)[10]) {
+  if (p - 4 >= 0 && p + 36 <= g.n_bytes && (((uintptr_t)(g.bytes + p) & 15) == 0)) {
+    const uint4 a = *(const uint4*)(g.bytes + p), b = *(const uint4*)(g.bytes + p + 16);
+    w[0] = *(const uint32_t*)(g.bytes + p - 4);
+    w[1] = a.x; w[2] = a.y; w[3] = a.z; w[4] = a.w;
+    w[5] = b.x; w[6] = b.y; w[7] = b.z; w[8] = b.w;
+    w[9] = *(const uint32_t*)(g.bytes + p + 32);
+    return;
+  }
+#pragma unroll
+  for (int i = 0; i < 10; ++i) {
+    uint32_t v = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int64_t q = p - 4 + 4 * i + k;
+      v |= (q >= 0 && q < g.n_bytes) ? (uint32_t)g.bytes[q] << (8 * k) : 0u;
+    }
+    w[i] = v;
+  }
+}
+
+struct PbSrc {  // psb::carries' view: the block's chunks from LDS, the others classified on the fly
+  PbArgs g;                         // (by value: a pointer to the kernel argument puts it on the stack)
+  const uint32_t (*m)[kPbChunks];   // [9][kPbChunks]: chunk c0 - 1 + j at column j
+  const uint32_t* ssb;              // the block's string-start bitmap (from b0 - kPbPre)
+  int64_t c0, b0, n_chunks;
+  bool cl;
+  __device__ uint32_t ss_at(int64_t q) const {  // string-start bits of [q, q + 32), any q
+    const int64_t r = q - (b0 - kPbPre);
+    if (r >= 0 && r + 32 <= (int64_t)kPbSsWords * 32) {
+      const int wi = (int)(r >> 5), sh = (int)(r & 31);
+      const uint64_t two = (uint64_t)ssb[wi] | ((wi + 1 < kPbSsWords ? (uint64_t)ssb[wi + 1] : 0ULL) << 32);
+      return (uint32_t)(two >> sh);
+    }
+    return pb_ss_global(g, q);
+  }
+  __device__ uint32_t ss(int64_t c) const { return ss_at(32 * c); }
+  __device__ psb::Masks get(int64_t c) const {
+    if (c < 0 || c >= n_chunks) return psb::Masks{};
+    const int64_t j = c - (c0 - 1);
+    if (j >= 0 && j < kPbChunks) {
+      const int k = (int)j;
+      return psb::Masks{m[0][k], m[1][k], m[2][k], m[3][k], m[4][k], m[5][k], m[6][k], m[7][k], m[8][k]};
+    }
+    uint32_t w[10];
+    pb_load40(g, 32 * c, w);
+    const uint64_t s = (uint64_t)ss_at(32 * c - 4) | ((uint64_t)(ss_at(32 * c + 28) & 0xFFu) << 32);
+    return psb::classify(w, s, UcdClass{}, cl);
+  }
+};
+
+#ifndef SW_PB_WAVES
+#define SW_PB_WAVES 4
+#endif
+__global__ void __launch_bounds__(kPbThreads, SW_PB_WAVES) k_presplit_bits(PbArgs g, int pattern, uint32_t* bits32) {
+  __shared__ uint32_t s_m[9][kPbChunks];
+  __shared__ uint32_t s_ss[kPbSsWords];
+  const int tid = threadIdx.x;
+  const int64_t b0 = (int64_t)blockIdx.x * kPbBlock, c0 = b0 / psb::kChunk;
+  const int64_t n_chunks = (g.n_bytes + psb::kChunk - 1) / psb::kChunk;
+  const bool cl = pattern == 0;
+  // 0. string starts of [b0 - kPbPre, b0 + kPbBlock + 64) (the batch end is str_off[n_str])
+  for (int i = tid; i < kPbSsWords; i += kPbThreads) s_ss[i] = 0;
+  __syncthreads();
+  {  // (from the first string of the tile holding b0 - kPbPre: no search)
+    const int64_t first = b0 >= kPbPre ? g.tile_slo[(b0 - kPbPre) / kTile] : 0;
+    for (int64_t i = first + tid; i <= g.n_str; i += kPbThreads) {
+      const int64_t r = g.str_off[i] - (b0 - kPbPre);
+      if (r >= (int64_t)kPbSsWords * 32) break;
+      if (r >= 0) atomicOr(&s_ss[r >> 5], 1u << (r & 31));
+    }
+  }
+  __syncthreads();
+  PbSrc src{g, s_m, s_ss, c0, b0, n_chunks, cl};
+  if (pattern == 2) {  // the chunks are the strings
+    const int64_t c = c0 + tid;
+    if (c < n_chunks) {
+      uint32_t r = src.ss(c);
+      if (32 * c + 32 > g.n_bytes) r &= (1u << (g.n_bytes - 32 * c)) - 1u;
+      bits32[c] = r;
+      if (c == n_chunks - 1 && (c & 1) == 0) bits32[c + 1] = 0;  // (the last word's upper half)
+    }
+    return;
+  }
+  // 1. class masks of chunks c0 - 1 .. c0 + 256
+  for (int j = tid; j < kPbChunks; j += kPbThreads) {
+    const int64_t c = c0 - 1 + j;
+    psb::Masks m{};
+    if (c >= 0 && c < n_chunks) {
+      uint32_t w[10];
+      pb_load40(g, 32 * c, w);
+      const uint64_t s = (uint64_t)src.ss_at(32 * c - 4) | ((uint64_t)(src.ss_at(32 * c + 28) & 0xFFu) << 32);
+#if defined(SW_PB_ABL) && (SW_PB_ABL == 2 || SW_PB_ABL == 3)  // (diagnostic timing builds only: wrong bitmaps)
+      m.L = w[1] ^ w[3] ^ w[5] ^ w[7] ^ (uint32_t)s; m.N = w[2] ^ w[4] ^ w[6] ^ w[8]; m.X = w[0] ^ w[9];
+#else
+      m = psb::classify(w, s, UcdClass{}, cl);
+#endif
+    }
+    s_m[0][j] = m.L; s_m[1][j] = m.N; s_m[2][j] = m.C; s_m[3][j] = m.P; s_m[4][j] = m.H;
+    s_m[5][j] = m.A; s_m[6][j] = m.X; s_m[7][j] = m.K1; s_m[8][j] = m.K2;
+  }
+  __syncthreads();
+  // 2. this thread's chunk
+  const int64_t c = c0 + tid;
+  if (c >= n_chunks) return;
+  const psb::Masks m0 = src.get(c - 1), m1 = src.get(c), m2 = src.get(c + 1);
+  const uint64_t ssw = (uint64_t)src.ss_at(32 * c - 16) | ((uint64_t)src.ss_at(32 * c + 16) << 32);
+  uint32_t need = 0;
+#if defined(SW_PB_ABL) && (SW_PB_ABL == 1 || SW_PB_ABL == 3)  // (diagnostic timing builds only: wrong bitmaps)
+  uint32_t r = m0.L ^ m1.N ^ m2.C ^ (uint32_t)ssw;
+#else
+  uint32_t r = psb::rules(m0, m1, m2, ssw, cl, psb::Carry{}, &need);
+#endif
+  if (need) {
+    const psb::Carry cy = psb::carries(src, c, need);
+    r = psb::rules(m0, m1, m2, ssw, cl, cy, &need);
+  }
+  if (32 * c + 32 > g.n_bytes) r &= (1u << (g.n_bytes - 32 * c)) - 1u;
+  bits32[c] = r;
+  if (c == n_chunks - 1 && (c & 1) == 0) bits32[c + 1] = 0;  // (the last word's upper half)
 }
 
 // number of set bits (chunks) in the bitmap

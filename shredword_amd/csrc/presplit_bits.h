@@ -71,8 +71,25 @@ SW_HD inline uint64_t fill_down(uint64_t Y, uint64_t R) { return rev64(fill_up(r
 // The class masks of the chunk at pos.  w: the bytes [pos - 4, pos + 36) as little-endian words
 // (zeros outside the batch); ss: string-start bits of those 40 bytes (bit k = byte pos - 4 + k;
 // the batch end counts as one).  Cls: cls(cp) -> kOther / kL / kN / kS (ucd_tables.h).
-template <class Cls>
-SW_HD inline Masks classify(const uint32_t (&w)[10], uint64_t ss, const Cls& cls, bool cl) {
+// The 40 bytes held in registers (w[0..9]); at4 by selects (no dynamically indexed registers)
+struct RegBytes {
+  uint32_t w[10];
+  SW_HD uint32_t word(int i) const { return w[i]; }
+  SW_HD uint32_t at4(int k) const {
+    uint32_t lo_w = w[0], hi_w = w[1];
+#pragma unroll
+    for (int q = 1; q < 10; ++q) {
+      lo_w = (k >> 2) == q ? w[q] : lo_w;
+      hi_w = (k >> 2) == q ? (q + 1 < 10 ? w[q + 1] : 0u) : hi_w;
+    }
+    return (uint32_t)((((uint64_t)hi_w << 32) | lo_w) >> (8 * (k & 3)));
+  }
+};
+
+// Bytes: word(i) = bytes [pos - 4 + 4i, pos + 4i) as a little-endian word (i < 10); at4(k) = the
+// bytes k .. k + 3 of those 40 (k <= 36).
+template <class Cls, class Bytes>
+SW_HD inline Masks classify(const Bytes& by, uint64_t ss, const Cls& cls, bool cl) {
   using fsm::in7;
   using fsm::kLane7;
   using fsm::kLow7;
@@ -80,7 +97,7 @@ SW_HD inline Masks classify(const uint32_t (&w)[10], uint64_t ss, const Cls& cls
   uint32_t L = 0, N = 0, C = 0, P = 0, H = 0, A = 0;
 #pragma unroll
   for (int i = 1; i < 9; ++i) {
-    const uint32_t x = w[i], asc = ~x & kLane7, x7 = x & kLow7;
+    const uint32_t x = by.word(i), asc = ~x & kLane7, x7 = x & kLow7;
     const int s = 4 * (i - 1);
     const uint32_t ws = in7(x7, 9, 13) & asc, cr = (in7(x7, '\n', '\n') | in7(x7, '\r', '\r')) & asc;
     L |= mm4(in7(x7 | 0x20202020u, 'a', 'z') & asc) << s;
@@ -90,33 +107,22 @@ SW_HD inline Masks classify(const uint32_t (&w)[10], uint64_t ss, const Cls& cls
     P |= mm4(in7(x7, ' ', ' ') & asc) << s;
     A |= mm4(in7(x7, '\'', '\'') & asc) << s;
   }
-  // the words' bytes k .. k + 3 of the 40 (zeros past them; selects: no dynamically indexed
-  // registers)
-  auto bytes4 = [&](int k) -> uint32_t {
-    uint32_t lo_w = w[0], hi_w = w[1];
-#pragma unroll
-    for (int q = 1; q < 10; ++q) {
-      lo_w = (k >> 2) == q ? w[q] : lo_w;
-      hi_w = (k >> 2) == q ? (q + 1 < 10 ? w[q + 1] : 0u) : hi_w;
-    }
-    return (uint32_t)((((uint64_t)hi_w << 32) | lo_w) >> (8 * (k & 3)));
-  };
   // UTF-8: every lead byte of [pos - 4, pos + 32) checked on its own (strict: no overlongs,
   // surrogates or code points past U+10FFFF, not crossing a string start); the continuation
   // bytes of the valid ones make X, and the chunk's non-ASCII code points get their class
   uint64_t X = 0;
   uint64_t hi40 = 0, ct40 = 0;
 #pragma unroll
-  for (int i = 0; i < 10; ++i) hi40 |= (uint64_t)mm4(w[i]) << (4 * i);
+  for (int i = 0; i < 10; ++i) hi40 |= (uint64_t)mm4(by.word(i)) << (4 * i);
   if (hi40) {
 #pragma unroll
     for (int i = 0; i < 10; ++i) {
-      const uint32_t h7 = (w[i] ^ kLane7) & kLow7;  // (bytes >= 0x80, less 0x80)
-      ct40 |= (uint64_t)mm4(in7(h7, 0x00, 0x3F) & w[i] & kLane7) << (4 * i);
+      const uint32_t x = by.word(i), h7 = (x ^ kLane7) & kLow7;  // (bytes >= 0x80, less 0x80)
+      ct40 |= (uint64_t)mm4(in7(h7, 0x00, 0x3F) & x & kLane7) << (4 * i);
     }
     for (uint64_t m = hi40 & ~ct40 & 0xFFFFFFFFFULL; m; m &= m - 1) {
       const int k = __builtin_ctzll(m);
-      const uint32_t b4 = bytes4(k), c0 = b4 & 0xFFu, c1 = (b4 >> 8) & 0xFFu;
+      const uint32_t b4 = by.at4(k), c0 = b4 & 0xFFu, c1 = (b4 >> 8) & 0xFFu;
       const int n = c0 >= 0xF0 ? 4 : c0 >= 0xE0 ? 3 : 2;
       const uint64_t tail = ((1ULL << (n - 1)) - 1ULL) << (k + 1);
       bool ok = (ct40 & tail) == tail && (ss & tail) == 0 && c0 >= 0xC2 && c0 <= 0xF4;
@@ -140,7 +146,7 @@ SW_HD inline Masks classify(const uint32_t (&w)[10], uint64_t ss, const Cls& cls
   for (uint32_t m = A; m; m &= m - 1) {
     const int a = __builtin_ctz(m), k = a + 5;  // (the byte after it, in the 40)
     if ((ss >> k) & 1) continue;
-    const uint32_t b4 = bytes4(k), c1 = b4 & 0xFFu, c2 = (b4 >> 8) & 0xFFu;
+    const uint32_t b4 = by.at4(k), c1 = b4 & 0xFFu, c2 = (b4 >> 8) & 0xFFu;
     const uint32_t l1 = cl && c1 >= 'A' && c1 <= 'Z' ? c1 | 0x20u : c1, l2 = cl && c2 >= 'A' && c2 <= 'Z' ? c2 | 0x20u : c2;
     const bool two_ok = !((ss >> (k + 1)) & 1);
     if (l1 == 's' || l1 == 'd' || l1 == 'm' || l1 == 't' || (cl && c1 == 0xC5 && c2 == 0xBF && two_ok)) {

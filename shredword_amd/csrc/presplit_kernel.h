@@ -223,11 +223,24 @@ __global__ void __launch_bounds__(kPsThreads) k_presplit(const uint8_t* bytes, i
 //      the LDS masks (and, for runs past the block, over chunks classified from global memory);
 //      the 32 chunk-start bits are stored as one dword of the bitmap (no atomics, no clearing).
 // ---------------------------------------------------------------------------------------------
-constexpr int kPbThreads = 256;
+#ifndef SW_PB_THREADS
+#define SW_PB_THREADS 256
+#endif
+constexpr int kPbThreads = SW_PB_THREADS;
 constexpr int kPbBlock = kPbThreads * psb::kChunk;      // 8 KiB
 constexpr int kPbPre = 64;                               // string starts staged before b0 ...
 constexpr int kPbSsWords = (kPbPre + kPbBlock + 128) / 32;  // ... and after the block
 constexpr int kPbChunks = kPbThreads + 2;                // chunks -1 .. 256
+constexpr int kPbStage = kPbPre + kPbBlock + 64;           // bytes staged in LDS, from b0 - kPbPre
+
+#ifndef SW_PB_STAGE
+#define SW_PB_STAGE 0  // 1: classify reads the block's bytes from LDS (0: each chunk's 40 bytes from global memory)
+#endif
+struct LdsBytes {  // classify's view of a chunk's 40 bytes in the staged block (word-aligned)
+  const uint32_t* s;  // (an LDS array) the word holding byte pos - 4
+  __device__ uint32_t word(int i) const { return s[i]; }
+  __device__ uint32_t at4(int k) const { return __builtin_amdgcn_alignbyte(s[(k >> 2) + 1], s[k >> 2], k & 3); }
+};
 
 struct PbArgs {
   const uint8_t* bytes;
@@ -254,7 +267,7 @@ __device__ inline uint32_t pb_ss_global(const PbArgs& g, int64_t p) {
 }
 
 // the 40 bytes [p - 4, p + 36) as words (zeros outside the batch); vector loads when in range
-__device__ inline void pb_load40(const PbArgs& g, int64_t p, uint32_t (&w)[10]) {
+__device__ inline void pb_load40(const PbArgs& g, int64_t p, uint32_t* w) {
   if (p - 4 >= 0 && p + 36 <= g.n_bytes && (((uintptr_t)(g.bytes + p) & 15) == 0)) {
     const uint4 a = *(const uint4*)(g.bytes + p), b = *(const uint4*)(g.bytes + p + 16);
     w[0] = *(const uint32_t*)(g.bytes + p - 4);
@@ -298,10 +311,10 @@ struct PbSrc {  // psb::carries' view: the block's chunks from LDS, the others c
       const int k = (int)j;
       return psb::Masks{m[0][k], m[1][k], m[2][k], m[3][k], m[4][k], m[5][k], m[6][k], m[7][k], m[8][k]};
     }
-    uint32_t w[10];
-    pb_load40(g, 32 * c, w);
+    psb::RegBytes by;
+    pb_load40(g, 32 * c, by.w);
     const uint64_t s = (uint64_t)ss_at(32 * c - 4) | ((uint64_t)(ss_at(32 * c + 28) & 0xFFu) << 32);
-    return psb::classify(w, s, UcdClass{}, cl);
+    return psb::classify(by, s, UcdClass{}, cl);
   }
 };
 
@@ -311,10 +324,36 @@ struct PbSrc {  // psb::carries' view: the block's chunks from LDS, the others c
 __global__ void __launch_bounds__(kPbThreads, SW_PB_WAVES) k_presplit_bits(PbArgs g, int pattern, uint32_t* bits32) {
   __shared__ uint32_t s_m[9][kPbChunks];
   __shared__ uint32_t s_ss[kPbSsWords];
+  __shared__ __attribute__((aligned(16))) uint32_t s_b[kPbStage / 4 + 4];  // bytes [b0 - kPbPre, ..)
   const int tid = threadIdx.x;
   const int64_t b0 = (int64_t)blockIdx.x * kPbBlock, c0 = b0 / psb::kChunk;
   const int64_t n_chunks = (g.n_bytes + psb::kChunk - 1) / psb::kChunk;
   const bool cl = pattern == 0;
+  if (SW_PB_STAGE && pattern != 2) {  // the block's bytes (zeros outside the batch), coalesced, before anything waits
+    const bool aligned = ((uintptr_t)g.bytes & 15) == 0;
+    for (int i = tid; i < kPbStage / 16; i += kPbThreads) {
+      const int64_t q = b0 - kPbPre + 16 * i;
+      uint4 v;
+      if (aligned && q >= 0 && q + 16 <= g.n_bytes) {
+        v = *(const uint4*)(g.bytes + q);
+      } else {
+        uint32_t t[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          uint32_t x = 0;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const int64_t p = q + 4 * k + e;
+            x |= (p >= 0 && p < g.n_bytes) ? (uint32_t)g.bytes[p] << (8 * e) : 0u;
+          }
+          t[k] = x;
+        }
+        v = make_uint4(t[0], t[1], t[2], t[3]);
+      }
+      *(uint4*)&s_b[4 * i] = v;
+    }
+    if (tid < 4) s_b[kPbStage / 4 + tid] = 0;
+  }
   // 0. string starts of [b0 - kPbPre, b0 + kPbBlock + 64) (the batch end is str_off[n_str])
   for (int i = tid; i < kPbSsWords; i += kPbThreads) s_ss[i] = 0;
   __syncthreads();
@@ -343,13 +382,18 @@ __global__ void __launch_bounds__(kPbThreads, SW_PB_WAVES) k_presplit_bits(PbArg
     const int64_t c = c0 - 1 + j;
     psb::Masks m{};
     if (c >= 0 && c < n_chunks) {
-      uint32_t w[10];
-      pb_load40(g, 32 * c, w);
+#if SW_PB_STAGE
+      const LdsBytes by{&s_b[(32 * j + kPbPre - 32 - 4) / 4]};
+#else
+      psb::RegBytes by;
+      pb_load40(g, 32 * c, by.w);
+#endif
       const uint64_t s = (uint64_t)src.ss_at(32 * c - 4) | ((uint64_t)(src.ss_at(32 * c + 28) & 0xFFu) << 32);
 #if defined(SW_PB_ABL) && (SW_PB_ABL == 2 || SW_PB_ABL == 3)  // (diagnostic timing builds only: wrong bitmaps)
-      m.L = w[1] ^ w[3] ^ w[5] ^ w[7] ^ (uint32_t)s; m.N = w[2] ^ w[4] ^ w[6] ^ w[8]; m.X = w[0] ^ w[9];
+      m.L = by.word(1) ^ by.word(3) ^ by.word(5) ^ by.word(7) ^ (uint32_t)s; m.N = by.word(2) ^ by.word(8);
+      m.X = by.word(0) ^ by.word(9);
 #else
-      m = psb::classify(w, s, UcdClass{}, cl);
+      m = psb::classify(by, s, UcdClass{}, cl);
 #endif
     }
     s_m[0][j] = m.L; s_m[1][j] = m.N; s_m[2][j] = m.C; s_m[3][j] = m.P; s_m[4][j] = m.H;

@@ -52,14 +52,14 @@ extern "C" int64_t psb_emul(const uint8_t* bytes, const int64_t* off, int64_t n_
   const bool cl = pattern == 0;
   std::vector<sw::psb::Masks> masks((size_t)nc);
   for (int64_t c = 0; c < nc; ++c) {
-    uint32_t w[10];
+    sw::psb::RegBytes by;
     uint64_t ss = 0;
     for (int i = 0; i < 10; ++i) {
-      w[i] = 0;
-      for (int k = 0; k < 4; ++k) w[i] |= byte(32 * c - 4 + 4 * i + k) << (8 * k);
+      by.w[i] = 0;
+      for (int k = 0; k < 4; ++k) by.w[i] |= byte(32 * c - 4 + 4 * i + k) << (8 * k);
     }
     for (int k = 0; k < 40; ++k) ss |= ssat(32 * c - 4 + k) << k;
-    masks[(size_t)c] = sw::psb::classify(w, ss, Ucd{}, cl);
+    masks[(size_t)c] = sw::psb::classify(by, ss, Ucd{}, cl);
   }
   Src src{&masks, &ssb, nc, n};
   int64_t slow = 0;

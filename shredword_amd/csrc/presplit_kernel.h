@@ -251,7 +251,7 @@ struct PbArgs {
 };
 
 // string-start bits of bytes [p, p + 32) from str_off (batch end included): global fallback
-__device__ inline uint32_t pb_ss_global(const PbArgs& g, int64_t p) {
+__device__ __forceinline__ uint32_t pb_ss_global(const PbArgs g, int64_t p) {
   int64_t lo = 0, hi = g.n_str;  // first string start >= p
   while (lo < hi) {
     const int64_t m = (lo + hi) >> 1;
@@ -267,7 +267,7 @@ __device__ inline uint32_t pb_ss_global(const PbArgs& g, int64_t p) {
 }
 
 // the 40 bytes [p - 4, p + 36) as words (zeros outside the batch); vector loads when in range
-__device__ inline void pb_load40(const PbArgs& g, int64_t p, uint32_t* w) {
+__device__ __forceinline__ void pb_load40(const PbArgs g, int64_t p, uint32_t* w) {
   if (p - 4 >= 0 && p + 36 <= g.n_bytes && (((uintptr_t)(g.bytes + p) & 15) == 0)) {
     const uint4 a = *(const uint4*)(g.bytes + p), b = *(const uint4*)(g.bytes + p + 16);
     w[0] = *(const uint32_t*)(g.bytes + p - 4);
@@ -294,7 +294,7 @@ struct PbSrc {  // psb::carries' view: the block's chunks from LDS, the others c
   const uint32_t* ssb;              // the block's string-start bitmap (from b0 - kPbPre)
   int64_t c0, b0, n_chunks;
   bool cl;
-  __device__ uint32_t ss_at(int64_t q) const {  // string-start bits of [q, q + 32), any q
+  __device__ __forceinline__ uint32_t ss_at(int64_t q) const {  // string-start bits of [q, q + 32), any q
     const int64_t r = q - (b0 - kPbPre);
     if (r >= 0 && r + 32 <= (int64_t)kPbSsWords * 32) {
       const int wi = (int)(r >> 5), sh = (int)(r & 31);
@@ -303,8 +303,8 @@ struct PbSrc {  // psb::carries' view: the block's chunks from LDS, the others c
     }
     return pb_ss_global(g, q);
   }
-  __device__ uint32_t ss(int64_t c) const { return ss_at(32 * c); }
-  __device__ psb::Masks get(int64_t c) const {
+  __device__ __forceinline__ uint32_t ss(int64_t c) const { return ss_at(32 * c); }
+  __device__ __forceinline__ psb::Masks get(int64_t c) const {
     if (c < 0 || c >= n_chunks) return psb::Masks{};
     const int64_t j = c - (c0 - 1);
     if (j >= 0 && j < kPbChunks) {

@@ -80,6 +80,7 @@ struct sw_encoder {
   uint2* d_inv = nullptr;             // merge value -> pair
   uint32_t n_inv = 0;
   int64_t max_launch = kMaxLaunchBytes;  // SW_OPT_MAX_LAUNCH_BYTES (sw_encode_batch splits above it)
+  int n_cu = 256;                     // compute units (persistent grids)
   // the workspace is reused by every call: a call on another stream waits for the last one
   hipEvent_t ws_done = nullptr;
   hipStream_t ws_stream = nullptr;
@@ -343,6 +344,10 @@ extern "C" int32_t sw_encoder_create(const int32_t* pairs, const int32_t* vals, 
   }
   h->n_chunk_entries = (int64_t)(ct.n_short + ct.n_long);
   DeviceGuard g(device);
+  {
+    int cu = 0;
+    if (hipDeviceGetAttribute(&cu, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess && cu > 0) h->n_cu = cu;
+  }
   hipError_t e = hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking);
   if (e == hipSuccess) e = hipMalloc(&h->d_table, table_bytes);
   if (e == hipSuccess) e = hipMemcpy(h->d_table, host.data(), table_bytes, hipMemcpyHostToDevice);

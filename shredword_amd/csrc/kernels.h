@@ -566,17 +566,11 @@ constexpr int kWinWords = kWin / 4 + 8;
 #else
 #define SW_CLS_ATTR
 #endif
-__global__ void __launch_bounds__(kThreads) SW_CLS_ATTR k_classify(EncArgs a) {
-  __shared__ __attribute__((aligned(16))) uint32_t s_b32_all[kWaves][kWinWords];  // window bytes (+ zero tail)
-  __shared__ uint16_t s_cs_all[kWaves][kTile + 1];   // chunk starts (tile-relative)
-  __shared__ uint16_t s_qb_all[kWaves][kQBuf];       // chunks not settled by a lookup, to dedupe
+// one tile (the body of k_classify's tile loop)
+__device__ __forceinline__ void classify_tile(const EncArgs& a, int64_t tile, uint32_t* s_b32, uint16_t* s_cstart,
+                                              uint16_t* s_qbuf) {
   SW_STAMP_INIT;
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const int64_t tile = (int64_t)blockIdx.x * kWaves + wv;
-  if (tile >= a.n_tiles) return;
-  uint32_t* s_b32 = s_b32_all[wv];
-  uint16_t* s_cstart = s_cs_all[wv];
-  uint16_t* s_qbuf = s_qb_all[wv];
+  const int lane = threadIdx.x & 63;
   const uint64_t lt_mask = (lane == 0) ? 0ULL : (~0ULL >> (64 - lane));
   const int64_t t0 = tile * kTile;
   const int64_t t1 = min(t0 + (int64_t)kTile, a.n_bytes);
@@ -767,6 +761,17 @@ __global__ void __launch_bounds__(kThreads) SW_CLS_ATTR k_classify(EncArgs a) {
     a.out_off[s] = (int64_t)lo;
   }
   SW_STAMP(3);
+  wave_sync_mem();  // (the next tile reuses the wave's LDS)
+}
+
+// one wave per tile
+__global__ void __launch_bounds__(kThreads) SW_CLS_ATTR k_classify(EncArgs a) {
+  __shared__ __attribute__((aligned(16))) uint32_t s_b32_all[kWaves][kWinWords];  // window bytes (+ zero tail)
+  __shared__ uint16_t s_cs_all[kWaves][kTile + 1];   // chunk starts (tile-relative)
+  __shared__ uint16_t s_qb_all[kWaves][kQBuf];       // chunks not settled by a lookup, to dedupe
+  const int wv = threadIdx.x >> 6;
+  const int64_t tile = (int64_t)blockIdx.x * kWaves + wv;
+  if (tile < a.n_tiles) classify_tile(a, tile, s_b32_all[wv], s_cs_all[wv], s_qb_all[wv]);
 }
 
 // ---------------------------------------------------------------------------------------

@@ -47,7 +47,8 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--e2e-steps", type=int, default=2,
                     help="N=1: also time host buffers -> host buffers (PCIe-inclusive, reported beside value)")
-    ap.add_argument("--threads", type=int, default=16, help="host threads for corpus/pre-split")
+    ap.add_argument("--threads", type=int, default=0,
+                    help="host threads for corpus/pre-split and the all-cores CPU baseline (0: every usable core)")
     ap.add_argument("--no-dedupe", action="store_true",
                     help="A/B only: every queued chunk runs its own merge loop (same results)")
     ap.add_argument("--dedupe-slots", type=int, default=0, help="A/B only: cap the dedupe table (power of two)")
@@ -56,8 +57,32 @@ def parse():
     return ap.parse_args()
 
 
+def host_cpu():
+    """(usable cores of this process, machine CPUs, CPU model name)."""
+    try:
+        usable = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        usable = os.cpu_count() or 1
+    share = os.environ.get("OMP_NUM_THREADS")  # (the GPU box states its CPU share this way)
+    if share and share.isdigit() and int(share) > 0:
+        usable = min(usable, int(share))
+    model = None
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return usable, os.cpu_count(), model
+
+
 def main():
     args = parse()
+    usable_cores, machine_cpus, cpu_model = host_cpu()
+    if args.threads <= 0:
+        args.threads = min(usable_cores, 64)
     rank = int(os.environ.get("RANK", 0))
     world = int(os.environ.get("WORLD_SIZE", args.gpus))
     local = int(os.environ.get("LOCAL_RANK", 0))
@@ -127,10 +152,18 @@ def main():
     n_tok = int(n_tok_c.value)
     gather = world > 1 and not args.no_gather
 
+    # the gathers' widths: every rank's counts are the same every step (same corpus), so the
+    # maxima are taken once here and the timed step has no host synchronisation
+    width = width_s = None
+    if gather:
+        mx = torch.tensor([n_tok, n_str], dtype=torch.int64, device=dev)
+        dist.all_reduce(mx, op=dist.ReduceOp.MAX)
+        width, width_s = int(mx[0].item()), int(mx[1].item()) + 1
+
     def step():
         encode()
-        if gather:  # shard.reassemble: counts, padded id buffers and string offsets, over RCCL
-            return shard.reassemble(d_out, d_oo, None, dev, concat=False)
+        if gather:  # shard.reassemble: one counts all-gather, padded id and offset all-gathers (RCCL)
+            return shard.reassemble(d_out, d_oo, None, dev, concat=False, width=width, width_s=width_s)
         return None
 
     for _ in range(args.warmup):
@@ -148,6 +181,17 @@ def main():
         dist.barrier()
     k_ms = L.sw_encoder_last_kernel_ms(h)
     _lib.check(L.sw_encoder_set_timing(h, 0))
+    if gather:
+        shard.check_bounds()
+    # what the launches did: chunks settled without the merge loop, distinct merged after dedupe
+    cnt4 = (ctypes.c_int64 * 4)()
+    _lib.check(L.sw_encoder_last_counts(h, cnt4))
+    l_chunks, l_refs, l_distinct = int(cnt4[0]), int(cnt4[1]), int(cnt4[2])
+    rates = {"chunks": l_chunks, "to_merge_loop": l_refs, "merged_distinct": l_distinct,
+             "settled_without_merge_loop": round(1 - l_refs / max(l_chunks, 1), 4),
+             "dedupe_distinct_fraction": round(l_distinct / max(l_refs, 1), 4),
+             "note": "settled = single bytes + whole-chunk-table hits; distinct = merge loops actually run "
+                     "per chunk sent to the merge loop (the in-launch dedupe shares the rest)"}
     elapsed = torch.tensor([t1 - t0], dtype=torch.float64, device=dev)
     totals = torch.tensor([n_bytes, n_tok, n_str, n_chunks], dtype=torch.float64, device=dev)
     if world > 1:
@@ -163,7 +207,7 @@ def main():
     b_algo = n_bytes + 4 * n_tok + 16 * (n_str + 1) + ((n_bytes + 7) // 8 if host_ps else 0)
     achieved = b_algo / (k_ms * 1e-3) / 1e9 if k_ms > 0 else None
     # traffic: HBM bytes per launch from the committed PMC profile of this same workload, if any
-    traffic, traffic_src = None, None
+    traffic, traffic_x2, traffic_src = None, None, None
     try:
         with open(os.path.join(ROOT, "profiles", "traffic.json")) as f:
             tj = json.load(f)
@@ -171,11 +215,18 @@ def main():
                 and tj.get("chunk_table") == (not args.no_chunk_table) and tj.get("dedupe") == (not args.no_dedupe)
                 and tj.get("presplit", "host") == args.presplit):
             traffic, traffic_src = int(tj["traffic_bytes_per_launch"]), tj["source"]
+            traffic_x2 = int(tj.get("traffic_bytes_per_launch_x2", 0)) or None
     except (OSError, ValueError, KeyError):
         pass
     roofline = {"bound": "hbm", "achieved": round(achieved, 2) if achieved else None, "peak": HBM_PEAK_GBS,
                 "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5) if achieved else None,
-                "traffic": traffic, "traffic_source": traffic_src, "kernel": ("sw_encode_device pipeline (k_presplit..k_string_offsets)" if not host_ps else "sw_encode_device pipeline (k_tile_strings..k_string_offsets)"),
+                "traffic": traffic, "traffic_x2": traffic_x2,
+                "traffic_over_algo": round(traffic / b_algo, 2) if traffic else None,
+                "traffic_x2_over_algo": round(traffic_x2 / b_algo, 2) if traffic_x2 else None,
+                "traffic_note": "HBM-side FETCH_SIZE + WRITE_SIZE per launch from the committed PMC profile; "
+                                "traffic raw, traffic_x2 with FETCH doubled (gfx950 wide-read rule, an upper "
+                                "bound here)",
+                "traffic_source": traffic_src, "kernel": ("sw_encode_device pipeline (k_presplit..k_string_offsets)" if not host_ps else "sw_encode_device pipeline (k_tile_strings..k_string_offsets)"),
                 "kernel_ms": round(k_ms, 4),
                 "algo_bytes_per_launch": int(b_algo)}
 
@@ -199,9 +250,30 @@ def main():
     # same corpus; the GPU ids for that prefix must be bit-identical
     cpu = None
     parity = None
+    c1 = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        # configs[0] (C1): 10 MB synthetic ASCII, the reference-trained 500-merge toy model, CPU only
         sys.path.insert(0, os.path.join(ROOT, "oracle"))
         import oracle
+        t1buf, t1off = corpus.synth(7, corpus.ASCII, 20000, 500, n_threads=args.threads)
+        k1 = int(np.searchsorted(t1off, 10_000_000, side="right")) - 1
+        t1buf, t1off = t1buf[:int(t1off[k1])], t1off[:k1 + 1]
+        toy = Tokenizer(device=local)
+        toy.load(os.path.join(ROOT, "tests", "golden", "toy500.model"))
+        om1 = oracle.OracleModel(toy.merges)
+        tc = time.perf_counter()
+        e1 = om1.encode_batch(t1buf, t1off, 0, n_threads=1)
+        c1_1 = len(t1buf) / (time.perf_counter() - tc) / 1e6
+        tc = time.perf_counter()
+        om1.encode_batch(t1buf, t1off, 0, n_threads=args.threads)
+        c1_all = len(t1buf) / (time.perf_counter() - tc) / 1e6
+        g1 = toy.encode_packed(t1buf, t1off)
+        c1 = {"workload": "C1: configs[0], %.1f MB synthetic ASCII, toy500 (reference-trained 500 merges)" % (
+                  len(t1buf) / 1e6),
+              "cpu_mb_s_1thread": round(c1_1, 3), "cpu_mb_s_all_cores": round(c1_all, 3), "cores": args.threads,
+              "kind": "port (oracle/sw_oracle.c)", "python_reference_mb_s": 0.41,
+              "gpu_same_ids": bool(np.array_equal(g1[0], e1[0]) and np.array_equal(g1[1], e1[1]))}
+        toy.close()
         k = int(np.searchsorted(off, args.cpu_sample_mb * 1e6, side="right")) - 1
         k = max(1, min(k, n_str))
         sbuf, soff = buf[:int(off[k])], off[:k + 1]
@@ -218,8 +290,9 @@ def main():
         cpu = {"value": round(len(sbuf) / dt1 / 1e6, 3), "unit": "MB/s", "cores": 1, "kind": "port",
                "sample": "first %d strings (%.1f MB) of the same corpus, oracle/sw_oracle.c, 1 thread, "
                          "host pre-split + merge loop" % (k, len(sbuf) / 1e6),
-               "value_all_threads": round(len(sbuf) / dtm / 1e6, 3), "threads_all": args.threads,
-               "python_reference_mb_s": 0.33}
+               "value_all_cores": round(len(sbuf) / dtm / 1e6, 3), "cores_all": args.threads,
+               "usable_cores": usable_cores, "machine_cpus": machine_cpus, "cpu_model": cpu_model,
+               "c1": c1, "python_reference_mb_s": 0.33}
 
     if rank == 0:
         line = {
@@ -239,6 +312,7 @@ def main():
             "mtok_per_s": round(all_tok * args.steps / sec / 1e6, 3),
             "bytes_per_token": round(all_bytes / max(all_tok, 1), 4),
             "chunks": int(all_chunks),
+            "rates": rates,
             "roofline": roofline,
             "cpu_baseline": cpu,
             "parity_vs_oracle_sample": parity,

@@ -114,6 +114,11 @@ int32_t sw_encoder_reserve(sw_encoder* h, int64_t max_bytes, int64_t max_strings
  *                          whole strings (0 = the 2 GiB device limit; testing: any value >= 64) */
 #define SW_OPT_LONG_SPLIT 7
 #define SW_OPT_MAX_LAUNCH_BYTES 8
+/*   SW_OPT_PIPE_RUN_BYTES  sw_encode_batch of more than 2 runs of this many bytes (default 64 MiB; 0:
+ *                          never) pipelines runs of whole strings: pinned staging copied by a pool of
+ *                          host threads, uploads, encodes and downloads of consecutive runs
+ *                          overlapping, ids downloaded as 16 bits when every id fits */
+#define SW_OPT_PIPE_RUN_BYTES 9
 int32_t sw_encoder_set_option(sw_encoder* h, int32_t option, int64_t value);
 
 /* Encoder facts (sw_encoder_get_info): distinct merges, whole-chunk table entries, whether the
@@ -200,6 +205,12 @@ int32_t sw_decode_device(sw_decoder* d, const int32_t* d_ids, int64_t n_ids, con
  * launch over that window (it synchronises on the last event), or -1. */
 int32_t sw_encoder_set_timing(sw_encoder* h, int32_t on);
 double sw_encoder_last_kernel_ms(const sw_encoder* h);
+
+/* What the last sw_encode_device launch did (synchronises on it): out4[0] chunks, out4[1] chunks
+ * that went to the merge loop (references to a merge result: not a single byte, not in the
+ * whole-chunk table), out4[2] distinct ones actually merged (after the in-launch dedupe),
+ * out4[3] tiles.  For reports; outside any timed region. */
+int32_t sw_encoder_last_counts(sw_encoder* h, int64_t* out4);
 
 /* Diagnostic builds only (compiled with -DSW_STAMPS): device cycles summed over workgroups,
  * per phase: 0 k_classify stage+enumerate, 1 classify lookups, 2 slot/queue writes, 3 string

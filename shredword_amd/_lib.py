@@ -23,6 +23,7 @@ SW_PAT_CL100K, SW_PAT_GPT2, SW_PAT_NONE = 0, 1, 2
 SW_CORPUS_ASCII, SW_CORPUS_MIXED, SW_CORPUS_STRESS = 0, 1, 2
 SW_OPT_CHUNK_TABLE, SW_OPT_DEDUPE, SW_OPT_DEDUPE_SLOTS, SW_OPT_DEDUPE_FP_BITS = 1, 2, 3, 4
 SW_OPT_PATTERN, SW_OPT_HOST_PRESPLIT, SW_OPT_LONG_SPLIT, SW_OPT_MAX_LAUNCH_BYTES = 5, 6, 7, 8
+SW_OPT_PIPE_RUN_BYTES = 9
 SW_INFO_MERGES, SW_INFO_CHUNK_ENTRIES, SW_INFO_WIDE_TABLE, SW_INFO_IDS16, SW_INFO_SPLIT = 1, 2, 3, 4, 5
 
 
@@ -81,6 +82,7 @@ _SIGNATURES = {
     "sw_encoder_get_info": (c_int64, [c_void_p, c_int32]),
     "sw_encoder_set_timing": (c_int32, [c_void_p, c_int32]),
     "sw_encoder_last_kernel_ms": (c_double, [c_void_p]),
+    "sw_encoder_last_counts": (c_int32, [c_void_p, POINTER(c_int64)]),
     "sw_encoder_phase_cycles": (c_int32, [c_void_p, POINTER(c_double), c_int32]),
     "sw_decoder_create": (c_int32, [POINTER(c_uint8), POINTER(c_int64), POINTER(c_uint8), c_int64, c_int32,
                                     POINTER(c_void_p)]),

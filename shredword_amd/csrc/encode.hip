@@ -31,6 +31,7 @@
 #include <vector>
 
 #include "capi.h"
+#include "hostpool.h"
 #include "kernels.h"
 #include "presplit_kernel.h"
 #include "shredword_hip.h"
@@ -85,6 +86,21 @@ struct sw_encoder {
   hipEvent_t ws_done = nullptr;
   hipStream_t ws_stream = nullptr;
   bool ws_pending = false;
+  int64_t last_tiles = 0;             // tiles of the last sw_encode_device launch (sw_encoder_last_counts)
+  // sw_encode_batch's pipeline for large host batches (SW_OPT_PIPE_RUN_BYTES): runs of whole
+  // strings go host -> pinned -> device -> encode -> (16-bit ids when they fit) -> pinned -> host,
+  // run k's copies overlapping run k-1's encode; two slots of buffers
+  struct PipeSlot {
+    uint8_t* h_in = nullptr; int64_t* h_off = nullptr; uint64_t* h_bits = nullptr;  // pinned
+    void* h_out = nullptr; int64_t* h_oo = nullptr; int64_t* h_ntok = nullptr;        // pinned
+    uint8_t* d_in = nullptr; int64_t* d_off = nullptr; uint64_t* d_bits = nullptr;
+    int32_t* d_out = nullptr; int64_t* d_oo = nullptr; uint16_t* d_out16 = nullptr;
+    hipEvent_t e_in = nullptr, e_comp = nullptr, e_out = nullptr;
+    int64_t cap_bytes = 0, cap_str = 0;
+  } pipe[2];
+  int64_t pipe_run = 64LL << 20;      // run size; batches over 2 runs take the pipeline (0: never)
+  hipStream_t s_h2d = nullptr, s_d2h = nullptr;
+  sw::HostPool* pool = nullptr;
   // workspace
   int64_t cap_bytes = -1, cap_str = -1;
   int32_t* d_scratch = nullptr;
@@ -157,6 +173,19 @@ void free_io(sw_encoder* h) {
   (void)hipFree(h->d_out); (void)hipFree(h->d_out_off);
   h->d_bytes = nullptr; h->d_str_off = nullptr; h->d_bits = nullptr; h->d_out = nullptr; h->d_out_off = nullptr;
   h->io_bytes = -1; h->io_str = -1;
+}
+
+void free_pipe(sw_encoder* h) {
+  for (auto& p : h->pipe) {
+    (void)hipHostFree(p.h_in); (void)hipHostFree(p.h_off); (void)hipHostFree(p.h_bits); (void)hipHostFree(p.h_out);
+    (void)hipHostFree(p.h_oo); (void)hipHostFree(p.h_ntok);
+    (void)hipFree(p.d_in); (void)hipFree(p.d_off); (void)hipFree(p.d_bits); (void)hipFree(p.d_out); (void)hipFree(p.d_oo);
+    (void)hipFree(p.d_out16);
+    if (p.e_in) (void)hipEventDestroy(p.e_in);
+    if (p.e_comp) (void)hipEventDestroy(p.e_comp);
+    if (p.e_out) (void)hipEventDestroy(p.e_out);
+    p = sw_encoder::PipeSlot{};
+  }
 }
 
 int32_t ensure_workspace(sw_encoder* h, int64_t n_bytes) {
@@ -399,6 +428,10 @@ extern "C" void sw_encoder_destroy(sw_encoder* h) {
     free_workspace(h);
     free_io(h);
     if (h->ws_done) (void)hipEventSynchronize(h->ws_done);
+    free_pipe(h);
+    delete h->pool;
+    if (h->s_h2d) (void)hipStreamDestroy(h->s_h2d);
+    if (h->s_d2h) (void)hipStreamDestroy(h->s_d2h);
     (void)hipFree(h->d_table);
     (void)hipFree(h->d_chunks);
     (void)hipFree(h->d_inv);
@@ -434,6 +467,10 @@ extern "C" int32_t sw_encoder_set_option(sw_encoder* h, int32_t option, int64_t 
       h->dedupe_fp_mask = (uint32_t)((1ULL << value) - 1);
       return SW_OK;
     case SW_OPT_LONG_SPLIT: h->long_split = value != 0; return SW_OK;
+    case SW_OPT_PIPE_RUN_BYTES:
+      if (value != 0 && value < 64) return fail(SW_ERR_ARG, "pipeline run bytes: 0 (off) or >= 64");
+      h->pipe_run = std::min<int64_t>(value, kMaxLaunchBytes);
+      return SW_OK;
     case SW_OPT_MAX_LAUNCH_BYTES:
       if (value != 0 && (value < 64 || value > kMaxLaunchBytes))
         return fail(SW_ERR_ARG, "max launch bytes: 0 (default) or 64 .. 2^31 - 128");
@@ -513,6 +550,7 @@ extern "C" int32_t sw_encode_device(sw_encoder* h, const uint8_t* d_bytes, int64
   int32_t rc = ensure_workspace(h, n_bytes);
   if (rc) return rc;
   const int64_t n_tiles = (n_bytes + kTile - 1) / kTile;
+  h->last_tiles = n_tiles;
   hipEvent_t e1 = nullptr;
   if (h->timing) {  // the whole device pipeline, k_tile_strings .. k_string_offsets
     while (h->ev_pool.size() < 2 * (h->ev_used + 1)) {
@@ -601,6 +639,187 @@ extern "C" int32_t sw_encode_device(sw_encoder* h, const uint8_t* d_bytes, int64
   return SW_OK;
 }
 
+// ids to 16 bits for the device -> host copy (every id of an ids16 table fits)
+__global__ void k_pack16(const int32_t* in, const int64_t* total, uint16_t* out) {
+  const int64_t n = *total;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    out[i] = (uint16_t)in[i];
+}
+
+namespace {
+
+// sw_encode_batch for a large host batch: runs of whole strings (<= pipe_run bytes, or one longer
+// string) through two slots of pinned and device buffers.  Host thread: stage run k (pool copies
+// into pinned memory), enqueue its upload and encode, then drain run k - 1 (its 16/32-bit ids and
+// offsets to pinned memory, pool copies out to the caller) while run k encodes.
+int32_t encode_batch_pipelined(sw_encoder* h, const uint8_t* bytes, const int64_t* str_off, int64_t n_str,
+                               int32_t pattern, const uint64_t* chunk_bits, int32_t* out_ids, int64_t out_cap,
+                               int64_t* out_off, sw_stats* stats, std::chrono::steady_clock::time_point T0) {
+  const int64_t b0 = str_off[0];
+  std::vector<std::pair<int64_t, int64_t>> runs;
+  int64_t max_b = 1, max_s = 1;
+  for (int64_t s_lo = 0; s_lo < n_str;) {
+    int64_t s_hi = s_lo + 1;
+    while (s_hi < n_str && str_off[s_hi + 1] - str_off[s_lo] <= h->pipe_run) ++s_hi;
+    const int64_t nb = str_off[s_hi] - str_off[s_lo];
+    if (nb > h->max_launch) return fail(SW_ERR_ARG, "sw_encode_batch: a single string exceeds the launch limit (2 GiB)");
+    runs.emplace_back(s_lo, s_hi);
+    max_b = std::max(max_b, nb);
+    max_s = std::max(max_s, s_hi - s_lo);
+    s_lo = s_hi;
+  }
+  DeviceGuard g(h->device);
+  if (!h->s_h2d) HIP_TRY(hipStreamCreateWithFlags(&h->s_h2d, hipStreamNonBlocking));
+  if (!h->s_d2h) HIP_TRY(hipStreamCreateWithFlags(&h->s_d2h, hipStreamNonBlocking));
+  if (!h->pool) h->pool = new sw::HostPool((int)std::max(1u, std::min(16u, std::thread::hardware_concurrency())) - 1);
+  const int64_t max_w = (max_b + 63) / 64 + 1;
+  for (auto& p : h->pipe) {
+    if (p.cap_bytes >= max_b && p.cap_str >= max_s) continue;
+    const int64_t cb = std::max(max_b, p.cap_bytes), cs = std::max(max_s, p.cap_str), cw = (cb + 63) / 64 + 1;
+    (void)hipHostFree(p.h_in); (void)hipHostFree(p.h_off); (void)hipHostFree(p.h_bits); (void)hipHostFree(p.h_out);
+    (void)hipHostFree(p.h_oo); (void)hipHostFree(p.h_ntok);
+    (void)hipFree(p.d_in); (void)hipFree(p.d_off); (void)hipFree(p.d_bits); (void)hipFree(p.d_out); (void)hipFree(p.d_oo);
+    (void)hipFree(p.d_out16);
+    p.cap_bytes = p.cap_str = 0;
+    HIP_TRY(hipHostMalloc(&p.h_in, cb + 16, hipHostMallocDefault));
+    HIP_TRY(hipHostMalloc(&p.h_off, sizeof(int64_t) * (cs + 1), hipHostMallocDefault));
+    HIP_TRY(hipHostMalloc(&p.h_bits, sizeof(uint64_t) * cw, hipHostMallocDefault));
+    HIP_TRY(hipHostMalloc(&p.h_out, sizeof(int32_t) * cb, hipHostMallocDefault));
+    HIP_TRY(hipHostMalloc(&p.h_oo, sizeof(int64_t) * (cs + 1), hipHostMallocDefault));
+    HIP_TRY(hipHostMalloc(&p.h_ntok, sizeof(int64_t), hipHostMallocDefault));
+    HIP_TRY(hipMalloc(&p.d_in, cb + 16));
+    HIP_TRY(hipMalloc(&p.d_off, sizeof(int64_t) * (cs + 1)));
+    HIP_TRY(hipMalloc(&p.d_bits, sizeof(uint64_t) * cw));
+    HIP_TRY(hipMalloc(&p.d_out, sizeof(int32_t) * cb));
+    HIP_TRY(hipMalloc(&p.d_oo, sizeof(int64_t) * (cs + 1)));
+    HIP_TRY(hipMalloc(&p.d_out16, sizeof(uint16_t) * cb));
+    if (!p.e_in) HIP_TRY(hipEventCreateWithFlags(&p.e_in, hipEventDisableTiming));
+    if (!p.e_comp) HIP_TRY(hipEventCreateWithFlags(&p.e_comp, hipEventDisableTiming));
+    if (!p.e_out) HIP_TRY(hipEventCreateWithFlags(&p.e_out, hipEventDisableTiming));
+    p.cap_bytes = cb;
+    p.cap_str = cs;
+  }
+  (void)max_w;
+  int32_t rc = ensure_workspace(h, max_b);
+  if (rc) return rc;
+  const bool count = stats && !chunk_bits;
+  if (count) HIP_TRY(hipMemsetAsync(h->d_pcount, 0, sizeof(unsigned long long), h->stream));
+  const bool was_timing = h->timing;
+  const size_t was_used = h->ev_used;
+  const int32_t was_pattern = h->pattern;
+  h->timing = true;
+  h->ev_used = 0;
+  if (!chunk_bits) h->pattern = pattern;
+  auto restore = [&]() {
+    h->timing = was_timing;
+    h->ev_used = was_timing ? was_used : 0;
+    h->pattern = was_pattern;
+  };
+  sw::HostPool& pool = *h->pool;
+  double ms_stage = 0, ms_drain = 0;
+  int64_t done = 0;
+  auto stage = [&](size_t k) -> int32_t {
+    auto& p = h->pipe[k & 1];
+    const int64_t s_lo = runs[k].first, s_hi = runs[k].second, a0 = str_off[s_lo], nb = str_off[s_hi] - a0;
+    auto t = std::chrono::steady_clock::now();
+    const uint8_t* src = bytes + a0;
+    pool.parallel_for(nb, [&](int64_t lo, int64_t hi) { std::memcpy(p.h_in + lo, src + lo, (size_t)(hi - lo)); });
+    for (int64_t j = 0; j <= s_hi - s_lo; ++j) p.h_off[j] = str_off[s_lo + j] - a0;
+    if (chunk_bits) {  // the run's bits, realigned to its first byte
+      const int64_t g0 = a0 - b0, nw = (nb + 63) / 64, last_q = (str_off[n_str] - b0 - 1) / 64;
+      pool.parallel_for(nw, [&](int64_t lo, int64_t hi) {
+        for (int64_t w = lo; w < hi; ++w) {
+          const int64_t bit = g0 + 64 * w, q = bit >> 6, r = bit & 63;
+          uint64_t x = chunk_bits[q] >> r;
+          if (r && q + 1 <= last_q) x |= chunk_bits[q + 1] << (64 - r);
+          p.h_bits[w] = x;
+        }
+      });
+    }
+    ms_stage += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t).count();
+    return SW_OK;
+  };
+  auto issue = [&](size_t k) -> int32_t {
+    auto& p = h->pipe[k & 1];
+    const int64_t s_lo = runs[k].first, s_hi = runs[k].second, nb = str_off[s_hi] - str_off[s_lo], ns = s_hi - s_lo;
+    HIP_TRY(hipMemcpyAsync(p.d_in, p.h_in, (size_t)nb, hipMemcpyHostToDevice, h->s_h2d));
+    HIP_TRY(hipMemcpyAsync(p.d_off, p.h_off, sizeof(int64_t) * (ns + 1), hipMemcpyHostToDevice, h->s_h2d));
+    if (chunk_bits)
+      HIP_TRY(hipMemcpyAsync(p.d_bits, p.h_bits, sizeof(uint64_t) * ((nb + 63) / 64), hipMemcpyHostToDevice, h->s_h2d));
+    HIP_TRY(hipEventRecord(p.e_in, h->s_h2d));
+    HIP_TRY(hipStreamWaitEvent(h->stream, p.e_in, 0));
+    const int32_t r = sw_encode_device(h, p.d_in, nb, p.d_off, ns, chunk_bits ? p.d_bits : nullptr, p.d_out, p.d_oo,
+                                       h->stream, nullptr);
+    if (r) return r;
+    if (count && nb > 0)
+      hipLaunchKernelGGL(k_popcount, dim3(1024), dim3(256), 0, h->stream, h->d_pbits, (nb + 63) / 64, h->d_pcount);
+    if (h->ids16) hipLaunchKernelGGL(k_pack16, dim3(2048), dim3(256), 0, h->stream, p.d_out, h->d_total, p.d_out16);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipMemcpyAsync(p.h_ntok, h->d_total, sizeof(int64_t), hipMemcpyDeviceToHost, h->stream));
+    HIP_TRY(hipEventRecord(p.e_comp, h->stream));
+    return SW_OK;
+  };
+  auto drain = [&](size_t k) -> int32_t {
+    auto& p = h->pipe[k & 1];
+    const int64_t s_lo = runs[k].first, s_hi = runs[k].second, ns = s_hi - s_lo;
+    HIP_TRY(hipEventSynchronize(p.e_comp));
+    const int64_t nt = *p.h_ntok;
+    if (done + nt > out_cap) return fail(SW_ERR_CAP, "sw_encode_batch: out_cap too small");
+    auto t = std::chrono::steady_clock::now();
+    HIP_TRY(hipStreamWaitEvent(h->s_d2h, p.e_comp, 0));
+    if (nt > 0)
+      HIP_TRY(hipMemcpyAsync(p.h_out, h->ids16 ? (void*)p.d_out16 : (void*)p.d_out,
+                             (size_t)nt * (h->ids16 ? 2 : 4), hipMemcpyDeviceToHost, h->s_d2h));
+    HIP_TRY(hipMemcpyAsync(p.h_oo, p.d_oo, sizeof(int64_t) * (ns + 1), hipMemcpyDeviceToHost, h->s_d2h));
+    HIP_TRY(hipEventRecord(p.e_out, h->s_d2h));
+    HIP_TRY(hipEventSynchronize(p.e_out));
+    int32_t* dst = out_ids + done;
+    if (h->ids16) {
+      const uint16_t* s16 = (const uint16_t*)p.h_out;
+      pool.parallel_for(nt, [&](int64_t lo, int64_t hi) {
+        for (int64_t i = lo; i < hi; ++i) dst[i] = (int32_t)s16[i];
+      });
+    } else {
+      const int32_t* s32 = (const int32_t*)p.h_out;
+      pool.parallel_for(nt, [&](int64_t lo, int64_t hi) { std::memcpy(dst + lo, s32 + lo, sizeof(int32_t) * (hi - lo)); });
+    }
+    for (int64_t j = 0; j <= ns; ++j) out_off[s_lo + j] = p.h_oo[j] + done;
+    done += nt;
+    ms_drain += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t).count();
+    return SW_OK;
+  };
+  for (size_t k = 0; k < runs.size(); ++k) {
+    rc = stage(k);
+    if (!rc) rc = issue(k);
+    if (!rc && k > 0) rc = drain(k - 1);
+    if (rc) { restore(); return rc; }
+  }
+  if (!runs.empty()) rc = drain(runs.size() - 1);
+  if (rc) { restore(); return rc; }
+  if (n_str == 0) out_off[0] = 0;
+  const double k_ms = sw_encoder_last_kernel_ms(h) * (double)runs.size();
+  int64_t n_chunks = -1;
+  if (count) {
+    unsigned long long c = 0;
+    HIP_TRY(hipMemcpy(&c, h->d_pcount, sizeof(c), hipMemcpyDeviceToHost));
+    n_chunks = (int64_t)c;
+  }
+  restore();
+  if (stats) {
+    stats->n_bytes = str_off[n_str] - b0;
+    stats->n_chunks = n_chunks;
+    stats->n_tokens = done;
+    stats->ms_presplit = 0;
+    stats->ms_h2d = ms_stage;   // (host staging into pinned memory; the uploads overlap)
+    stats->ms_kernels = k_ms;
+    stats->ms_d2h = ms_drain;   // (downloads + copies out, overlapped with the next run's encode)
+    stats->ms_total = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - T0).count();
+  }
+  return SW_OK;
+}
+
+}  // namespace
+
 extern "C" int32_t sw_encode_batch(sw_encoder* h, const uint8_t* bytes, const int64_t* str_off, int64_t n_str,
                                    int32_t pattern, const uint64_t* chunk_bits, int32_t* out_ids, int64_t out_cap,
                                    int64_t* out_off, sw_stats* stats) {
@@ -614,6 +833,8 @@ extern "C" int32_t sw_encode_batch(sw_encoder* h, const uint8_t* bytes, const in
   if (n_bytes > 0 && !out_ids) return fail(SW_ERR_ARG, "sw_encode_batch: null out_ids");
   if (!chunk_bits && pattern != SW_PAT_CL100K && pattern != SW_PAT_GPT2 && pattern != SW_PAT_NONE)
     return fail(SW_ERR_ARG, "sw_encode_batch: bad pattern");
+  if (h->pipe_run > 0 && n_bytes > 2 * h->pipe_run && !(h->host_presplit && !chunk_bits))
+    return encode_batch_pipelined(h, bytes, str_off, n_str, pattern, chunk_bits, out_ids, out_cap, out_off, stats, T0);
   if (n_bytes > h->max_launch) {
     // one device launch addresses < 2 GiB: encode runs of whole strings separately
     int64_t done = 0, s_lo = 0;
@@ -728,6 +949,23 @@ extern "C" int32_t sw_encode_batch(sw_encoder* h, const uint8_t* bytes, const in
     stats->ms_d2h = ms_d2h;
     stats->ms_total = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - T0).count();
   }
+  return SW_OK;
+}
+
+extern "C" int32_t sw_encoder_last_counts(sw_encoder* h, int64_t* out4) {
+  if (!h || !out4) return fail(SW_ERR_ARG, "sw_encoder_last_counts: bad arguments");
+  DeviceGuard g(h->device);
+  for (int i = 0; i < 4; ++i) out4[i] = 0;
+  out4[3] = h->last_tiles;
+  if (!h->ws_pending || h->last_tiles == 0) return SW_OK;
+  HIP_TRY(hipEventSynchronize(h->ws_done));
+  std::vector<uint32_t> slots((size_t)h->last_tiles), nref((size_t)h->last_tiles);
+  HIP_TRY(hipMemcpy(slots.data(), h->d_tile_slots, sizeof(uint32_t) * slots.size(), hipMemcpyDeviceToHost));
+  HIP_TRY(hipMemcpy(nref.data(), h->d_tile_nref, sizeof(uint32_t) * nref.size(), hipMemcpyDeviceToHost));
+  int64_t q = 0;
+  HIP_TRY(hipMemcpy(&q, h->d_qtotal, sizeof(q), hipMemcpyDeviceToHost));
+  for (size_t t = 0; t < slots.size(); ++t) { out4[0] += slots[t]; out4[1] += nref[t]; }
+  out4[2] = q;
   return SW_OK;
 }
 

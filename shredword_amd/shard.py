@@ -4,7 +4,7 @@ One process per GPU (torch.distributed; backend "nccl" = RCCL over xGMI on the M
 "gloo" for the CPU tests).  The batch is cut into contiguous string ranges balanced by bytes;
 every rank encodes its range on its own device with no communication, and the only exchange
 is the reassembly of the token-id buffers:
-  1. all-gather of the per-rank token counts (int64);
+  1. all-gather of the per-rank token and string counts (int64, one collective);
   2. exclusive scan -> each rank's displacement in the global id buffer;
   3. all-gather of the id buffers, padded to the largest rank's count (one collective: on
      xGMI every GPU receives 7/8 of the ids over its 7 links at once);
@@ -40,61 +40,92 @@ def shard_of(buf, str_off, lo, hi):
     return buf[a:b], str_off[lo:hi + 1] - a
 
 
-def reassemble(local_ids, local_off, group=None, device=None, concat=True):
+def reassemble(local_ids, local_off, group=None, device=None, concat=True, width=None, width_s=None):
     """Collective reassembly of per-rank encodes (steps 1-4 above) on every rank.
 
     local_ids: torch int32 [>= local count] on `device`; local_off: torch int64 [m+1] with
     local_off[0] == 0.  Returns (ids int32 [total], off int64 [n+1]) for the whole batch, on
-    `device`, identical on every rank.  concat=False skips the final copies and returns the
-    gathered buffers as they landed: (ids [world * width], counts, width, offsets
-    [world * width_s], string counts, width_s) -- rank r's ids start at r * width."""
+    `device`, identical on every rank.
+
+    The per-rank token and string counts travel in ONE all-gather.  Sizing the padded gathers
+    needs their maxima on the host -- one synchronisation -- unless the caller knows bounds:
+    `width` >= every rank's token count and `width_s` >= every rank's string count (e.g. from an
+    earlier step over the same batch); then nothing waits on the host, and a bound that was too
+    small raises at the next synchronising call (check_bounds).
+    concat=False skips the final copies and returns the gathered buffers as they landed:
+    (ids [world * width], counts [world] on the device, width, offsets [world * width_s],
+    string counts [world] on the device, width_s) -- rank r's ids start at r * width."""
     import torch
     import torch.distributed as dist
 
     world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
     dev = device if device is not None else local_ids.device
-    cnt = local_off[-1:].to(device=dev, dtype=torch.int64)
-    counts = torch.zeros(world, dtype=torch.int64, device=dev)
-    dist.all_gather_into_tensor(counts, cnt, group=group)
-    n_str = torch.tensor([local_off.numel() - 1], dtype=torch.int64, device=dev)
-    n_strs = torch.zeros(world, dtype=torch.int64, device=dev)
-    dist.all_gather_into_tensor(n_strs, n_str, group=group)
-    counts_h = counts.cpu().tolist()
-    n_strs_h = n_strs.cpu().tolist()
-    width = max(max(counts_h), 1)
-    c = int(counts_h[dist.get_rank(group)])
+    mine = torch.empty(2, dtype=torch.int64, device=dev)
+    mine[0:1] = local_off[-1:].to(device=dev, dtype=torch.int64)
+    mine[1] = local_off.numel() - 1
+    both = torch.empty(2 * world, dtype=torch.int64, device=dev)
+    dist.all_gather_into_tensor(both, mine, group=group)  # [count_0, n_str_0, count_1, ...]
+    counts, n_strs = both[0::2], both[1::2]
+    if width is None or width_s is None:  # the one host synchronisation: the gathers' sizes
+        h = both.cpu().tolist()
+        width = max(max(h[0::2]), 1) if width is None else width
+        width_s = max(max(h[1::2]), 1) if width_s is None else width_s
+    else:
+        _pending_checks.append((counts, n_strs, width, width_s))
+    width, width_s = int(width), int(width_s)
     if local_ids.numel() >= width and local_ids.dtype == torch.int32 and local_ids.device == dev:
-        send = local_ids[:width]  # (slots past c are padding: never read)
+        send = local_ids[:width]  # (slots past the count are padding: never read)
     else:
         send = torch.zeros(width, dtype=torch.int32, device=dev)
-        send[:c] = local_ids[:c].to(device=dev, dtype=torch.int32)
+        k = min(width, local_ids.numel())
+        send[:k] = local_ids[:k].to(device=dev, dtype=torch.int32)
     recv = torch.empty(world * width, dtype=torch.int32, device=dev)
     dist.all_gather_into_tensor(recv, send, group=group)
-    width_s = max(max(n_strs_h), 1)
-    m = int(n_strs_h[dist.get_rank(group)])
+    m = local_off.numel() - 1
     if local_off.numel() >= width_s and local_off.dtype == torch.int64 and local_off.device == dev:
         send_o = local_off[:width_s]
     else:
         send_o = torch.zeros(width_s, dtype=torch.int64, device=dev)
-        send_o[:m] = local_off[:m].to(device=dev, dtype=torch.int64)
+        send_o[:min(m, width_s)] = local_off[:min(m, width_s)].to(device=dev, dtype=torch.int64)
     recv_o = torch.empty(world * width_s, dtype=torch.int64, device=dev)
     dist.all_gather_into_tensor(recv_o, send_o, group=group)
     if not concat:
-        return recv, counts_h, width, recv_o, n_strs_h, width_s
+        return recv, counts, width, recv_o, n_strs, width_s
+    # the concatenation needs the counts on the host (as torch's slicing does)
+    ch, sh = counts.cpu().tolist(), n_strs.cpu().tolist()
+    if max(ch) > width or max(sh) > width_s:
+        raise RuntimeError("reassemble: a rank's count exceeds the given width bound")
     ids, offs, disp = [], [], 0
     for r in range(world):
-        ids.append(recv[r * width: r * width + counts_h[r]])
-        offs.append(recv_o[r * width_s: r * width_s + n_strs_h[r]] + disp)
-        disp += counts_h[r]
+        ids.append(recv[r * width: r * width + ch[r]])
+        offs.append(recv_o[r * width_s: r * width_s + sh[r]] + disp)
+        disp += ch[r]
     offs.append(torch.tensor([disp], dtype=torch.int64, device=dev))
     return torch.cat(ids), torch.cat(offs)
+
+
+_pending_checks = []
+
+
+def check_bounds():
+    """Raise if a width bound given to reassemble was exceeded by an actual count (synchronises)."""
+    bad = [(c.cpu().max().item(), w, s.cpu().max().item(), ws) for c, s, w, ws in _pending_checks
+           if c.cpu().max().item() > w or s.cpu().max().item() > ws]
+    _pending_checks.clear()
+    if bad:
+        raise RuntimeError("reassemble: counts %r exceeded the width bounds" % (bad,))
 
 
 def encode_sharded(tok, buf, str_off, chunk_bits_fn=None, group=None):
     """Encode the packed batch (buf, str_off) across the ranks of `group`: rank r encodes its
     byte-balanced string range with `tok` (a Tokenizer on this rank's GPU), then every rank
-    gets the whole batch's ids via `reassemble`.  chunk_bits_fn(sub_buf, sub_off) may supply a
-    pre-split bitmap for the sub-batch (default: the tokenizer's own host pre-split)."""
+    gets the whole batch's ids via `reassemble`.
+
+    With the nccl (RCCL) backend the rank's shard is uploaded once and encoded, pre-split
+    included, on device buffers (Tokenizer.encode_device); the ids stay on the device through
+    the all-gather.  chunk_bits_fn(sub_buf, sub_off) may supply a host pre-split bitmap.  With
+    gloo (CPU tests) the host-buffer path encode_packed is used."""
     import torch
     import torch.distributed as dist
 
@@ -102,6 +133,13 @@ def encode_sharded(tok, buf, str_off, chunk_bits_fn=None, group=None):
     lo, hi = partition(str_off, world)[rank]
     sub, sub_off = shard_of(buf, str_off, lo, hi)
     bits = chunk_bits_fn(sub, sub_off) if chunk_bits_fn else None
+    if dist.get_backend(group) == "nccl":
+        dev = torch.device("cuda", torch.cuda.current_device())
+        d_buf = torch.from_numpy(np.ascontiguousarray(sub) if len(sub) else np.zeros(1, np.uint8)).to(dev)
+        d_off = torch.from_numpy(np.ascontiguousarray(sub_off)).to(dev)
+        d_bits = torch.from_numpy(bits.view(np.int64)).to(dev) if bits is not None else None
+        ids, off = tok.encode_device(d_buf, d_off, d_bits)
+        return reassemble(ids, off, group, dev)
     ids, off = tok.encode_packed(sub, sub_off, bits)
-    dev = torch.device("cuda", torch.cuda.current_device()) if dist.get_backend(group) == "nccl" else torch.device("cpu")
+    dev = torch.device("cpu")
     return reassemble(torch.from_numpy(ids).to(dev), torch.from_numpy(off).to(dev), group, dev)

@@ -178,6 +178,30 @@ class Tokenizer(BaseTokenizer):
         self.last_stats = stats
         return out[:int(out_off[-1])], out_off
 
+    def encode_device(self, d_buf, d_off, d_bits=None, d_out=None, d_out_off=None, stream=None):
+        """Encode strings already on this tokenizer's device (torch tensors: uint8 bytes, int64
+        offsets from 0; optional pre-split bitmap as int64 words, else the device pre-splits with
+        `pattern`), on torch's current stream (or `stream`).  Returns (ids int32 [n_tokens],
+        offsets int64 [n+1]) as device tensors; the token count is read back (one
+        synchronisation).  d_out / d_out_off: optional output buffers (>= n_bytes / n+1)."""
+        import torch
+        dev = d_buf.device
+        n = int(d_off.numel()) - 1
+        n_bytes = int(d_off[-1].item()) if n >= 0 else 0
+        if d_out is None:
+            d_out = torch.empty(max(n_bytes, 1), dtype=torch.int32, device=dev)
+        if d_out_off is None:
+            d_out_off = torch.empty(n + 1, dtype=torch.int64, device=dev)
+        L = _lib.lib()
+        h = self._encoder()
+        _lib.check(L.sw_encoder_set_option(h, _lib.SW_OPT_PATTERN, pattern_id(self.pattern)))
+        st = stream if stream is not None else torch.cuda.current_stream(dev).cuda_stream
+        n_tok = ctypes.c_int64()
+        _lib.check(L.sw_encode_device(h, d_buf.data_ptr(), n_bytes, d_off.data_ptr(), n,
+                                      d_bits.data_ptr() if d_bits is not None else None,
+                                      d_out.data_ptr(), d_out_off.data_ptr(), st, ctypes.byref(n_tok)))
+        return d_out[:int(n_tok.value)], d_out_off
+
     def _split_specials(self, text):
         """Split on special tokens: leftmost occurrence first, dictionary order breaking ties
         (the reference stores special_tokens at base.py:103 but defines no split).  One regex

@@ -280,3 +280,40 @@ def test_workspace_ordered_across_streams():
     for d_out, d_oo in outs:
         oo = d_oo.cpu().numpy()
         assert_same((d_out[:int(oo[-1])].cpu().numpy(), oo), exp)
+
+
+# ------------------------------------------------------------------ pipelined host batches
+@pytest.mark.parametrize("run", [64, 5000, 300000])
+@pytest.mark.parametrize("host_bits", [False, True])
+@pytest.mark.parametrize("wide", [False, True])
+def test_pipelined_batch(run, host_bits, wide):
+    """sw_encode_batch over more than two pipeline runs: staging, 16-bit downloads (32-bit for a
+    table past 64k ids), realigned caller bits, offsets rebased across runs -- == the oracle."""
+    buf, off = corpus.synth(8, corpus.MIXED, 900, 700)
+    if run == 64:  # (every string must fit a run... or be a run of its own: both happen)
+        datas = [bytes(buf[off[i]:off[i + 1]][:200]).decode("utf-8", "ignore").encode("utf-8") for i in range(400)]
+        full, offs = pack([b"#" * 13] + datas)
+    else:
+        full, offs = pack([b"#" * 13] + [bytes(buf[off[i]:off[i + 1]]) for i in range(900)])
+    sub = offs[1:]
+    base = load_model_merges("bl32k.model")
+    if wide:
+        shift = lambda x: x if x < 256 else x + 70000  # noqa: E731
+        merges = {(shift(a), shift(b)): shift(v) for (a, b), v in base.items()}
+    else:
+        merges = base
+    t = sa.Tokenizer(device=0)
+    t.merges = merges
+    exp = oracle_encode(merges, full, sub, "cl100k")
+    bits = corpus.presplit(full, sub)[0] if host_bits else None
+    L, h = _lib.lib(), t._encoder()
+    assert L.sw_encoder_get_info(h, _lib.SW_INFO_IDS16) == (0 if wide else 1)
+    _lib.check(L.sw_encoder_set_option(h, _lib.SW_OPT_PIPE_RUN_BYTES, run))
+    got = t.encode_packed(full, sub, bits)
+    st = t.last_stats
+    assert_same(got, exp)
+    assert st.n_tokens == len(exp[0])
+    assert st.n_chunks == (-1 if host_bits else corpus.presplit(full, sub)[1])
+    got2 = t.encode_packed(full, sub, bits)  # (buffers reused)
+    assert_same(got2, exp)
+    t.close()

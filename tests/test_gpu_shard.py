@@ -1,0 +1,59 @@
+"""The multi-GPU path on the MI355X box: shard.encode_sharded over RCCL (torch.distributed
+backend "nccl") at world size 1 with the HIP encoder on device buffers, against the
+reference-generated golden ids; and the reassembly with caller width bounds (no host
+synchronisation before the gathers)."""
+import os
+import socket
+
+import numpy as np
+import pytest
+
+import shredword_amd as sa
+from shredword_amd import _lib, shard
+from conftest import GOLD, load_model_merges
+
+pytestmark = pytest.mark.gpu
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+@pytest.fixture(scope="module")
+def nccl_world1():
+    import torch
+    import torch.distributed as dist
+    if _lib.lib().sw_device_count() < 1:
+        pytest.fail("no HIP device visible: -m gpu must run on the MI355X box")
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()))
+    torch.cuda.set_device(0)
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+    yield
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("fixture,model", [("enc_bl32k_mixed.npz", "bl32k.model"),
+                                           ("enc_toy500_ascii.npz", "toy500.model")])
+def test_encode_sharded_rccl_world1(nccl_world1, fixture, model):
+    import torch
+    d = np.load(os.path.join(GOLD, fixture))
+    tok = sa.Tokenizer(device=0)
+    tok.merges = load_model_merges(model)
+    ids, off = shard.encode_sharded(tok, d["bytes"], d["off"])
+    assert ids.device.type == "cuda" and off.device.type == "cuda"
+    np.testing.assert_array_equal(off.cpu().numpy(), d["ids_off"])
+    np.testing.assert_array_equal(ids.cpu().numpy(), d["ids"])
+    # the gathered buffers with caller bounds (the bench's step): rank 0's ids at offset 0
+    d_buf = torch.from_numpy(d["bytes"]).cuda()
+    d_off = torch.from_numpy(d["off"]).cuda()
+    l_ids, l_off = tok.encode_device(d_buf, d_off)
+    recv, counts, width, recv_o, n_strs, width_s = shard.reassemble(l_ids, l_off, None, torch.device("cuda", 0),
+                                                                    concat=False, width=len(d["bytes"]),
+                                                                    width_s=len(d["off"]))
+    shard.check_bounds()
+    n = int(counts[0].item())
+    np.testing.assert_array_equal(recv[:n].cpu().numpy(), d["ids"])
+    np.testing.assert_array_equal(recv_o[:len(d["off"]) - 1].cpu().numpy(), d["ids_off"][:-1])
+    tok.close()

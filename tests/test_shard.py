@@ -61,6 +61,18 @@ def _rank_main(rank, world, port, fixture, model, result_dir):
         full_ids, full_off = shard.reassemble(torch.from_numpy(ids), torch.from_numpy(ids_off), None,
                                               torch.device("cpu"))
         ok = (np.array_equal(full_ids.numpy(), d["ids"]) and np.array_equal(full_off.numpy(), d["ids_off"]))
+        # with caller bounds (no host synchronisation before the gathers): the same result
+        b_ids, b_off = shard.reassemble(torch.from_numpy(ids), torch.from_numpy(ids_off), None, torch.device("cpu"),
+                                        width=len(buf), width_s=len(off))
+        shard.check_bounds()
+        ok = ok and np.array_equal(b_ids.numpy(), d["ids"]) and np.array_equal(b_off.numpy(), d["ids_off"])
+        # a bound below a rank's count is reported, never silently truncated
+        try:
+            shard.reassemble(torch.from_numpy(ids), torch.from_numpy(ids_off), None, torch.device("cpu"), width=1,
+                             width_s=len(off))
+            ok = False
+        except RuntimeError:
+            pass
         with open(os.path.join(result_dir, "rank%d" % rank), "w") as f:
             f.write("ok" if ok else "mismatch")
     finally:

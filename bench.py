@@ -52,6 +52,7 @@ def parse():
     ap.add_argument("--no-dedupe", action="store_true",
                     help="A/B only: every queued chunk runs its own merge loop (same results)")
     ap.add_argument("--dedupe-slots", type=int, default=0, help="A/B only: cap the dedupe table (power of two)")
+    ap.add_argument("--no-dedupe-exact", action="store_true", help="A/B only: fingerprint keys for every chunk")
     ap.add_argument("--no-chunk-table", action="store_true",
                     help="every chunk runs the merge loop (results identical; see DESIGN.md)")
     return ap.parse_args()
@@ -122,6 +123,8 @@ def main():
     _lib.check(L.sw_encoder_set_option(h, _lib.SW_OPT_CHUNK_TABLE, 0 if args.no_chunk_table else 1))
     _lib.check(L.sw_encoder_set_option(h, _lib.SW_OPT_DEDUPE, 0 if args.no_dedupe else 1))
     _lib.check(L.sw_encoder_set_option(h, _lib.SW_OPT_DEDUPE_SLOTS, args.dedupe_slots))
+    if args.no_dedupe_exact:
+        _lib.check(L.sw_encoder_set_option(h, _lib.SW_OPT_DEDUPE_EXACT, 0))
     _lib.check(L.sw_encoder_set_option(h, _lib.SW_OPT_PATTERN, pat))
 
     cap = torch.tensor([n_bytes], dtype=torch.int64, device=dev)

@@ -96,8 +96,9 @@ int32_t sw_encoder_reserve(sw_encoder* h, int64_t max_bytes, int64_t max_strings
 /* Testing knobs of the dedupe table (results are identical for any value):
  *   SW_OPT_DEDUPE_SLOTS    cap on the table's slots (0 = automatic, else a power of two >= 8);
  *                          a full table makes chunks merge on their own
- *   SW_OPT_DEDUPE_FP_BITS  fingerprint bits compared before the bytes (27 = default; 0 makes
- *                          every probe fall through to the byte comparison) */
+ *   SW_OPT_DEDUPE_FP_BITS  fingerprint bits compared before the bytes of chunks with
+ *                          fingerprint keys (26 = default; 0 makes every probe fall through to
+ *                          the byte comparison) */
 #define SW_OPT_DEDUPE_SLOTS 3
 #define SW_OPT_DEDUPE_FP_BITS 4
 /*   SW_OPT_PATTERN         pre-split pattern (SW_PAT_*) sw_encode_device uses when it is given
@@ -111,7 +112,8 @@ int32_t sw_encoder_reserve(sw_encoder* h, int64_t max_bytes, int64_t max_strings
  *                          conflicting pieces are joined and encoded again (well-formed tables
  *                          only, SW_INFO_SPLIT); 0: one wave loop per chunk.  Results identical.
  *   SW_OPT_MAX_LAUNCH_BYTES  sw_encode_batch encodes larger batches as several launches of
- *                          whole strings (0 = the 2 GiB device limit; testing: any value >= 64) */
+ *                          whole strings (0 = the 2^30 - 64 byte device limit; testing: any
+ *                          value >= 64) */
 #define SW_OPT_LONG_SPLIT 7
 #define SW_OPT_MAX_LAUNCH_BYTES 8
 /*   SW_OPT_PIPE_RUN_BYTES  sw_encode_batch of more than 2 runs of this many bytes (default 64 MiB; 0:
@@ -119,6 +121,10 @@ int32_t sw_encoder_reserve(sw_encoder* h, int64_t max_bytes, int64_t max_strings
  *                          host threads, uploads, encodes and downloads of consecutive runs
  *                          overlapping, ids downloaded as 16 bits when every id fits */
 #define SW_OPT_PIPE_RUN_BYTES 9
+/*   SW_OPT_DEDUPE_EXACT    1 (default): dedupe keys of chunks up to 7 bytes are the bytes
+ *                          themselves (no verification read); 0: every key is a fingerprint
+ *                          verified against the first occurrence's bytes (testing) */
+#define SW_OPT_DEDUPE_EXACT 10
 int32_t sw_encoder_set_option(sw_encoder* h, int32_t option, int64_t value);
 
 /* Encoder facts (sw_encoder_get_info): distinct merges, whole-chunk table entries, whether the
@@ -165,7 +171,7 @@ int32_t sw_presplit_device(sw_encoder* h, const uint8_t* d_bytes, int64_t n_byte
  * d_str_off[n_str+1] (relative to d_bytes, d_str_off[0] == 0, d_str_off[n_str] == n_bytes),
  * d_chunk_bits[ceil(n_bytes/64)] or NULL (then the device pre-splits with the SW_OPT_PATTERN
  * pattern first: the full path), d_out_ids[n_bytes], d_out_off[n_str+1].  One launch takes
- * n_bytes < 2^31 - 64 (SW_ERR_ARG otherwise); sw_encode_batch splits larger batches between
+ * n_bytes <= 2^30 - 64 (SW_ERR_ARG otherwise); sw_encode_batch splits larger batches between
  * strings by itself.
  * stream: a hipStream_t on that device; NULL is the null stream (torch's default stream, as
  * in every HIP library API).

@@ -117,13 +117,15 @@ struct sw_encoder {
   unsigned long long* d_stamps = nullptr;  // SW_STAMPS builds
   uint64_t* d_dtab = nullptr;         // chunk dedupe table
   uint32_t dmask = 0;
+  uint4* d_dres = nullptr;            // dense result heads, one per table entry
   bool dedupe = true;
+  bool dedupe_exact = true;           // SW_OPT_DEDUPE_EXACT
   int64_t dedupe_slots = 0;           // SW_OPT_DEDUPE_SLOTS (0: automatic)
   int32_t pattern = SW_PAT_CL100K;    // SW_OPT_PATTERN: device pre-split of sw_encode_device(bits = NULL)
   bool host_presplit = false;         // SW_OPT_HOST_PRESPLIT: sw_encode_batch pre-splits on the host
   uint64_t* d_pbits = nullptr;        // [n_bytes / 64] device pre-split bitmap
   unsigned long long* d_pcount = nullptr;
-  uint32_t dedupe_fp_mask = (1u << 27) - 1;
+  uint32_t dedupe_fp_mask = (1u << 26) - 1;
   uint32_t* d_tile_cnt = nullptr;
   int64_t* d_tile_base = nullptr;
   int64_t* d_total = nullptr;
@@ -162,6 +164,8 @@ void free_workspace(sw_encoder* h) {
   h->d_tile_slo = nullptr; h->d_stamps = nullptr; h->d_tile_slots = nullptr; h->d_tile_nref = nullptr; h->d_rlist = nullptr; h->d_queue = nullptr;
   h->d_bcnt = nullptr; h->d_boff = nullptr; h->d_qtotal = nullptr;
   (void)hipFree(h->d_dtab); (void)hipFree(h->d_tile_base); (void)hipFree(h->d_tile_cnt);
+  (void)hipFree(h->d_dres);
+  h->d_dres = nullptr;
   (void)hipFree(h->d_total);
   h->d_scratch = nullptr; h->d_res = nullptr; h->d_pbits = nullptr; h->d_pcount = nullptr; h->d_part = nullptr;
   h->d_dtab = nullptr; h->d_tile_base = nullptr; h->d_tile_cnt = nullptr; h->d_total = nullptr;
@@ -194,7 +198,8 @@ int32_t ensure_workspace(sw_encoder* h, int64_t n_bytes) {
   const int64_t nb = std::max<int64_t>(n_bytes, 1);
   const int64_t n_tiles = (nb + kTile - 1) / kTile;
   HIP_TRY(hipMalloc(&h->d_scratch, sizeof(int32_t) * n_tiles * kTile));  // whole tiles: see k_compact
-  HIP_TRY(hipMalloc(&h->d_res, sizeof(uint32_t) * (2 * nb + 16)));  // (+ slack for k_compact's head reads)
+  // (+ slack for k_compact's head reads; k_classify's tile-local queue, aliased here, takes whole tiles)
+  HIP_TRY(hipMalloc(&h->d_res, sizeof(uint32_t) * std::max<int64_t>(2 * nb + 16, n_tiles * kTile)));
   HIP_TRY(hipMalloc(&h->d_tile_slo, sizeof(int64_t) * n_tiles));
   HIP_TRY(hipMalloc(&h->d_tile_slots, sizeof(uint32_t) * n_tiles));
   HIP_TRY(hipMalloc(&h->d_tile_nref, sizeof(uint32_t) * n_tiles));
@@ -205,10 +210,12 @@ int32_t ensure_workspace(sw_encoder* h, int64_t n_bytes) {
   HIP_TRY(hipMalloc(&h->d_boff, sizeof(int64_t) * kNumBuckets * n_tiles));
   HIP_TRY(hipMalloc(&h->d_qtotal, sizeof(int64_t)));
   HIP_TRY(hipMalloc(&h->d_part, sizeof(int64_t) * ((kNumBuckets * n_tiles + kScanBlock - 1) / kScanBlock + 1)));
-  {  // dedupe table: ~1 slot per 4 input bytes, at most 2^24 slots (128 MiB)
+  {  // dedupe table: ~1 entry per 64 input bytes, 2^6 .. 2^22 entries (32 MiB), and a 16-byte
+     // result head per entry
     int64_t slots = 64;
-    while (slots < nb / 4 && slots < (1LL << 24)) slots <<= 1;
+    while (slots < nb / 64 && slots < (1LL << 22)) slots <<= 1;
     HIP_TRY(hipMalloc(&h->d_dtab, sizeof(uint64_t) * slots));
+    HIP_TRY(hipMalloc(&h->d_dres, sizeof(uint4) * slots));
     h->dmask = (uint32_t)(slots - 1);
   }
   HIP_TRY(hipMalloc(&h->d_tile_base, sizeof(int64_t) * n_tiles));
@@ -463,9 +470,10 @@ extern "C" int32_t sw_encoder_set_option(sw_encoder* h, int32_t option, int64_t 
       h->dedupe_slots = value;
       return SW_OK;
     case SW_OPT_DEDUPE_FP_BITS:
-      if (value < 0 || value > 27) return fail(SW_ERR_ARG, "dedupe fingerprint bits: 0..27");
+      if (value < 0 || value > 26) return fail(SW_ERR_ARG, "dedupe fingerprint bits: 0..26");
       h->dedupe_fp_mask = (uint32_t)((1ULL << value) - 1);
       return SW_OK;
+    case SW_OPT_DEDUPE_EXACT: h->dedupe_exact = value != 0; return SW_OK;
     case SW_OPT_LONG_SPLIT: h->long_split = value != 0; return SW_OK;
     case SW_OPT_PIPE_RUN_BYTES:
       if (value != 0 && value < 64) return fail(SW_ERR_ARG, "pipeline run bytes: 0 (off) or >= 64");
@@ -473,7 +481,7 @@ extern "C" int32_t sw_encoder_set_option(sw_encoder* h, int32_t option, int64_t 
       return SW_OK;
     case SW_OPT_MAX_LAUNCH_BYTES:
       if (value != 0 && (value < 64 || value > kMaxLaunchBytes))
-        return fail(SW_ERR_ARG, "max launch bytes: 0 (default) or 64 .. 2^31 - 128");
+        return fail(SW_ERR_ARG, "max launch bytes: 0 (default) or 64 .. 2^30 - 64");
       h->max_launch = value ? value : kMaxLaunchBytes;
       return SW_OK;
     default: return fail(SW_ERR_ARG, "sw_encoder_set_option: unknown option");
@@ -542,7 +550,7 @@ extern "C" int32_t sw_encode_device(sw_encoder* h, const uint8_t* d_bytes, int64
                                     int64_t* d_out_off, void* stream, int64_t* n_tokens_host) {
   if (!h || n_bytes < 0 || n_str < 0 || !d_str_off || !d_out_off || (n_bytes > 0 && (!d_bytes || !d_out_ids)))
     return fail(SW_ERR_ARG, "sw_encode_device: bad arguments");
-  if (n_bytes > kMaxLaunchBytes) return fail(SW_ERR_ARG, "sw_encode_device: n_bytes >= 2 GiB (split the batch)");
+  if (n_bytes > kMaxLaunchBytes) return fail(SW_ERR_ARG, "sw_encode_device: n_bytes > 2^30 - 64 (split the batch)");
   DeviceGuard g(h->device);
   hipStream_t st = (hipStream_t)stream;  // (NULL: the null stream, as torch's default stream)
   // the workspace belongs to the handle: order this launch after the previous one on any stream
@@ -576,12 +584,14 @@ extern "C" int32_t sw_encode_device(sw_encoder* h, const uint8_t* d_bytes, int64
     a.tile_slots = h->d_tile_slots; a.tile_nref = h->d_tile_nref; a.rlist = h->d_rlist; a.tile_cnt = h->d_tile_cnt;
     a.dtab = h->d_dtab; a.dedupe = h->dedupe ? 1u : 0u; a.dfp_mask = h->dedupe_fp_mask;
     a.dmask = h->dedupe_slots ? std::min<uint32_t>(h->dmask, (uint32_t)(h->dedupe_slots - 1)) : h->dmask;
+    a.dexact = h->dedupe_exact ? (uint32_t)kDdExactMax : 0u;
+    a.dres = h->d_dres;
     a.out_off = d_out_off; a.tile_slo = h->d_tile_slo;
     a.n_tiles = n_tiles; a.qtmp = h->d_res; a.bcnt = h->d_bcnt; a.boff = h->d_boff; a.q_total = h->d_qtotal;
     a.queue = h->d_queue; a.stamps = h->d_stamps;
-    a.inv = h->d_inv; a.n_inv = h->n_inv;
+    a.inv = h->d_inv; a.n_inv = h->n_inv; a.ids16 = h->ids16 ? 1u : 0u;
     const bool split = h->split_ok && h->long_split;
-    if (h->dedupe) HIP_TRY(hipMemsetAsync(h->d_dtab, 0, sizeof(uint64_t) * ((size_t)h->dmask + 1), st));
+    if (h->dedupe) HIP_TRY(hipMemsetAsync(h->d_dtab, 0, sizeof(uint64_t) * ((size_t)a.dmask + 1), st));
     hipLaunchKernelGGL(k_classify, dim3((unsigned)((n_tiles + kWaves - 1) / kWaves)), dim3(kThreads), 0, st, a);
     HIP_TRY(hipGetLastError());
     HIP_TRY(launch_scan(st, h->d_bcnt, kNumBuckets * n_tiles, h->d_part, h->d_boff, h->d_qtotal));
@@ -662,7 +672,7 @@ int32_t encode_batch_pipelined(sw_encoder* h, const uint8_t* bytes, const int64_
     int64_t s_hi = s_lo + 1;
     while (s_hi < n_str && str_off[s_hi + 1] - str_off[s_lo] <= h->pipe_run) ++s_hi;
     const int64_t nb = str_off[s_hi] - str_off[s_lo];
-    if (nb > h->max_launch) return fail(SW_ERR_ARG, "sw_encode_batch: a single string exceeds the launch limit (2 GiB)");
+    if (nb > h->max_launch) return fail(SW_ERR_ARG, "sw_encode_batch: a single string exceeds the launch limit (2^30 - 64 bytes)");
     runs.emplace_back(s_lo, s_hi);
     max_b = std::max(max_b, nb);
     max_s = std::max(max_s, s_hi - s_lo);
@@ -836,14 +846,14 @@ extern "C" int32_t sw_encode_batch(sw_encoder* h, const uint8_t* bytes, const in
   if (h->pipe_run > 0 && n_bytes > 2 * h->pipe_run && !(h->host_presplit && !chunk_bits))
     return encode_batch_pipelined(h, bytes, str_off, n_str, pattern, chunk_bits, out_ids, out_cap, out_off, stats, T0);
   if (n_bytes > h->max_launch) {
-    // one device launch addresses < 2 GiB: encode runs of whole strings separately
+    // one device launch addresses < 2^30 bytes: encode runs of whole strings separately
     int64_t done = 0, s_lo = 0;
     if (stats) *stats = sw_stats{};
     while (s_lo < n_str) {
       int64_t s_hi = s_lo + 1;
       while (s_hi < n_str && str_off[s_hi + 1] - str_off[s_lo] <= h->max_launch) ++s_hi;
       if (str_off[s_hi] - str_off[s_lo] > h->max_launch)
-        return fail(SW_ERR_ARG, "sw_encode_batch: a single string exceeds the launch limit (2 GiB)");
+        return fail(SW_ERR_ARG, "sw_encode_batch: a single string exceeds the launch limit (2^30 - 64 bytes)");
       std::vector<uint64_t> sub;
       if (chunk_bits) {  // the run's bits, realigned to its first byte
         const int64_t g0 = str_off[s_lo] - b0, nb = str_off[s_hi] - str_off[s_lo];

@@ -43,13 +43,31 @@ constexpr int kWin = kTile + 64;             // LDS byte window (tile + halo for
 constexpr int kTileWords = kTile / 64 + 1;   // bitmap words staged (tile + 64-bit halo)
 constexpr int kNumBuckets = 11;              // length buckets of the merge queue
 constexpr int kLongBucket = kNumBuckets - 1;
-constexpr int64_t kMaxLaunchBytes = (1LL << 31) - 64;  // slot references are int32 positions
+constexpr int64_t kRefSpace = 1LL << 30;              // position references below, dense ones above
+constexpr int64_t kMaxLaunchBytes = kRefSpace - 64;   // slot references are int32
 
-// A slot either holds a settled token (>= 0) or refers to the chunk starting at position p
-// whose merge result is res[2p + 1 .. 2p + 1 + res[2p]) (count, then the ids: one contiguous run,
-// and it fits, since a chunk of len bytes owns the 2 * len words from 2p).
+// A slot holds a settled token (>= 0) or refers to a merge result:
+//  - slot_ref(p): the result of the chunk starting at position p, res[2p + 1 .. 2p + 1 + res[2p])
+//    (count, then the ids: one contiguous run, and it fits, since a chunk of len bytes owns the
+//    2 * len words from 2p);
+//  - slot_dref(d): dense result d of the launch's dedupe (dres[d], below): the head of a result
+//    shared by every occurrence of a chunk, in an array of ~16 B per DISTINCT chunk, so the
+//    gathers of k_tile_count and k_compact stay in a few MB instead of spreading over res.
 __host__ __device__ inline int32_t slot_ref(int64_t p) { return -(int32_t)(p + 2); }
 __host__ __device__ inline int64_t slot_pos(int32_t v) { return -(int64_t)v - 2; }
+__host__ __device__ inline int32_t slot_dref(uint32_t d) { return -(int32_t)((int64_t)d + 2 + kRefSpace); }
+__host__ __device__ inline bool slot_is_dref(int32_t v) { return v <= -(int32_t)(2 + kRefSpace); }
+__host__ __device__ inline uint32_t slot_did(int32_t v) { return (uint32_t)(-(int64_t)v - 2 - kRefSpace); }
+// dense result heads, dres[d] (uint4, d: the chunk's dedupe table entry; count <= 32, p: the
+// position of the occurrence that was merged, whose full result is at res[2p]):
+//   16-bit ids:  count | id0 << 16, id1 | id2 << 16, id3 | id4 << 16, id5 | id6 << 16
+//                (count > 7: count | id0 << 16, p, -, -)
+//   32-bit ids:  count, id0, id1, id2 (count > 3: count, id0, id1, p)
+// so 99.9% of the shared results (2-3 ids typical, 7 at most for a 32k vocabulary on prose)
+// need no second read.  A reference list entry (rlist) is p or kRlDense | d.
+constexpr uint32_t kRlDense = 0x80000000u;
+constexpr uint32_t kNoDid = 0x7FFFFFFu;    // (27-bit dense result field of a queue entry: none)
+constexpr int kDdExactMax = 7;             // dedupe keys of <= this many bytes are exact (no verification)
 
 // streaming accesses (read or written once per launch) carry the non-temporal hint, so the
 // caches keep the randomly gathered merge results instead
@@ -419,14 +437,17 @@ struct EncArgs {
   uint32_t* bcnt;            // [kNumBuckets * n_tiles] queued chunks per (bucket, tile)
   const int64_t* boff;       // [kNumBuckets * n_tiles] exclusive scan of bcnt (bucket-major)
   const int64_t* q_total;    // queued chunks in all
-  uint64_t* queue;           // dense merge queue, bucket-major: start << 24 | len << 18 | slot
-  uint64_t* dtab;            // chunk dedupe table (dedupe_claim), dmask + 1 slots
+  uint64_t* queue;           // dense merge queue, bucket-major: start << 33 | len << 27 | dense result
+  uint64_t* dtab;            // chunk dedupe table (dedupe_claim), dmask + 1 entries
   uint32_t dmask;
-  uint32_t dfp_mask;         // fingerprint bits in use (all 27 except in collision tests)
+  uint32_t dfp_mask;         // fingerprint bits in use (all 26 except in collision tests)
   uint32_t dedupe;           // 0: every queued chunk runs its own merge loop
+  uint32_t dexact;           // longest exact dedupe key (kDdExactMax, or 0: every key verified)
+  uint4* dres;               // [dmask + 1] dense result heads (slot_dref), by table entry
   unsigned long long* stamps;  // SW_STAMPS builds: cycles per phase, summed
   const uint2* inv;          // [n_inv] merge value -> its pair (a, b); well-formed tables only
   uint32_t n_inv;
+  uint32_t ids16;            // every id fits 16 bits (dres layout)
 };
 
 #ifdef SW_STAMPS
@@ -461,17 +482,25 @@ __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t x, int lane) {
 // ---------------------------------------------------------------------------------------
 // Batch-wide dedupe of queued chunks (in k_classify).  Real text repeats its multi-token words
 // endlessly, and a chunk's encoding depends on its bytes alone, so the merge loop needs to run
-// once per DISTINCT chunk of the launch.  The table (cleared before every launch) maps a
-// chunk's bytes to the position of the first occurrence that claimed it; a slot packs a
-// 27-bit fingerprint, the length and that position.  A fingerprint match is confirmed by
-// comparing the bytes with the claimant's bytes in the (immutable) input, so a hash collision
-// can never change a result, and nothing but the CAS needs cross-XCD coherence.  A chunk that
-// finds no free slot among its 8 candidates is merged on its own.  Returns the position whose
-// result this chunk shares, or -1 if this chunk must be merged (it claimed a slot or found
-// none).  u: the chunk's bytes as zero-padded LE words (n <= kShort).
+// once per DISTINCT chunk of the launch.  The table (cleared before every launch) holds one
+// word per claimed chunk, 8 candidates per chunk in one 64-byte line:
+//   exact keys, chunks of <= 7 bytes:  bytes | length << 56 | 1 << 63
+//   longer chunks:                     26-bit fingerprint << 37 | length << 31 | position
+// The first occurrence claims an entry with a CAS and is merged; its result head lands in
+// dres at the entry's index, which every later occurrence refers to (slot_dref): nothing has to
+// be read back from the claimant.  Exact keys decide equality by themselves; a fingerprint match
+// is confirmed by comparing the bytes with the claimant's bytes in the (immutable) input, so no
+// hash collision can change a result.  A chunk that finds no free candidate merges itself.
+// Only the CAS needs cross-XCD coherence.  u: the chunk's bytes as zero-padded LE words.
 // ---------------------------------------------------------------------------------------
-__device__ __forceinline__ int64_t dedupe_claim(const EncArgs& a, const uint32_t* words, int64_t last_word, int64_t mis,
-                                                int64_t start, int n, const uint32_t (&u)[kShort / 4]) {
+constexpr uint64_t kDdExact = 1ULL << 63;
+struct DdOut {
+  int kind;    // 0: merge on its own (no claim); 1: claimed entry `v`; 2: shares entry `v`'s result
+  uint32_t v;
+};
+
+__device__ __forceinline__ DdOut dedupe_claim(const EncArgs& a, const uint32_t* words, int64_t last_word, int64_t mis,
+                                              int64_t start, int n, const uint32_t (&u)[kShort / 4]) {
   const int nw = (n + 3) >> 2;
   uint32_t h = 0x9E3779B9u ^ ((uint32_t)n << 24);
 #pragma unroll
@@ -482,20 +511,28 @@ __device__ __forceinline__ int64_t dedupe_claim(const EncArgs& a, const uint32_t
     }
   }
   const uint32_t h2 = (h ^ (h >> 16)) * 0x7FEB352Du;
-  const uint64_t tag = (uint64_t)((h2 >> 5) & a.dfp_mask) << 37 | (uint64_t)n << 31;  // fingerprint | length
-  const uint64_t mine = tag | (uint64_t)start;
+  const bool exact = n <= (int)a.dexact;
+  const uint64_t tag = exact ? ((uint64_t)u[0] | ((uint64_t)u[1] << 32) | ((uint64_t)n << 56) | kDdExact)
+                             : ((uint64_t)((h2 >> 6) & a.dfp_mask & 0x3FFFFFFu) << 37 | (uint64_t)n << 31);
+  const uint64_t mine = exact ? tag : (tag | (uint64_t)start);
   const uint32_t grp = h & a.dmask & ~7u;
   for (int j = 0; j < 8; ++j) {
-    unsigned long long* p = (unsigned long long*)a.dtab + (grp | ((h2 + j) & 7u));
-    // a slot changes once (0 -> final), so a cached plain load is safe: a stale 0 only sends
+    const uint32_t idx = grp | ((h2 + j) & 7u);
+    unsigned long long* p = (unsigned long long*)a.dtab + idx;
+    // an entry changes once (0 -> final), so a cached plain load is safe: a stale 0 only sends
     // this lane to the CAS, which returns the live value
     uint64_t cur = *p;
     if (cur == 0) {
       cur = atomicCAS(p, 0ULL, (unsigned long long)mine);
-      if (cur == 0) return -1;  // claimed: this chunk is merged and shared
+      if (cur == 0) return DdOut{1, idx};  // claimed: this chunk is merged and shared
+    }
+    if (exact) {
+      if (cur == mine) return DdOut{2, idx};
+      continue;
     }
     if ((cur & ~0x7FFFFFFFULL) != tag) continue;
     const int64_t other = (int64_t)(cur & 0x7FFFFFFFULL);
+#ifndef SW_ABL_NOVERIFY  // (diagnostic timing builds only: a fingerprint match is taken as equal)
     // compare with the claimant's bytes in the input, realigned
     const int64_t g = other + mis, w0 = g >> 2;
     const uint32_t sh = (uint32_t)(g & 3);
@@ -542,9 +579,11 @@ __device__ __forceinline__ int64_t dedupe_claim(const EncArgs& a, const uint32_t
         }
       }
     }
-    if (same) return other;
+    if (!same) continue;
+#endif
+    return DdOut{2, idx};
   }
-  return -1;
+  return DdOut{0, 0};
 }
 
 // ---------------------------------------------------------------------------------------
@@ -561,7 +600,13 @@ constexpr int kLookRounds = SW_LOOK_ROUNDS;          // lookup rounds in flight 
 constexpr int kQBuf = 64 * (kLookRounds + 1);        // dedupe buffer: one batch + a group of rounds
 constexpr int kWinWords = kWin / 4 + 8;
 
-#ifdef SW_CLS_WAVES_PER_EU  // (A/B builds: cap the VGPRs for this many waves per SIMD)
+// k_classify and k_compact wait on memory most of the time: 6 waves per SIMD (80 VGPRs, a few
+// spilled words) beat 5 unconstrained (81 / 88 VGPRs): 2.81 vs 3.05 ms and 1.15 vs 1.12 ms, net
+// 0.2 ms per launch (profiles/r2_e_ab.txt).  SW_CLS_WAVES_PER_EU=0: no cap (A/B builds).
+#ifndef SW_CLS_WAVES_PER_EU
+#define SW_CLS_WAVES_PER_EU 6
+#endif
+#if SW_CLS_WAVES_PER_EU > 0
 #define SW_CLS_ATTR __attribute__((amdgpu_waves_per_eu(SW_CLS_WAVES_PER_EU, SW_CLS_WAVES_PER_EU)))
 #else
 #define SW_CLS_ATTR
@@ -703,7 +748,7 @@ __device__ __forceinline__ void classify_tile(const EncArgs& a, int64_t tile, ui
       const int ls = act ? s_cstart[k] : 0;
       const int end = (k + 1 < C) ? (int)s_cstart[k + 1] : rel_end;
       const int len = act ? end - ls : 0;
-      int64_t other = -1;
+      DdOut dd{0, 0};
       if (act && a.dedupe && len <= kShort) {
         uint32_t u[kShort / 4];
         window_words(s_b32, ls, min(len, 16), *(uint32_t(*)[4])u);
@@ -711,22 +756,26 @@ __device__ __forceinline__ void classify_tile(const EncArgs& a, int64_t tile, ui
         else
 #pragma unroll
           for (int q = 4; q < kShort / 4; ++q) u[q] = 0;
-        other = dedupe_claim(a, gwords, last_word, mis, t0 + ls, len, u);
+        dd = dedupe_claim(a, gwords, last_word, mis, t0 + ls, len, u);
       }
+      const uint32_t did = dd.kind ? dd.v : kNoDid;
       if (act) {
-        const int64_t op = other >= 0 ? other : t0 + ls;
-        dst[k] = slot_ref(op);
-        a.rlist[t0 + nref + lane] = (uint32_t)op;  // (act lanes are 0 .. n-1: coalesced)
+        const int64_t own = t0 + ls;
+        dst[k] = dd.kind ? slot_dref(did) : slot_ref(own);
+        a.rlist[t0 + nref + lane] = dd.kind ? (kRlDense | did) : (uint32_t)own;  // (act lanes are 0 .. n-1: coalesced)
       }
       nref += (int)__popcll(__ballot(act));
-      const bool queued = act && other < 0;
+      const bool queued = act && dd.kind != 2;
       const int b = queued ? bucket_of(len) : 15;
       uint64_t pend = __ballot(queued);
       // tile-local queue entry (any order; k_scatter routes by length): chunk start in tile
-      // (kTileBits) | chunk index (kTileBits) | length (6 bits, 0 = long)
-      if (queued)
-        a.qtmp[t0 + nown + __popcll(pend & lt_mask)] =
-            (uint32_t)ls | ((uint32_t)k << kTileBits) | ((uint32_t)(len <= kShort ? len : 0) << (2 * kTileBits));
+      // (kTileBits) | chunk index (kTileBits) | length (6 bits, 0 = long); its dense result
+      // (or kNoDid) kTile / 2 entries on (a tile queues at most kTile / 2 chunks of >= 2 bytes)
+      if (queued) {
+        const int64_t qi = t0 + nown + __popcll(pend & lt_mask);
+        a.qtmp[qi] = (uint32_t)ls | ((uint32_t)k << kTileBits) | ((uint32_t)(len <= kShort ? len : 0) << (2 * kTileBits));
+        a.qtmp[qi + kTile / 2] = did;
+      }
       nown += __popcll(pend);
       while (pend) {  // one ballot per bucket present
         const int bb = __shfl(b, __ffsll((long long)pend) - 1, 64);
@@ -799,6 +848,7 @@ __global__ void __launch_bounds__(kThreads) k_scatter(EncArgs a) {
     const uint32_t i = i0 + lane;
     const bool act = i < n;
     const uint32_t e = act ? a.qtmp[t0 + i] : 0u;
+    const uint32_t did = act ? a.qtmp[t0 + kTile / 2 + i] : kNoDid;
     const uint32_t ns = e >> (2 * kTileBits);
     const int b = act ? (ns ? bucket_of(ns) : kLongBucket) : 15;
     int64_t d = 0;
@@ -813,7 +863,7 @@ __global__ void __launch_bounds__(kThreads) k_scatter(EncArgs a) {
     }
     if (act) {
       const uint64_t start = (uint64_t)(t0 + (e & (kTile - 1)));
-      a.queue[d] = (start << 24) | ((uint64_t)ns << 18) | ((e >> kTileBits) & (kTile - 1));
+      a.queue[d] = (start << 33) | ((uint64_t)ns << 27) | did;
     }
   }
 }
@@ -846,8 +896,9 @@ __device__ __forceinline__ void chunk_words(const uint32_t* words, int64_t last_
 template <bool kWide, bool k16, int N>
 __device__ __forceinline__ void merge_entry(const EncArgs& a, const uint32_t* words, int64_t last_word, int64_t mis,
                                             uint64_t e, bool act) {
-  const int64_t start = (int64_t)(e >> 24);
-  const int n = act ? (int)((e >> 18) & 63u) : 0;
+  const int64_t start = (int64_t)(e >> 33);
+  const int n = act ? (int)((e >> 27) & 63u) : 0;
+  const uint32_t did = (uint32_t)e & kNoDid;
   uint32_t u[N / 4];
   chunk_words<N>(words, last_word, start + mis, n, u);
   uint32_t id[N];
@@ -863,16 +914,32 @@ __device__ __forceinline__ void merge_entry(const EncArgs& a, const uint32_t* wo
   if (!act) return;
   uint32_t* dst = a.res + 2 * start;
   int m = 0;
+  // the dense result head (the first 7 ids as 16 bits, or 3 as 32 bits; see dres)
+  uint32_t h0 = 0, h1 = 0, h2 = 0, h3 = 0;
 #pragma unroll
   for (int k = 0; k < N; ++k) {
     if ((alive >> k) & 1u) {
 #ifndef SW_ABL_NOWRITE
       dst[1 + m] = id[k];
 #endif
+      if (k16) {
+        h0 |= m == 0 ? id[k] << 16 : 0u;
+        h1 |= m == 1 ? id[k] : m == 2 ? id[k] << 16 : 0u;
+        h2 |= m == 3 ? id[k] : m == 4 ? id[k] << 16 : 0u;
+        h3 |= m == 5 ? id[k] : m == 6 ? id[k] << 16 : 0u;
+      } else {
+        h1 = m == 0 ? id[k] : h1;
+        h2 = m == 1 ? id[k] : h2;
+        h3 = m == 2 ? id[k] : h3;
+      }
       ++m;
     }
   }
   dst[0] = (uint32_t)m;
+  if (did != kNoDid) {
+    if (k16) a.dres[did] = make_uint4((uint32_t)m | h0, m <= 7 ? h1 : (uint32_t)start, h2, h3);
+    else a.dres[did] = make_uint4((uint32_t)m, h1, h2, m <= 3 ? h3 : (uint32_t)start);
+  }
 }
 
 // ---------------------------------------------------------------------------------------
@@ -1103,7 +1170,7 @@ __global__ void __launch_bounds__(64) k_merge_long_lds(EncArgs a) {
   bucket_range(a, kLongBucket, kLongBucket, &lo, &hi);
   for (int64_t i = lo + blockIdx.x; i < hi; i += gridDim.x) {
     const uint64_t e = a.queue[i];
-    const int64_t start = (int64_t)(e >> 24);
+    const int64_t start = (int64_t)(e >> 33);
     const int64_t len = next_set_bit(a.bits, a.n_words, start + 1, a.n_bytes) - start;
     if (len > kLongLds) continue;  // (k_merge_long)
     for (int j = lane; j < len; j += 64) s_id[lds_pos(j)] = (T)a.bytes[start + j];
@@ -1289,7 +1356,7 @@ __global__ void __launch_bounds__(64) k_merge_long_split(EncArgs a) {
   bucket_range(a, kLongBucket, kLongBucket, &lo, &hi);
   for (int64_t i = lo + blockIdx.x; i < hi; i += gridDim.x) {
     const uint64_t e = a.queue[i];
-    const int64_t start = (int64_t)(e >> 24);
+    const int64_t start = (int64_t)(e >> 33);
     const int len = (int)(next_set_bit(a.bits, a.n_words, start + 1, a.n_bytes) - start);
     if (len > kLongLds) continue;  // (k_merge_long)
     SW_STAMP(18);
@@ -1519,7 +1586,7 @@ __global__ void __launch_bounds__(kThreads) k_merge_long(EncArgs a) {
   bucket_range(a, kLongBucket, kLongBucket, &lo, &hi);
   for (int64_t i = lo + gw; i < hi; i += n_waves) {
     const uint64_t e = a.queue[i];
-    const int64_t start = (int64_t)(e >> 24);
+    const int64_t start = (int64_t)(e >> 33);
     const int64_t end = next_set_bit(a.bits, a.n_words, start + 1, a.n_bytes);
     const int64_t len = end - start;
     if (len <= kLongLds) continue;  // (k_merge_long_lds)
@@ -1636,6 +1703,14 @@ __device__ __forceinline__ uint4 res_head(const uint32_t* res, int64_t p) {
   __builtin_memcpy(&q, res + 2 * p, sizeof(q));
   return q;
 }
+// the head {count, id0, id1, id2 | p} of the result a reference slot names
+// (one load from a selected address: a branch per kind would wait for one load before the other)
+__device__ __forceinline__ uint4 ref_head(const EncArgs& a, int32_t v) {
+  const uint32_t* src = slot_is_dref(v) ? (const uint32_t*)(a.dres + slot_did(v)) : a.res + 2 * slot_pos(v);
+  uint4 q;
+  __builtin_memcpy(&q, src, sizeof(q));
+  return q;
+}
 
 #ifndef SW_ROUNDS_IN_FLIGHT
 #define SW_ROUNDS_IN_FLIGHT 8
@@ -1644,6 +1719,12 @@ __device__ __forceinline__ uint4 res_head(const uint32_t* res, int64_t p) {
 #define SW_TC_ROUNDS 2
 #endif
 constexpr int kRoundsInFlight = SW_ROUNDS_IN_FLIGHT;  // slot rounds whose loads (then gathers) issue together
+
+// id count of the result a reference-list entry names
+__device__ __forceinline__ uint32_t ref_count(const EncArgs& a, uint32_t r) {
+  const uint32_t w = *((r & kRlDense) ? (const uint32_t*)(a.dres + (r & ~kRlDense)) : a.res + 2 * (int64_t)r);
+  return (r & kRlDense) ? (w & 0xFFFFu) : w;
+}
 
 __global__ void __launch_bounds__(kThreads) k_tile_count(EncArgs a) {
   // ids per tile = settled slots + the id counts of the results its references use (the
@@ -1660,7 +1741,7 @@ __global__ void __launch_bounds__(kThreads) k_tile_count(EncArgs a) {
   const int C = (int)a.tile_slots[t], nref = (int)a.tile_nref[t];
   uint32_t c = 0;
 #ifndef SW_NO_PREFETCH
-  c = lane < nref ? a.res[2 * (int64_t)p0] : 0u;
+  c = lane < nref ? ref_count(a, p0) : 0u;
   for (int i0 = 64; i0 < nref; i0 += 64 * SW_TC_ROUNDS) {
 #else
   for (int i0 = 0; i0 < nref; i0 += 64 * SW_TC_ROUNDS) {
@@ -1669,7 +1750,7 @@ __global__ void __launch_bounds__(kThreads) k_tile_count(EncArgs a) {
 #pragma unroll
     for (int u = 0; u < SW_TC_ROUNDS; ++u) p[u] = rl[min(i0 + 64 * u + lane, kTile - 1)];
 #pragma unroll
-    for (int u = 0; u < SW_TC_ROUNDS; ++u) g[u] = (i0 + 64 * u + lane < nref) ? a.res[2 * (int64_t)p[u]] : 0u;
+    for (int u = 0; u < SW_TC_ROUNDS; ++u) g[u] = (i0 + 64 * u + lane < nref) ? ref_count(a, p[u]) : 0u;
 #pragma unroll
     for (int u = 0; u < SW_TC_ROUNDS; ++u) c += g[u];
   }
@@ -1751,12 +1832,12 @@ __global__ void __launch_bounds__(kThreads) SW_CLS_ATTR k_compact(EncArgs a, con
       const bool ref = ((r0 + u) << 6) + lane < C && v[u] < 0;
       const uint64_t mk = __ballot(ref);
       ridx[u] = (uint32_t)(nref + __popcll(mk & lt_mask));
-      if (ref && ridx[u] < (uint32_t)kRefCap) s_rp[ridx[u]] = (uint32_t)slot_pos(v[u]);
+      if (ref && ridx[u] < (uint32_t)kRefCap) s_rp[ridx[u]] = (uint32_t)v[u];
       nref += __popcll(mk);
     }
     wave_sync_mem();
 #ifndef SW_ABL_NOGATHER
-    for (int i = lane; i < min(nref, kRefCap); i += 64) s_rq[i] = res_head(a.res, s_rp[i]);
+    for (int i = lane; i < min(nref, kRefCap); i += 64) s_rq[i] = ref_head(a, (int32_t)s_rp[i]);
 #endif
     wave_sync_mem();
     SW_STAMP(9);
@@ -1769,11 +1850,13 @@ __global__ void __launch_bounds__(kThreads) SW_CLS_ATTR k_compact(EncArgs a, con
       const bool valid = j < C;
       const bool ref = valid && v[u] < 0;
       uint4 q = make_uint4(0, 0, 0, 0);
-      if (ref) q = ridx[u] < (uint32_t)kRefCap ? s_rq[ridx[u]] : res_head(a.res, slot_pos(v[u]));
+      if (ref) q = ridx[u] < (uint32_t)kRefCap ? s_rq[ridx[u]] : ref_head(a, v[u]);
 #ifdef SW_ABL_NOGATHER
       q.x = 2;
 #endif
-      const uint32_t m = ref ? q.x : (valid ? 1u : 0u);
+      const bool dense = ref && slot_is_dref(v[u]);
+      const bool d16 = dense && a.ids16 != 0;
+      const uint32_t m = ref ? (dense ? (q.x & 0xFFFFu) : q.x) : (valid ? 1u : 0u);
       const uint32_t incl = wave_incl_scan(m, lane);
       const uint32_t o = carry + incl - m;
       carry += __shfl(incl, 63, 64);
@@ -1782,15 +1865,27 @@ __global__ void __launch_bounds__(kThreads) SW_CLS_ATTR k_compact(EncArgs a, con
         if (lo < (uint32_t)kOutCapW) s_out[lo] = v[u];
         else dst[o] = v[u];
       }
-      const int64_t p = ref ? slot_pos(v[u]) : 0;
+      // ids from the head while it has them (nh), then from res at the merged occurrence's p
+      const uint32_t nh = d16 ? (m <= 7 ? m : 1u) : dense ? (m <= 3 ? 3u : 2u) : 3u;
+      const int64_t p = !ref ? 0 : d16 ? (int64_t)q.y : dense ? (int64_t)q.w : slot_pos(v[u]);
       if (ref) {
-        const uint32_t hd[3] = {q.y, q.z, q.w};
         const uint32_t mm = m > kLaneCopy ? 3u : m;  // (long results: the head here, the rest below)
-        for (uint32_t k = 0; k < mm; ++k) {
-          const int32_t id = k < 3 ? (int32_t)hd[k] : (int32_t)a.res[2 * p + 1 + k];
-          if (lo + k < (uint32_t)kOutCapW) s_out[lo + k] = id;
-          else dst[o + k] = id;
+        const uint32_t hm = min(mm, nh);
+        auto put = [&](uint32_t k, uint32_t id) {
+          if (lo + k < (uint32_t)kOutCapW) s_out[lo + k] = (int32_t)id;
+          else dst[o + k] = (int32_t)id;
+        };
+        if (d16) {
+          const uint32_t w[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+          for (uint32_t k = 0; k < 7; ++k)
+            if (k < hm) put(k, (w[(k + 1) >> 1] >> (16 * ((k + 1) & 1))) & 0xFFFFu);
+        } else {
+          if (hm > 0) put(0, q.y);
+          if (hm > 1) put(1, q.z);
+          if (hm > 2) put(2, q.w);
         }
+        for (uint32_t k = hm; k < mm; ++k) put(k, a.res[2 * p + 1 + k]);
       }
       // long results (C5: whole 4 KiB chunks): one coalesced copy by the whole wave each
       for (uint64_t lm = __ballot(ref && m > kLaneCopy); lm; lm &= lm - 1) {

@@ -119,7 +119,10 @@ class Tokenizer(BaseTokenizer):
         return (id(self._merges), self._merges.version, tuple(getattr(self, "special_tokens", {}).items()))
 
     def __del__(self):
-        self.close()
+        try:
+            self.close()
+        except (TypeError, AttributeError):  # (interpreter shutdown: module globals already cleared)
+            pass
 
     def close(self):
         h, self._handle = getattr(self, "_handle", None), None

@@ -229,11 +229,13 @@ def test_device_api_with_torch_buffers():
     np.testing.assert_array_equal(d_oo.cpu().numpy(), exp[1])
 
 
-@pytest.mark.parametrize("slots,fp_bits", [(8, 0), (8, 27), (64, 0), (1 << 12, 3), (0, 27)])
-def test_dedupe_table_pressure_and_collisions(slots, fp_bits):
+@pytest.mark.parametrize("slots,fp_bits,exact", [
+    (8, 0, 1), (8, 26, 0), (64, 0, 0), (1 << 12, 3, 1), (0, 26, 1), (0, 2, 0)])
+def test_dedupe_table_pressure_and_collisions(slots, fp_bits, exact):
     """The batch-wide dedupe must never change a result: a table too small for the distinct
-    chunks (fallback: chunks merge on their own) and fingerprints cut to 0..3 bits (every probe
-    decided by the byte comparison alone) give the oracle's ids; so does dedupe switched off."""
+    chunks (fallback: chunks merge on their own), fingerprints cut to 0..3 bits (every probe
+    decided by the byte comparison alone), exact keys on or off give the oracle's ids; so does
+    dedupe switched off."""
     buf, off = corpus.synth(7, corpus.MIXED, 6000, 1074)
     t = tok_for("bl32k.model")
     exp = oracle_encode(t.merges, buf, off, "cl100k")
@@ -241,18 +243,41 @@ def test_dedupe_table_pressure_and_collisions(slots, fp_bits):
     try:
         _lib.check(L.sw_encoder_set_option(h, _lib.SW_OPT_DEDUPE_SLOTS, slots))
         _lib.check(L.sw_encoder_set_option(h, _lib.SW_OPT_DEDUPE_FP_BITS, fp_bits))
+        _lib.check(L.sw_encoder_set_option(h, _lib.SW_OPT_DEDUPE_EXACT, exact))
         assert_same(gpu_encode(t, buf, off), exp)
         _lib.check(L.sw_encoder_set_option(h, _lib.SW_OPT_DEDUPE, 0))
         assert_same(gpu_encode(t, buf, off), exp)
     finally:
         L.sw_encoder_set_option(h, _lib.SW_OPT_DEDUPE, 1)
         L.sw_encoder_set_option(h, _lib.SW_OPT_DEDUPE_SLOTS, 0)
-        L.sw_encoder_set_option(h, _lib.SW_OPT_DEDUPE_FP_BITS, 27)
+        L.sw_encoder_set_option(h, _lib.SW_OPT_DEDUPE_FP_BITS, 26)
+        L.sw_encoder_set_option(h, _lib.SW_OPT_DEDUPE_EXACT, 1)
+
+
+def test_dedupe_exact_key_prefix_collisions():
+    """Chunks equal in their first 7 bytes and length but not after (exact keys up to 7 bytes,
+    fingerprint keys beyond) must stay apart, each sharing only its own result, in a one-group
+    table where they all meet."""
+    rng = np.random.default_rng(11)
+    stems = [" abcdefg", " qwertyu", " zxcvbnm"]
+    words = [st + "".join(chr(0x61 + int(c)) for c in rng.integers(0, 26, size=k))
+             for st in stems for k in (0, 1, 2, 3, 4) for _ in range(6)]
+    texts = ["".join(rng.choice(words, size=40)) for _ in range(300)]
+    buf, off = pack([x.encode() for x in texts])
+    t = tok_for("bl32k.model")
+    exp = oracle_encode(t.merges, buf, off, "cl100k")
+    L, h = _lib.lib(), t._encoder()
+    try:
+        for slots in (8, 0):
+            _lib.check(L.sw_encoder_set_option(h, _lib.SW_OPT_DEDUPE_SLOTS, slots))
+            assert_same(gpu_encode(t, buf, off), exp)
+    finally:
+        L.sw_encoder_set_option(h, _lib.SW_OPT_DEDUPE_SLOTS, 0)
 
 
 def test_dedupe_options_validated():
     t = tok_for("toy500.model")
     L, h = _lib.lib(), t._encoder()
-    for opt, bad in ((_lib.SW_OPT_DEDUPE_SLOTS, 12), (_lib.SW_OPT_DEDUPE_SLOTS, 4), (_lib.SW_OPT_DEDUPE_FP_BITS, 28),
+    for opt, bad in ((_lib.SW_OPT_DEDUPE_SLOTS, 12), (_lib.SW_OPT_DEDUPE_SLOTS, 4), (_lib.SW_OPT_DEDUPE_FP_BITS, 27),
                      (99, 1)):
         assert L.sw_encoder_set_option(h, opt, bad) == _lib.SW_ERR_ARG

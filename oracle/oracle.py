@@ -6,7 +6,7 @@ as the checker (or the timed CPU baseline).  The product (shredword_amd) never i
 import ctypes
 import os
 import subprocess
-from ctypes import POINTER, c_int, c_int32, c_int64, c_uint8, c_void_p
+from ctypes import POINTER, c_float, c_int, c_int32, c_int64, c_uint8, c_uint64, c_void_p
 
 import numpy as np
 
@@ -46,6 +46,12 @@ def lib():
         L.orc_encode_with_specials.restype = c_int64
         L.orc_encode_with_specials.argtypes = [c_void_p, POINTER(c_uint8), c_int64, c_int, POINTER(c_uint8),
                                                POINTER(c_int64), POINTER(c_int32), c_int64, POINTER(c_int32)]
+        L.orc_train_words.restype = c_int64
+        L.orc_train_words.argtypes = [POINTER(c_uint8), c_int64, c_int32, c_float, POINTER(c_uint8),
+                                      POINTER(c_int64), POINTER(c_int64), POINTER(c_uint64), c_int64]
+        L.orc_train.restype = c_int64
+        L.orc_train.argtypes = [POINTER(c_uint8), c_int64, c_int64, c_int32, c_float, c_uint64,
+                                POINTER(c_int32), c_int64, POINTER(c_uint64)]
         _lib = L
     return _lib
 
@@ -133,3 +139,34 @@ def presplit(data, pattern=PAT_CL100K):
 
 def ucd_class(cp):
     return lib().orc_ucd_class(cp)
+
+
+def train(text, target_vocab_size, unk_id=0, character_coverage=0.995, min_pair_freq=2000):
+    """The reference BPE trainer restated (sw_train_oracle.c): (merges [m, 3] int32 rows
+    (a, b, new_id), final token frequencies [256 + m] uint64)."""
+    buf = np.frombuffer(bytes(text), dtype=np.uint8) if not isinstance(text, np.ndarray) else text
+    if len(buf) == 0:
+        buf = np.zeros(1, np.uint8)[:0]
+    cap = max(int(target_vocab_size) - 256, 0)
+    rows = np.zeros((max(cap, 1), 3), np.int32)
+    freq = np.zeros(256 + max(cap, 1), np.uint64)
+    src = buf if len(buf) else np.zeros(1, np.uint8)
+    m = lib().orc_train(_p(np.ascontiguousarray(src), c_uint8), len(buf), int(target_vocab_size), int(unk_id),
+                        float(character_coverage), int(min_pair_freq), _p(rows, c_int32), cap, _p(freq, c_uint64))
+    if m < 0:
+        raise ValueError("orc_train failed (%d)" % m)
+    return rows[:m].copy(), freq[:256 + m].copy()
+
+
+def train_words(text, unk_id=0, character_coverage=0.995):
+    """Distinct words in the reference's order: (offsets, lengths, counts, kept-char mask)."""
+    buf = np.frombuffer(bytes(text), dtype=np.uint8)
+    cap = len(buf) // 2 + 16
+    off, ln, cnt = np.zeros(cap, np.int64), np.zeros(cap, np.int64), np.zeros(cap, np.uint64)
+    keep = np.zeros(256, np.uint8)
+    src = buf if len(buf) else np.zeros(1, np.uint8)
+    n = lib().orc_train_words(_p(np.ascontiguousarray(src), c_uint8), len(buf), int(unk_id), float(character_coverage),
+                              _p(keep, c_uint8), _p(off, c_int64), _p(ln, c_int64), _p(cnt, c_uint64), cap)
+    if n < 0:
+        raise ValueError("orc_train_words failed (%d)" % n)
+    return off[:n].copy(), ln[:n].copy(), cnt[:n].copy(), keep

@@ -8,7 +8,8 @@
 from .base import (BaseTokenizer, CL100K_PATTERN, GPT2_PATTERN, apply_regex, build_vocab, get_stats, merge,
                    render_token, replace_control_characters)
 from .tokenizer import Tokenizer
+from .trainer import BPETrainer
 
 __version__ = "0.1.0"
-__all__ = ["BaseTokenizer", "Tokenizer", "apply_regex", "build_vocab", "get_stats", "merge", "render_token",
+__all__ = ["BaseTokenizer", "BPETrainer", "Tokenizer", "apply_regex", "build_vocab", "get_stats", "merge", "render_token",
            "replace_control_characters", "CL100K_PATTERN", "GPT2_PATTERN"]

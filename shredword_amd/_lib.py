@@ -1,4 +1,4 @@
-"""ctypes binding of the C-ABI in include/shredword_hip.h.
+"""ctypes binding of the C-ABI in include/shredword_hip.h and include/shredword_train.h.
 
 Follows the reference's native-binding pattern (`shredword/cbase.py:5-59`): search the package
 directory for the built library, `ctypes.CDLL` it, declare argtypes/restype per function, and map
@@ -12,7 +12,8 @@ differences from the reference:
 import ctypes
 import os
 import sysconfig
-from ctypes import POINTER, Structure, c_char_p, c_double, c_int32, c_int64, c_uint8, c_uint64, c_void_p
+from ctypes import (POINTER, Structure, c_char_p, c_double, c_float, c_int32, c_int64, c_size_t, c_uint8, c_uint64,
+                    c_void_p)
 
 LIB_NAMES = ("libshredword_hip",)
 
@@ -32,6 +33,12 @@ class SwStats(Structure):
     _fields_ = [("n_bytes", c_int64), ("n_chunks", c_int64), ("n_tokens", c_int64),
                 ("ms_presplit", c_double), ("ms_h2d", c_double), ("ms_kernels", c_double),
                 ("ms_d2h", c_double), ("ms_total", c_double)]
+
+
+class TrainConfig(Structure):
+    """sw_train_config: field for field the reference's BPEConfig (bpe.h:43-48, cbase.py:40)."""
+    _fields_ = [("target_vocab_size", c_size_t), ("unk_id", c_int32), ("character_coverage", c_float),
+                ("min_pair_freq", c_uint64)]
 
 
 class ShredwordError(RuntimeError):
@@ -94,6 +101,16 @@ _SIGNATURES = {
                                    c_void_p, POINTER(c_int64)]),
     "sw_synth_corpus": (c_int64, [c_uint64, c_int32, c_int64, c_int64, POINTER(c_uint8), c_int64,
                                   POINTER(c_int64), c_int32]),
+    # trainer (include/shredword_train.h)
+    "sw_trainer_create": (c_int32, [POINTER(TrainConfig), c_int32, POINTER(c_void_p)]),
+    "sw_trainer_destroy": (None, [c_void_p]),
+    "sw_trainer_load_corpus": (c_int32, [c_void_p, c_char_p]),
+    "sw_trainer_load_text": (c_int32, [c_void_p, POINTER(c_uint8), c_int64]),
+    "sw_trainer_train": (c_int64, [c_void_p]),
+    "sw_trainer_merges": (c_int64, [c_void_p, POINTER(c_int32), c_int64]),
+    "sw_trainer_token_freq": (c_int64, [c_void_p, POINTER(c_uint64), c_int64]),
+    "sw_trainer_save": (c_int32, [c_void_p, c_char_p, c_char_p]),
+    "sw_trainer_stats": (c_int32, [c_void_p, POINTER(c_double)]),
 }
 
 

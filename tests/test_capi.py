@@ -1,5 +1,5 @@
-"""The C-ABI library loads and exports every symbol include/shredword_hip.h declares.  No compute
-calls without a GPU, except the host-only entry points."""
+"""The C-ABI library loads and exports every symbol include/*.h declares.  No compute calls
+without a GPU, except the host-only entry points."""
 import ctypes
 import os
 import re
@@ -11,9 +11,12 @@ from conftest import ROOT
 
 
 def declared_functions():
-    text = open(os.path.join(ROOT, "include", "shredword_hip.h")).read()
-    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
-    return sorted(set(re.findall(r"\b(sw_[a-z0-9_]+)\s*\(", text)))
+    names = set()
+    for h in sorted(os.listdir(os.path.join(ROOT, "include"))):
+        text = open(os.path.join(ROOT, "include", h)).read()
+        text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+        names |= set(re.findall(r"\b(sw_[a-z0-9_]+)\s*\(", text))
+    return sorted(names)
 
 
 def test_header_symbols_exported():
@@ -41,6 +44,9 @@ def test_errors_are_status_codes_not_exit():
     assert L.sw_synth_corpus(1, 99, 10, 10, None, 0, None, 1) == _lib.SW_ERR_ARG
     assert L.sw_decoder_create(None, None, None, -1, 0, ctypes.byref(h)) == _lib.SW_ERR_ARG
     assert L.sw_decode_batch(None, None, None, 0, None, 0, None) == _lib.SW_ERR_ARG
+    assert L.sw_trainer_create(None, 0, ctypes.byref(h)) == _lib.SW_ERR_ARG
+    assert L.sw_trainer_train(None) == _lib.SW_ERR_ARG
+    assert L.sw_trainer_save(None, None, None) == _lib.SW_ERR_ARG
 
 
 def test_no_device_fails_loudly():
@@ -52,3 +58,5 @@ def test_no_device_fails_loudly():
     t.merges = {(104, 105): 256}
     with pytest.raises(_lib.ShredwordError):
         t.encode("hi")
+    with pytest.raises(_lib.ShredwordError):
+        sa.BPETrainer(target_vocab_size=300)

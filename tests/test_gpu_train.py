@@ -1,0 +1,75 @@
+"""GPU trainer (include/shredword_train.h) against the trainer oracle and the reference trainer's
+own outputs (tests/golden/train_*): merges and final token frequencies, bit for bit."""
+import json
+import os
+
+import numpy as np
+import pytest
+
+import oracle
+import shredword_amd as sa
+from test_train_oracle import INDEX, golden, recipe_text
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("entry", INDEX, ids=[e["name"] for e in INDEX])
+def test_gpu_trainer_matches_reference(entry):
+    text = recipe_text(entry["corpus"])
+    target, unk, cov, minf = entry["config"]
+    t = sa.BPETrainer(target, unk, cov, minf)
+    t.load_text(text)
+    assert t.train() == entry["merges"]
+    rows, freq = golden(entry["name"])
+    np.testing.assert_array_equal(t.merges, rows)
+    np.testing.assert_array_equal(t.token_freq, freq)
+    st = t.stats
+    assert st["merges"] == entry["merges"] and st["symbols"] > 0
+    t.destroy()
+
+
+@pytest.mark.parametrize("seed", [1, 2, 3])
+def test_gpu_trainer_matches_oracle_random(seed):
+    """Small random corpora over a tiny alphabet (many ties, runs, unk characters)."""
+    rng = np.random.default_rng(seed)
+    alphabet = np.frombuffer(b"aabbbcdde\xc3\xa9xy", dtype=np.uint8)
+    words = [bytes(rng.choice(alphabet, size=int(rng.integers(1, 12)))) for _ in range(400)]
+    text = b" ".join(words[int(i)] for i in rng.integers(0, len(words), size=5000))
+    cfg = (256 + 300, int(rng.integers(0, 3)), 0.9, 2)
+    exp_rows, exp_freq = oracle.train(text, *cfg)
+    t = sa.BPETrainer(*cfg)
+    t.load_text(text)
+    assert t.train() == len(exp_rows)
+    np.testing.assert_array_equal(t.merges, exp_rows)
+    np.testing.assert_array_equal(t.token_freq, exp_freq)
+
+
+def test_gpu_trainer_edges_and_save(tmp_path):
+    t = sa.BPETrainer(300, 0, 0.995, 2)
+    t.load_text(b"")
+    assert t.train() == 0
+    t.load_text(b"ab ab ab cd")
+    assert t.train() == 1
+    assert t.merges.tolist() == [[97, 98, 256]]
+    with pytest.raises(sa._lib.ShredwordError):
+        t.load_text(b"a\0b")
+    with pytest.raises(IOError):
+        t.load_corpus(str(tmp_path / "missing.txt"))
+    # file round trip: the same corpus from a file, saved model rows and vocab lines
+    text = recipe_text(INDEX[3]["corpus"])
+    p = tmp_path / "c.txt"
+    p.write_bytes(text)
+    target, unk, cov, minf = INDEX[3]["config"]
+    t2 = sa.BPETrainer(target, unk, cov, minf)
+    t2.load_corpus(str(p))
+    n = t2.train()
+    t2.save(str(tmp_path / "m.bin"), str(tmp_path / "v.txt"))
+    rows = np.frombuffer((tmp_path / "m.bin").read_bytes(), dtype="<i4").reshape(-1, 3)
+    np.testing.assert_array_equal(rows, golden(INDEX[3]["name"])[0])
+    raw = (tmp_path / "v.txt").read_bytes()
+    assert raw.count(b"\n") == 256 + n + 1  # one line per id, plus the token "\n" itself
+    assert raw.endswith(b" %d\n" % int(t2.token_freq[-1]))
+    # the trained merges encode through the GPU encoder like the oracle's encode does
+    tok = t2.tokenizer()
+    ids = tok.encode("aab ab ba xyz")
+    assert tok.decode(ids) == "aab ab ba xyz"

@@ -600,9 +600,10 @@ constexpr int kLookRounds = SW_LOOK_ROUNDS;          // lookup rounds in flight 
 constexpr int kQBuf = 64 * (kLookRounds + 1);        // dedupe buffer: one batch + a group of rounds
 constexpr int kWinWords = kWin / 4 + 8;
 
-// k_classify and k_compact wait on memory most of the time: 6 waves per SIMD (80 VGPRs, a few
-// spilled words) beat 5 unconstrained (81 / 88 VGPRs): 2.81 vs 3.05 ms and 1.15 vs 1.12 ms, net
-// 0.2 ms per launch (profiles/r2_e_ab.txt).  SW_CLS_WAVES_PER_EU=0: no cap (A/B builds).
+// k_classify waits on memory most of the time: 6 waves per SIMD (80 VGPRs, 12 spilled bytes
+// per lane) beat the compiler's 5 (81 VGPRs): 2.81 vs 3.05 ms (profiles/r2_e_ab.txt).  k_compact
+// stays at 5 (88 VGPRs): capped at 6 it spills 24 B per lane, +0.9 GB of writes, and is not
+// faster (1.15 vs 1.12 ms).  SW_CLS_WAVES_PER_EU=0: no cap (A/B builds).
 #ifndef SW_CLS_WAVES_PER_EU
 #define SW_CLS_WAVES_PER_EU 6
 #endif
@@ -1763,7 +1764,7 @@ constexpr int kRefCap = 128;    // references per 8-round group gathered through
 constexpr int kOutCapW = 1024;  // ids per group staged in LDS (the rest are stored directly)
 constexpr uint32_t kLaneCopy = 64;  // results longer than this are copied by the whole wave
 
-__global__ void __launch_bounds__(kThreads) SW_CLS_ATTR k_compact(EncArgs a, const int64_t* tile_base, int32_t* out) {
+__global__ void __launch_bounds__(kThreads) k_compact(EncArgs a, const int64_t* tile_base, int32_t* out) {
   // per wave: the group's references, gathered with full lanes before any store (a store
   // ahead of a load in the wave's vmcnt order would make the load wait for it)
   __shared__ uint32_t s_rp_all[kWaves][kRefCap];

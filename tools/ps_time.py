@@ -12,8 +12,9 @@ import torch  # noqa: E402
 from shredword_amd import Tokenizer, _lib, corpus  # noqa: E402
 
 pat = {"cl100k": 0, "gpt2": 1, "none": 2}[sys.argv[1] if len(sys.argv) > 1 else "cl100k"]
-kind = corpus.MIXED if (len(sys.argv) <= 2 or sys.argv[2] == "mixed") else corpus.STRESS
-buf, off = corpus.synth(1_000_003, kind, 1_000_000, 1074 if kind == corpus.MIXED else 600, n_threads=16)
+kname = sys.argv[2] if len(sys.argv) > 2 else "mixed"
+kind = {"mixed": corpus.MIXED, "stress": corpus.STRESS, "ascii": corpus.ASCII}[kname]
+buf, off = corpus.synth(1_000_003, kind, 1_000_000, 600 if kind == corpus.STRESS else 1074, n_threads=16)
 n = int(off[-1])
 dev = torch.device("cuda", 0)
 tok = Tokenizer(device=0)
@@ -45,5 +46,5 @@ if os.environ.get("SHREDWORD_HIP_LIB") is None:
     exp, _ = corpus.presplit(buf[:50_000_000], off[:int(off.searchsorted(50_000_000, 'right'))], pat)
     got = d_bits.cpu().numpy().view("uint64")
     ok = " parity(first 50MB)=%s" % bool((got[:len(exp) - 1] == exp[:-1]).all())
-print("%s: %.3f ms per presplit (incl. bitmap clear), %.1f GB/s%s" % (
-    os.path.basename(os.environ.get("SHREDWORD_HIP_LIB", "default")), ms, n / ms / 1e6, ok), flush=True)
+print("%s %s: %.3f ms per presplit (incl. bitmap clear), %.1f GB/s%s" % (
+    os.path.basename(os.environ.get("SHREDWORD_HIP_LIB", "default")), kname, ms, n / ms / 1e6, ok), flush=True)

@@ -5,7 +5,7 @@ set -u
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 OUT=$R/gpurun_out/ps_pmc; mkdir -p "$OUT"
 export TMPDIR=/tmp
-CNT="SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_VALU"
+CNT="SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVES SQ_WAIT_INST_ANY SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_INSTS_VMEM_RD"
 for lib in default "$@"; do
   if [ "$lib" = default ]; then unset SHREDWORD_HIP_LIB; else export SHREDWORD_HIP_LIB=$R/shredword_amd/$lib; fi
   cd /tmp && timeout -s KILL 120 rocprofv3 --pmc $CNT -d "$OUT/$lib" -o run --output-format csv -- python3 "$R/tools/ps_time.py" > "$OUT/$lib.log" 2>&1

@@ -19,6 +19,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <array>
 #include <chrono>
 #include <cstdint>
 #include <cstdio>
@@ -383,48 +384,77 @@ int32_t load_words(sw_trainer* t, const uint8_t* text, int64_t n) {
     for (auto& x : th) x.join();
   };
   run(count_range);
-  // merge by hash partition: partition p gathers every range's words with hash % T == p
+  // merge by hash partition: every range scatters its words by hash % T (in range order, so the
+  // smallest offset of a word arrives first), then partition p merges its share
+  struct Item {
+    uint64_t h;
+    int64_t off, len;
+    uint64_t cnt;
+  };
+  std::vector<std::vector<std::vector<Item>>> out((size_t)T, std::vector<std::vector<Item>>((size_t)T));
+  run([&](int k) {
+    for (const auto& x : local[k].e)
+      if (x.off >= 0) out[k][(size_t)((x.h >> 40) % (uint64_t)T)].push_back(Item{x.h, x.off, x.len, x.cnt});
+    std::vector<WordTable::E>().swap(local[k].e);
+  });
   std::vector<WordTable> part;
   part.reserve(T);
-  for (int p = 0; p < T; ++p) part.emplace_back(local[0].n / T + 16);
-  run([&](int p) {
-    for (int k = 0; k < T; ++k)  // (ranges in order: the smallest offset arrives first)
-      for (const auto& x : local[k].e)
-        if (x.off >= 0 && (int)((x.h >> 40) % (uint64_t)T) == p) part[p].add(text, x.h, x.off, x.len, x.cnt);
-  });
-  std::vector<std::string_view> words;
-  std::vector<uint64_t> counts;
-  std::vector<int64_t> first;
-  for (int p = 0; p < T; ++p)
-    for (const auto& x : part[p].e)
-      if (x.off >= 0) {
-        words.emplace_back((const char*)text + x.off, (size_t)x.len);
-        counts.push_back(x.cnt);
-        first.push_back(x.off);
-      }
-  // StrMap iteration order (hash.cpp:29-53, 61-72): djb2 & 4095, first occurrence within a bucket
-  std::vector<uint32_t> bucket(words.size());
-  for (size_t k = 0; k < words.size(); ++k) {
-    uint64_t h = 5381;
-    for (unsigned char c : words[k]) h = (h << 5) + h + c;
-    bucket[k] = (uint32_t)(h & 4095u);
+  for (int p = 0; p < T; ++p) {
+    size_t m = 16;
+    for (int k = 0; k < T; ++k) m += out[k][p].size();
+    part.emplace_back(m);
   }
+  run([&](int p) {
+    for (int k = 0; k < T; ++k)
+      for (const Item& x : out[k][p]) part[p].add(text, x.h, x.off, x.len, x.cnt);
+  });
+  std::vector<int64_t> pbase(T + 1, 0);
+  for (int p = 0; p < T; ++p) pbase[p + 1] = pbase[p] + (int64_t)part[p].n;
+  const int64_t nw = pbase[T];
+  std::vector<int64_t> woff0((size_t)nw), wlen0((size_t)nw), first((size_t)nw);
+  std::vector<uint64_t> counts((size_t)nw);
+  std::vector<uint32_t> bucket((size_t)nw);
+  std::vector<std::array<uint64_t, 256>> chs((size_t)T);
+  // StrMap iteration order (hash.cpp:29-53, 61-72) needs djb2 & 4095 of every word; the
+  // character histogram (histogram.cpp:30-36) counts the chars of every distinct word once
+  run([&](int p) {
+    auto& ch = chs[(size_t)p];
+    ch.fill(0);
+    int64_t k = pbase[p];
+    for (const auto& x : part[p].e) {
+      if (x.off < 0) continue;
+      const uint8_t* w = text + x.off;
+      uint64_t h = 5381;
+      for (int64_t q = 0; q < x.len; ++q) {
+        h = (h << 5) + h + w[q];
+        ch[w[q]]++;
+      }
+      woff0[(size_t)k] = x.off;
+      wlen0[(size_t)k] = x.len;
+      first[(size_t)k] = x.off;
+      counts[(size_t)k] = x.cnt;
+      bucket[(size_t)k] = (uint32_t)(h & 4095u);
+      ++k;
+    }
+  });
   // (counting sort by bucket, then each bucket's few words by first offset)
-  std::vector<int64_t> start(4097, 0), order(words.size());
+  std::vector<int64_t> start(4097, 0), order((size_t)nw);
   for (uint32_t b : bucket) start[b + 1]++;
   for (int b = 0; b < 4096; ++b) start[b + 1] += start[b];
   {
     std::vector<int64_t> fill(start.begin(), start.end() - 1);
-    for (size_t k = 0; k < words.size(); ++k) order[(size_t)fill[bucket[k]]++] = (int64_t)k;
+    for (int64_t k = 0; k < nw; ++k) order[(size_t)fill[bucket[(size_t)k]]++] = k;
   }
-  for (int b = 0; b < 4096; ++b)
-    std::sort(order.begin() + start[b], order.begin() + start[b + 1],
-              [&](int64_t x, int64_t y) { return first[x] < first[y]; });
-  // character coverage (histogram.cpp:30-53, bpe.cpp:256-279): per distinct word, chars in
-  // StrMap order ((c + 165) & 255), stable by count, the first (size_t)(n * coverage) kept
+  run([&](int p) {
+    for (int b = p; b < 4096; b += T)
+      std::sort(order.begin() + start[b], order.begin() + start[b + 1],
+                [&](int64_t x, int64_t y) { return first[(size_t)x] < first[(size_t)y]; });
+  });
+  // character coverage (bpe.cpp:256-279): chars in StrMap order ((c + 165) & 255), stable by
+  // count, the first (size_t)(n * coverage) kept
   uint64_t ch[256] = {0};
-  for (const auto& w : words)
-    for (unsigned char c : w) ch[c]++;
+  for (const auto& a : chs)
+    for (int c = 0; c < 256; ++c) ch[c] += a[(size_t)c];
   std::vector<int> chars;
   for (int b = 0; b < 256; ++b) {
     const int c = (b + 91) & 255;
@@ -434,18 +464,30 @@ int32_t load_words(sw_trainer* t, const uint8_t* text, int64_t n) {
   float cov = t->cfg.character_coverage;
   if (!(cov > 0.0f && cov < 1.0f)) cov = 0.995f;
   const size_t keep = (size_t)((float)chars.size() * cov);
-  bool kept[256] = {false};
-  for (size_t k = 0; k < keep && k < chars.size(); ++k) kept[chars[k]] = true;
-  // symbols
-  t->ids.clear(); t->woff.clear(); t->wlen.clear(); t->wcnt.clear();
-  t->woff.reserve(words.size()); t->wlen.reserve(words.size()); t->wcnt.reserve(words.size());
-  for (int64_t k : order) {
-    const auto& w = words[(size_t)k];
-    t->woff.push_back((int64_t)t->ids.size());
-    t->wlen.push_back((int32_t)w.size());
-    t->wcnt.push_back(counts[(size_t)k]);
-    for (unsigned char c : w) t->ids.push_back(kept[c] ? (int32_t)c : t->cfg.unk_id);
+  int32_t map[256];
+  for (int c = 0; c < 256; ++c) map[c] = t->cfg.unk_id;
+  for (size_t k = 0; k < keep && k < chars.size(); ++k) map[chars[k]] = chars[k];
+  // symbols, words in corpus order (filled by the threads)
+  t->woff.assign((size_t)nw, 0);
+  t->wlen.assign((size_t)nw, 0);
+  t->wcnt.assign((size_t)nw, 0);
+  int64_t total = 0;
+  for (int64_t r = 0; r < nw; ++r) {
+    const int64_t k = order[(size_t)r];
+    t->woff[(size_t)r] = total;
+    t->wlen[(size_t)r] = (int32_t)wlen0[(size_t)k];
+    t->wcnt[(size_t)r] = counts[(size_t)k];
+    total += wlen0[(size_t)k];
   }
+  t->ids.assign((size_t)total, 0);
+  run([&](int p) {
+    for (int64_t r = nw * p / T, e = nw * (p + 1) / T; r < e; ++r) {
+      const int64_t k = order[(size_t)r];
+      const uint8_t* w = text + woff0[(size_t)k];
+      int32_t* d = t->ids.data() + t->woff[(size_t)r];
+      for (int64_t q = 0; q < wlen0[(size_t)k]; ++q) d[q] = map[w[q]];
+    }
+  });
   t->loaded = true;
   t->merges.clear();
   t->tok_freq.clear();

@@ -112,11 +112,25 @@ __device__ __forceinline__ uint64_t phash(int32_t f, int32_t s) {
 // to right; each replaced pair's left neighbour (already rewritten) and right neighbour (not
 // yet) move their frequency to the pairs with X.  A change's `first` is its call's rank in the
 // reference's freq_change_add order: 4 * (word start) + call index within the word.
-__global__ void k_merge_words(int32_t* ids, const int64_t* woff, int32_t* len, const uint64_t* wcnt, int64_t nw,
-                              int32_t A, int32_t B, int32_t X, Slot* tab, uint64_t mask, uint32_t* used,
+__device__ __forceinline__ uint64_t sym_bit(int32_t id) { return 1ULL << ((uint32_t)id & 63u); }
+
+// per word: a 64-bit filter of the symbol ids it holds (bit id % 64); a merge reads only the
+// filters of the words that cannot hold its pair, ~5 B per symbol less
+__global__ void k_bloom_init(const int32_t* ids, const int64_t* woff, const int32_t* len, int64_t nw, uint64_t* bloom) {
+  const int64_t w = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (w >= nw) return;
+  uint64_t f = 0;
+  for (int k = 0, L = len[w]; k < L; ++k) f |= sym_bit(ids[woff[w] + k]);
+  bloom[w] = f;
+}
+
+__global__ void k_merge_words(int32_t* ids, const int64_t* woff, int32_t* len, const uint64_t* wcnt, uint64_t* bloom,
+                              int64_t nw, int32_t A, int32_t B, int32_t X, Slot* tab, uint64_t mask, uint32_t* used,
                               unsigned long long* n_used) {
   const int64_t w = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (w >= nw) return;
+  const uint64_t need = sym_bit(A) | sym_bit(B);
+  if ((bloom[w] & need) != need) return;
   const int64_t base = woff[w];
   int32_t* s = ids + base;
   const int L = len[w];
@@ -148,6 +162,9 @@ __global__ void k_merge_words(int32_t* ids, const int64_t* woff, int32_t* len, c
     }
   }
   len[w] = o;
+  uint64_t f = 0;
+  for (int k = 0; k < o; ++k) f |= sym_bit(s[k]);
+  bloom[w] = f;
 }
 
 // the table's claimed slots, densely (the first `hcap` also into host-mapped memory, with the
@@ -219,6 +236,51 @@ struct PairInfo {
   uint32_t version = 0;
 };
 
+// pair -> PairInfo, open addressing (the BIMap's role, hash.cpp:104-130; its iteration order
+// only matters for the heap seed, which is sorted explicitly)
+class PairMap {
+ public:
+  explicit PairMap(size_t n) { rehash(n); }
+  PairInfo& operator[](uint64_t key) {  // get or create (freq 0, version 0)
+    if (2 * (n_ + 1) > keys_.size()) rehash(keys_.size());
+    size_t i = slot(key);
+    if (keys_[i] != key) {
+      keys_[i] = key;
+      vals_[i] = PairInfo{};
+      ++n_;
+    }
+    return vals_[i];
+  }
+
+ private:
+  static uint64_t mix(uint64_t x) {
+    x ^= x >> 33;
+    x *= 0xff51afd7ed558ccdULL;
+    return x ^ (x >> 33);
+  }
+  size_t slot(uint64_t key) const {
+    size_t i = (size_t)mix(key) & (keys_.size() - 1);
+    while (keys_[i] != key && keys_[i] != kEmpty) i = (i + 1) & (keys_.size() - 1);
+    return i;
+  }
+  void rehash(size_t n) {
+    size_t cap = 1024;
+    while (cap < 2 * n) cap <<= 1;
+    std::vector<uint64_t> ok;
+    std::vector<PairInfo> ov;
+    ok.swap(keys_);
+    ov.swap(vals_);
+    keys_.assign(cap, kEmpty);
+    vals_.assign(cap, PairInfo{});
+    n_ = 0;
+    for (size_t i = 0; i < ok.size(); ++i)
+      if (ok[i] != kEmpty) (*this)[ok[i]] = ov[i];
+  }
+  std::vector<uint64_t> keys_;
+  std::vector<PairInfo> vals_;
+  size_t n_ = 0;
+};
+
 inline uint64_t pkey(int32_t a, int32_t b) { return ((uint64_t)(uint32_t)a << 32) | (uint32_t)b; }
 
 // BIMap bucket (hash.cpp:7-16, 109-110): FNV-1a over the 8-byte PairKey, 4096 buckets
@@ -263,6 +325,7 @@ struct sw_trainer {
   int64_t* d_woff = nullptr;
   int32_t* d_len = nullptr;
   uint64_t* d_wcnt = nullptr;
+  uint64_t* d_bloom = nullptr;        // per word: symbol-id filter (k_bloom_init)
   Slot* d_tab = nullptr;
   Slot* d_out = nullptr;
   uint32_t* d_used = nullptr;
@@ -282,6 +345,8 @@ constexpr int64_t kPinnedRecords = 4096;  // change records fetched with the cou
 
 void free_device(sw_trainer* t) {
   (void)hipFree(t->d_ids); (void)hipFree(t->d_woff); (void)hipFree(t->d_len); (void)hipFree(t->d_wcnt);
+  (void)hipFree(t->d_bloom);
+  t->d_bloom = nullptr;
   (void)hipFree(t->d_tab); (void)hipFree(t->d_out); (void)hipFree(t->d_used); (void)hipFree(t->d_nused);
   (void)hipHostFree(t->h_out); (void)hipHostFree(t->h_nused);
   t->d_ids = nullptr; t->d_woff = nullptr; t->d_len = nullptr; t->d_wcnt = nullptr; t->d_tab = nullptr;
@@ -530,6 +595,7 @@ int64_t train(sw_trainer* t) {
   SW_HIP_TRY(hipMalloc(&t->d_woff, sizeof(int64_t) * std::max<int64_t>(nw, 1)));
   SW_HIP_TRY(hipMalloc(&t->d_len, sizeof(int32_t) * std::max<int64_t>(nw, 1)));
   SW_HIP_TRY(hipMalloc(&t->d_wcnt, sizeof(uint64_t) * std::max<int64_t>(nw, 1)));
+  SW_HIP_TRY(hipMalloc(&t->d_bloom, sizeof(uint64_t) * std::max<int64_t>(nw, 1)));
   SW_HIP_TRY(hipMalloc(&t->d_tab, sizeof(Slot) * cap));
   SW_HIP_TRY(hipMalloc(&t->d_out, sizeof(Slot) * std::max<int64_t>(t->out_cap, kPinnedRecords)));
   SW_HIP_TRY(hipMalloc(&t->d_used, sizeof(uint32_t) * t->out_cap));
@@ -554,12 +620,13 @@ int64_t train(sw_trainer* t) {
   // pair histogram on the device, heap seeded in BIMap order (bpe.cpp:357-366)
   const auto t_cnt = clk::now();
   const unsigned grid = (unsigned)std::max<int64_t>((nw + kBlock - 1) / kBlock, 1);
+  if (nw) hipLaunchKernelGGL(k_bloom_init, dim3(grid), dim3(kBlock), 0, t->st, t->d_ids, t->d_woff, t->d_len, nw,
+                             t->d_bloom);
   if (nw) hipLaunchKernelGGL(k_count_pairs, dim3(grid), dim3(kBlock), 0, t->st, t->d_ids, t->d_woff, t->d_len, t->d_wcnt,
                              nw, t->cfg.unk_id, t->d_tab, t->tab_mask, t->d_used, t->d_nused + (t->pass & 1));
   std::vector<Slot> rec;
   if (int32_t rc = collect(t, &rec)) return rc;
-  std::unordered_map<uint64_t, PairInfo> info;
-  info.reserve(rec.size() * 2 + 1024);
+  PairMap info(rec.size() * 2 + 1024);
   struct Seed { uint32_t bucket; uint64_t first; int32_t a, b; uint64_t freq; };
   std::vector<Seed> seeds;
   seeds.reserve(rec.size());
@@ -589,7 +656,8 @@ int64_t train(sw_trainer* t) {
     if (pi.freq < min_freq) continue;
     const int32_t A = top.a, B = top.b, X = (int32_t)(256 + nm);
     const auto t0 = clk::now();
-    hipLaunchKernelGGL(k_merge_words, dim3(grid), dim3(kBlock), 0, t->st, t->d_ids, t->d_woff, t->d_len, t->d_wcnt, nw,
+    hipLaunchKernelGGL(k_merge_words, dim3(grid), dim3(kBlock), 0, t->st, t->d_ids, t->d_woff, t->d_len, t->d_wcnt,
+                       t->d_bloom, nw,
                        A, B, X, t->d_tab, t->tab_mask, t->d_used, t->d_nused + (t->pass & 1));
     if (int32_t rc = collect(t, &rec)) return rc;
     const auto t1 = clk::now();

@@ -73,3 +73,21 @@ def test_gpu_trainer_edges_and_save(tmp_path):
     tok = t2.tokenizer()
     ids = tok.encode("aab ab ba xyz")
     assert tok.decode(ids) == "aab ab ba xyz"
+
+
+def test_gpu_trainer_negative_unk_matches_oracle():
+    """unk_id -1 (the reference's default in docs): unk symbols never pair in the count, but the
+    merge deltas of their neighbours use the reference's change key, where a second member of -1
+    sign-extends over the whole key (bpe.cpp:456-467, restated by both); token frequencies skip
+    the negative id (bpe.cpp:709 would write freq[-1])."""
+    rng = np.random.default_rng(9)
+    alphabet = np.frombuffer(b"aaabbbcccdxyzQW!", dtype=np.uint8)
+    words = [bytes(rng.choice(alphabet, size=int(rng.integers(2, 9)))) for _ in range(300)]
+    text = b" ".join(words[int(i)] for i in rng.integers(0, len(words), size=8000))
+    cfg = (256 + 200, -1, 0.7, 2)
+    exp_rows, exp_freq = oracle.train(text, *cfg)
+    t = sa.BPETrainer(*cfg)
+    t.load_text(text)
+    assert t.train() == len(exp_rows) > 0
+    np.testing.assert_array_equal(t.merges, exp_rows)
+    np.testing.assert_array_equal(t.token_freq, exp_freq)

@@ -9,7 +9,8 @@ k_merge_bucket x4, k_merge_long*, k_tile_count + scan, k_compact, k_string_offse
        compaction.  --presplit host gives configs[2] (C3: host pre-split, GPU merge loop only).
   N>1  configs[3]: every rank encodes its own 1 GiB corpus (seed + rank; doc-sharded), then the
        token-id buffers are reassembled on every rank with an RCCL all-gather (padded to the
-       largest rank's count) -- weak scaling, the gather is inside the step.
+       largest rank's count; 16-bit ids when every id fits) -- weak scaling, the gather is inside
+       the step (--no-gather: without it).
 Prints ONE JSON line (rank 0).  Launch for N>1:
   python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \\
       --master-port P bench.py --gpus N
@@ -154,6 +155,7 @@ def main():
     encode(ctypes.byref(n_tok_c))
     n_tok = int(n_tok_c.value)
     gather = world > 1 and not args.no_gather
+    id_bits = 16 if tok.ids16 else 32  # (the ids cross xGMI as 16 bits when every id fits: SURVEY.md 8(e))
 
     # the gathers' widths: every rank's counts are the same every step (same corpus), so the
     # maxima are taken once here and the timed step has no host synchronisation
@@ -166,7 +168,8 @@ def main():
     def step():
         encode()
         if gather:  # shard.reassemble: one counts all-gather, padded id and offset all-gathers (RCCL)
-            return shard.reassemble(d_out, d_oo, None, dev, concat=False, width=width, width_s=width_s)
+            return shard.reassemble(d_out, d_oo, None, dev, concat=False, width=width, width_s=width_s,
+                                    id_bits=id_bits)
         return None
 
     for _ in range(args.warmup):
@@ -310,7 +313,8 @@ def main():
                        "presplit": args.presplit,
                        "bytes_per_rank": n_bytes, "strings_per_rank": n_str, "merges": len(tok.merges),
                        "model": model, "pattern": args.pattern, "parallelism": "doc-shard x%d" % world,
-                       "gather_in_step": gather, "chunk_table": not args.no_chunk_table,
+                       "gather_in_step": gather, "gather_id_bits": id_bits if gather else None,
+                       "chunk_table": not args.no_chunk_table,
                        "dedupe": not args.no_dedupe},
             "mtok_per_s": round(all_tok * args.steps / sec / 1e6, 3),
             "bytes_per_token": round(all_bytes / max(all_tok, 1), 4),

@@ -7,7 +7,8 @@ is the reassembly of the token-id buffers:
   1. all-gather of the per-rank token and string counts (int64, one collective);
   2. exclusive scan -> each rank's displacement in the global id buffer;
   3. all-gather of the id buffers, padded to the largest rank's count (one collective: on
-     xGMI every GPU receives 7/8 of the ids over its 7 links at once);
+     xGMI every GPU receives 7/8 of the ids over its 7 links at once), as 16-bit ids when the
+     vocabulary fits (id_bits=16: half the bytes on the links; widened on arrival);
   4. per-string offsets rebased by the displacement and concatenated.
 
 The reference has no multi-device path (its trainer is single-threaded, shredword/csrc/bpe);
@@ -40,7 +41,7 @@ def shard_of(buf, str_off, lo, hi):
     return buf[a:b], str_off[lo:hi + 1] - a
 
 
-def reassemble(local_ids, local_off, group=None, device=None, concat=True, width=None, width_s=None):
+def reassemble(local_ids, local_off, group=None, device=None, concat=True, width=None, width_s=None, id_bits=32):
     """Collective reassembly of per-rank encodes (steps 1-4 above) on every rank.
 
     local_ids: torch int32 [>= local count] on `device`; local_off: torch int64 [m+1] with
@@ -54,7 +55,10 @@ def reassemble(local_ids, local_off, group=None, device=None, concat=True, width
     small raises at the next synchronising call (check_bounds).
     concat=False skips the final copies and returns the gathered buffers as they landed:
     (ids [world * width], counts [world] on the device, width, offsets [world * width_s],
-    string counts [world] on the device, width_s) -- rank r's ids start at r * width."""
+    string counts [world] on the device, width_s) -- rank r's ids start at r * width.
+    id_bits=16 (every id < 65536, e.g. SW_INFO_IDS16): the ids travel as 16 bits; concat=True
+    widens them to int32, concat=False returns them as int16 holding the low 16 bits (an id is
+    `x & 0xFFFF` of the widened value)."""
     import torch
     import torch.distributed as dist
 
@@ -74,14 +78,23 @@ def reassemble(local_ids, local_off, group=None, device=None, concat=True, width
     else:
         _pending_checks.append((counts, n_strs, width, width_s))
     width, width_s = int(width), int(width_s)
+    if id_bits not in (16, 32):
+        raise ValueError("id_bits must be 16 or 32")
     if local_ids.numel() >= width and local_ids.dtype == torch.int32 and local_ids.device == dev:
         send = local_ids[:width]  # (slots past the count are padding: never read)
     else:
         send = torch.zeros(width, dtype=torch.int32, device=dev)
         k = min(width, local_ids.numel())
         send[:k] = local_ids[:k].to(device=dev, dtype=torch.int32)
-    recv = torch.empty(world * width, dtype=torch.int32, device=dev)
-    dist.all_gather_into_tensor(recv, send, group=group)
+    wide = id_bits == 32
+    if wide:
+        recv = torch.empty(world * width, dtype=torch.int32, device=dev)
+        dist.all_gather_into_tensor(recv, send, group=group)
+    else:  # the low 16 bits of each id (two's-complement truncation), moved as bytes (RCCL and gloo
+        # have no 16-bit integer type; an all-gather only copies)
+        send = send.to(torch.int16)
+        recv = torch.empty(world * width, dtype=torch.int16, device=dev)
+        dist.all_gather_into_tensor(recv.view(torch.uint8), send.view(torch.uint8), group=group)
     m = local_off.numel() - 1
     if local_off.numel() >= width_s and local_off.dtype == torch.int64 and local_off.device == dev:
         send_o = local_off[:width_s]
@@ -92,6 +105,8 @@ def reassemble(local_ids, local_off, group=None, device=None, concat=True, width
     dist.all_gather_into_tensor(recv_o, send_o, group=group)
     if not concat:
         return recv, counts, width, recv_o, n_strs, width_s
+    if not wide:
+        recv = recv.to(torch.int32) & 0xFFFF
     # the concatenation needs the counts on the host (as torch's slicing does)
     ch, sh = counts.cpu().tolist(), n_strs.cpu().tolist()
     if max(ch) > width or max(sh) > width_s:
@@ -139,7 +154,8 @@ def encode_sharded(tok, buf, str_off, chunk_bits_fn=None, group=None):
         d_off = torch.from_numpy(np.ascontiguousarray(sub_off)).to(dev)
         d_bits = torch.from_numpy(bits.view(np.int64)).to(dev) if bits is not None else None
         ids, off = tok.encode_device(d_buf, d_off, d_bits)
-        return reassemble(ids, off, group, dev)
+        return reassemble(ids, off, group, dev, id_bits=16 if tok.ids16 else 32)
     ids, off = tok.encode_packed(sub, sub_off, bits)
     dev = torch.device("cpu")
-    return reassemble(torch.from_numpy(ids).to(dev), torch.from_numpy(off).to(dev), group, dev)
+    return reassemble(torch.from_numpy(ids).to(dev), torch.from_numpy(off).to(dev), group, dev,
+                      id_bits=16 if tok.ids16 else 32)

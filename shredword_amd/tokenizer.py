@@ -152,6 +152,17 @@ class Tokenizer(BaseTokenizer):
         self._handle, self._handle_key = h, key
         return h
 
+    @property
+    def ids16(self):
+        """True when every id an ordinary encode can produce fits 16 bits (bytes, merge pair
+        members and values all < 65536): ids may then travel as 16 bits (shard.reassemble)."""
+        key = (id(self._merges), self._merges.version)
+        if getattr(self, "_ids16_key", None) != key:
+            m = self._merges
+            top = max((max(a, b, v) for (a, b), v in m.items()), default=255)
+            self._ids16, self._ids16_key = top < 65536, key
+        return self._ids16
+
     # ---------------------------------------------------------------- encode
     def encode_ordinary_batch_np(self, datas):
         """Encode a list of UTF-8 byte strings (no special-token handling) in one device batch.

@@ -56,4 +56,11 @@ def test_encode_sharded_rccl_world1(nccl_world1, fixture, model):
     n = int(counts[0].item())
     np.testing.assert_array_equal(recv[:n].cpu().numpy(), d["ids"])
     np.testing.assert_array_equal(recv_o[:len(d["off"]) - 1].cpu().numpy(), d["ids_off"][:-1])
+    # 16-bit transport over RCCL (the bench's step when every id fits): low 16 bits as landed
+    assert tok.ids16
+    r16 = shard.reassemble(l_ids, l_off, None, torch.device("cuda", 0), concat=False, width=len(d["bytes"]),
+                           width_s=len(d["off"]), id_bits=16)
+    shard.check_bounds()
+    assert r16[0].dtype == torch.int16
+    np.testing.assert_array_equal((r16[0][:n].to(torch.int32) & 0xFFFF).cpu().numpy(), d["ids"])
     tok.close()

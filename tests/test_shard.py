@@ -73,6 +73,13 @@ def _rank_main(rank, world, port, fixture, model, result_dir):
             ok = False
         except RuntimeError:
             pass
+        # 16-bit transport (every id of these tables < 65536): widened on arrival, the same
+        w_ids, w_off = shard.reassemble(torch.from_numpy(ids), torch.from_numpy(ids_off), None, torch.device("cpu"),
+                                        id_bits=16)
+        ok = ok and np.array_equal(w_ids.numpy(), d["ids"]) and np.array_equal(w_off.numpy(), d["ids_off"])
+        r16 = shard.reassemble(torch.from_numpy(ids), torch.from_numpy(ids_off), None, torch.device("cpu"),
+                               concat=False, id_bits=16)
+        ok = ok and r16[0].dtype == torch.int16
         with open(os.path.join(result_dir, "rank%d" % rank), "w") as f:
             f.write("ok" if ok else "mismatch")
     finally:

@@ -1217,6 +1217,9 @@ __global__ void __launch_bounds__(64) k_merge_long_lds(EncArgs a) {
 #ifndef SW_PIECE_N
 #define SW_PIECE_N 16
 #endif
+#ifndef SW_LS_V2
+#define SW_LS_V2 1  // 1: no chunk-sized rank array in LDS (pair ranks looked up where used)
+#endif
 constexpr int kPieceN = SW_PIECE_N;                              // per-lane register loop size
 constexpr int kPieceW = kPieceN == 32 ? 24 : 12;                 // cut spacing
 constexpr int kCutHalf = kPieceN == 32 ? 4 : 2;                  // cuts in [W k - H, W k + H)
@@ -1347,23 +1350,31 @@ __device__ uint64_t wave_merge64(const DevTable& t, uint32_t& id, uint32_t& rk, 
   return alive;
 }
 
+#ifndef SW_LS_WAVES
+#define SW_LS_WAVES 0  // (A/B builds: cap the VGPRs for this many waves per SIMD)
+#endif
+#if SW_LS_WAVES > 0
+#define SW_LS_ATTR __attribute__((amdgpu_waves_per_eu(SW_LS_WAVES, SW_LS_WAVES)))
+#else
+#define SW_LS_ATTR
+#endif
 template <bool kWide, bool k16>
-__global__ void __launch_bounds__(64) k_merge_long_split(EncArgs a) {
+__global__ void __launch_bounds__(64) SW_LS_ATTR k_merge_long_split(EncArgs a) {
   typedef typename std::conditional<k16, uint16_t, uint32_t>::type T;
   constexpr uint32_t TINF = k16 ? 0xFFFFu : kInf;  // (16-bit storage: values <= 0xFFFD)
   __shared__ T s_id[kLongLds];    // bytes, then each piece's ids from its first position
+#if SW_LS_V2
+  __shared__ T s_rkw[kMaxWindow];  // pair ranks of the rare window over 64 ids (one lane's loop)
+#else
   __shared__ T s_brk[kLongLds];   // rank of the byte pair (p, p + 1); output staging at the end
   __shared__ uint64_t s_kill[64], s_dirty[64];
+#endif
   __shared__ uint16_t s_cut[2][kMaxPieces + 1];  // piece k = [cut[k], cut[k + 1]) (double-buffered)
   __shared__ uint16_t s_cnt[2][kMaxPieces];      // its ids, at s_id[cut[k] ..)
   __shared__ uint8_t s_win[kMaxPieces];          // piece k is a window to encode again
   const int lane = threadIdx.x;
   const uint64_t lt_mask = (lane == 0) ? 0ULL : (~0ULL >> (64 - lane));
   const DevTable& tb = a.table;
-  auto brk = [&](int p) -> uint32_t {
-    const uint32_t r = s_brk[p];
-    return r == TINF ? kInf : r;
-  };
   int64_t lo, hi;
   SW_STAMP_INIT;
   bucket_range(a, kLongBucket, kLongBucket, &lo, &hi);
@@ -1383,6 +1394,15 @@ __global__ void __launch_bounds__(64) k_merge_long_split(EncArgs a) {
     uint32_t* gid = a.res + 2 * start + 1;
     for (int j = lane; j < len; j += 64) s_id[j] = (T)src[j];
     wave_sync_mem();
+#if SW_LS_V2
+    // byte-pair ranks looked up where they are used (the input bytes are immutable): no
+    // chunk-sized rank array in LDS, so ~12 KB per wave and 3 waves per SIMD instead of 1.75
+    auto brk = [&](int p) -> uint32_t { return lookup<kWide>(tb, src[p], src[p + 1]); };
+#else
+    auto brk = [&](int p) -> uint32_t {
+      const uint32_t r = s_brk[p];
+      return r == TINF ? kInf : r;
+    };
     // the rank of every byte pair, all lanes, kBrkBatch lookups in flight per lane
     for (int p0 = 0; p0 < len - 1; p0 += 64 * kBrkBatch) {
       uint32_t r[kBrkBatch];
@@ -1397,6 +1417,7 @@ __global__ void __launch_bounds__(64) k_merge_long_split(EncArgs a) {
         if (p < len - 1) s_brk[p] = (T)(r[u] == kInf ? TINF : r[u]);
       }
     }
+#endif
     int cur = 0;
     int P = (len + kPieceW - 1) / kPieceW;
     if (lane == 0) { s_cut[0][0] = 0; s_cut[0][P] = (uint16_t)len; }
@@ -1509,6 +1530,18 @@ __global__ void __launch_bounds__(64) k_merge_long_split(EncArgs a) {
 #ifdef SW_STAMPS
             big_win = true;
 #endif
+#if SW_LS_V2
+            for (int q = lane; q < n - 1; q += 64) {
+              const uint32_t r = lookup<kWide>(tb, src[c + q], src[c + q + 1]);
+              s_rkw[q] = (T)(r == kInf ? TINF : r);
+            }
+            wave_sync_mem();
+            if (lane == 0) {
+              for (int q = 0; q < n; ++q) s_id[c + q] = (T)src[c + q];
+              ncnt[j] = (uint16_t)lane_merge_lds<kWide, T>(tb, s_id + c, s_rkw, n);
+            }
+            wave_sync_mem();
+#else
             if (lane == 0) {
               for (int q = 0; q < n; ++q) s_id[c + q] = (T)src[c + q];
               ncnt[j] = (uint16_t)lane_merge_lds<kWide, T>(tb, s_id + c, s_brk + c, n);
@@ -1519,6 +1552,7 @@ __global__ void __launch_bounds__(64) k_merge_long_split(EncArgs a) {
               s_brk[c + q] = (T)(r == kInf ? TINF : r);
             }
             wave_sync_mem();
+#endif
             continue;
           }
           uint32_t id = lane < n ? (uint32_t)src[c + lane] : 0u;
@@ -1548,10 +1582,17 @@ __global__ void __launch_bounds__(64) k_merge_long_split(EncArgs a) {
       SW_COUNT(25, len);
       SW_COUNT(26, len > 1024 ? 1 : 0);
       wave_sync_mem();
+#if SW_LS_V2  // (the global work area of k_merge_long: ids then ranks, the chunk's 2 len words)
+      for (int j = lane; j < len; j += 64) gid[j] = src[j];
+      wave_sync_mem();
+      const int64_t m = coop_merge<kWide>(tb, gid, gid + len, len, lane);
+      if (lane == 0) gid[-1] = (uint32_t)m;
+#else
       for (int j = lane; j < len; j += 64) s_id[lds_pos(j)] = (T)src[j];
       wave_sync_mem();
       const int m = seg_merge<kWide, T>(tb, s_id, s_brk, s_kill, s_dirty, len, lane, gid);
       if (lane == 0) gid[-1] = (uint32_t)m;
+#endif
       wave_sync_mem();
       SW_STAMP(16);
       continue;
@@ -1569,12 +1610,18 @@ __global__ void __launch_bounds__(64) k_merge_long_split(EncArgs a) {
       const int o = total + (int)(incl - c);
       if (k < P) {
         const int b = cut[k];
+#if SW_LS_V2
+        for (uint32_t q = 0; q < c; ++q) gid[o + q] = (uint32_t)s_id[b + q];
+#else
         for (uint32_t q = 0; q < c; ++q) s_brk[o + q] = s_id[b + q];
+#endif
       }
       total += (int)__shfl(incl, 63, 64);
     }
     wave_sync_mem();
+#if !SW_LS_V2
     for (int q = lane; q < total; q += 64) gid[q] = (uint32_t)s_brk[q];
+#endif
     if (lane == 0) gid[-1] = (uint32_t)total;
     wave_sync_mem();
     SW_STAMP(17);

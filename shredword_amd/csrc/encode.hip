@@ -118,6 +118,7 @@ struct sw_encoder {
   uint64_t* d_dtab = nullptr;         // chunk dedupe table
   uint32_t dmask = 0;
   uint4* d_dres = nullptr;            // dense result heads, one per table entry
+  uint32_t* d_big = nullptr;          // chunks over kLongLds bytes: count, then their long-bucket indices
   bool dedupe = true;
   bool dedupe_exact = true;           // SW_OPT_DEDUPE_EXACT
   int64_t dedupe_slots = 0;           // SW_OPT_DEDUPE_SLOTS (0: automatic)
@@ -164,8 +165,8 @@ void free_workspace(sw_encoder* h) {
   h->d_tile_slo = nullptr; h->d_stamps = nullptr; h->d_tile_slots = nullptr; h->d_tile_nref = nullptr; h->d_rlist = nullptr; h->d_queue = nullptr;
   h->d_bcnt = nullptr; h->d_boff = nullptr; h->d_qtotal = nullptr;
   (void)hipFree(h->d_dtab); (void)hipFree(h->d_tile_base); (void)hipFree(h->d_tile_cnt);
-  (void)hipFree(h->d_dres);
-  h->d_dres = nullptr;
+  (void)hipFree(h->d_dres); (void)hipFree(h->d_big);
+  h->d_dres = nullptr; h->d_big = nullptr;
   (void)hipFree(h->d_total);
   h->d_scratch = nullptr; h->d_res = nullptr; h->d_pbits = nullptr; h->d_pcount = nullptr; h->d_part = nullptr;
   h->d_dtab = nullptr; h->d_tile_base = nullptr; h->d_tile_cnt = nullptr; h->d_total = nullptr;
@@ -218,6 +219,7 @@ int32_t ensure_workspace(sw_encoder* h, int64_t n_bytes) {
     HIP_TRY(hipMalloc(&h->d_dres, sizeof(uint4) * slots));
     h->dmask = (uint32_t)(slots - 1);
   }
+  HIP_TRY(hipMalloc(&h->d_big, sizeof(uint32_t) * (nb / (kLongLds + 1) + 2)));  // (count + list)
   HIP_TRY(hipMalloc(&h->d_tile_base, sizeof(int64_t) * n_tiles));
   HIP_TRY(hipMalloc(&h->d_tile_cnt, sizeof(uint32_t) * n_tiles));
   HIP_TRY(hipMalloc(&h->d_total, sizeof(int64_t)));
@@ -586,12 +588,14 @@ extern "C" int32_t sw_encode_device(sw_encoder* h, const uint8_t* d_bytes, int64
     a.dmask = h->dedupe_slots ? std::min<uint32_t>(h->dmask, (uint32_t)(h->dedupe_slots - 1)) : h->dmask;
     a.dexact = h->dedupe_exact ? (uint32_t)kDdExactMax : 0u;
     a.dres = h->d_dres;
+    a.big_count = h->d_big; a.big_list = h->d_big + 1;
     a.out_off = d_out_off; a.tile_slo = h->d_tile_slo;
     a.n_tiles = n_tiles; a.qtmp = h->d_res; a.bcnt = h->d_bcnt; a.boff = h->d_boff; a.q_total = h->d_qtotal;
     a.queue = h->d_queue; a.stamps = h->d_stamps;
     a.inv = h->d_inv; a.n_inv = h->n_inv; a.ids16 = h->ids16 ? 1u : 0u;
     const bool split = h->split_ok && h->long_split;
     if (h->dedupe) HIP_TRY(hipMemsetAsync(h->d_dtab, 0, sizeof(uint64_t) * ((size_t)a.dmask + 1), st));
+    HIP_TRY(hipMemsetAsync(h->d_big, 0, sizeof(uint32_t), st));
     hipLaunchKernelGGL(k_classify, dim3((unsigned)((n_tiles + kWaves - 1) / kWaves)), dim3(kThreads), 0, st, a);
     HIP_TRY(hipGetLastError());
     HIP_TRY(launch_scan(st, h->d_bcnt, kNumBuckets * n_tiles, h->d_part, h->d_boff, h->d_qtotal));

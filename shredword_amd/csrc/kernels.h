@@ -459,6 +459,8 @@ struct EncArgs {
   unsigned long long* stamps;  // SW_STAMPS builds: cycles per phase, summed
   const uint2* inv;          // [n_inv] merge value -> its pair (a, b); well-formed tables only
   uint32_t n_inv;
+  uint32_t* big_list;        // queued chunks over kLongLds bytes (their index in the long bucket)
+  uint32_t* big_count;       // ... how many (cleared per launch)
   uint32_t ids16;            // every id fits 16 bits (dres layout)
 };
 
@@ -1185,7 +1187,10 @@ __global__ void __launch_bounds__(64) k_merge_long_lds(EncArgs a) {
     const uint64_t e = a.queue[i];
     const int64_t start = (int64_t)(e >> 33);
     const int64_t len = next_set_bit(a.bits, a.n_words, start + 1, a.n_bytes) - start;
-    if (len > kLongLds) continue;  // (k_merge_long)
+    if (len > kLongLds) {  // (k_merge_long, from the list)
+      if (lane == 0) a.big_list[atomicAdd(a.big_count, 1u)] = (uint32_t)(i - lo);
+      continue;
+    }
     for (int j = lane; j < len; j += 64) s_id[lds_pos(j)] = (T)a.bytes[start + j];
     wave_sync_mem();
     uint32_t* gid = a.res + 2 * start + 1;
@@ -1382,7 +1387,10 @@ __global__ void __launch_bounds__(64) SW_LS_ATTR k_merge_long_split(EncArgs a) {
     const uint64_t e = a.queue[i];
     const int64_t start = (int64_t)(e >> 33);
     const int len = (int)(next_set_bit(a.bits, a.n_words, start + 1, a.n_bytes) - start);
-    if (len > kLongLds) continue;  // (k_merge_long)
+    if (len > kLongLds) {  // (k_merge_long, from the list)
+      if (lane == 0) a.big_list[atomicAdd(a.big_count, 1u)] = (uint32_t)(i - lo);
+      continue;
+    }
     SW_STAMP(18);
     SW_COUNT(20, 1);
     SW_COUNT(21, len);
@@ -1644,12 +1652,13 @@ __global__ void __launch_bounds__(kThreads) k_merge_long(EncArgs a) {
   const int lane = threadIdx.x & 63;
   int64_t lo, hi;
   bucket_range(a, kLongBucket, kLongBucket, &lo, &hi);
-  for (int64_t i = lo + gw; i < hi; i += n_waves) {
+  const uint32_t n_big = *a.big_count;  // (listed by k_merge_long_split / k_merge_long_lds)
+  for (int64_t b = gw; b < (int64_t)n_big; b += n_waves) {
+    const int64_t i = lo + a.big_list[b];
     const uint64_t e = a.queue[i];
     const int64_t start = (int64_t)(e >> 33);
     const int64_t end = next_set_bit(a.bits, a.n_words, start + 1, a.n_bytes);
     const int64_t len = end - start;
-    if (len <= kLongLds) continue;  // (k_merge_long_lds)
     uint32_t* gid = a.res + 2 * start + 1;  // ids: len words, then ranks: len - 1 words
     uint32_t* grk = gid + len;
     for (int64_t j = lane; j < len; j += 64) gid[j] = a.bytes[start + j];

@@ -125,6 +125,12 @@ int32_t sw_encoder_reserve(sw_encoder* h, int64_t max_bytes, int64_t max_strings
  *                          themselves (no verification read); 0: every key is a fingerprint
  *                          verified against the first occurrence's bytes (testing) */
 #define SW_OPT_DEDUPE_EXACT 10
+/*   SW_OPT_PIPE_COPY_KERNELS  1 (default): the pipeline's uploads and downloads are kernels that
+ *                          read and write the pinned host buffers directly over PCIe (about 57 GB/s
+ *                          each way on MI355X, both ways at once); 0: DMA copies (hipMemcpyAsync) */
+#define SW_OPT_PIPE_COPY_KERNELS 11
+/*   SW_OPT_PIPE_DEPTH      runs in flight in that pipeline, 2 .. 4 (default 3) */
+#define SW_OPT_PIPE_DEPTH 12
 int32_t sw_encoder_set_option(sw_encoder* h, int32_t option, int64_t value);
 
 /* Encoder facts (sw_encoder_get_info): distinct merges, whole-chunk table entries, whether the

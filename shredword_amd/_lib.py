@@ -26,6 +26,8 @@ SW_OPT_CHUNK_TABLE, SW_OPT_DEDUPE, SW_OPT_DEDUPE_SLOTS, SW_OPT_DEDUPE_FP_BITS = 
 SW_OPT_PATTERN, SW_OPT_HOST_PRESPLIT, SW_OPT_LONG_SPLIT, SW_OPT_MAX_LAUNCH_BYTES = 5, 6, 7, 8
 SW_OPT_PIPE_RUN_BYTES = 9
 SW_OPT_DEDUPE_EXACT = 10
+SW_OPT_PIPE_COPY_KERNELS = 11
+SW_OPT_PIPE_DEPTH = 12
 SW_INFO_MERGES, SW_INFO_CHUNK_ENTRIES, SW_INFO_WIDE_TABLE, SW_INFO_IDS16, SW_INFO_SPLIT = 1, 2, 3, 4, 5
 
 

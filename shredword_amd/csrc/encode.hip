@@ -95,10 +95,13 @@ struct sw_encoder {
     void* h_out = nullptr; int64_t* h_oo = nullptr; int64_t* h_ntok = nullptr;        // pinned
     uint8_t* d_in = nullptr; int64_t* d_off = nullptr; uint64_t* d_bits = nullptr;
     int32_t* d_out = nullptr; int64_t* d_oo = nullptr; uint16_t* d_out16 = nullptr;
+    int64_t* d_ntok = nullptr;  // this run's token count, kept apart from the shared workspace
     hipEvent_t e_in = nullptr, e_comp = nullptr, e_out = nullptr;
     int64_t cap_bytes = 0, cap_str = 0;
-  } pipe[2];
+  } pipe[4];
+  int pipe_depth = 3;                 // SW_OPT_PIPE_DEPTH: runs in flight (slots)
   int64_t pipe_run = 64LL << 20;      // run size; batches over 2 runs take the pipeline (0: never)
+  bool pipe_kcopy = true;             // SW_OPT_PIPE_COPY_KERNELS
   hipStream_t s_h2d = nullptr, s_d2h = nullptr;
   sw::HostPool* pool = nullptr;
   // workspace
@@ -185,7 +188,7 @@ void free_pipe(sw_encoder* h) {
     (void)hipHostFree(p.h_in); (void)hipHostFree(p.h_off); (void)hipHostFree(p.h_bits); (void)hipHostFree(p.h_out);
     (void)hipHostFree(p.h_oo); (void)hipHostFree(p.h_ntok);
     (void)hipFree(p.d_in); (void)hipFree(p.d_off); (void)hipFree(p.d_bits); (void)hipFree(p.d_out); (void)hipFree(p.d_oo);
-    (void)hipFree(p.d_out16);
+    (void)hipFree(p.d_out16); (void)hipFree(p.d_ntok);
     if (p.e_in) (void)hipEventDestroy(p.e_in);
     if (p.e_comp) (void)hipEventDestroy(p.e_comp);
     if (p.e_out) (void)hipEventDestroy(p.e_out);
@@ -477,6 +480,11 @@ extern "C" int32_t sw_encoder_set_option(sw_encoder* h, int32_t option, int64_t 
       return SW_OK;
     case SW_OPT_DEDUPE_EXACT: h->dedupe_exact = value != 0; return SW_OK;
     case SW_OPT_LONG_SPLIT: h->long_split = value != 0; return SW_OK;
+    case SW_OPT_PIPE_COPY_KERNELS: h->pipe_kcopy = value != 0; return SW_OK;
+    case SW_OPT_PIPE_DEPTH:
+      if (value < 2 || value > 4) return fail(SW_ERR_ARG, "pipeline depth: 2 .. 4");
+      h->pipe_depth = (int)value;
+      return SW_OK;
     case SW_OPT_PIPE_RUN_BYTES:
       if (value != 0 && value < 64) return fail(SW_ERR_ARG, "pipeline run bytes: 0 (off) or >= 64");
       h->pipe_run = std::min<int64_t>(value, kMaxLaunchBytes);
@@ -660,6 +668,59 @@ __global__ void k_pack16(const int32_t* in, const int64_t* total, uint16_t* out)
     out[i] = (uint16_t)in[i];
 }
 
+// Pipeline copies as kernels over PCIe: a few hundred waves of 16-byte loads keep enough requests
+// in flight to run a copy at the link rate (about 57 GB/s each way measured, tools/h2d_probe.hip)
+// while the encode kernels run beside them.  Host buffers are hipHostMalloc'd (page aligned), device
+// buffers hipMalloc'd, so every segment starts 16-byte aligned.
+typedef unsigned int v4u32 __attribute__((ext_vector_type(4)));
+
+struct CopySegs {
+  const uint8_t* src[3];
+  uint8_t* dst[3];
+  int64_t n[3];
+};
+
+__device__ inline void copy_seg(const uint8_t* src, uint8_t* dst, int64_t n, int64_t t, int64_t nt) {
+  const int64_t n16 = n >> 4;
+  const v4u32* s = (const v4u32*)src;
+  v4u32* d = (v4u32*)dst;
+  for (int64_t i = t; i < n16; i += nt) d[i] = __builtin_nontemporal_load(s + i);
+  for (int64_t i = (n16 << 4) + t; i < n; i += nt) dst[i] = src[i];
+}
+
+__global__ void __launch_bounds__(256) k_copy_segs(CopySegs c) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x, nt = (int64_t)gridDim.x * blockDim.x;
+  for (int k = 0; k < 3; ++k)
+    if (c.n[k] > 0) copy_seg(c.src[k], c.dst[k], c.n[k], t, nt);
+}
+
+// one run's results to pinned host memory: ids (16-bit when every id fits, 8 per 16-byte store;
+// else 32-bit) and the run's string offsets
+__global__ void __launch_bounds__(256) k_push_run(const int32_t* __restrict__ ids, const int64_t* ntok, int wide,
+                                                  void* h_ids, const int64_t* d_oo, int64_t n_oo, int64_t* h_oo) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x, nt = (int64_t)gridDim.x * blockDim.x;
+  const int64_t n = *ntok;
+  if (wide) {
+    copy_seg((const uint8_t*)ids, (uint8_t*)h_ids, n * 4, t, nt);
+  } else {
+    const int64_t n8 = n >> 3;
+    const v4u32* s = (const v4u32*)ids;
+    v4u32* d = (v4u32*)h_ids;
+    for (int64_t i = t; i < n8; i += nt) {
+      const v4u32 a = __builtin_nontemporal_load(s + 2 * i), b = __builtin_nontemporal_load(s + 2 * i + 1);
+      v4u32 o;
+      o.x = (a.x & 0xFFFFu) | (a.y << 16);
+      o.y = (a.z & 0xFFFFu) | (a.w << 16);
+      o.z = (b.x & 0xFFFFu) | (b.y << 16);
+      o.w = (b.z & 0xFFFFu) | (b.w << 16);
+      d[i] = o;
+    }
+    uint16_t* d16 = (uint16_t*)h_ids;
+    for (int64_t i = (n8 << 3) + t; i < n; i += nt) d16[i] = (uint16_t)ids[i];
+  }
+  copy_seg((const uint8_t*)d_oo, (uint8_t*)h_oo, n_oo * 8, t, nt);
+}
+
 namespace {
 
 // sw_encode_batch for a large host batch: runs of whole strings (<= pipe_run bytes, or one longer
@@ -687,13 +748,14 @@ int32_t encode_batch_pipelined(sw_encoder* h, const uint8_t* bytes, const int64_
   if (!h->s_d2h) HIP_TRY(hipStreamCreateWithFlags(&h->s_d2h, hipStreamNonBlocking));
   if (!h->pool) h->pool = new sw::HostPool((int)std::max(1u, std::min(16u, std::thread::hardware_concurrency())) - 1);
   const int64_t max_w = (max_b + 63) / 64 + 1;
-  for (auto& p : h->pipe) {
+  for (int slot = 0; slot < h->pipe_depth; ++slot) {
+    auto& p = h->pipe[slot];
     if (p.cap_bytes >= max_b && p.cap_str >= max_s) continue;
     const int64_t cb = std::max(max_b, p.cap_bytes), cs = std::max(max_s, p.cap_str), cw = (cb + 63) / 64 + 1;
     (void)hipHostFree(p.h_in); (void)hipHostFree(p.h_off); (void)hipHostFree(p.h_bits); (void)hipHostFree(p.h_out);
     (void)hipHostFree(p.h_oo); (void)hipHostFree(p.h_ntok);
     (void)hipFree(p.d_in); (void)hipFree(p.d_off); (void)hipFree(p.d_bits); (void)hipFree(p.d_out); (void)hipFree(p.d_oo);
-    (void)hipFree(p.d_out16);
+    (void)hipFree(p.d_out16); (void)hipFree(p.d_ntok);
     p.cap_bytes = p.cap_str = 0;
     HIP_TRY(hipHostMalloc(&p.h_in, cb + 16, hipHostMallocDefault));
     HIP_TRY(hipHostMalloc(&p.h_off, sizeof(int64_t) * (cs + 1), hipHostMallocDefault));
@@ -707,6 +769,7 @@ int32_t encode_batch_pipelined(sw_encoder* h, const uint8_t* bytes, const int64_
     HIP_TRY(hipMalloc(&p.d_out, sizeof(int32_t) * cb));
     HIP_TRY(hipMalloc(&p.d_oo, sizeof(int64_t) * (cs + 1)));
     HIP_TRY(hipMalloc(&p.d_out16, sizeof(uint16_t) * cb));
+    HIP_TRY(hipMalloc(&p.d_ntok, sizeof(int64_t)));
     if (!p.e_in) HIP_TRY(hipEventCreateWithFlags(&p.e_in, hipEventDisableTiming));
     if (!p.e_comp) HIP_TRY(hipEventCreateWithFlags(&p.e_comp, hipEventDisableTiming));
     if (!p.e_out) HIP_TRY(hipEventCreateWithFlags(&p.e_out, hipEventDisableTiming));
@@ -732,8 +795,14 @@ int32_t encode_batch_pipelined(sw_encoder* h, const uint8_t* bytes, const int64_
   sw::HostPool& pool = *h->pool;
   double ms_stage = 0, ms_drain = 0;
   int64_t done = 0;
+  static const bool trace = std::getenv("SW_PIPE_TRACE") != nullptr;  // (diagnostic timeline)
+  auto stamp = [&](const char* what, size_t k) {
+    if (trace)
+      std::fprintf(stderr, "pipe %8.3f %-10s %zu\n",
+                   std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - T0).count(), what, k);
+  };
   auto stage = [&](size_t k) -> int32_t {
-    auto& p = h->pipe[k & 1];
+    auto& p = h->pipe[k % h->pipe_depth];
     const int64_t s_lo = runs[k].first, s_hi = runs[k].second, a0 = str_off[s_lo], nb = str_off[s_hi] - a0;
     auto t = std::chrono::steady_clock::now();
     const uint8_t* src = bytes + a0;
@@ -751,15 +820,24 @@ int32_t encode_batch_pipelined(sw_encoder* h, const uint8_t* bytes, const int64_
       });
     }
     ms_stage += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t).count();
+    stamp("staged", k);
     return SW_OK;
   };
   auto issue = [&](size_t k) -> int32_t {
-    auto& p = h->pipe[k & 1];
+    auto& p = h->pipe[k % h->pipe_depth];
     const int64_t s_lo = runs[k].first, s_hi = runs[k].second, nb = str_off[s_hi] - str_off[s_lo], ns = s_hi - s_lo;
-    HIP_TRY(hipMemcpyAsync(p.d_in, p.h_in, (size_t)nb, hipMemcpyHostToDevice, h->s_h2d));
-    HIP_TRY(hipMemcpyAsync(p.d_off, p.h_off, sizeof(int64_t) * (ns + 1), hipMemcpyHostToDevice, h->s_h2d));
-    if (chunk_bits)
-      HIP_TRY(hipMemcpyAsync(p.d_bits, p.h_bits, sizeof(uint64_t) * ((nb + 63) / 64), hipMemcpyHostToDevice, h->s_h2d));
+    const int64_t n_bits = chunk_bits ? (int64_t)sizeof(uint64_t) * ((nb + 63) / 64) : 0;
+    if (h->pipe_kcopy) {
+      const CopySegs c{{p.h_in, (const uint8_t*)p.h_off, (const uint8_t*)p.h_bits},
+                       {p.d_in, (uint8_t*)p.d_off, (uint8_t*)p.d_bits},
+                       {nb, (int64_t)sizeof(int64_t) * (ns + 1), n_bits}};
+      hipLaunchKernelGGL(k_copy_segs, dim3(128), dim3(256), 0, h->s_h2d, c);
+      HIP_TRY(hipGetLastError());
+    } else {
+      HIP_TRY(hipMemcpyAsync(p.d_in, p.h_in, (size_t)nb, hipMemcpyHostToDevice, h->s_h2d));
+      HIP_TRY(hipMemcpyAsync(p.d_off, p.h_off, sizeof(int64_t) * (ns + 1), hipMemcpyHostToDevice, h->s_h2d));
+      if (chunk_bits) HIP_TRY(hipMemcpyAsync(p.d_bits, p.h_bits, (size_t)n_bits, hipMemcpyHostToDevice, h->s_h2d));
+    }
     HIP_TRY(hipEventRecord(p.e_in, h->s_h2d));
     HIP_TRY(hipStreamWaitEvent(h->stream, p.e_in, 0));
     const int32_t r = sw_encode_device(h, p.d_in, nb, p.d_off, ns, chunk_bits ? p.d_bits : nullptr, p.d_out, p.d_oo,
@@ -767,26 +845,42 @@ int32_t encode_batch_pipelined(sw_encoder* h, const uint8_t* bytes, const int64_
     if (r) return r;
     if (count && nb > 0)
       hipLaunchKernelGGL(k_popcount, dim3(1024), dim3(256), 0, h->stream, h->d_pbits, (nb + 63) / 64, h->d_pcount);
-    if (h->ids16) hipLaunchKernelGGL(k_pack16, dim3(2048), dim3(256), 0, h->stream, p.d_out, h->d_total, p.d_out16);
+    if (h->pipe_kcopy) {
+      // the download kernel runs on s_d2h beside the next run's encode, which rewrites d_total
+      HIP_TRY(hipMemcpyAsync(p.d_ntok, h->d_total, sizeof(int64_t), hipMemcpyDeviceToDevice, h->stream));
+    } else if (h->ids16) {
+      hipLaunchKernelGGL(k_pack16, dim3(2048), dim3(256), 0, h->stream, p.d_out, h->d_total, p.d_out16);
+    }
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipMemcpyAsync(p.h_ntok, h->d_total, sizeof(int64_t), hipMemcpyDeviceToHost, h->stream));
     HIP_TRY(hipEventRecord(p.e_comp, h->stream));
+    if (h->pipe_kcopy) {
+      HIP_TRY(hipStreamWaitEvent(h->s_d2h, p.e_comp, 0));
+      hipLaunchKernelGGL(k_push_run, dim3(128), dim3(256), 0, h->s_d2h, p.d_out, p.d_ntok, h->ids16 ? 0 : 1,
+                         p.h_out, p.d_oo, ns + 1, p.h_oo);
+      HIP_TRY(hipGetLastError());
+      HIP_TRY(hipEventRecord(p.e_out, h->s_d2h));
+    }
     return SW_OK;
   };
   auto drain = [&](size_t k) -> int32_t {
-    auto& p = h->pipe[k & 1];
+    auto& p = h->pipe[k % h->pipe_depth];
     const int64_t s_lo = runs[k].first, s_hi = runs[k].second, ns = s_hi - s_lo;
     HIP_TRY(hipEventSynchronize(p.e_comp));
+    stamp("encoded", k);
     const int64_t nt = *p.h_ntok;
     if (done + nt > out_cap) return fail(SW_ERR_CAP, "sw_encode_batch: out_cap too small");
     auto t = std::chrono::steady_clock::now();
-    HIP_TRY(hipStreamWaitEvent(h->s_d2h, p.e_comp, 0));
-    if (nt > 0)
-      HIP_TRY(hipMemcpyAsync(p.h_out, h->ids16 ? (void*)p.d_out16 : (void*)p.d_out,
-                             (size_t)nt * (h->ids16 ? 2 : 4), hipMemcpyDeviceToHost, h->s_d2h));
-    HIP_TRY(hipMemcpyAsync(p.h_oo, p.d_oo, sizeof(int64_t) * (ns + 1), hipMemcpyDeviceToHost, h->s_d2h));
-    HIP_TRY(hipEventRecord(p.e_out, h->s_d2h));
+    if (!h->pipe_kcopy) {
+      HIP_TRY(hipStreamWaitEvent(h->s_d2h, p.e_comp, 0));
+      if (nt > 0)
+        HIP_TRY(hipMemcpyAsync(p.h_out, h->ids16 ? (void*)p.d_out16 : (void*)p.d_out,
+                               (size_t)nt * (h->ids16 ? 2 : 4), hipMemcpyDeviceToHost, h->s_d2h));
+      HIP_TRY(hipMemcpyAsync(p.h_oo, p.d_oo, sizeof(int64_t) * (ns + 1), hipMemcpyDeviceToHost, h->s_d2h));
+      HIP_TRY(hipEventRecord(p.e_out, h->s_d2h));
+    }
     HIP_TRY(hipEventSynchronize(p.e_out));
+    stamp("pushed", k);
     int32_t* dst = out_ids + done;
     if (h->ids16) {
       const uint16_t* s16 = (const uint16_t*)p.h_out;
@@ -799,17 +893,29 @@ int32_t encode_batch_pipelined(sw_encoder* h, const uint8_t* bytes, const int64_
     }
     for (int64_t j = 0; j <= ns; ++j) out_off[s_lo + j] = p.h_oo[j] + done;
     done += nt;
+    stamp("drained", k);
     ms_drain += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t).count();
     return SW_OK;
   };
+  // host order: stage k, issue k, then drain the oldest run when every slot is taken (pipe_depth
+  // runs in flight: run k's upload overlaps the encodes and downloads of the runs before it)
+  auto bail = [&](int32_t r) {  // leave nothing in flight on the slots' buffers
+    (void)hipStreamSynchronize(h->s_h2d);
+    (void)hipStreamSynchronize(h->stream);
+    (void)hipStreamSynchronize(h->s_d2h);
+    restore();
+    return r;
+  };
+  const size_t depth = (size_t)h->pipe_depth;
+  size_t next_drain = 0;
   for (size_t k = 0; k < runs.size(); ++k) {
     rc = stage(k);
     if (!rc) rc = issue(k);
-    if (!rc && k > 0) rc = drain(k - 1);
-    if (rc) { restore(); return rc; }
+    if (!rc && next_drain + depth <= k + 1) rc = drain(next_drain++);  // frees run k + 1's slot
+    if (rc) return bail(rc);
   }
-  if (!runs.empty()) rc = drain(runs.size() - 1);
-  if (rc) { restore(); return rc; }
+  while (next_drain < runs.size())
+    if ((rc = drain(next_drain++))) return bail(rc);
   if (n_str == 0) out_off[0] = 0;
   const double k_ms = sw_encoder_last_kernel_ms(h) * (double)runs.size();
   int64_t n_chunks = -1;

@@ -286,9 +286,11 @@ def test_workspace_ordered_across_streams():
 @pytest.mark.parametrize("run", [64, 5000, 300000])
 @pytest.mark.parametrize("host_bits", [False, True])
 @pytest.mark.parametrize("wide", [False, True])
-def test_pipelined_batch(run, host_bits, wide):
+@pytest.mark.parametrize("kcopy", [True, False])
+def test_pipelined_batch(run, host_bits, wide, kcopy):
     """sw_encode_batch over more than two pipeline runs: staging, 16-bit downloads (32-bit for a
-    table past 64k ids), realigned caller bits, offsets rebased across runs -- == the oracle."""
+    table past 64k ids), realigned caller bits, offsets rebased across runs, copies by kernels
+    over PCIe or by DMA -- == the oracle."""
     buf, off = corpus.synth(8, corpus.MIXED, 900, 700)
     if run == 64:  # (every string must fit a run... or be a run of its own: both happen)
         datas = [bytes(buf[off[i]:off[i + 1]][:200]).decode("utf-8", "ignore").encode("utf-8") for i in range(400)]
@@ -309,6 +311,7 @@ def test_pipelined_batch(run, host_bits, wide):
     L, h = _lib.lib(), t._encoder()
     assert L.sw_encoder_get_info(h, _lib.SW_INFO_IDS16) == (0 if wide else 1)
     _lib.check(L.sw_encoder_set_option(h, _lib.SW_OPT_PIPE_RUN_BYTES, run))
+    _lib.check(L.sw_encoder_set_option(h, _lib.SW_OPT_PIPE_COPY_KERNELS, int(kcopy)))
     got = t.encode_packed(full, sub, bits)
     st = t.last_stats
     assert_same(got, exp)
@@ -317,3 +320,23 @@ def test_pipelined_batch(run, host_bits, wide):
     got2 = t.encode_packed(full, sub, bits)  # (buffers reused)
     assert_same(got2, exp)
     t.close()
+
+
+@pytest.mark.parametrize("depth", [2, 4])
+def test_pipelined_depth(depth):
+    """Every pipeline depth gives the oracle's ids (slots reused across runs and calls)."""
+    buf, off = corpus.synth(9, corpus.MIXED, 600, 700)
+    full, offs = pack([bytes(buf[off[i]:off[i + 1]]) for i in range(600)])
+    merges = load_model_merges("bl32k.model")
+    t = sa.Tokenizer(device=0)
+    t.merges = merges
+    exp = oracle_encode(merges, full, offs, "cl100k")
+    L, h = _lib.lib(), t._encoder()
+    _lib.check(L.sw_encoder_set_option(h, _lib.SW_OPT_PIPE_RUN_BYTES, 4000))
+    _lib.check(L.sw_encoder_set_option(h, _lib.SW_OPT_PIPE_DEPTH, depth))
+    assert_same(t.encode_packed(full, offs), exp)
+    _lib.check(L.sw_encoder_set_option(h, _lib.SW_OPT_PIPE_DEPTH, 6 - depth))
+    assert_same(t.encode_packed(full, offs), exp)
+    assert L.sw_encoder_set_option(h, _lib.SW_OPT_PIPE_DEPTH, 5) == _lib.SW_ERR_ARG
+    t.close()
+

@@ -131,6 +131,10 @@ int32_t sw_encoder_reserve(sw_encoder* h, int64_t max_bytes, int64_t max_strings
 #define SW_OPT_PIPE_COPY_KERNELS 11
 /*   SW_OPT_PIPE_DEPTH      runs in flight in that pipeline, 2 .. 4 (default 3) */
 #define SW_OPT_PIPE_DEPTH 12
+/*   SW_OPT_MERGE_STREAMS   1 (default): the merge kernels of the different chunk-length buckets
+ *                          run side by side on forked streams (joined before the counts); 0: one
+ *                          after another on the launch stream.  Results identical. */
+#define SW_OPT_MERGE_STREAMS 13
 int32_t sw_encoder_set_option(sw_encoder* h, int32_t option, int64_t value);
 
 /* Encoder facts (sw_encoder_get_info): distinct merges, whole-chunk table entries, whether the

@@ -103,6 +103,11 @@ struct sw_encoder {
   int64_t pipe_run = 64LL << 20;      // run size; batches over 2 runs take the pipeline (0: never)
   bool pipe_kcopy = true;             // SW_OPT_PIPE_COPY_KERNELS
   hipStream_t s_h2d = nullptr, s_d2h = nullptr;
+  // the merge kernels of different length buckets are independent: forked onto these streams
+  // they overlap (each alone leaves most of the chip idle), joined before k_tile_count
+  bool merge_fork = true;             // SW_OPT_MERGE_STREAMS
+  hipStream_t s_fork[3] = {nullptr, nullptr, nullptr};
+  hipEvent_t ev_fork = nullptr, ev_join[3] = {nullptr, nullptr, nullptr};
   sw::HostPool* pool = nullptr;
   // workspace
   int64_t cap_bytes = -1, cap_str = -1;
@@ -444,6 +449,11 @@ extern "C" void sw_encoder_destroy(sw_encoder* h) {
     delete h->pool;
     if (h->s_h2d) (void)hipStreamDestroy(h->s_h2d);
     if (h->s_d2h) (void)hipStreamDestroy(h->s_d2h);
+    for (int k = 0; k < 3; ++k) {
+      if (h->s_fork[k]) (void)hipStreamDestroy(h->s_fork[k]);
+      if (h->ev_join[k]) (void)hipEventDestroy(h->ev_join[k]);
+    }
+    if (h->ev_fork) (void)hipEventDestroy(h->ev_fork);
     (void)hipFree(h->d_table);
     (void)hipFree(h->d_chunks);
     (void)hipFree(h->d_inv);
@@ -481,6 +491,7 @@ extern "C" int32_t sw_encoder_set_option(sw_encoder* h, int32_t option, int64_t 
     case SW_OPT_DEDUPE_EXACT: h->dedupe_exact = value != 0; return SW_OK;
     case SW_OPT_LONG_SPLIT: h->long_split = value != 0; return SW_OK;
     case SW_OPT_PIPE_COPY_KERNELS: h->pipe_kcopy = value != 0; return SW_OK;
+    case SW_OPT_MERGE_STREAMS: h->merge_fork = value != 0; return SW_OK;
     case SW_OPT_PIPE_DEPTH:
       if (value < 2 || value > 4) return fail(SW_ERR_ARG, "pipeline depth: 2 .. 4");
       h->pipe_depth = (int)value;
@@ -610,30 +621,50 @@ extern "C" int32_t sw_encode_device(sw_encoder* h, const uint8_t* d_bytes, int64
     hipLaunchKernelGGL(k_scatter, dim3((unsigned)((n_tiles + 3) / 4)), dim3(kThreads), 0, st, a);
     const dim3 pg(2048), pb(kThreads);  // persistent grid for the queue kernels
     constexpr unsigned kLongGrid = 32768;  // k_merge_long_lds: a workgroup per long chunk (grid-stride past that)
+    // streams of the merge kernels: [0] buckets 17..32 B, [1] 9..16 B, [2] 2..8 B, [3] long
+    hipStream_t ms[4] = {st, st, st, st};
+    if (h->merge_fork) {
+      for (int k = 0; k < 3; ++k) {
+        if (!h->s_fork[k]) HIP_TRY(hipStreamCreateWithFlags(&h->s_fork[k], hipStreamNonBlocking));
+        if (!h->ev_join[k]) HIP_TRY(hipEventCreateWithFlags(&h->ev_join[k], hipEventDisableTiming));
+      }
+      if (!h->ev_fork) HIP_TRY(hipEventCreateWithFlags(&h->ev_fork, hipEventDisableTiming));
+      HIP_TRY(hipEventRecord(h->ev_fork, st));
+      for (int k = 0; k < 3; ++k) {
+        HIP_TRY(hipStreamWaitEvent(h->s_fork[k], h->ev_fork, 0));
+        ms[k + 1] = h->s_fork[k];
+      }
+    }
     if (h->table.wide) {
-      hipLaunchKernelGGL((k_merge_bucket<true, false, 4>), pg, pb, 0, st, a, 0, 2);
-      hipLaunchKernelGGL((k_merge_bucket<true, false, 8>), pg, pb, 0, st, a, 3, 4);
-      hipLaunchKernelGGL((k_merge_bucket<true, false, 16>), pg, pb, 0, st, a, 5, 7);
-      hipLaunchKernelGGL((k_merge_bucket<true, false, 32>), pg, pb, 0, st, a, 8, 9);
-      if (split) hipLaunchKernelGGL((k_merge_long_split<true, false>), dim3(kLongGrid), dim3(64), 0, st, a);
-      else hipLaunchKernelGGL((k_merge_long_lds<true, false>), dim3(kLongGrid), dim3(64), 0, st, a);
-      hipLaunchKernelGGL((k_merge_long<true>), dim3(512), pb, 0, st, a);
+      hipLaunchKernelGGL((k_merge_bucket<true, false, 32>), pg, pb, 0, ms[0], a, 8, 9);
+      hipLaunchKernelGGL((k_merge_bucket<true, false, 16>), pg, pb, 0, ms[1], a, 5, 7);
+      hipLaunchKernelGGL((k_merge_bucket<true, false, 8>), pg, pb, 0, ms[2], a, 3, 4);
+      hipLaunchKernelGGL((k_merge_bucket<true, false, 4>), pg, pb, 0, ms[2], a, 0, 2);
+      if (split) hipLaunchKernelGGL((k_merge_long_split<true, false>), dim3(kLongGrid), dim3(64), 0, ms[3], a);
+      else hipLaunchKernelGGL((k_merge_long_lds<true, false>), dim3(kLongGrid), dim3(64), 0, ms[3], a);
+      hipLaunchKernelGGL((k_merge_long<true>), dim3(512), pb, 0, ms[3], a);
     } else if (h->ids16) {
-      hipLaunchKernelGGL((k_merge_bucket<false, true, 4>), pg, pb, 0, st, a, 0, 2);
-      hipLaunchKernelGGL((k_merge_bucket<false, true, 8>), pg, pb, 0, st, a, 3, 4);
-      hipLaunchKernelGGL((k_merge_bucket<false, true, 16>), pg, pb, 0, st, a, 5, 7);
-      hipLaunchKernelGGL((k_merge_bucket<false, true, 32>), pg, pb, 0, st, a, 8, 9);
-      if (split) hipLaunchKernelGGL((k_merge_long_split<false, true>), dim3(kLongGrid), dim3(64), 0, st, a);
-      else hipLaunchKernelGGL((k_merge_long_lds<false, true>), dim3(kLongGrid), dim3(64), 0, st, a);
-      hipLaunchKernelGGL((k_merge_long<false>), dim3(512), pb, 0, st, a);
+      hipLaunchKernelGGL((k_merge_bucket<false, true, 32>), pg, pb, 0, ms[0], a, 8, 9);
+      hipLaunchKernelGGL((k_merge_bucket<false, true, 16>), pg, pb, 0, ms[1], a, 5, 7);
+      hipLaunchKernelGGL((k_merge_bucket<false, true, 8>), pg, pb, 0, ms[2], a, 3, 4);
+      hipLaunchKernelGGL((k_merge_bucket<false, true, 4>), pg, pb, 0, ms[2], a, 0, 2);
+      if (split) hipLaunchKernelGGL((k_merge_long_split<false, true>), dim3(kLongGrid), dim3(64), 0, ms[3], a);
+      else hipLaunchKernelGGL((k_merge_long_lds<false, true>), dim3(kLongGrid), dim3(64), 0, ms[3], a);
+      hipLaunchKernelGGL((k_merge_long<false>), dim3(512), pb, 0, ms[3], a);
     } else {
-      hipLaunchKernelGGL((k_merge_bucket<false, false, 4>), pg, pb, 0, st, a, 0, 2);
-      hipLaunchKernelGGL((k_merge_bucket<false, false, 8>), pg, pb, 0, st, a, 3, 4);
-      hipLaunchKernelGGL((k_merge_bucket<false, false, 16>), pg, pb, 0, st, a, 5, 7);
-      hipLaunchKernelGGL((k_merge_bucket<false, false, 32>), pg, pb, 0, st, a, 8, 9);
-      if (split) hipLaunchKernelGGL((k_merge_long_split<false, false>), dim3(kLongGrid), dim3(64), 0, st, a);
-      else hipLaunchKernelGGL((k_merge_long_lds<false, false>), dim3(kLongGrid), dim3(64), 0, st, a);
-      hipLaunchKernelGGL((k_merge_long<false>), dim3(512), pb, 0, st, a);
+      hipLaunchKernelGGL((k_merge_bucket<false, false, 32>), pg, pb, 0, ms[0], a, 8, 9);
+      hipLaunchKernelGGL((k_merge_bucket<false, false, 16>), pg, pb, 0, ms[1], a, 5, 7);
+      hipLaunchKernelGGL((k_merge_bucket<false, false, 8>), pg, pb, 0, ms[2], a, 3, 4);
+      hipLaunchKernelGGL((k_merge_bucket<false, false, 4>), pg, pb, 0, ms[2], a, 0, 2);
+      if (split) hipLaunchKernelGGL((k_merge_long_split<false, false>), dim3(kLongGrid), dim3(64), 0, ms[3], a);
+      else hipLaunchKernelGGL((k_merge_long_lds<false, false>), dim3(kLongGrid), dim3(64), 0, ms[3], a);
+      hipLaunchKernelGGL((k_merge_long<false>), dim3(512), pb, 0, ms[3], a);
+    }
+    if (h->merge_fork) {
+      for (int k = 0; k < 3; ++k) {
+        HIP_TRY(hipEventRecord(h->ev_join[k], h->s_fork[k]));
+        HIP_TRY(hipStreamWaitEvent(st, h->ev_join[k], 0));
+      }
     }
     HIP_TRY(hipGetLastError());
     const dim3 wg((unsigned)((n_tiles + 3) / 4));  // one wave per tile

@@ -10,7 +10,9 @@ k_merge_bucket x4, k_merge_long*, k_tile_count + scan, k_compact, k_string_offse
   N>1  configs[3]: every rank encodes its own 1 GiB corpus (seed + rank; doc-sharded), then the
        token-id buffers are reassembled on every rank with an RCCL all-gather (padded to the
        largest rank's count; 16-bit ids when every id fits) -- weak scaling, the gather is inside
-       the step (--no-gather: without it).
+       the step (--no-gather: without it); batch k's gather runs on RCCL's stream beside batch
+       k+1's encode, every gather waited on before the clock stops (--no-overlap: one after the
+       other).
 Prints ONE JSON line (rank 0).  Launch for N>1:
   python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \\
       --master-port P bench.py --gpus N
@@ -44,6 +46,10 @@ def parse():
     ap.add_argument("--presplit", default="device", choices=["device", "host"],
                     help="device: C2 full path (pre-split inside the step); host: C3 (bitmap made on the host)")
     ap.add_argument("--no-gather", action="store_true", help="N>1: skip the RCCL reassembly")
+    ap.add_argument("--gather-world1", action="store_true",
+                    help="testing: N=1 with an RCCL process group and the reassembly in the step")
+    ap.add_argument("--no-overlap", action="store_true",
+                    help="N>1: each step's reassembly completes before the next step's encode")
     ap.add_argument("--cpu-sample-mb", type=float, default=320.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--e2e-steps", type=int, default=2,
@@ -100,7 +106,10 @@ def main():
 
     from shredword_amd import Tokenizer, _lib, corpus, shard
 
-    if world > 1:
+    use_dist = world > 1 or args.gather_world1
+    if use_dist:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29533")
         dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", local))
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
@@ -166,7 +175,7 @@ def main():
     n_tok_c = ctypes.c_int64()
     encode(ctypes.byref(n_tok_c))
     n_tok = int(n_tok_c.value)
-    gather = world > 1 and not args.no_gather
+    gather = use_dist and not args.no_gather
     id_bits = 16 if tok.ids16 else 32  # (the ids cross xGMI as 16 bits when every id fits: SURVEY.md 8(e))
 
     # the gathers' widths: every rank's counts are the same every step (same corpus), so the
@@ -177,15 +186,40 @@ def main():
         dist.all_reduce(mx, op=dist.ReduceOp.MAX)
         width, width_s = int(mx[0].item()), int(mx[1].item()) + 1
 
+    # N>1: batch k's reassembly (RCCL, on its own stream) overlaps batch k+1's encode; two sets of
+    # output buffers, and a set is rewritten only after its gathers have been waited on
+    overlap = gather and not args.no_overlap
+    outs = [(d_out, d_oo)]
+    if overlap:
+        outs.append((torch.empty_like(d_out), torch.empty_like(d_oo)))
+    pending = [[] for _ in outs]
+    n_step = [0]
+
     def step():
-        encode()
-        if gather:  # shard.reassemble: one counts all-gather, padded id and offset all-gathers (RCCL)
-            return shard.reassemble(d_out, d_oo, None, dev, concat=False, width=width, width_s=width_s,
-                                    id_bits=id_bits)
-        return None
+        slot = n_step[0] % len(outs)
+        n_step[0] += 1
+        for w in pending[slot]:
+            w.wait()
+        pending[slot] = []
+        o_ids, o_off = outs[slot]
+        _lib.check(L.sw_encode_device(h, d_buf.data_ptr(), n_bytes, d_off.data_ptr(), n_str,
+                                      d_bits.data_ptr() if host_ps else None, o_ids.data_ptr(), o_off.data_ptr(),
+                                      stream, None))
+        if overlap:  # shard.reassemble: one counts all-gather, padded id and offset all-gathers (RCCL)
+            pending[slot], _ = shard.reassemble(o_ids, o_off, None, dev, concat=False, width=width, width_s=width_s,
+                                                id_bits=id_bits, async_op=True)
+        elif gather:
+            shard.reassemble(o_ids, o_off, None, dev, concat=False, width=width, width_s=width_s, id_bits=id_bits)
+
+    def finish():  # every issued reassembly waited on (the caller's stream)
+        for p in pending:
+            for w in p:
+                w.wait()
+            p.clear()
 
     for _ in range(args.warmup):
         step()
+    finish()
     _lib.check(L.sw_encoder_set_timing(h, 1))
     if world > 1:
         dist.barrier()
@@ -193,6 +227,7 @@ def main():
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
+    finish()
     torch.cuda.synchronize()
     t1 = time.perf_counter()
     if world > 1:
@@ -331,7 +366,7 @@ def main():
                        "presplit": args.presplit,
                        "bytes_per_rank": n_bytes, "strings_per_rank": n_str, "merges": len(tok.merges),
                        "model": model, "pattern": args.pattern, "parallelism": "doc-shard x%d" % world,
-                       "gather_in_step": gather, "gather_id_bits": id_bits if gather else None,
+                       "gather_in_step": gather, "gather_overlaps_next_encode": overlap, "gather_id_bits": id_bits if gather else None,
                        "chunk_table": not args.no_chunk_table,
                        "dedupe": not args.no_dedupe},
             "mtok_per_s": round(all_tok * args.steps / sec / 1e6, 3),
@@ -346,7 +381,7 @@ def main():
         }
         print(json.dumps(line), flush=True)
     tok.close()
-    if world > 1:
+    if use_dist:
         dist.destroy_process_group()
 
 

@@ -41,7 +41,8 @@ def shard_of(buf, str_off, lo, hi):
     return buf[a:b], str_off[lo:hi + 1] - a
 
 
-def reassemble(local_ids, local_off, group=None, device=None, concat=True, width=None, width_s=None, id_bits=32):
+def reassemble(local_ids, local_off, group=None, device=None, concat=True, width=None, width_s=None, id_bits=32,
+               async_op=False):
     """Collective reassembly of per-rank encodes (steps 1-4 above) on every rank.
 
     local_ids: torch int32 [>= local count] on `device`; local_off: torch int64 [m+1] with
@@ -58,24 +59,36 @@ def reassemble(local_ids, local_off, group=None, device=None, concat=True, width
     string counts [world] on the device, width_s) -- rank r's ids start at r * width.
     id_bits=16 (every id < 65536, e.g. SW_INFO_IDS16): the ids travel as 16 bits; concat=True
     widens them to int32, concat=False returns them as int16 holding the low 16 bits (an id is
-    `x & 0xFFFF` of the widened value)."""
+    `x & 0xFFFF` of the widened value).
+    async_op=True (concat=False and both widths given): the collectives are only issued; returns
+    (works, result) where result is concat=False's tuple, valid once every work in `works` has
+    been waited on (Work.wait(): with RCCL the caller's stream waits, the host does not).  The
+    next batch's encode can run meanwhile -- the reassembly of batch k overlaps the encode of
+    batch k + 1; local_ids / local_off must not be rewritten before the wait."""
     import torch
     import torch.distributed as dist
 
+    if async_op and (concat or width is None or width_s is None):
+        raise ValueError("reassemble: async_op needs concat=False and both width bounds")
     world = dist.get_world_size(group)
-    rank = dist.get_rank(group)
+    works = []
+
+    def gather(out, inp):
+        w = dist.all_gather_into_tensor(out, inp, group=group, async_op=async_op)
+        if async_op:
+            works.append(w)
     dev = device if device is not None else local_ids.device
     mine = torch.empty(2, dtype=torch.int64, device=dev)
     mine[0:1] = local_off[-1:].to(device=dev, dtype=torch.int64)
     mine[1] = local_off.numel() - 1
     both = torch.empty(2 * world, dtype=torch.int64, device=dev)
-    dist.all_gather_into_tensor(both, mine, group=group)  # [count_0, n_str_0, count_1, ...]
+    gather(both, mine)  # [count_0, n_str_0, count_1, ...]
     counts, n_strs = both[0::2], both[1::2]
     if width is None or width_s is None:  # the one host synchronisation: the gathers' sizes
         h = both.cpu().tolist()
         width = max(max(h[0::2]), 1) if width is None else width
         width_s = max(max(h[1::2]), 1) if width_s is None else width_s
-    else:
+    elif not concat:  # (concat=True checks the counts itself below)
         _pending_checks.append((counts, n_strs, width, width_s))
     width, width_s = int(width), int(width_s)
     if id_bits not in (16, 32):
@@ -89,12 +102,12 @@ def reassemble(local_ids, local_off, group=None, device=None, concat=True, width
     wide = id_bits == 32
     if wide:
         recv = torch.empty(world * width, dtype=torch.int32, device=dev)
-        dist.all_gather_into_tensor(recv, send, group=group)
+        gather(recv, send)
     else:  # the low 16 bits of each id (two's-complement truncation), moved as bytes (RCCL and gloo
         # have no 16-bit integer type; an all-gather only copies)
         send = send.to(torch.int16)
         recv = torch.empty(world * width, dtype=torch.int16, device=dev)
-        dist.all_gather_into_tensor(recv.view(torch.uint8), send.view(torch.uint8), group=group)
+        gather(recv.view(torch.uint8), send.view(torch.uint8))
     m = local_off.numel() - 1
     if local_off.numel() >= width_s and local_off.dtype == torch.int64 and local_off.device == dev:
         send_o = local_off[:width_s]
@@ -102,9 +115,10 @@ def reassemble(local_ids, local_off, group=None, device=None, concat=True, width
         send_o = torch.zeros(width_s, dtype=torch.int64, device=dev)
         send_o[:min(m, width_s)] = local_off[:min(m, width_s)].to(device=dev, dtype=torch.int64)
     recv_o = torch.empty(world * width_s, dtype=torch.int64, device=dev)
-    dist.all_gather_into_tensor(recv_o, send_o, group=group)
+    gather(recv_o, send_o)
     if not concat:
-        return recv, counts, width, recv_o, n_strs, width_s
+        res = (recv, counts, width, recv_o, n_strs, width_s)
+        return (works, res) if async_op else res
     if not wide:
         recv = recv.to(torch.int32) & 0xFFFF
     # the concatenation needs the counts on the host (as torch's slicing does)

@@ -63,4 +63,21 @@ def test_encode_sharded_rccl_world1(nccl_world1, fixture, model):
     shard.check_bounds()
     assert r16[0].dtype == torch.int16
     np.testing.assert_array_equal((r16[0][:n].to(torch.int32) & 0xFFFF).cpu().numpy(), d["ids"])
+    # the bench's overlapped step: batch k's gathers issued (RCCL stream), batch k+1 encoded into
+    # the other buffers meanwhile, then every gather waited on (the stream waits, not the host)
+    outs = [(torch.empty(len(d["bytes"]), dtype=torch.int32, device="cuda"),
+             torch.empty(len(d["off"]), dtype=torch.int64, device="cuda")) for _ in range(2)]
+    flights = []
+    for o_ids, o_off in outs:
+        tok.encode_device(d_buf, d_off, d_out=o_ids, d_out_off=o_off)
+        flights.append(shard.reassemble(o_ids, o_off, None, torch.device("cuda", 0), concat=False,
+                                        width=len(d["bytes"]), width_s=len(d["off"]), id_bits=16, async_op=True))
+    for works, res in flights:
+        for w in works:
+            w.wait()
+        torch.cuda.synchronize()
+        assert int(res[1][0].item()) == n
+        np.testing.assert_array_equal((res[0][:n].to(torch.int32) & 0xFFFF).cpu().numpy(), d["ids"])
+        np.testing.assert_array_equal(res[3][:len(d["off"]) - 1].cpu().numpy(), d["ids_off"][:-1])
+    shard.check_bounds()
     tok.close()

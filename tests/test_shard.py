@@ -80,6 +80,29 @@ def _rank_main(rank, world, port, fixture, model, result_dir):
         r16 = shard.reassemble(torch.from_numpy(ids), torch.from_numpy(ids_off), None, torch.device("cpu"),
                                concat=False, id_bits=16)
         ok = ok and r16[0].dtype == torch.int16
+        # issued only (async_op): two batches in flight, then waited on -- both the whole batch
+        t_ids, t_off = torch.from_numpy(ids), torch.from_numpy(ids_off)
+        flights = [shard.reassemble(t_ids, t_off, None, torch.device("cpu"), concat=False, width=len(buf),
+                                    width_s=len(off), id_bits=bits, async_op=True) for bits in (16, 32)]
+        for works, res in flights:
+            for w in works:
+                w.wait()
+            recv, counts, width, recv_o, n_strs, width_s = res
+            got_ids, got_off, disp = [], [], 0
+            for r in range(world):
+                c, m = int(counts[r]), int(n_strs[r])
+                got_ids.append(recv[r * width: r * width + c].to(torch.int32) & 0xFFFF)
+                got_off.append(recv_o[r * width_s: r * width_s + m] + disp)
+                disp += c
+            got_off.append(torch.tensor([disp]))
+            ok = ok and np.array_equal(torch.cat(got_ids).numpy(), d["ids"])
+            ok = ok and np.array_equal(torch.cat(got_off).numpy(), d["ids_off"])
+        shard.check_bounds()
+        try:  # async needs the bounds (no host synchronisation allowed)
+            shard.reassemble(t_ids, t_off, None, torch.device("cpu"), concat=False, async_op=True)
+            ok = False
+        except ValueError:
+            pass
         with open(os.path.join(result_dir, "rank%d" % rank), "w") as f:
             f.write("ok" if ok else "mismatch")
     finally:

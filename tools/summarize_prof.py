@@ -49,12 +49,29 @@ def main():
 
     per_launch_ms = sum(float(r["AverageNs"]) * per_launch(r["Name"].split("(")[0].replace("void ", ""))
                         for r in rows if r["Name"].startswith(("sw::", "void sw::"))) / 1e6
+    spans = []  # wall span of each launch (k_tile_strings start .. k_string_offsets end): the
+    # merge kernels run side by side on forked streams, so the kernel-time sum over-counts them
+    tr = os.path.join(src, "trace", "run_kernel_trace.csv")
+    if os.path.exists(tr):
+        ev = sorted(((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"])
+                     for r in csv.DictReader(open(tr))), key=lambda x: x[0])
+        t_start = None
+        for a0, b0, nm in ev:
+            if "k_tile_strings" in nm:
+                t_start = a0
+            elif "k_string_offsets" in nm and t_start is not None:
+                spans.append((b0 - t_start) / 1e6)
+                t_start = None
+    span_txt = ("  Wall span per launch (first kernel start to last kernel end, from the kernel trace): "
+                "**%.3f ms** median, %.3f ms min over %d launches (the first includes one-time setup)." % (
+                    sorted(spans)[len(spans) // 2], min(spans), len(spans))
+                if spans else "")
     lines = ["# rocprofv3 summary: %s" % tag, "",
              "Command: `tools/profile_gpu.sh %s` (bench.py --steps 3 --warmup 1 --no-cpu-baseline; kernel trace + "
              "stats pass, then one rocprofv3 --pmc pass per counter group)." % tag, "",
              "Encode launches traced: %d.  Sum of the pipeline's kernel time per launch: **%.3f ms** "
              "(per launch = average x dispatches per launch; bench.py's one extra pre-split for the "
-             "chunk count, outside the timed steps, is not counted)." % (launches, per_launch_ms), "",
+             "chunk count, outside the timed steps, is not counted)." % (launches, per_launch_ms) + span_txt, "",
              "| kernel | calls | avg ms | per launch ms | % |", "|---|---|---|---|---|"]
     for r in rows:
         nm = r["Name"].split("(")[0].replace("void ", "")
@@ -94,7 +111,7 @@ def main():
     for ln in open(os.path.join(src, "trace.log"), errors="replace"):
         if ln.startswith("{") and '"metric"' in ln:
             bench = json.loads(ln)
-    if bench and "traffic_bytes_per_launch" in derived:
+    if bench and "traffic_bytes_per_launch" in derived and bench["config"].get("workload", "").startswith("C2:"):
         with open(os.path.join(out, "traffic.json"), "w") as f:
             json.dump({"source": "profiles/%s.md" % tag, "n_bytes": bench["config"]["bytes_per_rank"],
                        "merges": bench["config"]["merges"], "pattern": bench["config"]["pattern"],

@@ -260,7 +260,7 @@ def main():
     b_algo = n_bytes + 4 * n_tok + 16 * (n_str + 1) + ((n_bytes + 7) // 8 if host_ps else 0)
     achieved = b_algo / (k_ms * 1e-3) / 1e9 if k_ms > 0 else None
     # traffic: HBM bytes per launch from the committed PMC profile of this same workload, if any
-    traffic, traffic_x2, traffic_src = None, None, None
+    traffic, traffic_x2, traffic_src, counters = None, None, None, None
     try:
         with open(os.path.join(ROOT, "profiles", "traffic.json")) as f:
             tj = json.load(f)
@@ -269,6 +269,7 @@ def main():
                 and tj.get("presplit", "host") == args.presplit):
             traffic, traffic_src = int(tj["traffic_bytes_per_launch"]), tj["source"]
             traffic_x2 = int(tj.get("traffic_bytes_per_launch_x2", 0)) or None
+            counters = tj.get("counters")
     except (OSError, ValueError, KeyError):
         pass
     roofline = {"bound": "hbm", "achieved": round(achieved, 2) if achieved else None, "peak": HBM_PEAK_GBS,
@@ -281,7 +282,8 @@ def main():
                                 "bound here)",
                 "traffic_source": traffic_src, "kernel": ("sw_encode_device pipeline (k_presplit..k_string_offsets)" if not host_ps else "sw_encode_device pipeline (k_tile_strings..k_string_offsets)"),
                 "kernel_ms": round(k_ms, 4),
-                "algo_bytes_per_launch": int(b_algo)}
+                "algo_bytes_per_launch": int(b_algo),
+                "counters": counters}
 
     # PCIe-inclusive rate (rank 0, N=1): the same batch from pageable host buffers to host
     # buffers through sw_encode_batch (Tokenizer.encode_packed).  Reported beside, never `value`.

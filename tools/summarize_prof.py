@@ -119,6 +119,21 @@ def main():
                        "presplit": bench["config"].get("presplit", "host"),
                        "traffic_bytes_per_launch": derived["traffic_bytes_per_launch"],
                        "traffic_bytes_per_launch_x2": derived["traffic_bytes_per_launch_x2"],
+                       # the LDS bank-conflict and VALU counters beside the bytes
+                       "counters": {"valu_wave_insts": tot.get("SQ_INSTS_VALU"),
+                                    "valu_issue_floor_ms": (tot["SQ_INSTS_VALU"] * 2 / 1024 / 2.4e6
+                                                            if "SQ_INSTS_VALU" in tot else None),
+                                    "lds_insts": tot.get("SQ_INSTS_LDS"),
+                                    "lds_bank_conflict_cycles": tot.get("SQ_LDS_BANK_CONFLICT"),
+                                    "lds_conflict_cycles_per_lds_inst": (
+                                        tot["SQ_LDS_BANK_CONFLICT"] / tot["SQ_INSTS_LDS"]
+                                        if tot.get("SQ_INSTS_LDS") else None),
+                                    "wait_fraction_of_wave_cycles": (
+                                        tot["SQ_WAIT_ANY"] / tot["SQ_WAVE_CYCLES"]
+                                        if tot.get("SQ_WAVE_CYCLES") else None),
+                                    "l2_hit_rate": derived.get("l2_hit_rate"),
+                                    "note": "pipeline totals per launch; VALU floor = wave instructions x 2 "
+                                            "cycles / 1024 SIMDs / 2.4 GHz"},
                        "note": "FETCH_SIZE+WRITE_SIZE summed over the pipeline's kernels per launch (raw FETCH; "
                                "_x2 doubles FETCH per the gfx950 wide-read correction)"}, f, indent=1)
     print("\n".join(lines))

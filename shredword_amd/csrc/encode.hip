@@ -126,6 +126,7 @@ struct sw_encoder {
   uint64_t* d_dtab = nullptr;         // chunk dedupe table
   uint32_t dmask = 0;
   uint4* d_dres = nullptr;            // dense result heads, one per table entry
+  uint8_t* d_dcnt = nullptr;          // their id counts (<= 32), one byte per table entry
   uint32_t* d_big = nullptr;          // chunks over kLongLds bytes: count, then their long-bucket indices
   bool dedupe = true;
   bool dedupe_exact = true;           // SW_OPT_DEDUPE_EXACT
@@ -173,8 +174,8 @@ void free_workspace(sw_encoder* h) {
   h->d_tile_slo = nullptr; h->d_stamps = nullptr; h->d_tile_slots = nullptr; h->d_tile_nref = nullptr; h->d_rlist = nullptr; h->d_queue = nullptr;
   h->d_bcnt = nullptr; h->d_boff = nullptr; h->d_qtotal = nullptr;
   (void)hipFree(h->d_dtab); (void)hipFree(h->d_tile_base); (void)hipFree(h->d_tile_cnt);
-  (void)hipFree(h->d_dres); (void)hipFree(h->d_big);
-  h->d_dres = nullptr; h->d_big = nullptr;
+  (void)hipFree(h->d_dres); (void)hipFree(h->d_big); (void)hipFree(h->d_dcnt);
+  h->d_dres = nullptr; h->d_big = nullptr; h->d_dcnt = nullptr;
   (void)hipFree(h->d_total);
   h->d_scratch = nullptr; h->d_res = nullptr; h->d_pbits = nullptr; h->d_pcount = nullptr; h->d_part = nullptr;
   h->d_dtab = nullptr; h->d_tile_base = nullptr; h->d_tile_cnt = nullptr; h->d_total = nullptr;
@@ -225,6 +226,7 @@ int32_t ensure_workspace(sw_encoder* h, int64_t n_bytes) {
     while (slots < nb / 64 && slots < (1LL << 22)) slots <<= 1;
     HIP_TRY(hipMalloc(&h->d_dtab, sizeof(uint64_t) * slots));
     HIP_TRY(hipMalloc(&h->d_dres, sizeof(uint4) * slots));
+    HIP_TRY(hipMalloc(&h->d_dcnt, slots));
     h->dmask = (uint32_t)(slots - 1);
   }
   HIP_TRY(hipMalloc(&h->d_big, sizeof(uint32_t) * (nb / (kLongLds + 1) + 2)));  // (count + list)
@@ -607,6 +609,7 @@ extern "C" int32_t sw_encode_device(sw_encoder* h, const uint8_t* d_bytes, int64
     a.dmask = h->dedupe_slots ? std::min<uint32_t>(h->dmask, (uint32_t)(h->dedupe_slots - 1)) : h->dmask;
     a.dexact = h->dedupe_exact ? (uint32_t)kDdExactMax : 0u;
     a.dres = h->d_dres;
+    a.dcnt = h->d_dcnt;
     a.big_count = h->d_big; a.big_list = h->d_big + 1;
     a.out_off = d_out_off; a.tile_slo = h->d_tile_slo;
     a.n_tiles = n_tiles; a.qtmp = h->d_res; a.bcnt = h->d_bcnt; a.boff = h->d_boff; a.q_total = h->d_qtotal;

@@ -456,6 +456,7 @@ struct EncArgs {
   uint32_t dedupe;           // 0: every queued chunk runs its own merge loop
   uint32_t dexact;           // longest exact dedupe key (kDdExactMax, or 0: every key verified)
   uint4* dres;               // [dmask + 1] dense result heads (slot_dref), by table entry
+  uint8_t* dcnt;             // [dmask + 1] their id counts (<= 32): k_tile_count's reads stay in L2
   unsigned long long* stamps;  // SW_STAMPS builds: cycles per phase, summed
   const uint2* inv;          // [n_inv] merge value -> its pair (a, b); well-formed tables only
   uint32_t n_inv;
@@ -954,6 +955,7 @@ __device__ __forceinline__ void merge_entry(const EncArgs& a, const uint32_t* wo
   if (did != kNoDid) {
     if (k16) a.dres[did] = make_uint4((uint32_t)m | h0, m <= 7 ? h1 : (uint32_t)start, h2, h3);
     else a.dres[did] = make_uint4((uint32_t)m, h1, h2, m <= 3 ? h3 : (uint32_t)start);
+    a.dcnt[did] = (uint8_t)m;
   }
 }
 
@@ -1790,9 +1792,13 @@ __device__ __forceinline__ uint4 ref_head(const EncArgs& a, int32_t v) {
 constexpr int kRoundsInFlight = SW_ROUNDS_IN_FLIGHT;  // slot rounds whose loads (then gathers) issue together
 
 // id count of the result a reference-list entry names
+// (a dense result's count from the byte array: 4 MiB at most, so these random reads mostly hit
+// L2 where the 16-byte heads (64 MiB) went to the Infinity Cache; both loads issue together)
 __device__ __forceinline__ uint32_t ref_count(const EncArgs& a, uint32_t r) {
-  const uint32_t w = *((r & kRlDense) ? (const uint32_t*)(a.dres + (r & ~kRlDense)) : a.res + 2 * (int64_t)r);
-  return (r & kRlDense) ? (w & 0xFFFFu) : w;
+  const bool dn = (r & kRlDense) != 0;
+  const uint32_t c8 = a.dcnt[dn ? (r & ~kRlDense) : 0u];
+  const uint32_t c32 = a.res[dn ? 0 : 2 * (int64_t)r];
+  return dn ? c8 : c32;
 }
 
 __global__ void __launch_bounds__(kThreads) k_tile_count(EncArgs a) {

@@ -68,6 +68,20 @@ def test_golden_bit_exact(entry):
     assert_same(got, (fx["ids"], fx["ids_off"]))
 
 
+@pytest.mark.parametrize("fork", [0, 1])
+def test_merge_streams_option(fork):
+    """The length buckets' merge kernels forked onto parallel streams (default) or one after
+    another on the launch stream: the same ids as the reference-generated fixtures."""
+    for entry in golden_index()["fixtures"]:
+        fx = load_fixture(entry)
+        t = sa.Tokenizer(device=0)
+        t.merges = load_model_merges(entry["model"])
+        t.pattern = PAT_STR[entry["pattern"]]
+        _lib.check(_lib.lib().sw_encoder_set_option(t._encoder(), _lib.SW_OPT_MERGE_STREAMS, fork))
+        assert_same(gpu_encode(t, fx["bytes"], fx["off"]), (fx["ids"], fx["ids_off"]))
+        t.close()
+
+
 def test_tokenizer_encode_decode_surface():
     t = tok_for("bl32k.model")
     text = "Hello world's 12345 \n\n  x 中文 😀"

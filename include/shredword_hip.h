@@ -135,6 +135,12 @@ int32_t sw_encoder_reserve(sw_encoder* h, int64_t max_bytes, int64_t max_strings
  *                          run side by side on forked streams (joined before the counts); 0: one
  *                          after another on the launch stream.  Results identical. */
 #define SW_OPT_MERGE_STREAMS 13
+/*   SW_OPT_PRESPLIT_SEGMENTS  1 .. 16 (default 1): > 1: sw_encode_device's device pre-split runs as
+ *                          this many segments (1 MiB at least) on a second stream, and k_classify
+ *                          of segment k runs beside the pre-split of segment k + 1 (an A/B knob:
+ *                          slower on MI355X); 1: one pre-split launch, then k_classify.  Same ids
+ *                          either way. */
+#define SW_OPT_PRESPLIT_SEGMENTS 14
 int32_t sw_encoder_set_option(sw_encoder* h, int32_t option, int64_t value);
 
 /* Encoder facts (sw_encoder_get_info): distinct merges, whole-chunk table entries, whether the

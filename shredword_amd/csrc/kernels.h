@@ -463,6 +463,12 @@ struct EncArgs {
   uint32_t* big_list;        // queued chunks over kLongLds bytes (their index in the long bucket)
   uint32_t* big_count;       // ... how many (cleared per launch)
   uint32_t ids16;            // every id fits 16 bits (dres layout)
+  // k_classify over a segment of the tiles while the pre-split of the next segment runs
+  // (sw_encode_device): tiles [tile0, tile_end); bitmap words below bits_ready are final.  A tile
+  // that needs a word at or past bits_ready (< n_words) is listed in defer (count, then tile
+  // indices) and classified by k_classify_deferred once the whole bitmap is written.
+  int64_t tile0, tile_end, bits_ready;
+  uint32_t* defer;
 };
 
 #ifdef SW_STAMPS
@@ -636,6 +642,11 @@ __device__ __forceinline__ void classify_tile(const EncArgs& a, int64_t tile, ui
   const int64_t t0 = tile * kTile;
   const int64_t t1 = min(t0 + (int64_t)kTile, a.n_bytes);
   const int64_t w0 = t0 >> 6;
+  const bool partial_bits = a.bits_ready < a.n_words;  // (wave-uniform)
+  if (partial_bits && w0 + kTileWords > a.bits_ready) {  // the halo word is not written yet
+    if (lane == 0) a.defer[1 + atomicAdd(&a.defer[0], 1u)] = (uint32_t)tile;
+    return;
+  }
 
   // 1. stage the window's bytes (1-KiB coalesced 16-byte loads) and the bitmap words (in
   //    registers)
@@ -696,7 +707,13 @@ __device__ __forceinline__ void classify_tile(const EncArgs& a, int64_t tile, ui
       const int64_t q = t0 + 64 * (int64_t)src + __ffsll((long long)__shfl(hw, src, 64)) - 1;
       last_end = min(q, a.n_bytes);
     } else if (C > 0) {
-      last_end = min(next_set_bit(a.bits, a.n_words, t0 + 64 * kTileWords, a.n_bytes), a.n_bytes);
+      // (a chunk running past the halo: scan the written words only; none set there -> defer)
+      const int64_t q = next_set_bit(a.bits, a.bits_ready, t0 + 64 * kTileWords, a.n_bytes);
+      if (partial_bits && q >= a.n_bytes) {
+        if (lane == 0) a.defer[1 + atomicAdd(&a.defer[0], 1u)] = (uint32_t)tile;
+        return;
+      }
+      last_end = min(q, a.n_bytes);
     }
   }
   const int rel_end = (int)(last_end - t0);
@@ -835,8 +852,19 @@ __global__ void __launch_bounds__(kThreads) SW_CLS_ATTR k_classify(EncArgs a) {
   __shared__ uint16_t s_cs_all[kWaves][kTile + 1];   // chunk starts (tile-relative)
   __shared__ uint16_t s_qb_all[kWaves][kQBuf];       // chunks not settled by a lookup, to dedupe
   const int wv = threadIdx.x >> 6;
-  const int64_t tile = (int64_t)blockIdx.x * kWaves + wv;
-  if (tile < a.n_tiles) classify_tile(a, tile, s_b32_all[wv], s_cs_all[wv], s_qb_all[wv]);
+  const int64_t tile = a.tile0 + (int64_t)blockIdx.x * kWaves + wv;
+  if (tile < a.tile_end) classify_tile(a, tile, s_b32_all[wv], s_cs_all[wv], s_qb_all[wv]);
+}
+
+// the tiles k_classify deferred (a.defer), once the whole bitmap is written (bits_ready = n_words)
+__global__ void __launch_bounds__(kThreads) SW_CLS_ATTR k_classify_deferred(EncArgs a) {
+  __shared__ __attribute__((aligned(16))) uint32_t s_b32_all[kWaves][kWinWords];
+  __shared__ uint16_t s_cs_all[kWaves][kTile + 1];
+  __shared__ uint16_t s_qb_all[kWaves][kQBuf];
+  const int wv = threadIdx.x >> 6;
+  const uint32_t n = a.defer[0];  // (counted by the earlier launches)
+  for (uint32_t i = blockIdx.x * kWaves + wv; i < n; i += gridDim.x * kWaves)
+    classify_tile(a, (int64_t)a.defer[1 + i], s_b32_all[wv], s_cs_all[wv], s_qb_all[wv]);
 }
 
 // ---------------------------------------------------------------------------------------

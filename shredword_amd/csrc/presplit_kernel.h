@@ -248,6 +248,7 @@ struct PbArgs {
   const int64_t* str_off;
   int64_t n_str;
   const int64_t* tile_slo;  // first string starting at or after each 2 KiB tile (k_tile_strings)
+  int64_t blk0;             // first block of this launch (a segment of the batch, see sw_encode_device)
 };
 
 // string-start bits of bytes [p, p + 32) from str_off (batch end included): global fallback
@@ -326,7 +327,7 @@ __global__ void __launch_bounds__(kPbThreads, SW_PB_WAVES) k_presplit_bits(PbArg
   __shared__ uint32_t s_ss[kPbSsWords];
   __shared__ __attribute__((aligned(16))) uint32_t s_b[kPbStage / 4 + 4];  // bytes [b0 - kPbPre, ..)
   const int tid = threadIdx.x;
-  const int64_t b0 = (int64_t)blockIdx.x * kPbBlock, c0 = b0 / psb::kChunk;
+  const int64_t b0 = (g.blk0 + (int64_t)blockIdx.x) * kPbBlock, c0 = b0 / psb::kChunk;
   const int64_t n_chunks = (g.n_bytes + psb::kChunk - 1) / psb::kChunk;
   const bool cl = pattern == 0;
   if (SW_PB_STAGE && pattern != 2) {  // the block's bytes (zeros outside the batch), coalesced, before anything waits

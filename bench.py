@@ -61,6 +61,8 @@ def parse():
     ap.add_argument("--dedupe-slots", type=int, default=0, help="A/B only: cap the dedupe table (power of two)")
     ap.add_argument("--no-dedupe-exact", action="store_true", help="A/B only: fingerprint keys for every chunk")
     ap.add_argument("--no-merge-streams", action="store_true", help="A/B only: merge kernels one after another")
+    ap.add_argument("--fused-compact", action="store_true",
+                    help="A/B only: the one-pass look-back k_compact_lb instead of k_tile_count + scan + k_compact")
     ap.add_argument("--presplit-segs", type=int, default=0,
                     help="A/B only: device pre-split segments overlapped with k_classify (1 = none; 0 = library default)")
     ap.add_argument("--pipe-dma", action="store_true", help="A/B only: e2e pipeline copies by DMA, not kernels")
@@ -141,6 +143,8 @@ def main():
     _lib.check(L.sw_encoder_set_option(h, _lib.SW_OPT_DEDUPE_SLOTS, args.dedupe_slots))
     if args.no_dedupe_exact:
         _lib.check(L.sw_encoder_set_option(h, _lib.SW_OPT_DEDUPE_EXACT, 0))
+    if args.fused_compact:
+        _lib.check(L.sw_encoder_set_option(h, _lib.SW_OPT_FUSED_COMPACT, 1))
     if args.presplit_segs:
         _lib.check(L.sw_encoder_set_option(h, _lib.SW_OPT_PRESPLIT_SEGMENTS, args.presplit_segs))
     if args.no_merge_streams:

@@ -141,6 +141,11 @@ int32_t sw_encoder_reserve(sw_encoder* h, int64_t max_bytes, int64_t max_strings
  *                          slower on MI355X); 1: one pre-split launch, then k_classify.  Same ids
  *                          either way. */
 #define SW_OPT_PRESPLIT_SEGMENTS 14
+/*   SW_OPT_FUSED_COMPACT   0 (default): the per-tile id counts, their scan and the compaction of
+ *                          the ids as three steps (k_tile_count, scan, k_compact); 1: one pass
+ *                          (k_compact_lb, a decoupled look-back over the tiles; an A/B knob, slower
+ *                          on MI355X).  Same ids. */
+#define SW_OPT_FUSED_COMPACT 15
 int32_t sw_encoder_set_option(sw_encoder* h, int32_t option, int64_t value);
 
 /* Encoder facts (sw_encoder_get_info): distinct merges, whole-chunk table entries, whether the

@@ -112,6 +112,10 @@ struct sw_encoder {
   // pre-split of segment k + 1 (one is issue-bound, the other waits on memory)
   // (measured slower than one launch each, profiles/r2_k_presplit_segments_ab.txt: default 1)
   int presplit_segs = 1;              // SW_OPT_PRESPLIT_SEGMENTS (1: pre-split, then classify)
+  // SW_OPT_FUSED_COMPACT: k_compact_lb (count + scan + compact in one pass); measured 6.0 -> 11.1 ms
+  // on C2 (profiles/r2_k_fused_compact_ab.txt): the look-back's chain of prefixes over 524 k tiles
+  // advances about one 64-tile window per coherent memory round trip
+  bool fused_compact = false;
   hipEvent_t ev_pre[kMaxPresplitSegs] = {};
   hipStream_t s_fork[3] = {nullptr, nullptr, nullptr};
   hipEvent_t ev_fork = nullptr, ev_join[3] = {nullptr, nullptr, nullptr};
@@ -135,6 +139,7 @@ struct sw_encoder {
   uint4* d_dres = nullptr;            // dense result heads, one per table entry
   uint8_t* d_dcnt = nullptr;          // their id counts (<= 32), one byte per table entry
   uint32_t* d_big = nullptr;          // chunks over kLongLds bytes: count, then their long-bucket indices
+  uint64_t* d_lbflags = nullptr;      // k_compact_lb: per tile, its count or inclusive prefix (+ a ticket word)
   uint32_t* d_defer = nullptr;        // tiles k_classify deferred to k_classify_deferred: count, then indices
   bool dedupe = true;
   bool dedupe_exact = true;           // SW_OPT_DEDUPE_EXACT
@@ -183,7 +188,8 @@ void free_workspace(sw_encoder* h) {
   h->d_bcnt = nullptr; h->d_boff = nullptr; h->d_qtotal = nullptr;
   (void)hipFree(h->d_dtab); (void)hipFree(h->d_tile_base); (void)hipFree(h->d_tile_cnt);
   (void)hipFree(h->d_dres); (void)hipFree(h->d_big); (void)hipFree(h->d_dcnt); (void)hipFree(h->d_defer);
-  h->d_dres = nullptr; h->d_big = nullptr; h->d_dcnt = nullptr; h->d_defer = nullptr;
+  (void)hipFree(h->d_lbflags);
+  h->d_dres = nullptr; h->d_big = nullptr; h->d_dcnt = nullptr; h->d_defer = nullptr; h->d_lbflags = nullptr;
   (void)hipFree(h->d_total);
   h->d_scratch = nullptr; h->d_res = nullptr; h->d_pbits = nullptr; h->d_pcount = nullptr; h->d_part = nullptr;
   h->d_dtab = nullptr; h->d_tile_base = nullptr; h->d_tile_cnt = nullptr; h->d_total = nullptr;
@@ -239,6 +245,7 @@ int32_t ensure_workspace(sw_encoder* h, int64_t n_bytes) {
   }
   HIP_TRY(hipMalloc(&h->d_big, sizeof(uint32_t) * (nb / (kLongLds + 1) + 2)));  // (count + list)
   HIP_TRY(hipMalloc(&h->d_defer, sizeof(uint32_t) * (n_tiles + 1)));
+  HIP_TRY(hipMalloc(&h->d_lbflags, sizeof(uint64_t) * (n_tiles + 1)));
   HIP_TRY(hipMalloc(&h->d_tile_base, sizeof(int64_t) * n_tiles));
   HIP_TRY(hipMalloc(&h->d_tile_cnt, sizeof(uint32_t) * n_tiles));
   HIP_TRY(hipMalloc(&h->d_total, sizeof(int64_t)));
@@ -510,6 +517,7 @@ extern "C" int32_t sw_encoder_set_option(sw_encoder* h, int32_t option, int64_t 
     case SW_OPT_LONG_SPLIT: h->long_split = value != 0; return SW_OK;
     case SW_OPT_PIPE_COPY_KERNELS: h->pipe_kcopy = value != 0; return SW_OK;
     case SW_OPT_MERGE_STREAMS: h->merge_fork = value != 0; return SW_OK;
+    case SW_OPT_FUSED_COMPACT: h->fused_compact = value != 0; return SW_OK;
     case SW_OPT_PRESPLIT_SEGMENTS:
       if (value < 1 || value > kMaxPresplitSegs) return fail(SW_ERR_ARG, "SW_OPT_PRESPLIT_SEGMENTS: 1 .. 16");
       h->presplit_segs = (int)value;
@@ -732,9 +740,15 @@ extern "C" int32_t sw_encode_device(sw_encoder* h, const uint8_t* d_bytes, int64
     }
     HIP_TRY(hipGetLastError());
     const dim3 wg((unsigned)((n_tiles + 3) / 4));  // one wave per tile
-    hipLaunchKernelGGL(k_tile_count, wg, dim3(kThreads), 0, st, a);
-    HIP_TRY(launch_scan(st, h->d_tile_cnt, n_tiles, h->d_part, h->d_tile_base, h->d_total));
-    hipLaunchKernelGGL(k_compact, wg, dim3(kThreads), 0, st, a, h->d_tile_base, d_out_ids);
+    if (h->fused_compact) {  // (flags, then the ticket word, zeroed together)
+      HIP_TRY(hipMemsetAsync(h->d_lbflags, 0, sizeof(uint64_t) * (n_tiles + 1), st));
+      hipLaunchKernelGGL(k_compact_lb, wg, dim3(kThreads), 0, st, a, h->d_lbflags, (uint32_t*)(h->d_lbflags + n_tiles),
+                         h->d_total, d_out_ids);
+    } else {
+      hipLaunchKernelGGL(k_tile_count, wg, dim3(kThreads), 0, st, a);
+      HIP_TRY(launch_scan(st, h->d_tile_cnt, n_tiles, h->d_part, h->d_tile_base, h->d_total));
+      hipLaunchKernelGGL(k_compact, wg, dim3(kThreads), 0, st, a, h->d_tile_base, d_out_ids);
+    }
     HIP_TRY(hipGetLastError());
   } else {
     HIP_TRY(hipMemsetAsync(h->d_total, 0, sizeof(int64_t), st));

@@ -1829,12 +1829,9 @@ __device__ __forceinline__ uint32_t ref_count(const EncArgs& a, uint32_t r) {
   return dn ? c8 : c32;
 }
 
-__global__ void __launch_bounds__(kThreads) k_tile_count(EncArgs a) {
-  // ids per tile = settled slots + the id counts of the results its references use (the
-  // tile's reference list from k_classify: no pass over the slots)
-  const int64_t t = ((int64_t)blockIdx.x * kThreads + threadIdx.x) >> 6;
-  const int lane = threadIdx.x & 63;
-  if (t >= a.n_tiles) return;
+// ids of tile t (wave-uniform) = settled slots + the id counts of the results its references use
+// (the tile's reference list from k_classify: no pass over the slots)
+__device__ __forceinline__ uint32_t tile_id_count(const EncArgs& a, int64_t t, int lane) {
   const uint32_t* rl = a.rlist + t * kTile;
 #ifndef SW_NO_PREFETCH
   // the first round's list entries load with the counts, not after them: one dependent memory
@@ -1859,27 +1856,28 @@ __global__ void __launch_bounds__(kThreads) k_tile_count(EncArgs a) {
   }
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) c += __shfl_xor(c, off, 64);
-  if (lane == 0) a.tile_cnt[t] = c + (uint32_t)(C - nref);
+  return c + (uint32_t)(C - nref);
+}
+
+__global__ void __launch_bounds__(kThreads) k_tile_count(EncArgs a) {
+  const int64_t t = ((int64_t)blockIdx.x * kThreads + threadIdx.x) >> 6;
+  const int lane = threadIdx.x & 63;
+  if (t >= a.n_tiles) return;
+  const uint32_t c = tile_id_count(a, t, lane);
+  if (lane == 0) a.tile_cnt[t] = c;
 }
 
 constexpr int kRefCap = 128;    // references per 8-round group gathered through LDS
 constexpr int kOutCapW = 1024;  // ids per group staged in LDS (the rest are stored directly)
 constexpr uint32_t kLaneCopy = 64;  // results longer than this are copied by the whole wave
 
-__global__ void __launch_bounds__(kThreads) k_compact(EncArgs a, const int64_t* tile_base, int32_t* out) {
-  // per wave: the group's references, gathered with full lanes before any store (a store
-  // ahead of a load in the wave's vmcnt order would make the load wait for it)
-  __shared__ uint32_t s_rp_all[kWaves][kRefCap];
-  __shared__ uint4 s_rq_all[kWaves][kRefCap];
-  __shared__ int32_t s_out_all[kWaves][kOutCapW];  // a group's ids, staged for 256-B stores
+// tile t's ids to out + base (base: the ids of the tiles before it); per wave: the group's
+// references, gathered with full lanes before any store (a store ahead of a load in the wave's
+// vmcnt order would make the load wait for it)
+__device__ __forceinline__ void compact_tile(const EncArgs& a, int64_t t, int64_t base, int32_t* out, uint32_t* s_rp,
+                                             uint4* s_rq, int32_t* s_out) {
   SW_STAMP_INIT;
-  const int wv = threadIdx.x >> 6;
-  const int64_t t = ((int64_t)blockIdx.x * kThreads + threadIdx.x) >> 6;
   const int lane = threadIdx.x & 63;
-  if (t >= a.n_tiles) return;
-  uint32_t* s_rp = s_rp_all[wv];
-  uint4* s_rq = s_rq_all[wv];
-  int32_t* s_out = s_out_all[wv];
   const uint64_t lt_mask = (lane == 0) ? 0ULL : (~0ULL >> (64 - lane));
   constexpr int R = kRoundsInFlight;
   const int32_t* src = a.scratch + t * kTile;
@@ -1889,7 +1887,7 @@ __global__ void __launch_bounds__(kThreads) k_compact(EncArgs a, const int64_t* 
   for (int u = 0; u < R; ++u) v0[u] = SW_LDNT(&src[min((u << 6) + lane, kTile - 1)]);
 #endif
   const int C = (int)a.tile_slots[t];
-  int32_t* dst = out + tile_base[t];
+  int32_t* dst = out + base;
   // strings starting in this tile: lane i holds string s_lo + i's chunk index (k_classify)
   const int64_t t1 = min(t * kTile + (int64_t)kTile, a.n_bytes);
   const int64_t s_lo = a.tile_slo[t];
@@ -2020,7 +2018,6 @@ __global__ void __launch_bounds__(kThreads) k_compact(EncArgs a, const int64_t* 
     SW_STAMP(10);
 #endif
   }
-  const int64_t base = tile_base[t];
   if (has_s) a.out_off[my_s] = ~(base + (int64_t)(sj >= C ? carry : s_off));
   if (many) {
     wave_sync_mem();
@@ -2037,6 +2034,62 @@ __global__ void __launch_bounds__(kThreads) k_compact(EncArgs a, const int64_t* 
 #ifdef SW_STAMPS
   SW_STAMP(11);
 #endif
+}
+
+__global__ void __launch_bounds__(kThreads) k_compact(EncArgs a, const int64_t* tile_base, int32_t* out) {
+  __shared__ uint32_t s_rp_all[kWaves][kRefCap];
+  __shared__ uint4 s_rq_all[kWaves][kRefCap];
+  __shared__ int32_t s_out_all[kWaves][kOutCapW];  // a group's ids, staged for 256-B stores
+  const int wv = threadIdx.x >> 6;
+  const int64_t t = ((int64_t)blockIdx.x * kThreads + threadIdx.x) >> 6;
+  if (t >= a.n_tiles) return;
+  compact_tile(a, t, tile_base[t], out, s_rp_all[wv], s_rq_all[wv], s_out_all[wv]);
+}
+
+// ---------------------------------------------------------------------------------------
+// k_compact_lb: k_tile_count, the scan of the tile counts and k_compact in one pass.  A wave
+// takes the next tile in dispatch order (a ticket), counts its ids, publishes the count, finds
+// the ids before it by a decoupled look-back over the tiles before it (each holds its count or,
+// once known, its inclusive prefix), publishes its prefix, then compacts.  A tile only waits on
+// tiles that took their ticket earlier and publish their count without waiting: no deadlock.
+// flags[t] = status << 62 | value (0: not yet, 1: count, 2: inclusive prefix); zeroed per launch.
+// ---------------------------------------------------------------------------------------
+constexpr uint64_t kLbCount = 1ULL << 62, kLbIncl = 2ULL << 62, kLbValue = (1ULL << 62) - 1;
+constexpr uint32_t kLbMaxPolls = 1u << 22;  // (a bound on every wait: a bug gives wrong ids, never a hang)
+
+__global__ void __launch_bounds__(kThreads) k_compact_lb(EncArgs a, uint64_t* flags, uint32_t* ticket, int64_t* total,
+                                                         int32_t* out) {
+  __shared__ uint32_t s_rp_all[kWaves][kRefCap];
+  __shared__ uint4 s_rq_all[kWaves][kRefCap];
+  __shared__ int32_t s_out_all[kWaves][kOutCapW];
+  const int wv = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63;
+  uint32_t tk = 0;
+  if (lane == 0) tk = atomicAdd(ticket, 1u);
+  const int64_t t = (int64_t)__shfl((int)tk, 0, 64);
+  if (t >= a.n_tiles) return;
+  const uint64_t c = tile_id_count(a, t, lane);
+  if (lane == 0) __hip_atomic_store(&flags[t], (t == 0 ? kLbIncl : kLbCount) | c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  int64_t base = 0;
+  for (int64_t e = t - 1; e >= 0;) {  // window: tiles e, e - 1, .., e - 63 (lane i: e - i)
+    const int64_t i = e - lane;
+    uint64_t f = i >= 0 ? __hip_atomic_load(&flags[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : kLbIncl;
+    for (uint32_t polls = 0; __ballot((f >> 62) == 0) && polls < kLbMaxPolls; ++polls) {
+      __builtin_amdgcn_s_sleep(1);
+      if ((f >> 62) == 0) f = __hip_atomic_load(&flags[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    const uint64_t incl = __ballot((f >> 62) == 2);
+    const int stop = incl ? __ffsll((long long)incl) - 1 : 64;  // nearest inclusive prefix
+    uint64_t v = lane <= stop ? (f & kLbValue) : 0;
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+    base += (int64_t)v;
+    if (incl) break;
+    e -= 64;
+  }
+  if (t > 0 && lane == 0) __hip_atomic_store(&flags[t], kLbIncl | (uint64_t)(base + c), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (t == a.n_tiles - 1 && lane == 0) *total = base + (int64_t)c;
+  compact_tile(a, t, base, out, s_rp_all[wv], s_rq_all[wv], s_out_all[wv]);
 }
 
 // every string offset: a complemented value is one k_compact finished; strings starting at or

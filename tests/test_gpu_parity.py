@@ -82,6 +82,33 @@ def test_merge_streams_option(fork):
         t.close()
 
 
+@pytest.mark.parametrize("fused", [0, 1])
+def test_fused_compact_option(fused):
+    """Tile counts + scan + compaction in one look-back pass (k_compact_lb, default) or in three
+    steps: the reference-generated fixtures, then MIXED (20k strings, several per tile) and STRESS
+    (4 KiB results) batches against the oracle, and tiny strings (many string starts per tile)."""
+    t = sa.Tokenizer(device=0)
+    t.merges = load_model_merges("bl32k.model")
+    L = _lib.lib()
+    _lib.check(L.sw_encoder_set_option(t._encoder(), _lib.SW_OPT_FUSED_COMPACT, fused))
+    try:
+        for entry in golden_index()["fixtures"]:
+            if entry["model"] != "bl32k.model":
+                continue
+            fx = load_fixture(entry)
+            t.pattern = PAT_STR[entry["pattern"]]
+            assert_same(gpu_encode(t, fx["bytes"], fx["off"]), (fx["ids"], fx["ids_off"]))
+        t.pattern = ""
+        for seed, kind, n, mean in ((3, corpus.MIXED, 20000, 300), (4, corpus.STRESS, 3000, 600)):
+            buf, off = corpus.synth(seed, kind, n, mean)
+            assert_same(gpu_encode(t, buf, off), oracle_encode(t.merges, buf, off, "cl100k"))
+        rng = random.Random(5)
+        buf, off = pack([bytes(rng.choice(b"ab ,.1") for _ in range(rng.randrange(0, 5))) for _ in range(50000)])
+        assert_same(gpu_encode(t, buf, off), oracle_encode(t.merges, buf, off, "cl100k"))
+    finally:
+        t.close()
+
+
 def test_tokenizer_encode_decode_surface():
     t = tok_for("bl32k.model")
     text = "Hello world's 12345 \n\n  x 中文 😀"

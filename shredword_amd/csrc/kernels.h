@@ -622,9 +622,10 @@ constexpr int kQBuf = 64 * (kLookRounds + 1);        // dedupe buffer: one batch
 constexpr int kWinWords = kWin / 4 + 8;
 
 // k_classify waits on memory most of the time: 6 waves per SIMD (80 VGPRs, 12 spilled bytes
-// per lane) beat the compiler's 5 (81 VGPRs): 2.81 vs 3.05 ms (profiles/r2_e_ab.txt).  k_compact
-// stays at 5 (88 VGPRs): capped at 6 it spills 24 B per lane, +0.9 GB of writes, and is not
-// faster (1.15 vs 1.12 ms).  SW_CLS_WAVES_PER_EU=0: no cap (A/B builds).
+// per lane) beat the compiler's 5 (81 VGPRs): 2.81 vs 3.05 ms (profiles/r2_e_ab.txt).  k_compact:
+// capped at 6 it spilled 24 B per lane (+0.9 GB of writes, not faster); with its body as a
+// function of (tile, base) (compact_tile) the compiler fits 78 VGPRs, 6 waves, no spill: 1.11 ->
+// 0.95 ms (profiles/r2_k.md).  SW_CLS_WAVES_PER_EU=0: no cap (A/B builds).
 #ifndef SW_CLS_WAVES_PER_EU
 #define SW_CLS_WAVES_PER_EU 6
 #endif

@@ -1869,7 +1869,18 @@ __global__ void __launch_bounds__(kThreads) k_tile_count(EncArgs a) {
 }
 
 constexpr int kRefCap = 128;    // references per 8-round group gathered through LDS
-constexpr int kOutCapW = 1024;  // ids per group staged in LDS (the rest are stored directly)
+#ifndef SW_CP_OUTCAP
+#define SW_CP_OUTCAP 1024
+#endif
+constexpr int kOutCapW = SW_CP_OUTCAP;  // ids per group staged in LDS (the rest are stored directly)
+#ifndef SW_CP_WAVES
+#define SW_CP_WAVES 0  // (A/B builds: cap k_compact's VGPRs for this many waves per SIMD)
+#endif
+#if SW_CP_WAVES > 0
+#define SW_CP_ATTR __attribute__((amdgpu_waves_per_eu(SW_CP_WAVES, SW_CP_WAVES)))
+#else
+#define SW_CP_ATTR
+#endif
 constexpr uint32_t kLaneCopy = 64;  // results longer than this are copied by the whole wave
 
 // tile t's ids to out + base (base: the ids of the tiles before it); per wave: the group's
@@ -2037,7 +2048,7 @@ __device__ __forceinline__ void compact_tile(const EncArgs& a, int64_t t, int64_
 #endif
 }
 
-__global__ void __launch_bounds__(kThreads) k_compact(EncArgs a, const int64_t* tile_base, int32_t* out) {
+__global__ void __launch_bounds__(kThreads) SW_CP_ATTR k_compact(EncArgs a, const int64_t* tile_base, int32_t* out) {
   __shared__ uint32_t s_rp_all[kWaves][kRefCap];
   __shared__ uint4 s_rq_all[kWaves][kRefCap];
   __shared__ int32_t s_out_all[kWaves][kOutCapW];  // a group's ids, staged for 256-B stores

@@ -230,7 +230,15 @@ constexpr int kPbThreads = SW_PB_THREADS;
 constexpr int kPbBlock = kPbThreads * psb::kChunk;      // 8 KiB
 constexpr int kPbPre = 64;                               // string starts staged before b0 ...
 constexpr int kPbSsWords = (kPbPre + kPbBlock + 128) / 32;  // ... and after the block
-constexpr int kPbChunks = kPbThreads + 2;                // chunks -1 .. 256
+// SW_PB_HALO 0 (default): LDS holds the block's own chunks 0 .. 255, one per thread, and the two
+// neighbours of the block (chunks -1 and 256) are classified where they are needed (threads 0 and
+// 255); 1: they are classified into LDS too, a second pass of step 1 for two lanes of wave 0
+// that the workgroup barrier makes every wave wait for
+#ifndef SW_PB_HALO
+#define SW_PB_HALO 0
+#endif
+constexpr int kPbHalo = SW_PB_HALO;
+constexpr int kPbChunks = kPbThreads + 2 * kPbHalo;      // chunks -halo .. 255 + halo
 constexpr int kPbStage = kPbPre + kPbBlock + 64;           // bytes staged in LDS, from b0 - kPbPre
 
 #ifndef SW_PB_STAGE
@@ -291,7 +299,7 @@ __device__ __forceinline__ void pb_load40(const PbArgs g, int64_t p, uint32_t* w
 
 struct PbSrc {  // psb::carries' view: the block's chunks from LDS, the others classified on the fly
   PbArgs g;                         // (by value: a pointer to the kernel argument puts it on the stack)
-  const uint32_t (*m)[kPbChunks];   // [9][kPbChunks]: chunk c0 - 1 + j at column j
+  const uint32_t (*m)[kPbChunks];   // [9][kPbChunks]: chunk c0 - kPbHalo + j at column j
   const uint32_t* ssb;              // the block's string-start bitmap (from b0 - kPbPre)
   int64_t c0, b0, n_chunks;
   bool cl;
@@ -307,7 +315,7 @@ struct PbSrc {  // psb::carries' view: the block's chunks from LDS, the others c
   __device__ __forceinline__ uint32_t ss(int64_t c) const { return ss_at(32 * c); }
   __device__ __forceinline__ psb::Masks get(int64_t c) const {
     if (c < 0 || c >= n_chunks) return psb::Masks{};
-    const int64_t j = c - (c0 - 1);
+    const int64_t j = c - (c0 - kPbHalo);
     if (j >= 0 && j < kPbChunks) {
       const int k = (int)j;
       return psb::Masks{m[0][k], m[1][k], m[2][k], m[3][k], m[4][k], m[5][k], m[6][k], m[7][k], m[8][k]};
@@ -378,13 +386,13 @@ __global__ void __launch_bounds__(kPbThreads, SW_PB_WAVES) k_presplit_bits(PbArg
     }
     return;
   }
-  // 1. class masks of chunks c0 - 1 .. c0 + 256
+  // 1. class masks of chunks c0 - kPbHalo .. c0 + 255 + kPbHalo
   for (int j = tid; j < kPbChunks; j += kPbThreads) {
-    const int64_t c = c0 - 1 + j;
+    const int64_t c = c0 - kPbHalo + j;
     psb::Masks m{};
     if (c >= 0 && c < n_chunks) {
 #if SW_PB_STAGE
-      const LdsBytes by{&s_b[(32 * j + kPbPre - 32 - 4) / 4]};
+      const LdsBytes by{&s_b[(32 * j + kPbPre - 32 * kPbHalo - 4) / 4]};
 #else
       psb::RegBytes by;
       pb_load40(g, 32 * c, by.w);

@@ -745,7 +745,8 @@ extern "C" int32_t sw_encode_device(sw_encoder* h, const uint8_t* d_bytes, int64
       hipLaunchKernelGGL(k_compact_lb, wg, dim3(kThreads), 0, st, a, h->d_lbflags, (uint32_t*)(h->d_lbflags + n_tiles),
                          h->d_total, d_out_ids);
     } else {
-      hipLaunchKernelGGL(k_tile_count, wg, dim3(kThreads), 0, st, a);
+      hipLaunchKernelGGL(k_tile_count, dim3((unsigned)((n_tiles + kWaves * kTcTiles - 1) / (kWaves * kTcTiles))),
+                         dim3(kThreads), 0, st, a);
       HIP_TRY(launch_scan(st, h->d_tile_cnt, n_tiles, h->d_part, h->d_tile_base, h->d_total));
       hipLaunchKernelGGL(k_compact, wg, dim3(kThreads), 0, st, a, h->d_tile_base, d_out_ids);
     }

@@ -1860,12 +1860,41 @@ __device__ __forceinline__ uint32_t tile_id_count(const EncArgs& a, int64_t t, i
   return c + (uint32_t)(C - nref);
 }
 
+// k_tile_count: kTcTiles tiles per wave, their first 64 list entries and sizes loaded together,
+// then their counts: one dependent round trip serves kTcTiles tiles (a tile holds ~58
+// references on prose, so one wave per tile spent most of its life waiting)
+#ifndef SW_TC_TILES
+#define SW_TC_TILES 2
+#endif
+constexpr int kTcTiles = SW_TC_TILES;
 __global__ void __launch_bounds__(kThreads) k_tile_count(EncArgs a) {
-  const int64_t t = ((int64_t)blockIdx.x * kThreads + threadIdx.x) >> 6;
+  const int64_t tb = (((int64_t)blockIdx.x * kThreads + threadIdx.x) >> 6) * kTcTiles;
   const int lane = threadIdx.x & 63;
-  if (t >= a.n_tiles) return;
-  const uint32_t c = tile_id_count(a, t, lane);
-  if (lane == 0) a.tile_cnt[t] = c;
+  if (tb >= a.n_tiles) return;
+  uint32_t p0[kTcTiles], c[kTcTiles];
+  int C[kTcTiles], nr[kTcTiles];
+#pragma unroll
+  for (int k = 0; k < kTcTiles; ++k) {
+    const int64_t t = min(tb + k, a.n_tiles - 1);  // (a clamped duplicate is not stored)
+    p0[k] = SW_LDNT2(&a.rlist[t * kTile + lane]);
+    C[k] = (int)a.tile_slots[t];
+    nr[k] = (int)a.tile_nref[t];
+  }
+#pragma unroll
+  for (int k = 0; k < kTcTiles; ++k) c[k] = lane < nr[k] ? ref_count(a, p0[k]) : 0u;
+#pragma unroll
+  for (int k = 0; k < kTcTiles; ++k) {
+    const uint32_t* rl = a.rlist + min(tb + k, a.n_tiles - 1) * kTile;
+    for (int i0 = 64; i0 < nr[k]; i0 += 64)  // (long lists: the rest a round at a time)
+      if (i0 + lane < nr[k]) c[k] += ref_count(a, SW_LDNT2(&rl[i0 + lane]));
+  }
+#pragma unroll
+  for (int k = 0; k < kTcTiles; ++k) {
+    uint32_t v = c[k];
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+    if (lane == 0 && tb + k < a.n_tiles) a.tile_cnt[tb + k] = v + (uint32_t)(C[k] - nr[k]);
+  }
 }
 
 constexpr int kRefCap = 128;    // references per 8-round group gathered through LDS

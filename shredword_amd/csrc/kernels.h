@@ -614,6 +614,9 @@ __device__ __forceinline__ DdOut dedupe_claim(const EncArgs& a, const uint32_t* 
 static_assert(kTile <= 0x10000, "chunk starts are uint16");
 // ---------------------------------------------------------------------------------------
 constexpr int kWaves = kThreads / 64;
+#ifndef SW_CLS_PREF_STR
+#define SW_CLS_PREF_STR 0
+#endif
 #ifndef SW_LOOK_ROUNDS
 #define SW_LOOK_ROUNDS 1
 #endif
@@ -671,6 +674,9 @@ __device__ __forceinline__ void classify_tile(const EncArgs& a, int64_t tile, ui
   if (lane < 8) s_b32[kWin / 4 + lane] = 0;
   const uint64_t bw = (lane < kTileWords && w0 + lane < a.n_words) ? SW_LDNT2(&a.bits[w0 + lane]) : 0ULL;
   const int64_t s_first = a.tile_slo[tile];  // (prefetched: used by step 6)
+#if SW_CLS_PREF_STR  // (A/B builds: the first 64 strings' offsets loaded before the lookups)
+  const int64_t s_pref = a.str_off[min(s_first + lane, a.n_str)];
+#endif
 
   // 2. chunk starts in [t0, t1): lane w owns bitmap word w
   constexpr int nw_tile = kTile / 64;
@@ -833,7 +839,11 @@ __device__ __forceinline__ void classify_tile(const EncArgs& a, int64_t tile, ui
 
   // 6. strings starting in this tile: chunk (= slot) index within the tile (k_compact converts)
   for (int64_t s = s_first + lane; s < a.n_str; s += 64) {
+#if SW_CLS_PREF_STR
+    const int64_t p = s == s_first + lane ? s_pref : a.str_off[s];
+#else
     const int64_t p = a.str_off[s];
+#endif
     if (p >= t1) break;
     int lo = 0, hi = C;  // first chunk with start >= p
     const int lp = (int)(p - t0);

@@ -627,13 +627,13 @@ extern "C" int32_t sw_encode_device(sw_encoder* h, const uint8_t* d_bytes, int64
   int segs = 1;
   int64_t seg_blocks = 0;
 #ifndef SW_PS_FSM
-  if (n_tiles > 0 && !d_chunk_bits && h->presplit_segs > 1) {
+  // (a segment holds whole k_classify workgroups: 8 KiB pre-split blocks)
+  if (n_tiles > 0 && !d_chunk_bits && h->presplit_segs > 1 && kPbBlock % (kTile * kWaves) == 0) {
     const int64_t n_blocks = (n_bytes + kPbBlock - 1) / kPbBlock;
     seg_blocks = std::max<int64_t>((n_blocks + h->presplit_segs - 1) / h->presplit_segs, (1 << 20) / kPbBlock);
     segs = (int)((n_blocks + seg_blocks - 1) / seg_blocks);
   }
 #endif
-  static_assert(kPbBlock % (kTile * kWaves) == 0, "a pre-split segment holds whole k_classify workgroups");
   if (n_tiles > 0 && !d_chunk_bits && segs == 1) {  // the full path: device pre-split first
     HIP_TRY(launch_presplit(st, d_bytes, n_bytes, d_str_off, n_str, h->pattern, h->d_pbits, h->d_tile_slo));
     d_chunk_bits = h->d_pbits;

@@ -61,10 +61,6 @@ def parse():
     ap.add_argument("--dedupe-slots", type=int, default=0, help="A/B only: cap the dedupe table (power of two)")
     ap.add_argument("--no-dedupe-exact", action="store_true", help="A/B only: fingerprint keys for every chunk")
     ap.add_argument("--no-merge-streams", action="store_true", help="A/B only: merge kernels one after another")
-    ap.add_argument("--fused-compact", action="store_true",
-                    help="A/B only: the one-pass look-back k_compact_lb instead of k_tile_count + scan + k_compact")
-    ap.add_argument("--presplit-segs", type=int, default=0,
-                    help="A/B only: device pre-split segments overlapped with k_classify (1 = none; 0 = library default)")
     ap.add_argument("--pipe-dma", action="store_true", help="A/B only: e2e pipeline copies by DMA, not kernels")
     ap.add_argument("--pipe-depth", type=int, default=0, help="A/B only: e2e pipeline runs in flight (2..4)")
     ap.add_argument("--pipe-run-mb", type=int, default=0, help="A/B only: e2e pipeline run size (MiB)")
@@ -143,10 +139,6 @@ def main():
     _lib.check(L.sw_encoder_set_option(h, _lib.SW_OPT_DEDUPE_SLOTS, args.dedupe_slots))
     if args.no_dedupe_exact:
         _lib.check(L.sw_encoder_set_option(h, _lib.SW_OPT_DEDUPE_EXACT, 0))
-    if args.fused_compact:
-        _lib.check(L.sw_encoder_set_option(h, _lib.SW_OPT_FUSED_COMPACT, 1))
-    if args.presplit_segs:
-        _lib.check(L.sw_encoder_set_option(h, _lib.SW_OPT_PRESPLIT_SEGMENTS, args.presplit_segs))
     if args.no_merge_streams:
         _lib.check(L.sw_encoder_set_option(h, _lib.SW_OPT_MERGE_STREAMS, 0))
     if args.pipe_dma:
@@ -194,36 +186,55 @@ def main():
         dist.all_reduce(mx, op=dist.ReduceOp.MAX)
         width, width_s = int(mx[0].item()), int(mx[1].item()) + 1
 
-    # N>1: batch k's reassembly (RCCL, on its own stream) overlaps batch k+1's encode; two sets of
-    # output buffers, and a set is rewritten only after its gathers have been waited on
+    # N>1: batch k's reassembly overlaps batch k+1's encode.  The all-gathers run on RCCL's stream;
+    # the compaction into the batch's contiguous int32 ids and rebased offsets (SURVEY.md 8(e) step 4,
+    # sw_reassemble_device) runs on a side stream that waits for them; two sets of output buffers,
+    # and a set is rewritten only after the side stream's event for it (a stream wait, no host
+    # round trip)
     overlap = gather and not args.no_overlap
     outs = [(d_out, d_oo)]
     if overlap:
         outs.append((torch.empty_like(d_out), torch.empty_like(d_oo)))
-    pending = [[] for _ in outs]
+    finals = []
+    if gather:  # the reassembled batch: world * width ids, world * width_s + 1 offsets
+        finals = [(torch.empty(world * width, dtype=torch.int32, device=dev),
+                   torch.empty(world * width_s + 1, dtype=torch.int64, device=dev)) for _ in outs]
+    side = torch.cuda.Stream(dev) if gather else None
+    done_ev = [None for _ in outs]
     n_step = [0]
 
     def step():
         slot = n_step[0] % len(outs)
         n_step[0] += 1
-        for w in pending[slot]:
-            w.wait()
-        pending[slot] = []
+        if done_ev[slot] is not None:
+            torch.cuda.current_stream(dev).wait_event(done_ev[slot])
+            done_ev[slot] = None
         o_ids, o_off = outs[slot]
         _lib.check(L.sw_encode_device(h, d_buf.data_ptr(), n_bytes, d_off.data_ptr(), n_str,
                                       d_bits.data_ptr() if host_ps else None, o_ids.data_ptr(), o_off.data_ptr(),
                                       stream, None))
-        if overlap:  # shard.reassemble: one counts all-gather, padded id and offset all-gathers (RCCL)
-            pending[slot], _ = shard.reassemble(o_ids, o_off, None, dev, concat=False, width=width, width_s=width_s,
-                                                id_bits=id_bits, async_op=True)
-        elif gather:
-            shard.reassemble(o_ids, o_off, None, dev, concat=False, width=width, width_s=width_s, id_bits=id_bits)
-
-    def finish():  # every issued reassembly waited on (the caller's stream)
-        for p in pending:
-            for w in p:
+        if not gather:
+            return
+        # steps 1-3: one counts all-gather, padded id and offset all-gathers (RCCL)
+        works, res = shard.reassemble(o_ids, o_off, None, dev, concat=False, width=width, width_s=width_s,
+                                      id_bits=id_bits, async_op=True)
+        side.wait_stream(torch.cuda.current_stream(dev))
+        with torch.cuda.stream(side):  # step 4 once the gathers have landed
+            for w in works:
                 w.wait()
-            p.clear()
+            shard.compact(res, id_bits, finals[slot][0], finals[slot][1])
+            ev = torch.cuda.Event()
+            ev.record(side)
+        done_ev[slot] = ev
+        if not overlap:
+            torch.cuda.current_stream(dev).wait_event(ev)
+            done_ev[slot] = None
+
+    def finish():  # every issued reassembly complete before the clock stops (the caller's stream)
+        for k, ev in enumerate(done_ev):
+            if ev is not None:
+                torch.cuda.current_stream(dev).wait_event(ev)
+                done_ev[k] = None
 
     for _ in range(args.warmup):
         step()
@@ -242,8 +253,26 @@ def main():
         dist.barrier()
     k_ms = L.sw_encoder_last_kernel_ms(h)
     _lib.check(L.sw_encoder_set_timing(h, 0))
+    reassembly_ok = None
     if gather:
         shard.check_bounds()
+        # the last step's reassembled batch holds this rank's own encode at its displacement, and its
+        # offsets end at the batch total
+        last = (n_step[0] - 1) % len(outs)
+        mine = torch.tensor([n_tok, n_str], dtype=torch.int64, device=dev)
+        all_c = torch.empty(2 * world, dtype=torch.int64, device=dev)
+        dist.all_gather_into_tensor(all_c, mine)
+        cs, ss = all_c[0::2].tolist(), all_c[1::2].tolist()
+        disp, sdisp = sum(cs[:rank]), sum(ss[:rank])
+        f_ids, f_off = finals[last]
+        o_ids, o_off = outs[last]
+        reassembly_ok = bool(torch.equal(f_ids[disp:disp + n_tok], o_ids[:n_tok])
+                             and torch.equal(f_off[sdisp:sdisp + n_str] - disp, o_off[:n_str])
+                             and int(f_off[sum(ss)].item()) == sum(cs))
+        ok_t = torch.tensor([1 if reassembly_ok else 0], dtype=torch.int64, device=dev)
+        dist.all_reduce(ok_t, op=dist.ReduceOp.MIN)  # (every rank's check)
+        reassembly_ok = bool(ok_t.item())
+
     # what the launches did: chunks settled without the merge loop, distinct merged after dedupe
     cnt4 = (ctypes.c_int64 * 4)()
     _lib.check(L.sw_encoder_last_counts(h, cnt4))
@@ -372,7 +401,8 @@ def main():
                                     ("C3: configs[2], host %s pre-split, GPU merge loop" % args.pattern) if host_ps else
                                     ("C2: configs[1] full path, 1 GiB MIXED UTF-8, 1M strings, GPU %s pre-split + "
                                      "merge loop + id compaction" % args.pattern))
-                       + (" + RCCL all-gather of ids" if gather else ""),
+                       + (" + RCCL all-gather of ids + reassembly (offsets rebased, ids widened to int32)"
+                          if gather else ""),
                        "presplit": args.presplit,
                        "bytes_per_rank": n_bytes, "strings_per_rank": n_str, "merges": len(tok.merges),
                        "model": model, "pattern": args.pattern, "parallelism": "doc-shard x%d" % world,
@@ -386,6 +416,7 @@ def main():
             "roofline": roofline,
             "cpu_baseline": cpu,
             "parity_vs_oracle_sample": parity,
+            "reassembly_check": reassembly_ok,
             "e2e_pcie": e2e,
             "host_prep_s": round(t_prep, 2),
         }

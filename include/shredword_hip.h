@@ -135,17 +135,7 @@ int32_t sw_encoder_reserve(sw_encoder* h, int64_t max_bytes, int64_t max_strings
  *                          run side by side on forked streams (joined before the counts); 0: one
  *                          after another on the launch stream.  Results identical. */
 #define SW_OPT_MERGE_STREAMS 13
-/*   SW_OPT_PRESPLIT_SEGMENTS  1 .. 16 (default 1): > 1: sw_encode_device's device pre-split runs as
- *                          this many segments (1 MiB at least) on a second stream, and k_classify
- *                          of segment k runs beside the pre-split of segment k + 1 (an A/B knob:
- *                          slower on MI355X); 1: one pre-split launch, then k_classify.  Same ids
- *                          either way. */
-#define SW_OPT_PRESPLIT_SEGMENTS 14
-/*   SW_OPT_FUSED_COMPACT   0 (default): the per-tile id counts, their scan and the compaction of
- *                          the ids as three steps (k_tile_count, scan, k_compact); 1: one pass
- *                          (k_compact_lb, a decoupled look-back over the tiles; an A/B knob, slower
- *                          on MI355X).  Same ids. */
-#define SW_OPT_FUSED_COMPACT 15
+/* (options 14 and 15 were A/B knobs of round 2, removed: set_option rejects them) */
 int32_t sw_encoder_set_option(sw_encoder* h, int32_t option, int64_t value);
 
 /* Encoder facts (sw_encoder_get_info): distinct merges, whole-chunk table entries, whether the
@@ -245,6 +235,21 @@ int32_t sw_encoder_last_counts(sw_encoder* h, int64_t* out4);
  * 8..11 k_compact: slots + reference list, result gathers, chained scan, expansion + strings.
  * out32 holds 32 values.  reset != 0 zeroes the counters.  Regular builds return SW_ERR_ARG. */
 int32_t sw_encoder_phase_cycles(sw_encoder* h, double* out32, int32_t reset);
+
+/* ---- multi-GPU reassembly (no reference counterpart: the reference has
+ * no multi-device path) ------------------------------------------------------------------------
+ * The gathered, padded buffers of a doc-sharded encode over `world` ranks -> the batch's ids and
+ * string offsets, contiguous, on the device.  Rank r's ids are d_recv[r*width .. r*width +
+ * counts[r]) (id_bits 16: the low 16 bits of each id, an unsigned value widened here; 32: int32)
+ * and its string offsets d_recv_off[r*width_s .. r*width_s + n_strs[r]) (relative to its own
+ * ids).  d_counts / d_n_strs: int64[world] device arrays (the counts all-gather); a count above
+ * its width is taken as the width (the caller checks its bounds: shard.check_bounds).  Writes
+ * d_out_ids[0 .. sum counts) and d_out_off[0 .. sum n_strs] (rank r's offsets plus the ids of the
+ * ranks before it; the last one is the total), so d_out_ids must hold world*width ids and
+ * d_out_off world*width_s + 1 offsets.  Asynchronous on `stream` (NULL: the null stream). */
+int32_t sw_reassemble_device(const void* d_recv, int32_t id_bits, const int64_t* d_counts, int64_t width,
+                             const int64_t* d_recv_off, const int64_t* d_n_strs, int64_t width_s, int32_t world,
+                             int32_t* d_out_ids, int64_t* d_out_off, void* stream);
 
 /* ---- synthetic corpora (bench inputs; deterministic for any thread count) --------------
  * Fills out_off[0..n_strings] with string offsets; when out_bytes is non-NULL also writes

@@ -29,8 +29,6 @@ SW_OPT_DEDUPE_EXACT = 10
 SW_OPT_PIPE_COPY_KERNELS = 11
 SW_OPT_PIPE_DEPTH = 12
 SW_OPT_MERGE_STREAMS = 13
-SW_OPT_PRESPLIT_SEGMENTS = 14
-SW_OPT_FUSED_COMPACT = 15
 SW_INFO_MERGES, SW_INFO_CHUNK_ENTRIES, SW_INFO_WIDE_TABLE, SW_INFO_IDS16, SW_INFO_SPLIT = 1, 2, 3, 4, 5
 
 
@@ -97,6 +95,8 @@ _SIGNATURES = {
     "sw_encoder_last_kernel_ms": (c_double, [c_void_p]),
     "sw_encoder_last_counts": (c_int32, [c_void_p, POINTER(c_int64)]),
     "sw_encoder_phase_cycles": (c_int32, [c_void_p, POINTER(c_double), c_int32]),
+    "sw_reassemble_device": (c_int32, [c_void_p, c_int32, c_void_p, c_int64, c_void_p, c_void_p, c_int64, c_int32,
+                                       c_void_p, c_void_p, c_void_p]),
     "sw_decoder_create": (c_int32, [POINTER(c_uint8), POINTER(c_int64), POINTER(c_uint8), c_int64, c_int32,
                                     POINTER(c_void_p)]),
     "sw_decoder_destroy": (None, [c_void_p]),

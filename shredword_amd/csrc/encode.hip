@@ -65,8 +65,6 @@ extern "C" int32_t sw_device_count(void) {
 // ------------------------------------------------------------------------------------------
 // host side
 // ------------------------------------------------------------------------------------------
-constexpr int kMaxPresplitSegs = 16;
-
 struct sw_encoder {
   int device = 0;
   hipStream_t stream = nullptr;
@@ -108,15 +106,6 @@ struct sw_encoder {
   // the merge kernels of different length buckets are independent: forked onto these streams
   // they overlap (each alone leaves most of the chip idle), joined before k_tile_count
   bool merge_fork = true;             // SW_OPT_MERGE_STREAMS
-  // the device pre-split runs in segments on s_fork[0], k_classify of segment k beside the
-  // pre-split of segment k + 1 (one is issue-bound, the other waits on memory)
-  // (measured slower than one launch each, profiles/r2_k_presplit_segments_ab.txt: default 1)
-  int presplit_segs = 1;              // SW_OPT_PRESPLIT_SEGMENTS (1: pre-split, then classify)
-  // SW_OPT_FUSED_COMPACT: k_compact_lb (count + scan + compact in one pass); measured 6.0 -> 11.1 ms
-  // on C2 (profiles/r2_k_fused_compact_ab.txt): the look-back's chain of prefixes over 524 k tiles
-  // advances about one 64-tile window per coherent memory round trip
-  bool fused_compact = false;
-  hipEvent_t ev_pre[kMaxPresplitSegs] = {};
   hipStream_t s_fork[3] = {nullptr, nullptr, nullptr};
   hipEvent_t ev_fork = nullptr, ev_join[3] = {nullptr, nullptr, nullptr};
   sw::HostPool* pool = nullptr;
@@ -139,8 +128,6 @@ struct sw_encoder {
   uint4* d_dres = nullptr;            // dense result heads, one per table entry
   uint8_t* d_dcnt = nullptr;          // their id counts (<= 32), one byte per table entry
   uint32_t* d_big = nullptr;          // chunks over kLongLds bytes: count, then their long-bucket indices
-  uint64_t* d_lbflags = nullptr;      // k_compact_lb: per tile, its count or inclusive prefix (+ a ticket word)
-  uint32_t* d_defer = nullptr;        // tiles k_classify deferred to k_classify_deferred: count, then indices
   bool dedupe = true;
   bool dedupe_exact = true;           // SW_OPT_DEDUPE_EXACT
   int64_t dedupe_slots = 0;           // SW_OPT_DEDUPE_SLOTS (0: automatic)
@@ -187,9 +174,8 @@ void free_workspace(sw_encoder* h) {
   h->d_tile_slo = nullptr; h->d_stamps = nullptr; h->d_tile_slots = nullptr; h->d_tile_nref = nullptr; h->d_rlist = nullptr; h->d_queue = nullptr;
   h->d_bcnt = nullptr; h->d_boff = nullptr; h->d_qtotal = nullptr;
   (void)hipFree(h->d_dtab); (void)hipFree(h->d_tile_base); (void)hipFree(h->d_tile_cnt);
-  (void)hipFree(h->d_dres); (void)hipFree(h->d_big); (void)hipFree(h->d_dcnt); (void)hipFree(h->d_defer);
-  (void)hipFree(h->d_lbflags);
-  h->d_dres = nullptr; h->d_big = nullptr; h->d_dcnt = nullptr; h->d_defer = nullptr; h->d_lbflags = nullptr;
+  (void)hipFree(h->d_dres); (void)hipFree(h->d_big); (void)hipFree(h->d_dcnt);
+  h->d_dres = nullptr; h->d_big = nullptr; h->d_dcnt = nullptr;
   (void)hipFree(h->d_total);
   h->d_scratch = nullptr; h->d_res = nullptr; h->d_pbits = nullptr; h->d_pcount = nullptr; h->d_part = nullptr;
   h->d_dtab = nullptr; h->d_tile_base = nullptr; h->d_tile_cnt = nullptr; h->d_total = nullptr;
@@ -244,8 +230,6 @@ int32_t ensure_workspace(sw_encoder* h, int64_t n_bytes) {
     h->dmask = (uint32_t)(slots - 1);
   }
   HIP_TRY(hipMalloc(&h->d_big, sizeof(uint32_t) * (nb / (kLongLds + 1) + 2)));  // (count + list)
-  HIP_TRY(hipMalloc(&h->d_defer, sizeof(uint32_t) * (n_tiles + 1)));
-  HIP_TRY(hipMalloc(&h->d_lbflags, sizeof(uint64_t) * (n_tiles + 1)));
   HIP_TRY(hipMalloc(&h->d_tile_base, sizeof(int64_t) * n_tiles));
   HIP_TRY(hipMalloc(&h->d_tile_cnt, sizeof(uint32_t) * n_tiles));
   HIP_TRY(hipMalloc(&h->d_total, sizeof(int64_t)));
@@ -318,27 +302,14 @@ bool build_cuckoo(const std::unordered_map<uint64_t, int32_t>& dict, const std::
 }
 
 
-// device pre-split of [d_bytes, d_bytes + n_bytes) into d_bits (zeroed here)
-// (blocks [blk0, blk1) of kPbBlock bytes; blk1 < 0: to the end)
+// device pre-split of [d_bytes, d_bytes + n_bytes) into d_bits (every dword of the bitmap is
+// stored: no clearing)
 hipError_t launch_presplit(hipStream_t st, const uint8_t* d_bytes, int64_t n_bytes, const int64_t* d_str_off,
-                           int64_t n_str, int32_t pattern, uint64_t* d_bits, const int64_t* d_tile_slo,
-                           int64_t blk0 = 0, int64_t blk1 = -1) {
+                           int64_t n_str, int32_t pattern, uint64_t* d_bits, const int64_t* d_tile_slo) {
   if (n_bytes <= 0) return hipSuccess;
-  if (blk1 < 0) blk1 = (n_bytes + kPbBlock - 1) / kPbBlock;
-  if (blk1 <= blk0) return hipSuccess;
-#ifdef SW_PS_FSM  // (A/B builds: the byte-stepped transducer of round 1; one launch only)
-  (void)d_tile_slo;
-  if (blk0 != 0) return hipSuccess;
-  hipError_t e = hipMemsetAsync(d_bits, 0, sizeof(uint64_t) * ((n_bytes + 63) / 64), st);
-  if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(k_presplit, dim3((unsigned)((n_bytes + kPsBlock - 1) / kPsBlock)), dim3(kPsThreads), 0, st,
-                     d_bytes, n_bytes, d_str_off, n_str, (int)pattern, d_bits);
-#else
-  // every dword of the bitmap is stored (no clearing)
-  PbArgs g{d_bytes, n_bytes, d_str_off, n_str, d_tile_slo, blk0};
-  hipLaunchKernelGGL(k_presplit_bits, dim3((unsigned)(blk1 - blk0)), dim3(kPbThreads), 0, st, g,
+  PbArgs g{d_bytes, n_bytes, d_str_off, n_str, d_tile_slo};
+  hipLaunchKernelGGL(k_presplit_bits, dim3((unsigned)((n_bytes + kPbBlock - 1) / kPbBlock)), dim3(kPbThreads), 0, st, g,
                      (int)pattern, (uint32_t*)d_bits);
-#endif
   return hipGetLastError();
 }
 
@@ -477,8 +448,6 @@ extern "C" void sw_encoder_destroy(sw_encoder* h) {
       if (h->ev_join[k]) (void)hipEventDestroy(h->ev_join[k]);
     }
     if (h->ev_fork) (void)hipEventDestroy(h->ev_fork);
-    for (hipEvent_t e : h->ev_pre)
-      if (e) (void)hipEventDestroy(e);
     (void)hipFree(h->d_table);
     (void)hipFree(h->d_chunks);
     (void)hipFree(h->d_inv);
@@ -517,11 +486,6 @@ extern "C" int32_t sw_encoder_set_option(sw_encoder* h, int32_t option, int64_t 
     case SW_OPT_LONG_SPLIT: h->long_split = value != 0; return SW_OK;
     case SW_OPT_PIPE_COPY_KERNELS: h->pipe_kcopy = value != 0; return SW_OK;
     case SW_OPT_MERGE_STREAMS: h->merge_fork = value != 0; return SW_OK;
-    case SW_OPT_FUSED_COMPACT: h->fused_compact = value != 0; return SW_OK;
-    case SW_OPT_PRESPLIT_SEGMENTS:
-      if (value < 1 || value > kMaxPresplitSegs) return fail(SW_ERR_ARG, "SW_OPT_PRESPLIT_SEGMENTS: 1 .. 16");
-      h->presplit_segs = (int)value;
-      return SW_OK;
     case SW_OPT_PIPE_DEPTH:
       if (value < 2 || value > 4) return fail(SW_ERR_ARG, "pipeline depth: 2 .. 4");
       h->pipe_depth = (int)value;
@@ -623,33 +587,8 @@ extern "C" int32_t sw_encode_device(sw_encoder* h, const uint8_t* d_bytes, int64
   if (n_tiles > 0)  // (the pre-split and k_classify start from each tile's first string)
     hipLaunchKernelGGL(k_tile_strings, dim3((unsigned)((n_tiles + 255) / 256)), dim3(256), 0, st, d_str_off, n_str,
                        n_tiles, h->d_tile_slo);
-  // segments of the device pre-split (whole 8 KiB blocks = 4 tiles; 1 MiB at least)
-  int segs = 1;
-  int64_t seg_blocks = 0;
-#ifndef SW_PS_FSM
-  // (a segment holds whole k_classify workgroups: 8 KiB pre-split blocks)
-  if (n_tiles > 0 && !d_chunk_bits && h->presplit_segs > 1 && kPbBlock % (kTile * kWaves) == 0) {
-    const int64_t n_blocks = (n_bytes + kPbBlock - 1) / kPbBlock;
-    seg_blocks = std::max<int64_t>((n_blocks + h->presplit_segs - 1) / h->presplit_segs, (1 << 20) / kPbBlock);
-    segs = (int)((n_blocks + seg_blocks - 1) / seg_blocks);
-  }
-#endif
-  if (n_tiles > 0 && !d_chunk_bits && segs == 1) {  // the full path: device pre-split first
+  if (n_tiles > 0 && !d_chunk_bits) {  // the full path: device pre-split first
     HIP_TRY(launch_presplit(st, d_bytes, n_bytes, d_str_off, n_str, h->pattern, h->d_pbits, h->d_tile_slo));
-    d_chunk_bits = h->d_pbits;
-  }
-  if (n_tiles > 0 && segs > 1) {  // ... or in segments on s_fork[0]
-    if (!h->s_fork[0]) HIP_TRY(hipStreamCreateWithFlags(&h->s_fork[0], hipStreamNonBlocking));
-    if (!h->ev_fork) HIP_TRY(hipEventCreateWithFlags(&h->ev_fork, hipEventDisableTiming));
-    HIP_TRY(hipMemsetAsync(h->d_defer, 0, sizeof(uint32_t), st));
-    HIP_TRY(hipEventRecord(h->ev_fork, st));  // (after k_tile_strings: the pre-split reads tile_slo)
-    HIP_TRY(hipStreamWaitEvent(h->s_fork[0], h->ev_fork, 0));
-    for (int k = 0; k < segs; ++k) {
-      if (!h->ev_pre[k]) HIP_TRY(hipEventCreateWithFlags(&h->ev_pre[k], hipEventDisableTiming));
-      HIP_TRY(launch_presplit(h->s_fork[0], d_bytes, n_bytes, d_str_off, n_str, h->pattern, h->d_pbits, h->d_tile_slo,
-                              k * seg_blocks, std::min<int64_t>((k + 1) * seg_blocks, (n_bytes + kPbBlock - 1) / kPbBlock)));
-      HIP_TRY(hipEventRecord(h->ev_pre[k], h->s_fork[0]));
-    }
     d_chunk_bits = h->d_pbits;
   }
   if (n_tiles > 0) {
@@ -671,23 +610,7 @@ extern "C" int32_t sw_encode_device(sw_encoder* h, const uint8_t* d_bytes, int64
     const bool split = h->split_ok && h->long_split;
     if (h->dedupe) HIP_TRY(hipMemsetAsync(h->d_dtab, 0, sizeof(uint64_t) * ((size_t)a.dmask + 1), st));
     HIP_TRY(hipMemsetAsync(h->d_big, 0, sizeof(uint32_t), st));
-    a.tile0 = 0; a.tile_end = n_tiles; a.bits_ready = a.n_words; a.defer = h->d_defer;
-    if (segs == 1) {
-      hipLaunchKernelGGL(k_classify, dim3((unsigned)((n_tiles + kWaves - 1) / kWaves)), dim3(kThreads), 0, st, a);
-    } else {
-      const int64_t seg_tiles = seg_blocks * (kPbBlock / kTile);
-      for (int k = 0; k < segs; ++k) {
-        HIP_TRY(hipStreamWaitEvent(st, h->ev_pre[k], 0));
-        EncArgs as = a;
-        as.tile0 = k * seg_tiles;
-        as.tile_end = std::min<int64_t>(as.tile0 + seg_tiles, n_tiles);
-        as.bits_ready = k + 1 < segs ? (k + 1) * seg_blocks * (kPbBlock / 64) : a.n_words;
-        hipLaunchKernelGGL(k_classify, dim3((unsigned)((as.tile_end - as.tile0 + kWaves - 1) / kWaves)), dim3(kThreads), 0,
-                           st, as);
-      }
-      hipLaunchKernelGGL(k_classify_deferred, dim3((unsigned)std::min<int64_t>(h->n_cu * 4, (n_tiles + kWaves - 1) / kWaves)),
-                         dim3(kThreads), 0, st, a);
-    }
+    hipLaunchKernelGGL(k_classify, dim3((unsigned)((n_tiles + kWaves - 1) / kWaves)), dim3(kThreads), 0, st, a);
     HIP_TRY(hipGetLastError());
     HIP_TRY(launch_scan(st, h->d_bcnt, kNumBuckets * n_tiles, h->d_part, h->d_boff, h->d_qtotal));
     hipLaunchKernelGGL(k_scatter, dim3((unsigned)((n_tiles + 3) / 4)), dim3(kThreads), 0, st, a);
@@ -740,16 +663,10 @@ extern "C" int32_t sw_encode_device(sw_encoder* h, const uint8_t* d_bytes, int64
     }
     HIP_TRY(hipGetLastError());
     const dim3 wg((unsigned)((n_tiles + 3) / 4));  // one wave per tile
-    if (h->fused_compact) {  // (flags, then the ticket word, zeroed together)
-      HIP_TRY(hipMemsetAsync(h->d_lbflags, 0, sizeof(uint64_t) * (n_tiles + 1), st));
-      hipLaunchKernelGGL(k_compact_lb, wg, dim3(kThreads), 0, st, a, h->d_lbflags, (uint32_t*)(h->d_lbflags + n_tiles),
-                         h->d_total, d_out_ids);
-    } else {
-      hipLaunchKernelGGL(k_tile_count, dim3((unsigned)((n_tiles + kWaves * kTcTiles - 1) / (kWaves * kTcTiles))),
-                         dim3(kThreads), 0, st, a);
-      HIP_TRY(launch_scan(st, h->d_tile_cnt, n_tiles, h->d_part, h->d_tile_base, h->d_total));
-      hipLaunchKernelGGL(k_compact, wg, dim3(kThreads), 0, st, a, h->d_tile_base, d_out_ids);
-    }
+    hipLaunchKernelGGL(k_tile_count, dim3((unsigned)((n_tiles + kWaves * kTcTiles - 1) / (kWaves * kTcTiles))),
+                       dim3(kThreads), 0, st, a);
+    HIP_TRY(launch_scan(st, h->d_tile_cnt, n_tiles, h->d_part, h->d_tile_base, h->d_total));
+    hipLaunchKernelGGL(k_compact, wg, dim3(kThreads), 0, st, a, h->d_tile_base, d_out_ids);
     HIP_TRY(hipGetLastError());
   } else {
     HIP_TRY(hipMemsetAsync(h->d_total, 0, sizeof(int64_t), st));
@@ -843,11 +760,13 @@ int32_t encode_batch_pipelined(sw_encoder* h, const uint8_t* bytes, const int64_
   const int64_t b0 = str_off[0];
   std::vector<std::pair<int64_t, int64_t>> runs;
   int64_t max_b = 1, max_s = 1;
+  const int64_t run_cap = std::min(h->pipe_run, h->max_launch);  // (a run is one launch)
   for (int64_t s_lo = 0; s_lo < n_str;) {
     int64_t s_hi = s_lo + 1;
-    while (s_hi < n_str && str_off[s_hi + 1] - str_off[s_lo] <= h->pipe_run) ++s_hi;
+    while (s_hi < n_str && str_off[s_hi + 1] - str_off[s_lo] <= run_cap) ++s_hi;
     const int64_t nb = str_off[s_hi] - str_off[s_lo];
-    if (nb > h->max_launch) return fail(SW_ERR_ARG, "sw_encode_batch: a single string exceeds the launch limit (2^30 - 64 bytes)");
+    if (nb > h->max_launch)  // (only a run of one string can be over run_cap)
+      return fail(SW_ERR_ARG, "sw_encode_batch: a single string exceeds the launch limit");
     runs.emplace_back(s_lo, s_hi);
     max_b = std::max(max_b, nb);
     max_s = std::max(max_s, s_hi - s_lo);

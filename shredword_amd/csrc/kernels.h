@@ -32,10 +32,7 @@
 
 namespace sw {
 
-#ifndef SW_TILE_BITS
-#define SW_TILE_BITS 11
-#endif
-constexpr int kTileBits = SW_TILE_BITS;
+constexpr int kTileBits = 11;
 constexpr int kTile = 1 << kTileBits;        // input bytes per classify workgroup
 constexpr int kThreads = 256;                // 4 waves
 constexpr int kShort = 32;                   // per-lane merge loop up to this many bytes
@@ -72,25 +69,12 @@ constexpr int kDdExactMax = 7;             // dedupe keys of <= this many bytes 
 // streaming accesses (read or written once per launch) carry the non-temporal hint, so the
 // caches keep the randomly gathered merge results instead
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-#ifdef SW_NO_NT
-#define SW_LDNT(p) (*(p))
-#define SW_STNT(p, v) (*(p) = (v))
-#else
 #define SW_LDNT(p) __builtin_nontemporal_load(p)
 #define SW_STNT(p, v) __builtin_nontemporal_store((v), (p))
-#endif
 // the other streaming arrays -- bitmap words, reference lists, tile-local queues -- too
 // (SW_MORE_NT=0: plain accesses; 6.333 -> 6.318 ms per launch, A/B kernel trace)
-#ifndef SW_MORE_NT
-#define SW_MORE_NT 1
-#endif
-#if SW_MORE_NT && !defined(SW_NO_NT)
 #define SW_LDNT2(p) __builtin_nontemporal_load(p)
 #define SW_STNT2(p, v) __builtin_nontemporal_store((v), (p))
-#else
-#define SW_LDNT2(p) (*(p))
-#define SW_STNT2(p, v) (*(p) = (v))
-#endif
 
 // length -> bucket: groups of similar loop trip count
 //   [2] [3] [4] [5,6] [7,8] [9,10] [11,12] [13,16] [17,24] [25,32] long(>32)
@@ -143,11 +127,7 @@ __device__ __forceinline__ uint32_t chunk_lookup(const DevChunkTable& c, const u
     const uint4 q1 = c.sb[chunk_b1(f, c.s_shift)];
     const bool hit = q1.x == w[0] && q1.y == w[1] && (q1.z >> 24) == len;
     v = hit ? (q1.z & 0xFFFFFFu) : v;
-#ifdef SW_CT_TWO_PROBES  // (A/B builds: always probe both candidates)
-    if (!hit) {
-#else
     if (!hit && (q1.w & 1u)) {
-#endif
       const uint4 q2 = c.sb[chunk_b2(f, c.s_m2, c.s_shift)];
       v = (q2.x == w[0] && q2.y == w[1] && (q2.z >> 24) == len) ? (q2.z & 0xFFFFFFu) : v;
     }
@@ -157,11 +137,7 @@ __device__ __forceinline__ uint32_t chunk_lookup(const DevChunkTable& c, const u
     const uint4 a1 = c.lb[2 * b1], t1 = c.lb[2 * b1 + 1];
     const bool hit = a1.x == w[0] && a1.y == w[1] && a1.z == w[2] && a1.w == w[3] && (t1.x >> 24) == len;
     v = hit ? (t1.x & 0xFFFFFFu) : v;
-#ifdef SW_CT_TWO_PROBES
-    if (!hit) {
-#else
     if (!hit && (t1.y & 1u)) {
-#endif
       const uint32_t b2 = chunk_b2(f, c.l_m2, c.l_shift);
       const uint4 a2 = c.lb[2 * b2], t2 = c.lb[2 * b2 + 1];
       v = (a2.x == w[0] && a2.y == w[1] && a2.z == w[2] && a2.w == w[3] && (t2.x >> 24) == len) ? (t2.x & 0xFFFFFFu)
@@ -463,12 +439,6 @@ struct EncArgs {
   uint32_t* big_list;        // queued chunks over kLongLds bytes (their index in the long bucket)
   uint32_t* big_count;       // ... how many (cleared per launch)
   uint32_t ids16;            // every id fits 16 bits (dres layout)
-  // k_classify over a segment of the tiles while the pre-split of the next segment runs
-  // (sw_encode_device): tiles [tile0, tile_end); bitmap words below bits_ready are final.  A tile
-  // that needs a word at or past bits_ready (< n_words) is listed in defer (count, then tile
-  // indices) and classified by k_classify_deferred once the whole bitmap is written.
-  int64_t tile0, tile_end, bits_ready;
-  uint32_t* defer;
 };
 
 #ifdef SW_STAMPS
@@ -553,16 +523,11 @@ __device__ __forceinline__ DdOut dedupe_claim(const EncArgs& a, const uint32_t* 
     }
     if ((cur & ~0x7FFFFFFFULL) != tag) continue;
     const int64_t other = (int64_t)(cur & 0x7FFFFFFFULL);
-#ifndef SW_ABL_NOVERIFY  // (diagnostic timing builds only: a fingerprint match is taken as equal)
     // compare with the claimant's bytes in the input, realigned
     const int64_t g = other + mis, w0 = g >> 2;
     const uint32_t sh = (uint32_t)(g & 3);
     bool same = true;
-#ifdef SW_DD_WORDS  // (A/B builds: word-by-word verification only)
-    if (false) {
-#else
     if ((((uintptr_t)words & 15) == 0) && ((g + n - 1) >> 4) <= ((last_word + 1) >> 2) - 1) {
-#endif
       // 16-byte aligned loads: one memory request per 16-byte block the chunk touches (1-3),
       // not one per word; then the words from the chunk's first word on (selects, no
       // dynamically indexed registers)
@@ -601,7 +566,6 @@ __device__ __forceinline__ DdOut dedupe_claim(const EncArgs& a, const uint32_t* 
       }
     }
     if (!same) continue;
-#endif
     return DdOut{2, idx};
   }
   return DdOut{0, 0};
@@ -614,13 +578,7 @@ __device__ __forceinline__ DdOut dedupe_claim(const EncArgs& a, const uint32_t* 
 static_assert(kTile <= 0x10000, "chunk starts are uint16");
 // ---------------------------------------------------------------------------------------
 constexpr int kWaves = kThreads / 64;
-#ifndef SW_CLS_PREF_STR
-#define SW_CLS_PREF_STR 0
-#endif
-#ifndef SW_LOOK_ROUNDS
-#define SW_LOOK_ROUNDS 1
-#endif
-constexpr int kLookRounds = SW_LOOK_ROUNDS;          // lookup rounds in flight together
+constexpr int kLookRounds = 1;          // lookup rounds in flight together
 constexpr int kQBuf = 64 * (kLookRounds + 1);        // dedupe buffer: one batch + a group of rounds
 constexpr int kWinWords = kWin / 4 + 8;
 
@@ -628,15 +586,8 @@ constexpr int kWinWords = kWin / 4 + 8;
 // per lane) beat the compiler's 5 (81 VGPRs): 2.81 vs 3.05 ms (profiles/r2_e_ab.txt).  k_compact:
 // capped at 6 it spilled 24 B per lane (+0.9 GB of writes, not faster); with its body as a
 // function of (tile, base) (compact_tile) the compiler fits 78 VGPRs, 6 waves, no spill: 1.11 ->
-// 0.95 ms (profiles/r2_k.md).  SW_CLS_WAVES_PER_EU=0: no cap (A/B builds).
-#ifndef SW_CLS_WAVES_PER_EU
-#define SW_CLS_WAVES_PER_EU 6
-#endif
-#if SW_CLS_WAVES_PER_EU > 0
-#define SW_CLS_ATTR __attribute__((amdgpu_waves_per_eu(SW_CLS_WAVES_PER_EU, SW_CLS_WAVES_PER_EU)))
-#else
-#define SW_CLS_ATTR
-#endif
+// 0.95 ms (profiles/r2_k.md).
+#define SW_CLS_ATTR __attribute__((amdgpu_waves_per_eu(6, 6)))
 // one tile (the body of k_classify's tile loop)
 __device__ __forceinline__ void classify_tile(const EncArgs& a, int64_t tile, uint32_t* s_b32, uint16_t* s_cstart,
                                               uint16_t* s_qbuf) {
@@ -646,11 +597,6 @@ __device__ __forceinline__ void classify_tile(const EncArgs& a, int64_t tile, ui
   const int64_t t0 = tile * kTile;
   const int64_t t1 = min(t0 + (int64_t)kTile, a.n_bytes);
   const int64_t w0 = t0 >> 6;
-  const bool partial_bits = a.bits_ready < a.n_words;  // (wave-uniform)
-  if (partial_bits && w0 + kTileWords > a.bits_ready) {  // the halo word is not written yet
-    if (lane == 0) a.defer[1 + atomicAdd(&a.defer[0], 1u)] = (uint32_t)tile;
-    return;
-  }
 
   // 1. stage the window's bytes (1-KiB coalesced 16-byte loads) and the bitmap words (in
   //    registers)
@@ -674,9 +620,6 @@ __device__ __forceinline__ void classify_tile(const EncArgs& a, int64_t tile, ui
   if (lane < 8) s_b32[kWin / 4 + lane] = 0;
   const uint64_t bw = (lane < kTileWords && w0 + lane < a.n_words) ? SW_LDNT2(&a.bits[w0 + lane]) : 0ULL;
   const int64_t s_first = a.tile_slo[tile];  // (prefetched: used by step 6)
-#if SW_CLS_PREF_STR  // (A/B builds: the first 64 strings' offsets loaded before the lookups)
-  const int64_t s_pref = a.str_off[min(s_first + lane, a.n_str)];
-#endif
 
   // 2. chunk starts in [t0, t1): lane w owns bitmap word w
   constexpr int nw_tile = kTile / 64;
@@ -714,12 +657,8 @@ __device__ __forceinline__ void classify_tile(const EncArgs& a, int64_t tile, ui
       const int64_t q = t0 + 64 * (int64_t)src + __ffsll((long long)__shfl(hw, src, 64)) - 1;
       last_end = min(q, a.n_bytes);
     } else if (C > 0) {
-      // (a chunk running past the halo: scan the written words only; none set there -> defer)
-      const int64_t q = next_set_bit(a.bits, a.bits_ready, t0 + 64 * kTileWords, a.n_bytes);
-      if (partial_bits && q >= a.n_bytes) {
-        if (lane == 0) a.defer[1 + atomicAdd(&a.defer[0], 1u)] = (uint32_t)tile;
-        return;
-      }
+      // (a chunk running past the halo)
+      const int64_t q = next_set_bit(a.bits, a.n_words, t0 + 64 * kTileWords, a.n_bytes);
       last_end = min(q, a.n_bytes);
     }
   }
@@ -839,11 +778,7 @@ __device__ __forceinline__ void classify_tile(const EncArgs& a, int64_t tile, ui
 
   // 6. strings starting in this tile: chunk (= slot) index within the tile (k_compact converts)
   for (int64_t s = s_first + lane; s < a.n_str; s += 64) {
-#if SW_CLS_PREF_STR
-    const int64_t p = s == s_first + lane ? s_pref : a.str_off[s];
-#else
     const int64_t p = a.str_off[s];
-#endif
     if (p >= t1) break;
     int lo = 0, hi = C;  // first chunk with start >= p
     const int lp = (int)(p - t0);
@@ -863,19 +798,8 @@ __global__ void __launch_bounds__(kThreads) SW_CLS_ATTR k_classify(EncArgs a) {
   __shared__ uint16_t s_cs_all[kWaves][kTile + 1];   // chunk starts (tile-relative)
   __shared__ uint16_t s_qb_all[kWaves][kQBuf];       // chunks not settled by a lookup, to dedupe
   const int wv = threadIdx.x >> 6;
-  const int64_t tile = a.tile0 + (int64_t)blockIdx.x * kWaves + wv;
-  if (tile < a.tile_end) classify_tile(a, tile, s_b32_all[wv], s_cs_all[wv], s_qb_all[wv]);
-}
-
-// the tiles k_classify deferred (a.defer), once the whole bitmap is written (bits_ready = n_words)
-__global__ void __launch_bounds__(kThreads) SW_CLS_ATTR k_classify_deferred(EncArgs a) {
-  __shared__ __attribute__((aligned(16))) uint32_t s_b32_all[kWaves][kWinWords];
-  __shared__ uint16_t s_cs_all[kWaves][kTile + 1];
-  __shared__ uint16_t s_qb_all[kWaves][kQBuf];
-  const int wv = threadIdx.x >> 6;
-  const uint32_t n = a.defer[0];  // (counted by the earlier launches)
-  for (uint32_t i = blockIdx.x * kWaves + wv; i < n; i += gridDim.x * kWaves)
-    classify_tile(a, (int64_t)a.defer[1 + i], s_b32_all[wv], s_cs_all[wv], s_qb_all[wv]);
+  const int64_t tile = (int64_t)blockIdx.x * kWaves + wv;
+  if (tile < a.n_tiles) classify_tile(a, tile, s_b32_all[wv], s_cs_all[wv], s_qb_all[wv]);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -961,11 +885,7 @@ __device__ __forceinline__ void merge_entry(const EncArgs& a, const uint32_t* wo
   for (int q = 0; q < N / 4; ++q)
 #pragma unroll
     for (int r = 0; r < 4; ++r) id[4 * q + r] = (u[q] >> (8 * r)) & 0xFFu;
-#ifdef SW_ABL_NOLOOP  // ablation builds only: timing experiments, results are wrong
-  const uint32_t alive = (n >= 32) ? ~0u : ((1u << n) - 1u);
-#else
   const uint32_t alive = lane_merge_reg<kWide, k16, N>(a.table, id, n);
-#endif
   if (!act) return;
   uint32_t* dst = a.res + 2 * start;
   int m = 0;
@@ -974,9 +894,7 @@ __device__ __forceinline__ void merge_entry(const EncArgs& a, const uint32_t* wo
 #pragma unroll
   for (int k = 0; k < N; ++k) {
     if ((alive >> k) & 1u) {
-#ifndef SW_ABL_NOWRITE
       dst[1 + m] = id[k];
-#endif
       if (k16) {
         h0 |= m == 0 ? id[k] << 16 : 0u;
         h1 |= m == 1 ? id[k] : m == 2 ? id[k] << 16 : 0u;
@@ -1260,23 +1178,14 @@ __global__ void __launch_bounds__(64) k_merge_long_lds(EncArgs a) {
 // whole chunk runs the wave loop (seg_merge).  Cut points are chosen where the byte pair ranks
 // highest (ideally not a merge at all), which leaves ~1% of the junctions in conflict.
 // ---------------------------------------------------------------------------------------
-#ifndef SW_PIECE_N
-#define SW_PIECE_N 16
-#endif
-#ifndef SW_LS_V2
-#define SW_LS_V2 1  // 1: no chunk-sized rank array in LDS (pair ranks looked up where used)
-#endif
-constexpr int kPieceN = SW_PIECE_N;                              // per-lane register loop size
+constexpr int kPieceN = 16;                              // per-lane register loop size
 constexpr int kPieceW = kPieceN == 32 ? 24 : 12;                 // cut spacing
 constexpr int kCutHalf = kPieceN == 32 ? 4 : 2;                  // cuts in [W k - H, W k + H)
 constexpr int kMaxPieces = (kLongLds + kPieceW - 1) / kPieceW;   // 171 (342)
 constexpr int kJWords = (kMaxPieces + 63) / 64;                  // junction bitmask words
 static_assert(kPieceW + 2 * kCutHalf - 1 <= kPieceN && kPieceW + kCutHalf <= kPieceN, "pieces fit the loop");
 constexpr int kSplitRounds = 6;
-#ifndef SW_BRK_BATCH
-#define SW_BRK_BATCH 8
-#endif
-constexpr int kBrkBatch = SW_BRK_BATCH;                          // byte-pair lookups in flight per lane
+constexpr int kBrkBatch = 8;                          // byte-pair lookups in flight per lane
 constexpr int kMaxWindow = 512;
 
 // May the joint encoding of two adjacent segments differ from their separate encodings?  a: the
@@ -1396,25 +1305,12 @@ __device__ uint64_t wave_merge64(const DevTable& t, uint32_t& id, uint32_t& rk, 
   return alive;
 }
 
-#ifndef SW_LS_WAVES
-#define SW_LS_WAVES 0  // (A/B builds: cap the VGPRs for this many waves per SIMD)
-#endif
-#if SW_LS_WAVES > 0
-#define SW_LS_ATTR __attribute__((amdgpu_waves_per_eu(SW_LS_WAVES, SW_LS_WAVES)))
-#else
-#define SW_LS_ATTR
-#endif
 template <bool kWide, bool k16>
-__global__ void __launch_bounds__(64) SW_LS_ATTR k_merge_long_split(EncArgs a) {
+__global__ void __launch_bounds__(64) k_merge_long_split(EncArgs a) {
   typedef typename std::conditional<k16, uint16_t, uint32_t>::type T;
   constexpr uint32_t TINF = k16 ? 0xFFFFu : kInf;  // (16-bit storage: values <= 0xFFFD)
   __shared__ T s_id[kLongLds];    // bytes, then each piece's ids from its first position
-#if SW_LS_V2
   __shared__ T s_rkw[kMaxWindow];  // pair ranks of the rare window over 64 ids (one lane's loop)
-#else
-  __shared__ T s_brk[kLongLds];   // rank of the byte pair (p, p + 1); output staging at the end
-  __shared__ uint64_t s_kill[64], s_dirty[64];
-#endif
   __shared__ uint16_t s_cut[2][kMaxPieces + 1];  // piece k = [cut[k], cut[k + 1]) (double-buffered)
   __shared__ uint16_t s_cnt[2][kMaxPieces];      // its ids, at s_id[cut[k] ..)
   __shared__ uint8_t s_win[kMaxPieces];          // piece k is a window to encode again
@@ -1443,30 +1339,9 @@ __global__ void __launch_bounds__(64) SW_LS_ATTR k_merge_long_split(EncArgs a) {
     uint32_t* gid = a.res + 2 * start + 1;
     for (int j = lane; j < len; j += 64) s_id[j] = (T)src[j];
     wave_sync_mem();
-#if SW_LS_V2
     // byte-pair ranks looked up where they are used (the input bytes are immutable): no
     // chunk-sized rank array in LDS, so ~12 KB per wave and 3 waves per SIMD instead of 1.75
     auto brk = [&](int p) -> uint32_t { return lookup<kWide>(tb, src[p], src[p + 1]); };
-#else
-    auto brk = [&](int p) -> uint32_t {
-      const uint32_t r = s_brk[p];
-      return r == TINF ? kInf : r;
-    };
-    // the rank of every byte pair, all lanes, kBrkBatch lookups in flight per lane
-    for (int p0 = 0; p0 < len - 1; p0 += 64 * kBrkBatch) {
-      uint32_t r[kBrkBatch];
-#pragma unroll
-      for (int u = 0; u < kBrkBatch; ++u) {
-        const int p = p0 + 64 * u + lane;
-        r[u] = p < len - 1 ? lookup<kWide>(tb, s_id[p], s_id[p + 1]) : kInf;
-      }
-#pragma unroll
-      for (int u = 0; u < kBrkBatch; ++u) {
-        const int p = p0 + 64 * u + lane;
-        if (p < len - 1) s_brk[p] = (T)(r[u] == kInf ? TINF : r[u]);
-      }
-    }
-#endif
     int cur = 0;
     int P = (len + kPieceW - 1) / kPieceW;
     if (lane == 0) { s_cut[0][0] = 0; s_cut[0][P] = (uint16_t)len; }
@@ -1579,7 +1454,6 @@ __global__ void __launch_bounds__(64) SW_LS_ATTR k_merge_long_split(EncArgs a) {
 #ifdef SW_STAMPS
             big_win = true;
 #endif
-#if SW_LS_V2
             for (int q = lane; q < n - 1; q += 64) {
               const uint32_t r = lookup<kWide>(tb, src[c + q], src[c + q + 1]);
               s_rkw[q] = (T)(r == kInf ? TINF : r);
@@ -1590,18 +1464,6 @@ __global__ void __launch_bounds__(64) SW_LS_ATTR k_merge_long_split(EncArgs a) {
               ncnt[j] = (uint16_t)lane_merge_lds<kWide, T>(tb, s_id + c, s_rkw, n);
             }
             wave_sync_mem();
-#else
-            if (lane == 0) {
-              for (int q = 0; q < n; ++q) s_id[c + q] = (T)src[c + q];
-              ncnt[j] = (uint16_t)lane_merge_lds<kWide, T>(tb, s_id + c, s_brk + c, n);
-            }
-            wave_sync_mem();
-            for (int q = lane; q < n - 1; q += 64) {
-              const uint32_t r = lookup<kWide>(tb, src[c + q], src[c + q + 1]);
-              s_brk[c + q] = (T)(r == kInf ? TINF : r);
-            }
-            wave_sync_mem();
-#endif
             continue;
           }
           uint32_t id = lane < n ? (uint32_t)src[c + lane] : 0u;
@@ -1631,17 +1493,10 @@ __global__ void __launch_bounds__(64) SW_LS_ATTR k_merge_long_split(EncArgs a) {
       SW_COUNT(25, len);
       SW_COUNT(26, len > 1024 ? 1 : 0);
       wave_sync_mem();
-#if SW_LS_V2  // (the global work area of k_merge_long: ids then ranks, the chunk's 2 len words)
       for (int j = lane; j < len; j += 64) gid[j] = src[j];
       wave_sync_mem();
       const int64_t m = coop_merge<kWide>(tb, gid, gid + len, len, lane);
       if (lane == 0) gid[-1] = (uint32_t)m;
-#else
-      for (int j = lane; j < len; j += 64) s_id[lds_pos(j)] = (T)src[j];
-      wave_sync_mem();
-      const int m = seg_merge<kWide, T>(tb, s_id, s_brk, s_kill, s_dirty, len, lane, gid);
-      if (lane == 0) gid[-1] = (uint32_t)m;
-#endif
       wave_sync_mem();
       SW_STAMP(16);
       continue;
@@ -1659,18 +1514,11 @@ __global__ void __launch_bounds__(64) SW_LS_ATTR k_merge_long_split(EncArgs a) {
       const int o = total + (int)(incl - c);
       if (k < P) {
         const int b = cut[k];
-#if SW_LS_V2
         for (uint32_t q = 0; q < c; ++q) gid[o + q] = (uint32_t)s_id[b + q];
-#else
-        for (uint32_t q = 0; q < c; ++q) s_brk[o + q] = s_id[b + q];
-#endif
       }
       total += (int)__shfl(incl, 63, 64);
     }
     wave_sync_mem();
-#if !SW_LS_V2
-    for (int q = lane; q < total; q += 64) gid[q] = (uint32_t)s_brk[q];
-#endif
     if (lane == 0) gid[-1] = (uint32_t)total;
     wave_sync_mem();
     SW_STAMP(17);
@@ -1822,13 +1670,7 @@ __device__ __forceinline__ uint4 ref_head(const EncArgs& a, int32_t v) {
   return q;
 }
 
-#ifndef SW_ROUNDS_IN_FLIGHT
-#define SW_ROUNDS_IN_FLIGHT 8
-#endif
-#ifndef SW_TC_ROUNDS
-#define SW_TC_ROUNDS 2
-#endif
-constexpr int kRoundsInFlight = SW_ROUNDS_IN_FLIGHT;  // slot rounds whose loads (then gathers) issue together
+constexpr int kRoundsInFlight = 8;  // slot rounds whose loads (then gathers) issue together
 
 // id count of the result a reference-list entry names
 // (a dense result's count from the byte array: 4 MiB at most, so these random reads mostly hit
@@ -1840,43 +1682,10 @@ __device__ __forceinline__ uint32_t ref_count(const EncArgs& a, uint32_t r) {
   return dn ? c8 : c32;
 }
 
-// ids of tile t (wave-uniform) = settled slots + the id counts of the results its references use
-// (the tile's reference list from k_classify: no pass over the slots)
-__device__ __forceinline__ uint32_t tile_id_count(const EncArgs& a, int64_t t, int lane) {
-  const uint32_t* rl = a.rlist + t * kTile;
-#ifndef SW_NO_PREFETCH
-  // the first round's list entries load with the counts, not after them: one dependent memory
-  // round trip less per tile (most tiles have < 64 references)
-  const uint32_t p0 = SW_LDNT2(&rl[lane]);
-#endif
-  const int C = (int)a.tile_slots[t], nref = (int)a.tile_nref[t];
-  uint32_t c = 0;
-#ifndef SW_NO_PREFETCH
-  c = lane < nref ? ref_count(a, p0) : 0u;
-  for (int i0 = 64; i0 < nref; i0 += 64 * SW_TC_ROUNDS) {
-#else
-  for (int i0 = 0; i0 < nref; i0 += 64 * SW_TC_ROUNDS) {
-#endif
-    uint32_t p[SW_TC_ROUNDS], g[SW_TC_ROUNDS];
-#pragma unroll
-    for (int u = 0; u < SW_TC_ROUNDS; ++u) p[u] = SW_LDNT2(&rl[min(i0 + 64 * u + lane, kTile - 1)]);
-#pragma unroll
-    for (int u = 0; u < SW_TC_ROUNDS; ++u) g[u] = (i0 + 64 * u + lane < nref) ? ref_count(a, p[u]) : 0u;
-#pragma unroll
-    for (int u = 0; u < SW_TC_ROUNDS; ++u) c += g[u];
-  }
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) c += __shfl_xor(c, off, 64);
-  return c + (uint32_t)(C - nref);
-}
-
 // k_tile_count: kTcTiles tiles per wave, their first 64 list entries and sizes loaded together,
 // then their counts: one dependent round trip serves kTcTiles tiles (a tile holds ~58
 // references on prose, so one wave per tile spent most of its life waiting)
-#ifndef SW_TC_TILES
-#define SW_TC_TILES 2
-#endif
-constexpr int kTcTiles = SW_TC_TILES;
+constexpr int kTcTiles = 2;
 __global__ void __launch_bounds__(kThreads) k_tile_count(EncArgs a) {
   const int64_t tb = (((int64_t)blockIdx.x * kThreads + threadIdx.x) >> 6) * kTcTiles;
   const int lane = threadIdx.x & 63;
@@ -1908,18 +1717,7 @@ __global__ void __launch_bounds__(kThreads) k_tile_count(EncArgs a) {
 }
 
 constexpr int kRefCap = 128;    // references per 8-round group gathered through LDS
-#ifndef SW_CP_OUTCAP
-#define SW_CP_OUTCAP 1024
-#endif
-constexpr int kOutCapW = SW_CP_OUTCAP;  // ids per group staged in LDS (the rest are stored directly)
-#ifndef SW_CP_WAVES
-#define SW_CP_WAVES 0  // (A/B builds: cap k_compact's VGPRs for this many waves per SIMD)
-#endif
-#if SW_CP_WAVES > 0
-#define SW_CP_ATTR __attribute__((amdgpu_waves_per_eu(SW_CP_WAVES, SW_CP_WAVES)))
-#else
-#define SW_CP_ATTR
-#endif
+constexpr int kOutCapW = 1024;  // ids per group staged in LDS (the rest are stored directly)
 constexpr uint32_t kLaneCopy = 64;  // results longer than this are copied by the whole wave
 
 // tile t's ids to out + base (base: the ids of the tiles before it); per wave: the group's
@@ -1932,11 +1730,6 @@ __device__ __forceinline__ void compact_tile(const EncArgs& a, int64_t t, int64_
   const uint64_t lt_mask = (lane == 0) ? 0ULL : (~0ULL >> (64 - lane));
   constexpr int R = kRoundsInFlight;
   const int32_t* src = a.scratch + t * kTile;
-#ifdef SW_CP_V0  // (A/B builds: the first group's slots before the slot count is known)
-  int32_t v0[R];
-#pragma unroll
-  for (int u = 0; u < R; ++u) v0[u] = SW_LDNT(&src[min((u << 6) + lane, kTile - 1)]);
-#endif
   const int C = (int)a.tile_slots[t];
   int32_t* dst = out + base;
   // strings starting in this tile: lane i holds string s_lo + i's chunk index (k_classify)
@@ -1944,7 +1737,6 @@ __device__ __forceinline__ void compact_tile(const EncArgs& a, int64_t t, int64_
   const int64_t s_lo = a.tile_slo[t];
   const int64_t s_hi = (t + 1 < a.n_tiles) ? a.tile_slo[t + 1] : a.n_str;
   const int64_t my_s = s_lo + lane;
-#ifndef SW_NO_PREFETCH
   // a string's chunk index loads with its offset, not after it (one dependent round trip
   // less); the out_off of a string past this tile may be being rewritten by its own tile's
   // wave: the value is read but not used then
@@ -1952,10 +1744,6 @@ __device__ __forceinline__ void compact_tile(const EncArgs& a, int64_t t, int64_
   const int64_t s_at = a.str_off[ms], s_cj = a.out_off[ms];
   const bool has_s = my_s < s_hi && s_at < t1;
   const int sj = has_s ? (int)s_cj : -1;
-#else
-  const bool has_s = my_s < s_hi && a.str_off[my_s] < t1;
-  const int sj = has_s ? (int)a.out_off[my_s] : -1;
-#endif
   const bool many = s_hi - s_lo > 64;  // rare: slot offsets go through scratch instead
   uint32_t s_off = 0, carry = 0;
 #ifdef SW_STAMPS
@@ -1964,18 +1752,8 @@ __device__ __forceinline__ void compact_tile(const EncArgs& a, int64_t t, int64_
 #endif
   for (int r0 = 0; r0 * 64 < C; r0 += R) {
     int32_t v[R];
-#ifdef SW_CP_V0
-    if (r0 == 0) {
-#pragma unroll
-      for (int u = 0; u < R; ++u) v[u] = v0[u];
-    } else {
-#pragma unroll
-      for (int u = 0; u < R; ++u) v[u] = SW_LDNT(&src[min(((r0 + u) << 6) + lane, kTile - 1)]);
-    }
-#else
 #pragma unroll
     for (int u = 0; u < R; ++u) v[u] = SW_LDNT(&src[min(((r0 + u) << 6) + lane, kTile - 1)]);
-#endif
     // dense list of the group's references (their index in the list per round and lane)
     uint32_t ridx[R];
     int nref = 0;  // wave-uniform
@@ -1988,9 +1766,7 @@ __device__ __forceinline__ void compact_tile(const EncArgs& a, int64_t t, int64_
       nref += __popcll(mk);
     }
     wave_sync_mem();
-#ifndef SW_ABL_NOGATHER
     for (int i = lane; i < min(nref, kRefCap); i += 64) s_rq[i] = ref_head(a, (int32_t)s_rp[i]);
-#endif
     wave_sync_mem();
     SW_STAMP(9);
     const uint32_t gbase = carry;  // the group's first id, tile-relative
@@ -2003,9 +1779,6 @@ __device__ __forceinline__ void compact_tile(const EncArgs& a, int64_t t, int64_
       const bool ref = valid && v[u] < 0;
       uint4 q = make_uint4(0, 0, 0, 0);
       if (ref) q = ridx[u] < (uint32_t)kRefCap ? s_rq[ridx[u]] : ref_head(a, v[u]);
-#ifdef SW_ABL_NOGATHER
-      q.x = 2;
-#endif
       const bool dense = ref && slot_is_dref(v[u]);
       const bool d16 = dense && a.ids16 != 0;
       const uint32_t m = ref ? (dense ? (q.x & 0xFFFFu) : q.x) : (valid ? 1u : 0u);
@@ -2058,11 +1831,7 @@ __device__ __forceinline__ void compact_tile(const EncArgs& a, int64_t t, int64_
     wave_sync_mem();
     // the staged ids: one contiguous 256-byte store per 64 ids
     const uint32_t staged = min(carry - gbase, (uint32_t)kOutCapW);
-#ifndef SW_ABL_NOSTORE  // ablation builds only: timing experiments, results are wrong
     for (uint32_t i = lane; i < staged; i += 64) SW_STNT(&dst[gbase + i], s_out[i]);
-#else
-    if (staged == 0xFFFFFFFFu) dst[0] = s_out[lane];
-#endif
     wave_sync_mem();  // (s_rp / s_rq / s_out are rewritten by the next group)
 #ifdef SW_STAMPS
     __builtin_amdgcn_s_waitcnt(0);
@@ -2087,7 +1856,7 @@ __device__ __forceinline__ void compact_tile(const EncArgs& a, int64_t t, int64_
 #endif
 }
 
-__global__ void __launch_bounds__(kThreads) SW_CP_ATTR k_compact(EncArgs a, const int64_t* tile_base, int32_t* out) {
+__global__ void __launch_bounds__(kThreads) k_compact(EncArgs a, const int64_t* tile_base, int32_t* out) {
   __shared__ uint32_t s_rp_all[kWaves][kRefCap];
   __shared__ uint4 s_rq_all[kWaves][kRefCap];
   __shared__ int32_t s_out_all[kWaves][kOutCapW];  // a group's ids, staged for 256-B stores
@@ -2095,52 +1864,6 @@ __global__ void __launch_bounds__(kThreads) SW_CP_ATTR k_compact(EncArgs a, cons
   const int64_t t = ((int64_t)blockIdx.x * kThreads + threadIdx.x) >> 6;
   if (t >= a.n_tiles) return;
   compact_tile(a, t, tile_base[t], out, s_rp_all[wv], s_rq_all[wv], s_out_all[wv]);
-}
-
-// ---------------------------------------------------------------------------------------
-// k_compact_lb: k_tile_count, the scan of the tile counts and k_compact in one pass.  A wave
-// takes the next tile in dispatch order (a ticket), counts its ids, publishes the count, finds
-// the ids before it by a decoupled look-back over the tiles before it (each holds its count or,
-// once known, its inclusive prefix), publishes its prefix, then compacts.  A tile only waits on
-// tiles that took their ticket earlier and publish their count without waiting: no deadlock.
-// flags[t] = status << 62 | value (0: not yet, 1: count, 2: inclusive prefix); zeroed per launch.
-// ---------------------------------------------------------------------------------------
-constexpr uint64_t kLbCount = 1ULL << 62, kLbIncl = 2ULL << 62, kLbValue = (1ULL << 62) - 1;
-constexpr uint32_t kLbMaxPolls = 1u << 22;  // (a bound on every wait: a bug gives wrong ids, never a hang)
-
-__global__ void __launch_bounds__(kThreads) k_compact_lb(EncArgs a, uint64_t* flags, uint32_t* ticket, int64_t* total,
-                                                         int32_t* out) {
-  __shared__ uint32_t s_rp_all[kWaves][kRefCap];
-  __shared__ uint4 s_rq_all[kWaves][kRefCap];
-  __shared__ int32_t s_out_all[kWaves][kOutCapW];
-  const int wv = threadIdx.x >> 6;
-  const int lane = threadIdx.x & 63;
-  uint32_t tk = 0;
-  if (lane == 0) tk = atomicAdd(ticket, 1u);
-  const int64_t t = (int64_t)__shfl((int)tk, 0, 64);
-  if (t >= a.n_tiles) return;
-  const uint64_t c = tile_id_count(a, t, lane);
-  if (lane == 0) __hip_atomic_store(&flags[t], (t == 0 ? kLbIncl : kLbCount) | c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  int64_t base = 0;
-  for (int64_t e = t - 1; e >= 0;) {  // window: tiles e, e - 1, .., e - 63 (lane i: e - i)
-    const int64_t i = e - lane;
-    uint64_t f = i >= 0 ? __hip_atomic_load(&flags[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : kLbIncl;
-    for (uint32_t polls = 0; __ballot((f >> 62) == 0) && polls < kLbMaxPolls; ++polls) {
-      __builtin_amdgcn_s_sleep(1);
-      if ((f >> 62) == 0) f = __hip_atomic_load(&flags[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    const uint64_t incl = __ballot((f >> 62) == 2);
-    const int stop = incl ? __ffsll((long long)incl) - 1 : 64;  // nearest inclusive prefix
-    uint64_t v = lane <= stop ? (f & kLbValue) : 0;
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
-    base += (int64_t)v;
-    if (incl) break;
-    e -= 64;
-  }
-  if (t > 0 && lane == 0) __hip_atomic_store(&flags[t], kLbIncl | (uint64_t)(base + c), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  if (t == a.n_tiles - 1 && lane == 0) *total = base + (int64_t)c;
-  compact_tile(a, t, base, out, s_rp_all[wv], s_rq_all[wv], s_out_all[wv]);
 }
 
 // every string offset: a complemented value is one k_compact finished; strings starting at or

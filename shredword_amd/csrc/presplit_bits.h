@@ -31,7 +31,6 @@
 #pragma once
 #include <cstdint>
 
-#include "presplit_fsm.h"
 #include "presplit_match.h"
 
 namespace sw {
@@ -40,6 +39,15 @@ namespace psb {
 #define SW_PSB_FI __attribute__((always_inline))  // (the walks take the source by reference: keep it in registers)
 
 constexpr int kChunk = 32;  // payload bytes per lane
+
+// SWAR byte classes: a 32-bit word holds 4 bytes, and a mask has bit 7 of a byte lane set where
+// that byte has the property
+constexpr uint32_t kLane7 = 0x80808080u, kLow7 = 0x7F7F7F7Fu, kLane0 = 0x01010101u;
+
+// lanes with lo <= x <= hi, for x7 < 0x80 in every lane and 0 <= lo <= hi <= 0x7F
+SW_HD inline uint32_t in7(uint32_t x7, uint32_t lo, uint32_t hi) {
+  return (x7 + kLane0 * (0x80 - lo)) & ~(x7 + kLane0 * (0x7F - hi)) & kLane7;
+}
 
 // Class masks of a 32-byte chunk: bit k = byte pos + k.  Classes are set at code-point leads;
 // X marks the continuation bytes of valid UTF-8 sequences.  K1 / K2: an apostrophe followed by a
@@ -90,9 +98,6 @@ struct RegBytes {
 // bytes k .. k + 3 of those 40 (k <= 36).
 template <class Cls, class Bytes>
 SW_HD inline Masks classify(const Bytes& by, uint64_t ss, const Cls& cls, bool cl) {
-  using fsm::in7;
-  using fsm::kLane7;
-  using fsm::kLow7;
   // ASCII classes of the chunk's bytes (words 1..8)
   uint32_t L = 0, N = 0, C = 0, P = 0, H = 0, A = 0;
 #pragma unroll

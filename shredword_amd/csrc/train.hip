@@ -589,6 +589,8 @@ int64_t train(sw_trainer* t) {
   // <= 2 per rewritten symbol)
   uint64_t cap = 1024;
   while (cap < 4 * (uint64_t)std::max<int64_t>(ns, 1)) cap <<= 1;
+  if (cap > (1ULL << 32))  // (slot indices and word lengths are 32-bit)
+    return sw::set_error(SW_ERR_CAP, "sw_trainer_train: more than 2^30 symbols in distinct words");
   t->tab_mask = cap - 1;
   t->out_cap = (int64_t)cap / 2;
   SW_HIP_TRY(hipMalloc(&t->d_ids, sizeof(int32_t) * std::max<int64_t>(ns, 1)));
@@ -787,8 +789,10 @@ extern "C" int32_t sw_trainer_save(const sw_trainer* t, const char* model_path, 
   if (vocab_path) {  // tokens as the reference's C strings (bpe.cpp:686-701): byte 0 is ""
     std::vector<std::string> toks(256 + M);
     for (int i = 1; i < 256; ++i) toks[(size_t)i] = std::string(1, (char)i);
-    for (size_t m = 0; m < M; ++m)
-      toks[256 + m] = toks[(size_t)t->merges[3 * m]] + toks[(size_t)t->merges[3 * m + 1]];
+    // a member can be the UNK id (< 0 with a negative unk_id: bpe.cpp:486-516 does not filter
+    // such pairs); the reference then reads toks[-1] (undefined), here it is the empty string
+    auto tok = [&](int32_t id) -> std::string { return id >= 0 && (size_t)id < 256 + M ? toks[(size_t)id] : std::string(); };
+    for (size_t m = 0; m < M; ++m) toks[256 + m] = tok(t->merges[3 * m]) + tok(t->merges[3 * m + 1]);
     FILE* f = std::fopen(vocab_path, "wb");
     if (!f) return sw::set_error(SW_ERR_ARG, std::string("sw_trainer_save: cannot write ") + vocab_path);
     for (size_t i = 0; i < toks.size(); ++i)

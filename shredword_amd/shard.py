@@ -62,16 +62,17 @@ def reassemble(local_ids, local_off, group=None, device=None, concat=True, width
     `x & 0xFFFF` of the widened value).
     async_op=True (concat=False and both widths given): the collectives are only issued; returns
     (works, result) where result is concat=False's tuple, valid once every work in `works` has
-    been waited on (Work.wait(): with RCCL the caller's stream waits, the host does not).  The
-    next batch's encode can run meanwhile -- the reassembly of batch k overlaps the encode of
-    batch k + 1; local_ids / local_off must not be rewritten before the wait."""
+    been waited on, in order (Work.wait(): with RCCL the caller's stream waits, the host does
+    not; the last work folds the width check into the flag check_bounds reads).  The next
+    batch's encode can run meanwhile -- the reassembly of batch k overlaps the encode of batch
+    k + 1; local_ids / local_off must not be rewritten before the wait."""
     import torch
     import torch.distributed as dist
 
     if async_op and (concat or width is None or width_s is None):
         raise ValueError("reassemble: async_op needs concat=False and both width bounds")
     world = dist.get_world_size(group)
-    works = []
+    works, works_tail = [], []
 
     def gather(out, inp):
         w = dist.all_gather_into_tensor(out, inp, group=group, async_op=async_op)
@@ -88,8 +89,11 @@ def reassemble(local_ids, local_off, group=None, device=None, concat=True, width
         h = both.cpu().tolist()
         width = max(max(h[0::2]), 1) if width is None else width
         width_s = max(max(h[1::2]), 1) if width_s is None else width_s
-    elif not concat:  # (concat=True checks the counts itself below)
-        _pending_checks.append((counts, n_strs, width, width_s))
+    elif not concat:  # (concat=True checks the counts itself below); async: once the gathers are waited on
+        if async_op:
+            works_tail.append(_BoundsCheck(counts, n_strs, int(width), int(width_s)))
+        else:
+            _note_bounds(counts, n_strs, int(width), int(width_s))
     width, width_s = int(width), int(width_s)
     if id_bits not in (16, 32):
         raise ValueError("id_bits must be 16 or 32")
@@ -118,32 +122,98 @@ def reassemble(local_ids, local_off, group=None, device=None, concat=True, width
     gather(recv_o, send_o)
     if not concat:
         res = (recv, counts, width, recv_o, n_strs, width_s)
-        return (works, res) if async_op else res
-    if not wide:
-        recv = recv.to(torch.int32) & 0xFFFF
-    # the concatenation needs the counts on the host (as torch's slicing does)
+        return (works + works_tail, res) if async_op else res
+    # the exact-size result needs the counts on the host (one synchronisation)
     ch, sh = counts.cpu().tolist(), n_strs.cpu().tolist()
     if max(ch) > width or max(sh) > width_s:
         raise RuntimeError("reassemble: a rank's count exceeds the given width bound")
-    ids, offs, disp = [], [], 0
+    out_ids, out_off = compact((recv, counts, width, recv_o, n_strs, width_s), id_bits)
+    return out_ids[:sum(ch)], out_off[:sum(sh) + 1]
+
+
+def compact(res, id_bits=32, out_ids=None, out_off=None, stream=None):
+    """Step 4 on the gathered buffers of reassemble(concat=False) `res`: the batch's contiguous
+    int32 ids and rebased string offsets, without a host synchronisation.  Returns (out_ids,
+    out_off), sized by the bounds (world * width ids, world * width_s + 1 offsets); the batch's
+    ids are out_ids[:counts.sum()] and its offsets out_off[:n_strs.sum() + 1].
+
+    On a GPU this is one HIP pass (sw_reassemble_device; `stream`: a torch stream, default the
+    current one) -- 16-bit ids are widened on the way; on the CPU (gloo tests) torch ops."""
+    import torch
+
+    recv, counts, width, recv_o, n_strs, width_s = res
+    world = counts.numel()
+    dev = recv.device
+    if out_ids is None:
+        out_ids = torch.empty(max(world * width, 1), dtype=torch.int32, device=dev)
+    if out_off is None:
+        out_off = torch.empty(world * width_s + 1, dtype=torch.int64, device=dev)
+    if out_ids.numel() < world * width or out_off.numel() < world * width_s + 1:
+        raise ValueError("compact: output buffers below the bounds")
+    if dev.type == "cuda":
+        from . import _lib
+        stream = stream or torch.cuda.current_stream(dev)
+        for t in (recv, recv_o, counts, n_strs, out_ids, out_off):  # (buffers the caller may drop before the pass ran)
+            t.record_stream(stream)
+        with torch.cuda.stream(stream):  # (the counts are strided views of the counts all-gather)
+            counts, n_strs = counts.contiguous(), n_strs.contiguous()
+            _lib.check(_lib.lib().sw_reassemble_device(recv.data_ptr() if recv.numel() else None, int(id_bits),
+                                                       counts.data_ptr(), int(width),
+                                                       recv_o.data_ptr() if recv_o.numel() else None,
+                                                       n_strs.data_ptr(), int(width_s), int(world),
+                                                       out_ids.data_ptr(), out_off.data_ptr(), stream.cuda_stream))
+        return out_ids, out_off
+    ch = [min(max(int(c), 0), width) for c in counts.tolist()]
+    sh = [min(max(int(c), 0), width_s) for c in n_strs.tolist()]
+    disp = sdisp = 0
     for r in range(world):
-        ids.append(recv[r * width: r * width + ch[r]])
-        offs.append(recv_o[r * width_s: r * width_s + sh[r]] + disp)
+        blk = recv[r * width: r * width + ch[r]].to(torch.int32)
+        out_ids[disp: disp + ch[r]] = (blk & 0xFFFF) if id_bits == 16 else blk
+        out_off[sdisp: sdisp + sh[r]] = recv_o[r * width_s: r * width_s + sh[r]] + disp
         disp += ch[r]
-    offs.append(torch.tensor([disp], dtype=torch.int64, device=dev))
-    return torch.cat(ids), torch.cat(offs)
+        sdisp += sh[r]
+    out_off[sdisp] = disp
+    return out_ids, out_off
 
 
-_pending_checks = []
+# Width bounds given to reassemble are checked without a host synchronisation: each call folds
+# "some count exceeded its bound" into one flag tensor per device (constant memory however many
+# calls run); check_bounds() reads the flags (one synchronisation) and clears them.
+_bound_flags = {}
+
+
+def _note_bounds(counts, n_strs, width, width_s):
+    import torch
+    over = torch.logical_or((counts > width).any(), (n_strs > width_s).any())
+    flag = _bound_flags.get(counts.device)
+    if flag is None:
+        _bound_flags[counts.device] = over.clone()
+    else:
+        flag.logical_or_(over)
+
+
+class _BoundsCheck:
+    """The bounds check of an async reassembly, as the last entry of its works: its wait() runs
+    after the gathers' waits, so the comparison is ordered after the counts have landed."""
+
+    def __init__(self, counts, n_strs, width, width_s):
+        self.args = (counts, n_strs, width, width_s)
+
+    def wait(self):
+        if self.args is not None:
+            _note_bounds(*self.args)
+            self.args = None
+        return True
 
 
 def check_bounds():
-    """Raise if a width bound given to reassemble was exceeded by an actual count (synchronises)."""
-    bad = [(c.cpu().max().item(), w, s.cpu().max().item(), ws) for c, s, w, ws in _pending_checks
-           if c.cpu().max().item() > w or s.cpu().max().item() > ws]
-    _pending_checks.clear()
+    """Raise if a width bound given to reassemble (concat=False) since the last call was exceeded by
+    an actual count; a too-small bound truncates the gathered ids, so call this once per batch (or
+    per group of batches) before using their results.  Synchronises with the devices."""
+    bad = [str(dev) for dev, flag in _bound_flags.items() if bool(flag.item())]
+    _bound_flags.clear()
     if bad:
-        raise RuntimeError("reassemble: counts %r exceeded the width bounds" % (bad,))
+        raise RuntimeError("reassemble: a rank's count exceeded the width bounds (devices %s)" % ", ".join(bad))
 
 
 def encode_sharded(tok, buf, str_off, chunk_bits_fn=None, group=None):

@@ -27,7 +27,12 @@ class BPETrainer:
         self.trainer = h
 
     def load_corpus(self, path: str):
-        """bpe_load_corpus (bpe.cpp:208-297); IOError as the reference's wrapper raises."""
+        """bpe_load_corpus (bpe.cpp:208-297); IOError as the reference's wrapper raises.
+
+        One difference: a corpus holding NUL bytes is rejected (IOError).  The reference reads it
+        with fgets + strtok (bpe.cpp:230-251), which silently drops the rest of a line after a
+        NUL, up to its 4096-byte read buffer's boundary -- behaviour that depends on that buffer's
+        size, so it is not restated."""
         if _lib.lib().sw_trainer_load_corpus(self.trainer, path.encode("utf-8")) != 0:
             raise IOError(f"Failed to load corpus from {path}: {_lib.lib().sw_last_error().decode()}")
 
@@ -74,10 +79,12 @@ class BPETrainer:
         _lib.check(_lib.lib().sw_trainer_save(self.trainer, model_path.encode("utf-8"), vocab_path.encode("utf-8")))
 
     def tokenizer(self, device=0):
-        """The trained merges as a Tokenizer (merge value = new id, as the .model format)."""
+        """The trained merges as a Tokenizer (merge value = new id, as the .model format).  Merges
+        with a negative member (the UNK id when unk_id < 0) are left out: no byte sequence can
+        produce them, so the encodings are the same."""
         from .tokenizer import Tokenizer
         tok = Tokenizer(device)
-        tok.merges = {(int(a), int(b)): int(v) for a, b, v in self.merges}
+        tok.merges = {(int(a), int(b)): int(v) for a, b, v in self.merges if a >= 0 and b >= 0}
         return tok
 
     def destroy(self):

@@ -146,6 +146,28 @@ def test_batch_split_launches(limit, host_bits):
         assert st.n_chunks == corpus.presplit(full, sub)[1]
 
 
+def test_pipeline_runs_cut_at_launch_limit():
+    """The pipelined host path (batches over 2 runs) with a launch limit BELOW the run size: runs
+    are cut at the smaller of the two, so many small strings never make a run over the limit
+    (ADVICE r2); a single string over the limit is still rejected."""
+    buf, off = corpus.synth(6, corpus.MIXED, 2000, 300)
+    t = tok_for("bl32k.model")
+    exp = oracle_encode(t.merges, buf, off, "cl100k")
+    L, h = _lib.lib(), t._encoder()
+    limit = max(int(np.diff(off).max()), 2000)
+    _lib.check(L.sw_encoder_set_option(h, _lib.SW_OPT_PIPE_RUN_BYTES, 4 * limit))
+    _lib.check(L.sw_encoder_set_option(h, _lib.SW_OPT_MAX_LAUNCH_BYTES, limit))
+    try:
+        assert int(off[-1]) > 2 * 4 * limit  # (the pipelined path)
+        assert_same(t.encode_packed(buf, off), exp)
+        big, boff = pack([b"a" * 10] * 50 + [b"b" * (limit + 1)] + [b"c" * 10] * 50000)
+        with pytest.raises(_lib.ShredwordError):
+            t.encode_packed(big, boff)
+    finally:
+        L.sw_encoder_set_option(h, _lib.SW_OPT_MAX_LAUNCH_BYTES, 0)
+        L.sw_encoder_set_option(h, _lib.SW_OPT_PIPE_RUN_BYTES, 64 << 20)
+
+
 def test_batch_split_string_over_limit_rejected():
     t = tok_for("toy500.model")
     buf, off = pack([b"a" * 100, b"b" * 300])

@@ -91,3 +91,19 @@ def test_gpu_trainer_negative_unk_matches_oracle():
     assert t.train() == len(exp_rows) > 0
     np.testing.assert_array_equal(t.merges, exp_rows)
     np.testing.assert_array_equal(t.token_freq, exp_freq)
+    # save and tokenizer() with members that are the (negative) UNK id: a negative member renders
+    # as the empty string, and tokenizer() leaves such merges out (no byte sequence reaches them)
+    neg = [(int(a), int(b)) for a, b, _ in exp_rows if a < 0 or b < 0]
+    import tempfile
+    with tempfile.TemporaryDirectory() as d:
+        t.save(d + "/m.model", d + "/m.vocab")
+        rows = np.fromfile(d + "/m.model", dtype=np.int32).reshape(-1, 3)
+        np.testing.assert_array_equal(rows, exp_rows)
+        vocab = open(d + "/m.vocab", "rb").read()
+        assert vocab.endswith(b"\n") and vocab.count(b"\n") == 256 + len(exp_rows) + 1  # (+1: byte 10's own)
+    tok = t.tokenizer()
+    assert all(a >= 0 and b >= 0 for a, b in tok.merges)
+    assert len(tok.merges) == len(exp_rows) - len(neg)
+    sample = b" ".join(words[:50]).decode()
+    assert tok.decode(tok.encode(sample)) == sample
+    tok.close()

@@ -1,10 +1,14 @@
 """Pin the oracle (oracle/sw_oracle.c) to the golden vectors generated from the reference's own
 primitives (oracle/make_golden.py).  CPU only."""
+import hashlib
+import json
+import os
+
 import numpy as np
 import pytest
 
 import oracle
-from conftest import PATTERNS, golden_index, load_fixture, load_model_merges
+from conftest import GOLD, PATTERNS, golden_index, load_fixture, load_model_merges
 
 FIXTURES = golden_index()["fixtures"]
 
@@ -50,3 +54,28 @@ def test_oracle_primitive_kats(primitives):
         # one merge step only applies when the pair is the sole merge; the full loop may merge
         # again on the new ids, which a one-pair table with idx > 255 never does
         assert m.encode_chunk(data) == case["out"]
+
+
+SCALE = os.path.join(GOLD, "scale_digests.json")
+
+
+@pytest.mark.parametrize("name", sorted(json.load(open(SCALE))["configs"]) if os.path.exists(SCALE) else [])
+def test_oracle_matches_reference_at_scale(name):
+    """The oracle on >= 16 MB prefixes of the bench's own C2 / C5 batches (4 MB with the GPT-2
+    pattern) against digests of the REFERENCE's encode of the same strings (oracle/
+    make_golden_scale.py: per block of strings, the token count and the sha256 of the ids)."""
+    from shredword_amd import corpus
+    g = json.load(open(SCALE))
+    cfg = g["configs"][name]
+    n = cfg["n_strings"]
+    buf, off = corpus.synth(g["seed"], cfg["kind"], n, cfg["mean_len"], n_threads=8)
+    assert int(off[-1]) == cfg["n_bytes"]
+    m = oracle.OracleModel(load_model_merges(cfg["model"]))
+    ids, ids_off = m.encode_batch(buf, off, PATTERNS[cfg["pattern"]], n_threads=8)
+    assert len(ids) == cfg["n_tokens"]
+    B = g["block_strings"]
+    for k, (cnt, digest) in enumerate(cfg["blocks"]):
+        s0, s1 = k * B, min(n, (k + 1) * B)
+        blk = np.ascontiguousarray(ids[ids_off[s0]:ids_off[s1]], dtype="<i4")
+        assert len(blk) == cnt, "block %d: %d ids, the reference %d" % (k, len(blk), cnt)
+        assert hashlib.sha256(blk.tobytes()).hexdigest() == digest, "block %d (strings %d..%d)" % (k, s0, s1)

@@ -13,9 +13,26 @@ import numpy as np
 import pytest
 
 from shredword_amd import corpus
-from test_presplit_fsm import ALPHABET, fuzz_strings, pack
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def pack(datas):
+    off = np.zeros(len(datas) + 1, dtype=np.int64)
+    np.cumsum([len(d) for d in datas], out=off[1:])
+    return np.frombuffer(b"".join(datas) or b"\0", dtype=np.uint8)[:int(off[-1])].copy(), off
+
+
+ALPHABET = ["a", "Z", "s", "l", "ll", "ve", "re", "e", "T", " ", "  ", "\n", "\r\n", "\t", "'", "'s", "'LL", "'ve",
+            "'Re", "1", "12345", ".", "!!", "...", "\u00a0", "\u3000", "\u00e9", "\u017f", "\u4e2d\u6587",
+            "\U0001f642", "\u0301", "\ud7ff", "x\n\n", " 1", " .", " '", "\x00", "\x7f", "\x0b", "\x85", "\u2028",
+            "\u00b2", "\u0663", "word", "Hello", " world"]
+
+
+def fuzz_strings(seed, n, kmax=40, alphabet=ALPHABET):
+    rng = random.Random(seed)
+    return ["".join(rng.choice(alphabet) for _ in range(rng.randint(0, kmax))).encode("utf-8", "surrogatepass")
+            for _ in range(n)]
 
 
 @pytest.fixture(scope="module")

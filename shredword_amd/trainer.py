@@ -80,11 +80,17 @@ class BPETrainer:
 
     def tokenizer(self, device=0):
         """The trained merges as a Tokenizer (merge value = new id, as the .model format).  Merges
-        with a negative member (the UNK id when unk_id < 0) are left out: no byte sequence can
-        produce them, so the encodings are the same."""
+        with a negative member (the UNK id when unk_id < 0), and transitively the merges built on
+        them, are left out: no byte sequence can produce them, so the encodings are the same (and
+        build_vocab, base.py:60-79, can render every kept merge)."""
         from .tokenizer import Tokenizer
         tok = Tokenizer(device)
-        tok.merges = {(int(a), int(b)): int(v) for a, b, v in self.merges if a >= 0 and b >= 0}
+        made, merges = set(range(256)), {}
+        for a, b, v in self.merges.tolist():
+            if a in made and b in made:
+                merges[(a, b)] = v
+                made.add(v)
+        tok.merges = merges
         return tok
 
     def destroy(self):

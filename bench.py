@@ -155,7 +155,14 @@ def main():
     d_buf = torch.from_numpy(buf).to(dev)
     d_off = torch.from_numpy(off).to(dev)
     d_bits = torch.from_numpy(bits.view(np.int64)).to(dev) if host_ps else None
-    d_out = torch.empty(int(cap.item()), dtype=torch.int32, device=dev)
+    gather = use_dist and not args.no_gather
+    id_bits = 16 if tok.ids16 else 32  # (the ids cross xGMI as 16 bits when every id fits: SURVEY.md 8(e))
+    # the multi-GPU step encodes straight into the transport's width (SW_OPT_OUT_BITS 16: no
+    # conversion pass before the gather, half the output bytes); N=1 writes int32
+    out16 = gather and id_bits == 16
+    if out16:
+        _lib.check(L.sw_encoder_set_option(h, _lib.SW_OPT_OUT_BITS, 16))
+    d_out = torch.empty(int(cap.item()), dtype=torch.int16 if out16 else torch.int32, device=dev)
     d_oo = torch.empty(n_str + 1, dtype=torch.int64, device=dev)
     stream = torch.cuda.current_stream(dev).cuda_stream
 
@@ -175,8 +182,6 @@ def main():
     n_tok_c = ctypes.c_int64()
     encode(ctypes.byref(n_tok_c))
     n_tok = int(n_tok_c.value)
-    gather = use_dist and not args.no_gather
-    id_bits = 16 if tok.ids16 else 32  # (the ids cross xGMI as 16 bits when every id fits: SURVEY.md 8(e))
 
     # the gathers' widths: every rank's counts are the same every step (same corpus), so the
     # maxima are taken once here and the timed step has no host synchronisation
@@ -266,7 +271,8 @@ def main():
         disp, sdisp = sum(cs[:rank]), sum(ss[:rank])
         f_ids, f_off = finals[last]
         o_ids, o_off = outs[last]
-        reassembly_ok = bool(torch.equal(f_ids[disp:disp + n_tok], o_ids[:n_tok])
+        mine_ids = (o_ids[:n_tok].to(torch.int32) & 0xFFFF) if out16 else o_ids[:n_tok]
+        reassembly_ok = bool(torch.equal(f_ids[disp:disp + n_tok], mine_ids)
                              and torch.equal(f_off[sdisp:sdisp + n_str] - disp, o_off[:n_str])
                              and int(f_off[sum(ss)].item()) == sum(cs))
         ok_t = torch.tensor([1 if reassembly_ok else 0], dtype=torch.int64, device=dev)
@@ -383,6 +389,8 @@ def main():
         om.encode_batch(sbuf, soff, pat, n_threads=args.threads)
         dtm = time.perf_counter() - tc
         got = d_out[:int(ooff_cpu[-1])].cpu().numpy()
+        if out16:
+            got = got.astype(np.int32) & 0xFFFF
         got_off = d_oo[:k + 1].cpu().numpy()
         parity = bool(np.array_equal(got, ids_cpu) and np.array_equal(got_off, ooff_cpu))
         cpu = {"value": round(len(sbuf) / dt1 / 1e6, 3), "unit": "MB/s", "cores": 1, "kind": "port",
@@ -407,6 +415,7 @@ def main():
                        "bytes_per_rank": n_bytes, "strings_per_rank": n_str, "merges": len(tok.merges),
                        "model": model, "pattern": args.pattern, "parallelism": "doc-shard x%d" % world,
                        "gather_in_step": gather, "gather_overlaps_next_encode": overlap, "gather_id_bits": id_bits if gather else None,
+                       "encode_out_bits": 16 if out16 else 32,
                        "chunk_table": not args.no_chunk_table,
                        "dedupe": not args.no_dedupe},
             "mtok_per_s": round(all_tok * args.steps / sec / 1e6, 3),

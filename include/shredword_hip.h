@@ -136,6 +136,12 @@ int32_t sw_encoder_reserve(sw_encoder* h, int64_t max_bytes, int64_t max_strings
  *                          after another on the launch stream.  Results identical. */
 #define SW_OPT_MERGE_STREAMS 13
 /* (options 14 and 15 were A/B knobs of round 2, removed: set_option rejects them) */
+/*   SW_OPT_OUT_BITS        32 (default): sw_encode_device writes int32 ids; 16: it writes uint16
+ *                          ids (d_out_ids is then a uint16_t*; only for tables whose every id
+ *                          fits, SW_INFO_IDS16 -- SW_ERR_ARG otherwise).  The multi-GPU driver's
+ *                          16-bit transport: no conversion pass, half the output bytes.
+ *                          sw_encode_batch is not affected (host results are int32). */
+#define SW_OPT_OUT_BITS 16
 int32_t sw_encoder_set_option(sw_encoder* h, int32_t option, int64_t value);
 
 /* Encoder facts (sw_encoder_get_info): distinct merges, whole-chunk table entries, whether the

@@ -106,6 +106,7 @@ struct sw_encoder {
   // the merge kernels of different length buckets are independent: forked onto these streams
   // they overlap (each alone leaves most of the chip idle), joined before k_tile_count
   bool merge_fork = true;             // SW_OPT_MERGE_STREAMS
+  bool out16 = false;                 // SW_OPT_OUT_BITS 16: sw_encode_device writes uint16 ids
   hipStream_t s_fork[3] = {nullptr, nullptr, nullptr};
   hipEvent_t ev_fork = nullptr, ev_join[3] = {nullptr, nullptr, nullptr};
   sw::HostPool* pool = nullptr;
@@ -486,6 +487,11 @@ extern "C" int32_t sw_encoder_set_option(sw_encoder* h, int32_t option, int64_t 
     case SW_OPT_LONG_SPLIT: h->long_split = value != 0; return SW_OK;
     case SW_OPT_PIPE_COPY_KERNELS: h->pipe_kcopy = value != 0; return SW_OK;
     case SW_OPT_MERGE_STREAMS: h->merge_fork = value != 0; return SW_OK;
+    case SW_OPT_OUT_BITS:
+      if (value != 16 && value != 32) return fail(SW_ERR_ARG, "SW_OPT_OUT_BITS: 16 or 32");
+      if (value == 16 && !h->ids16) return fail(SW_ERR_ARG, "SW_OPT_OUT_BITS 16: a table id does not fit 16 bits");
+      h->out16 = value == 16;
+      return SW_OK;
     case SW_OPT_PIPE_DEPTH:
       if (value < 2 || value > 4) return fail(SW_ERR_ARG, "pipeline depth: 2 .. 4");
       h->pipe_depth = (int)value;
@@ -560,11 +566,14 @@ extern "C" int32_t sw_encoder_phase_cycles(sw_encoder* h, double* out32, int32_t
 #endif
 }
 
-extern "C" int32_t sw_encode_device(sw_encoder* h, const uint8_t* d_bytes, int64_t n_bytes, const int64_t* d_str_off,
-                                    int64_t n_str, const uint64_t* d_chunk_bits, int32_t* d_out_ids,
-                                    int64_t* d_out_off, void* stream, int64_t* n_tokens_host) {
+namespace {
+// the device pipeline; d_out_ids is int32_t*, or uint16_t* when out16 (the table is ids16)
+int32_t encode_device(sw_encoder* h, const uint8_t* d_bytes, int64_t n_bytes, const int64_t* d_str_off, int64_t n_str,
+                      const uint64_t* d_chunk_bits, void* d_out_ids, bool out16, int64_t* d_out_off, void* stream,
+                      int64_t* n_tokens_host) {
   if (!h || n_bytes < 0 || n_str < 0 || !d_str_off || !d_out_off || (n_bytes > 0 && (!d_bytes || !d_out_ids)))
     return fail(SW_ERR_ARG, "sw_encode_device: bad arguments");
+  if (out16 && !h->ids16) return fail(SW_ERR_ARG, "sw_encode_device: 16-bit output needs a table whose ids fit 16 bits");
   if (n_bytes > kMaxLaunchBytes) return fail(SW_ERR_ARG, "sw_encode_device: n_bytes > 2^30 - 64 (split the batch)");
   DeviceGuard g(h->device);
   hipStream_t st = (hipStream_t)stream;  // (NULL: the null stream, as torch's default stream)
@@ -666,7 +675,10 @@ extern "C" int32_t sw_encode_device(sw_encoder* h, const uint8_t* d_bytes, int64
     hipLaunchKernelGGL(k_tile_count, dim3((unsigned)((n_tiles + kWaves * kTcTiles - 1) / (kWaves * kTcTiles))),
                        dim3(kThreads), 0, st, a);
     HIP_TRY(launch_scan(st, h->d_tile_cnt, n_tiles, h->d_part, h->d_tile_base, h->d_total));
-    hipLaunchKernelGGL(k_compact, wg, dim3(kThreads), 0, st, a, h->d_tile_base, d_out_ids);
+    if (out16)
+      hipLaunchKernelGGL(k_compact<uint16_t>, wg, dim3(kThreads), 0, st, a, h->d_tile_base, (uint16_t*)d_out_ids);
+    else
+      hipLaunchKernelGGL(k_compact<int32_t>, wg, dim3(kThreads), 0, st, a, h->d_tile_base, (int32_t*)d_out_ids);
     HIP_TRY(hipGetLastError());
   } else {
     HIP_TRY(hipMemsetAsync(h->d_total, 0, sizeof(int64_t), st));
@@ -686,6 +698,15 @@ extern "C" int32_t sw_encode_device(sw_encoder* h, const uint8_t* d_bytes, int64
     HIP_TRY(hipStreamSynchronize(st));
   }
   return SW_OK;
+}
+
+}  // namespace
+
+extern "C" int32_t sw_encode_device(sw_encoder* h, const uint8_t* d_bytes, int64_t n_bytes, const int64_t* d_str_off,
+                                    int64_t n_str, const uint64_t* d_chunk_bits, int32_t* d_out_ids,
+                                    int64_t* d_out_off, void* stream, int64_t* n_tokens_host) {
+  return encode_device(h, d_bytes, n_bytes, d_str_off, n_str, d_chunk_bits, d_out_ids, h && h->out16, d_out_off, stream,
+                       n_tokens_host);
 }
 
 // ids to 16 bits for the device -> host copy (every id of an ids16 table fits)
@@ -869,8 +890,8 @@ int32_t encode_batch_pipelined(sw_encoder* h, const uint8_t* bytes, const int64_
     }
     HIP_TRY(hipEventRecord(p.e_in, h->s_h2d));
     HIP_TRY(hipStreamWaitEvent(h->stream, p.e_in, 0));
-    const int32_t r = sw_encode_device(h, p.d_in, nb, p.d_off, ns, chunk_bits ? p.d_bits : nullptr, p.d_out, p.d_oo,
-                                       h->stream, nullptr);
+    const int32_t r = encode_device(h, p.d_in, nb, p.d_off, ns, chunk_bits ? p.d_bits : nullptr, p.d_out, false,
+                                    p.d_oo, h->stream, nullptr);
     if (r) return r;
     if (count && nb > 0)
       hipLaunchKernelGGL(k_popcount, dim3(1024), dim3(256), 0, h->stream, h->d_pbits, (nb + 63) / 64, h->d_pcount);
@@ -1067,8 +1088,8 @@ extern "C" int32_t sw_encode_batch(sw_encoder* h, const uint8_t* bytes, const in
   h->ev_used = 0;
   const int32_t was_pattern = h->pattern;
   if (device_presplit) h->pattern = pattern;
-  int32_t rc = sw_encode_device(h, h->d_bytes, n_bytes, h->d_str_off, n_str, device_presplit ? nullptr : h->d_bits,
-                                h->d_out, h->d_out_off, st, &n_tok);
+  int32_t rc = encode_device(h, h->d_bytes, n_bytes, h->d_str_off, n_str, device_presplit ? nullptr : h->d_bits,
+                             h->d_out, false, h->d_out_off, st, &n_tok);
   h->pattern = was_pattern;
   if (rc == SW_OK && device_presplit && stats && n_bytes > 0) {  // chunk count for the stats
     HIP_TRY(hipMemsetAsync(h->d_pcount, 0, sizeof(unsigned long long), st));

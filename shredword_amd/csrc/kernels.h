@@ -120,28 +120,46 @@ __device__ __forceinline__ uint32_t lookup(const DevTable& t, uint32_t a, uint32
 // nor carries the spill bit (chunktable.h): one 16-byte request (two for 9..16 bytes) for most
 // chunks.  k_classify is bound by the L2 request rate, not by latency, so fewer requests win
 // over the rare second round trip.
+// one 16-byte load, all of it in registers before any use: otherwise the compiler narrows the load
+// to the words the first compare needs and fetches the rest (the spill bit, the second key word)
+// in a branch -- a second dependent round trip for a share of the lanes, which the wave waits for
+__device__ __forceinline__ u32x4 load16_whole(const uint4* p) {
+  u32x4 q = *(const u32x4*)p;
+  asm volatile("" : "+v"(q));
+  return q;
+}
+// two such loads in flight together (a 32-byte entry)
+__device__ __forceinline__ void load32_whole(const uint4* p, u32x4& a, u32x4& b) {
+  a = *(const u32x4*)p;
+  b = *(const u32x4*)(p + 1);
+  asm volatile("" : "+v"(a), "+v"(b));
+}
+
 __device__ __forceinline__ uint32_t chunk_lookup(const DevChunkTable& c, const uint32_t (&w)[4], uint32_t len) {
   uint32_t v = kInf;
   if (len <= 8) {
     const uint32_t f = chunk_hash(w[0], w[1], 0, 0, len, c.s_m1);
-    const uint4 q1 = c.sb[chunk_b1(f, c.s_shift)];
-    const bool hit = q1.x == w[0] && q1.y == w[1] && (q1.z >> 24) == len;
-    v = hit ? (q1.z & 0xFFFFFFu) : v;
-    if (!hit && (q1.w & 1u)) {
-      const uint4 q2 = c.sb[chunk_b2(f, c.s_m2, c.s_shift)];
-      v = (q2.x == w[0] && q2.y == w[1] && (q2.z >> 24) == len) ? (q2.z & 0xFFFFFFu) : v;
+    const u32x4 q1 = load16_whole(&c.sb[chunk_b1(f, c.s_shift)]);
+    const bool hit = (q1[0] == w[0]) & (q1[1] == w[1]) & ((q1[2] >> 24) == len);
+    v = hit ? (q1[2] & 0xFFFFFFu) : v;
+    if (!hit && (q1[3] & 1u)) {
+      const u32x4 q2 = load16_whole(&c.sb[chunk_b2(f, c.s_m2, c.s_shift)]);
+      v = ((q2[0] == w[0]) & (q2[1] == w[1]) & ((q2[2] >> 24) == len)) ? (q2[2] & 0xFFFFFFu) : v;
     }
   } else {
     const uint32_t f = chunk_hash(w[0], w[1], w[2], w[3], len, c.l_m1);
     const uint32_t b1 = chunk_b1(f, c.l_shift);
-    const uint4 a1 = c.lb[2 * b1], t1 = c.lb[2 * b1 + 1];
-    const bool hit = a1.x == w[0] && a1.y == w[1] && a1.z == w[2] && a1.w == w[3] && (t1.x >> 24) == len;
-    v = hit ? (t1.x & 0xFFFFFFu) : v;
-    if (!hit && (t1.y & 1u)) {
+    u32x4 a1, t1;
+    load32_whole(&c.lb[2 * b1], a1, t1);
+    const bool hit = (a1[0] == w[0]) & (a1[1] == w[1]) & (a1[2] == w[2]) & (a1[3] == w[3]) & ((t1[0] >> 24) == len);
+    v = hit ? (t1[0] & 0xFFFFFFu) : v;
+    if (!hit && (t1[1] & 1u)) {
       const uint32_t b2 = chunk_b2(f, c.l_m2, c.l_shift);
-      const uint4 a2 = c.lb[2 * b2], t2 = c.lb[2 * b2 + 1];
-      v = (a2.x == w[0] && a2.y == w[1] && a2.z == w[2] && a2.w == w[3] && (t2.x >> 24) == len) ? (t2.x & 0xFFFFFFu)
-                                                                                                 : v;
+      u32x4 a2, t2;
+      load32_whole(&c.lb[2 * b2], a2, t2);
+      v = ((a2[0] == w[0]) & (a2[1] == w[1]) & (a2[2] == w[2]) & (a2[3] == w[3]) & ((t2[0] >> 24) == len))
+              ? (t2[0] & 0xFFFFFFu)
+              : v;
     }
   }
   return v;
@@ -1723,7 +1741,8 @@ constexpr uint32_t kLaneCopy = 64;  // results longer than this are copied by th
 // tile t's ids to out + base (base: the ids of the tiles before it); per wave: the group's
 // references, gathered with full lanes before any store (a store ahead of a load in the wave's
 // vmcnt order would make the load wait for it)
-__device__ __forceinline__ void compact_tile(const EncArgs& a, int64_t t, int64_t base, int32_t* out, uint32_t* s_rp,
+template <typename OutT>  // int32_t, or uint16_t (SW_OPT_OUT_BITS 16: every id of the table fits)
+__device__ __forceinline__ void compact_tile(const EncArgs& a, int64_t t, int64_t base, OutT* out, uint32_t* s_rp,
                                              uint4* s_rq, int32_t* s_out) {
   SW_STAMP_INIT;
   const int lane = threadIdx.x & 63;
@@ -1731,7 +1750,7 @@ __device__ __forceinline__ void compact_tile(const EncArgs& a, int64_t t, int64_
   constexpr int R = kRoundsInFlight;
   const int32_t* src = a.scratch + t * kTile;
   const int C = (int)a.tile_slots[t];
-  int32_t* dst = out + base;
+  OutT* dst = out + base;
   // strings starting in this tile: lane i holds string s_lo + i's chunk index (k_classify)
   const int64_t t1 = min(t * kTile + (int64_t)kTile, a.n_bytes);
   const int64_t s_lo = a.tile_slo[t];
@@ -1788,7 +1807,7 @@ __device__ __forceinline__ void compact_tile(const EncArgs& a, int64_t t, int64_
       const uint32_t lo = o - gbase;
       if (valid && !ref) {
         if (lo < (uint32_t)kOutCapW) s_out[lo] = v[u];
-        else dst[o] = v[u];
+        else dst[o] = (OutT)v[u];
       }
       // ids from the head while it has them (nh), then from res at the merged occurrence's p
       const uint32_t nh = d16 ? (m <= 7 ? m : 1u) : dense ? (m <= 3 ? 3u : 2u) : 3u;
@@ -1798,7 +1817,7 @@ __device__ __forceinline__ void compact_tile(const EncArgs& a, int64_t t, int64_
         const uint32_t hm = min(mm, nh);
         auto put = [&](uint32_t k, uint32_t id) {
           if (lo + k < (uint32_t)kOutCapW) s_out[lo + k] = (int32_t)id;
-          else dst[o + k] = (int32_t)id;
+          else dst[o + k] = (OutT)id;
         };
         if (d16) {
           const uint32_t w[4] = {q.x, q.y, q.z, q.w};
@@ -1821,7 +1840,7 @@ __device__ __forceinline__ void compact_tile(const EncArgs& a, int64_t t, int64_
         for (uint32_t k = 3 + lane; k < mL; k += 64) {
           const int32_t id = (int32_t)a.res[2 * pL + 1 + k];
           if (loL + k < (uint32_t)kOutCapW) s_out[loL + k] = id;
-          else dst[oL + k] = id;
+          else dst[oL + k] = (OutT)id;
         }
       }
       const uint32_t got = (uint32_t)__shfl((int)o, sj & 63, 64);
@@ -1831,7 +1850,7 @@ __device__ __forceinline__ void compact_tile(const EncArgs& a, int64_t t, int64_
     wave_sync_mem();
     // the staged ids: one contiguous 256-byte store per 64 ids
     const uint32_t staged = min(carry - gbase, (uint32_t)kOutCapW);
-    for (uint32_t i = lane; i < staged; i += 64) SW_STNT(&dst[gbase + i], s_out[i]);
+    for (uint32_t i = lane; i < staged; i += 64) SW_STNT(&dst[gbase + i], (OutT)s_out[i]);
     wave_sync_mem();  // (s_rp / s_rq / s_out are rewritten by the next group)
 #ifdef SW_STAMPS
     __builtin_amdgcn_s_waitcnt(0);
@@ -1856,7 +1875,8 @@ __device__ __forceinline__ void compact_tile(const EncArgs& a, int64_t t, int64_
 #endif
 }
 
-__global__ void __launch_bounds__(kThreads) k_compact(EncArgs a, const int64_t* tile_base, int32_t* out) {
+template <typename OutT>
+__global__ void __launch_bounds__(kThreads) k_compact(EncArgs a, const int64_t* tile_base, OutT* out) {
   __shared__ uint32_t s_rp_all[kWaves][kRefCap];
   __shared__ uint4 s_rq_all[kWaves][kRefCap];
   __shared__ int32_t s_out_all[kWaves][kOutCapW];  // a group's ids, staged for 256-B stores

@@ -45,7 +45,8 @@ def reassemble(local_ids, local_off, group=None, device=None, concat=True, width
                async_op=False):
     """Collective reassembly of per-rank encodes (steps 1-4 above) on every rank.
 
-    local_ids: torch int32 [>= local count] on `device`; local_off: torch int64 [m+1] with
+    local_ids: torch int32 [>= local count] on `device` (or int16 holding each id's low 16 bits, e.g.
+    from an encode with SW_OPT_OUT_BITS 16, when id_bits=16); local_off: torch int64 [m+1] with
     local_off[0] == 0.  Returns (ids int32 [total], off int64 [n+1]) for the whole batch, on
     `device`, identical on every rank.
 
@@ -97,20 +98,21 @@ def reassemble(local_ids, local_off, group=None, device=None, concat=True, width
     width, width_s = int(width), int(width_s)
     if id_bits not in (16, 32):
         raise ValueError("id_bits must be 16 or 32")
-    if local_ids.numel() >= width and local_ids.dtype == torch.int32 and local_ids.device == dev:
+    wide = id_bits == 32
+    # the send buffer: the caller's ids as they are when they already have the transport's width
+    # (16-bit: an encode with SW_OPT_OUT_BITS 16 -- no conversion pass), else converted
+    want = torch.int32 if wide else torch.int16
+    if local_ids.numel() >= width and local_ids.dtype == want and local_ids.device == dev:
         send = local_ids[:width]  # (slots past the count are padding: never read)
     else:
-        send = torch.zeros(width, dtype=torch.int32, device=dev)
+        send = torch.zeros(width, dtype=want, device=dev)
         k = min(width, local_ids.numel())
-        send[:k] = local_ids[:k].to(device=dev, dtype=torch.int32)
-    wide = id_bits == 32
+        # (16 bits: the low 16 bits of each id, two's-complement truncation of the int32 value)
+        send[:k] = local_ids[:k].to(device=dev, dtype=torch.int32).to(want)
+    recv = torch.empty(world * width, dtype=want, device=dev)
     if wide:
-        recv = torch.empty(world * width, dtype=torch.int32, device=dev)
         gather(recv, send)
-    else:  # the low 16 bits of each id (two's-complement truncation), moved as bytes (RCCL and gloo
-        # have no 16-bit integer type; an all-gather only copies)
-        send = send.to(torch.int16)
-        recv = torch.empty(world * width, dtype=torch.int16, device=dev)
+    else:  # moved as bytes (RCCL and gloo have no 16-bit integer type; an all-gather only copies)
         gather(recv.view(torch.uint8), send.view(torch.uint8))
     m = local_off.numel() - 1
     if local_off.numel() >= width_s and local_off.dtype == torch.int64 and local_off.device == dev:

@@ -5,6 +5,7 @@ primitives (tests/golden), and against the oracle restatement (oracle/sw_oracle.
 to those vectors by test_oracle_golden.py) on seeded inputs and edge cases.  All calls go
 through the C-ABI (shredword_amd -> libshredword_hip.so).
 """
+import os
 import random
 
 import numpy as np
@@ -13,7 +14,7 @@ import pytest
 import oracle
 import shredword_amd as sa
 from shredword_amd import _lib, corpus
-from conftest import PATTERNS, golden_index, load_fixture, load_model_merges
+from conftest import GOLD, PATTERNS, golden_index, load_fixture, load_model_merges
 
 pytestmark = pytest.mark.gpu
 
@@ -296,3 +297,39 @@ def test_dedupe_options_validated():
     for opt, bad in ((_lib.SW_OPT_DEDUPE_SLOTS, 12), (_lib.SW_OPT_DEDUPE_SLOTS, 4), (_lib.SW_OPT_DEDUPE_FP_BITS, 27),
                      (99, 1)):
         assert L.sw_encoder_set_option(h, opt, bad) == _lib.SW_ERR_ARG
+
+
+@pytest.mark.parametrize("fixture,model", [("enc_bl50k_stress.npz", "bl50k.model"), ("enc_bl32k_mixed.npz", "bl32k.model")])
+def test_out_bits16_option(fixture, model):
+    """SW_OPT_OUT_BITS 16: sw_encode_device writes uint16 ids (the multi-GPU transport's width) --
+    the reference-generated ids' low 16 bits, ids >= 32768 included (bl50k); rejected for a table
+    with an id over 16 bits; sw_encode_batch still returns int32."""
+    import ctypes
+
+    import torch
+    fx = np.load(os.path.join(GOLD, fixture))
+    t = sa.Tokenizer(device=0)
+    t.merges = load_model_merges(model)
+    L, h = _lib.lib(), t._encoder()
+    _lib.check(L.sw_encoder_set_option(h, _lib.SW_OPT_OUT_BITS, 16))
+    dev = torch.device("cuda", 0)
+    d_buf, d_off = torch.from_numpy(fx["bytes"]).to(dev), torch.from_numpy(fx["off"]).to(dev)
+    d_out = torch.full((len(fx["bytes"]) + 8,), -1, dtype=torch.int16, device=dev)
+    d_oo = torch.empty(len(fx["off"]), dtype=torch.int64, device=dev)
+    n_tok = ctypes.c_int64()
+    _lib.check(L.sw_encode_device(h, d_buf.data_ptr(), len(fx["bytes"]), d_off.data_ptr(), len(fx["off"]) - 1, None,
+                                  d_out.data_ptr(), d_oo.data_ptr(), torch.cuda.current_stream(dev).cuda_stream,
+                                  ctypes.byref(n_tok)))
+    n = n_tok.value
+    assert n == len(fx["ids"])
+    np.testing.assert_array_equal(d_out[:n].cpu().numpy().view(np.uint16).astype(np.int64), fx["ids"])
+    assert int(d_out[n].item()) == -1  # (nothing written past the ids)
+    np.testing.assert_array_equal(d_oo.cpu().numpy(), fx["ids_off"])
+    assert_same(t.encode_packed(fx["bytes"], fx["off"]), (fx["ids"], fx["ids_off"]))  # (host path: int32)
+    _lib.check(L.sw_encoder_set_option(h, _lib.SW_OPT_OUT_BITS, 32))
+    assert L.sw_encoder_set_option(h, _lib.SW_OPT_OUT_BITS, 8) == _lib.SW_ERR_ARG
+    t.close()
+    w = sa.Tokenizer(device=0)
+    w.merges = {(97, 98): 70000}
+    assert L.sw_encoder_set_option(w._encoder(), _lib.SW_OPT_OUT_BITS, 16) == _lib.SW_ERR_ARG
+    w.close()

@@ -114,56 +114,12 @@ __device__ __forceinline__ uint32_t lookup(const DevTable& t, uint32_t a, uint32
   }
 }
 
-// Whole-chunk table lookup (chunktable.h): the single token a 2..16-byte chunk encodes to, or
-// kInf if the chunk does not encode to exactly one token.  w: the chunk's bytes as LE words,
-// zero padded.  The first candidate bucket, then the second only when the first neither matches
-// nor carries the spill bit (chunktable.h): one 16-byte request (two for 9..16 bytes) for most
-// chunks.  k_classify is bound by the L2 request rate, not by latency, so fewer requests win
-// over the rare second round trip.
-// one 16-byte load, all of it in registers before any use: otherwise the compiler narrows the load
-// to the words the first compare needs and fetches the rest (the spill bit, the second key word)
-// in a branch -- a second dependent round trip for a share of the lanes, which the wave waits for
-__device__ __forceinline__ u32x4 load16_whole(const uint4* p) {
-  u32x4 q = *(const u32x4*)p;
-  asm volatile("" : "+v"(q));
-  return q;
-}
-// two such loads in flight together (a 32-byte entry)
-__device__ __forceinline__ void load32_whole(const uint4* p, u32x4& a, u32x4& b) {
-  a = *(const u32x4*)p;
-  b = *(const u32x4*)(p + 1);
-  asm volatile("" : "+v"(a), "+v"(b));
-}
-
-__device__ __forceinline__ uint32_t chunk_lookup(const DevChunkTable& c, const uint32_t (&w)[4], uint32_t len) {
-  uint32_t v = kInf;
-  if (len <= 8) {
-    const uint32_t f = chunk_hash(w[0], w[1], 0, 0, len, c.s_m1);
-    const u32x4 q1 = load16_whole(&c.sb[chunk_b1(f, c.s_shift)]);
-    const bool hit = (q1[0] == w[0]) & (q1[1] == w[1]) & ((q1[2] >> 24) == len);
-    v = hit ? (q1[2] & 0xFFFFFFu) : v;
-    if (!hit && (q1[3] & 1u)) {
-      const u32x4 q2 = load16_whole(&c.sb[chunk_b2(f, c.s_m2, c.s_shift)]);
-      v = ((q2[0] == w[0]) & (q2[1] == w[1]) & ((q2[2] >> 24) == len)) ? (q2[2] & 0xFFFFFFu) : v;
-    }
-  } else {
-    const uint32_t f = chunk_hash(w[0], w[1], w[2], w[3], len, c.l_m1);
-    const uint32_t b1 = chunk_b1(f, c.l_shift);
-    u32x4 a1, t1;
-    load32_whole(&c.lb[2 * b1], a1, t1);
-    const bool hit = (a1[0] == w[0]) & (a1[1] == w[1]) & (a1[2] == w[2]) & (a1[3] == w[3]) & ((t1[0] >> 24) == len);
-    v = hit ? (t1[0] & 0xFFFFFFu) : v;
-    if (!hit && (t1[1] & 1u)) {
-      const uint32_t b2 = chunk_b2(f, c.l_m2, c.l_shift);
-      u32x4 a2, t2;
-      load32_whole(&c.lb[2 * b2], a2, t2);
-      v = ((a2[0] == w[0]) & (a2[1] == w[1]) & (a2[2] == w[2]) & (a2[3] == w[3]) & ((t2[0] >> 24) == len))
-              ? (t2[0] & 0xFFFFFFu)
-              : v;
-    }
-  }
-  return v;
-}
+// Whole-chunk table (chunktable.h): the single token a 2..16-byte chunk encodes to, or kInf if the
+// chunk does not encode to exactly one token -- table_lookups below.  The first candidate bucket,
+// then the second only when the first neither matches nor carries the spill bit (chunktable.h).
+// The compares are bitwise and every entry is loaded whole into registers before any use:
+// otherwise the compiler narrows a 16-byte load to the words the first compare needs and fetches
+// the rest in a branch, a second dependent round trip (5.97 -> 5.52 ms per C2 launch).
 
 // bytes [ls, ls + len) of an LDS byte window as four zero-padded little-endian words (len <= 16)
 __device__ __forceinline__ void window_words(const uint32_t* w32, int ls, int len, uint32_t (&b)[4]) {
@@ -179,6 +135,84 @@ __device__ __forceinline__ void window_words(const uint32_t* w32, int ls, int le
     const uint32_t m = keep >= 4 ? ~0u : keep <= 0 ? 0u : ((1u << (8 * keep)) - 1u);
     b[i] &= m;
   }
+}
+
+// every loaded value in registers at this point (one wait for all the loads before it, none
+// narrowed into a branch)
+template <int R>
+__device__ __forceinline__ void regs_barrier(u32x4 (&x)[R], u32x4 (&y)[R]) {
+  static_assert(R >= 1 && R <= 4, "rounds");
+  if constexpr (R == 1) asm volatile("" : "+v"(x[0]), "+v"(y[0]));
+  if constexpr (R == 2) asm volatile("" : "+v"(x[0]), "+v"(y[0]), "+v"(x[1]), "+v"(y[1]));
+  if constexpr (R == 3) asm volatile("" : "+v"(x[0]), "+v"(y[0]), "+v"(x[1]), "+v"(y[1]), "+v"(x[2]), "+v"(y[2]));
+  if constexpr (R == 4)
+    asm volatile("" : "+v"(x[0]), "+v"(y[0]), "+v"(x[1]), "+v"(y[1]), "+v"(x[2]), "+v"(y[2]), "+v"(x[3]), "+v"(y[3]));
+}
+
+// The whole-chunk-table answers (chunk_lookup) for R rounds of a tile's chunks (chunk 64 r + lane
+// in round r), every round's probe in flight at once: the first candidate entry of every lane
+// and round is loaded (16 bytes for 2..8-byte chunks, 32 for 9..16), one wait, the compares,
+// then the (rare) second candidates the same way.  The chunk's bytes are read from the LDS
+// window again after the wait rather than held in registers across it.
+template <int R>
+__device__ __forceinline__ void table_lookups(const DevChunkTable& c, const uint32_t* s_b32, const uint16_t* s_cstart,
+                                              int C, int rel_end, int r0, int lane, uint32_t (&tok)[R]) {
+  u32x4 qa[R], qb[R];
+  uint32_t w[R][4];
+  int len[R];
+  uint32_t need2 = 0;  // rounds whose lane must probe the second candidate
+#pragma unroll
+  for (int u = 0; u < R; ++u) {  // first candidates: issue (the 32-byte entries' second half only
+    const int k = ((r0 + u) << 6) + lane;  // for 9..16-byte chunks: no extra request for the rest)
+    const bool valid = k < C;
+    const int ls = valid ? s_cstart[k] : 0;
+    const int end = (k + 1 < C) ? (int)s_cstart[k + 1] : rel_end;
+    len[u] = valid ? end - ls : 0;
+    window_words(s_b32, ls, min(max(len[u], 1), 16), w[u]);
+    tok[u] = len[u] == 1 ? (w[u][0] & 0xFFu) : kInf;
+    const uint4* pa = c.sb;  // (a lane without a probe loads the first bucket, unused)
+    if (len[u] >= 2 && len[u] <= 8) pa = &c.sb[chunk_b1(chunk_hash(w[u][0], w[u][1], 0, 0, len[u], c.s_m1), c.s_shift)];
+    if (len[u] > 8 && len[u] <= 16)
+      pa = &c.lb[2 * chunk_b1(chunk_hash(w[u][0], w[u][1], w[u][2], w[u][3], len[u], c.l_m1), c.l_shift)];
+    qa[u] = *(const u32x4*)pa;
+    qb[u] = u32x4{0u, 0u, 0u, 0u};
+    if (len[u] > 8 && len[u] <= 16) qb[u] = *(const u32x4*)(pa + 1);
+  }
+  regs_barrier<R>(qa, qb);
+  auto compare = [&](int u) -> bool {  // the entry in qa/qb holds the chunk: tok[u] set
+    bool hit;
+    if (len[u] <= 8) {
+      hit = (qa[u][0] == w[u][0]) & (qa[u][1] == w[u][1]) & ((qa[u][2] >> 24) == (uint32_t)len[u]);
+      tok[u] = hit ? (qa[u][2] & 0xFFFFFFu) : tok[u];
+    } else {
+      hit = (qa[u][0] == w[u][0]) & (qa[u][1] == w[u][1]) & (qa[u][2] == w[u][2]) & (qa[u][3] == w[u][3]) &
+            ((qb[u][0] >> 24) == (uint32_t)len[u]);
+      tok[u] = hit ? (qb[u][0] & 0xFFFFFFu) : tok[u];
+    }
+    return hit;
+  };
+#pragma unroll
+  for (int u = 0; u < R; ++u) {  // compares; second candidates: issue
+    if (len[u] < 2 || len[u] > 16) continue;
+    const bool hit = compare(u);
+    const bool spill = ((len[u] <= 8 ? qa[u][3] : qb[u][1]) & 1u) != 0;
+    if (!hit && spill) {
+      need2 |= 1u << u;
+      if (len[u] <= 8) {
+        qa[u] = *(const u32x4*)&c.sb[chunk_b2(chunk_hash(w[u][0], w[u][1], 0, 0, len[u], c.s_m1), c.s_m2, c.s_shift)];
+      } else {
+        const uint4* pa =
+            &c.lb[2 * chunk_b2(chunk_hash(w[u][0], w[u][1], w[u][2], w[u][3], len[u], c.l_m1), c.l_m2, c.l_shift)];
+        qa[u] = *(const u32x4*)pa;
+        qb[u] = *(const u32x4*)(pa + 1);
+      }
+    }
+  }
+  if (!__ballot(need2 != 0)) return;
+  regs_barrier<R>(qa, qb);
+#pragma unroll
+  for (int u = 0; u < R; ++u)  // second candidates: compares
+    if ((need2 >> u) & 1u) compare(u);
 }
 
 __device__ __forceinline__ uint64_t wave_min_u64(uint64_t v) {
@@ -596,7 +630,9 @@ __device__ __forceinline__ DdOut dedupe_claim(const EncArgs& a, const uint32_t* 
 static_assert(kTile <= 0x10000, "chunk starts are uint16");
 // ---------------------------------------------------------------------------------------
 constexpr int kWaves = kThreads / 64;
-constexpr int kLookRounds = 1;          // lookup rounds in flight together
+// two rounds of table probes in flight per wave: 5.52 -> 5.46 ms per C2 launch (one round or
+// three: 5.55 / 5.75 ms; four cap the kernel at 5 waves per SIMD)
+constexpr int kLookRounds = 2;
 constexpr int kQBuf = 64 * (kLookRounds + 1);        // dedupe buffer: one batch + a group of rounds
 constexpr int kWinWords = kWin / 4 + 8;
 
@@ -702,20 +738,16 @@ __device__ __forceinline__ void classify_tile(const EncArgs& a, int64_t tile, ui
   for (int r0 = 0; r0 < rounds || nq > 0; r0 += kLookRounds) {
     if (r0 < rounds) {
       uint32_t tok[kLookRounds];
+      if (use_table) {
+        table_lookups<kLookRounds>(a.chunks, s_b32, s_cstart, C, rel_end, r0, lane, tok);
+      } else {
 #pragma unroll
-      for (int u = 0; u < kLookRounds; ++u) {
-        const int k = ((r0 + u) << 6) + lane;
-        const bool valid = k < C;
-        const int ls = valid ? s_cstart[k] : 0;
-        const int end = (k + 1 < C) ? (int)s_cstart[k + 1] : rel_end;
-        const int len = valid ? end - ls : 0;
-        tok[u] = kInf;
-        if (len == 1) {
-          tok[u] = (s_b32[ls >> 2] >> (8 * (ls & 3))) & 0xFFu;
-        } else if (len >= 2 && len <= 16 && use_table) {
-          uint32_t w[4];
-          window_words(s_b32, ls, len, w);
-          tok[u] = chunk_lookup(a.chunks, w, (uint32_t)len);
+        for (int u = 0; u < kLookRounds; ++u) {  // (no table: single bytes only)
+          const int k = ((r0 + u) << 6) + lane;
+          const bool valid = k < C;
+          const int ls = valid ? s_cstart[k] : 0;
+          const int end = (k + 1 < C) ? (int)s_cstart[k + 1] : rel_end;
+          tok[u] = (valid && end - ls == 1) ? (s_b32[ls >> 2] >> (8 * (ls & 3))) & 0xFFu : kInf;
         }
       }
 #pragma unroll

@@ -107,10 +107,11 @@ int32_t sw_encoder_reserve(sw_encoder* h, int64_t max_bytes, int64_t max_strings
  *                          (sw_presplit_host) instead of on the device (default 0) */
 #define SW_OPT_PATTERN 5
 #define SW_OPT_HOST_PRESPLIT 6
-/*   SW_OPT_LONG_SPLIT      1 (default): chunks of 33..4096 bytes are cut into pieces that are
- *                          encoded on their own, then every junction is verified exactly and
- *                          conflicting pieces are joined and encoded again (well-formed tables
- *                          only, SW_INFO_SPLIT); 0: one wave loop per chunk.  Results identical.
+/*   SW_OPT_LONG_SPLIT      1 (default): long chunks (> 32 bytes, any length) on well-formed tables
+ *                          (SW_INFO_SPLIT) are cut into ~12-byte pieces, all pieces of all long
+ *                          chunks of the launch encoded side by side over the whole GPU, every
+ *                          junction verified exactly and conflicting pieces joined and encoded
+ *                          again; 0: one wave loop per chunk.  Results identical.
  *   SW_OPT_MAX_LAUNCH_BYTES  sw_encode_batch encodes larger batches as several launches of
  *                          whole strings (0 = the 2^30 - 64 byte device limit; testing: any
  *                          value >= 64) */

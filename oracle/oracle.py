@@ -36,8 +36,11 @@ def lib():
         L.orc_ucd_class.argtypes = [ctypes.c_uint32]
         L.orc_presplit.restype = c_int64
         L.orc_presplit.argtypes = [POINTER(c_uint8), c_int64, c_int, POINTER(c_int64), c_int64]
-        L.orc_encode_chunk.restype = c_int64
-        L.orc_encode_chunk.argtypes = [c_void_p, POINTER(c_uint8), c_int64, POINTER(c_int32)]
+        for name in ("orc_encode_chunk", "orc_encode_chunk_naive", "orc_encode_chunk_heap"):
+            getattr(L, name).restype = c_int64
+            getattr(L, name).argtypes = [c_void_p, POINTER(c_uint8), c_int64, POINTER(c_int32)]
+        L.orc_model_well_formed.restype = c_int
+        L.orc_model_well_formed.argtypes = [c_void_p]
         L.orc_encode_ordinary.restype = c_int64
         L.orc_encode_ordinary.argtypes = [c_void_p, POINTER(c_uint8), c_int64, c_int, POINTER(c_int32)]
         L.orc_encode_batch.restype = c_int64
@@ -78,11 +81,18 @@ class OracleModel:
         r = lib().orc_model_get(self._h, a, b)
         return None if r < 0 else int(r)
 
-    def encode_chunk(self, data):
+    def encode_chunk(self, data, form=""):
+        """form "": the oracle's choice; "naive": the reference loop step by step; "heap": the
+        O(n log n) form (well-formed tables only)."""
         buf = np.frombuffer(bytes(data), dtype=np.uint8) if len(data) else np.zeros(1, np.uint8)
         out = np.empty(max(len(data), 1), dtype=np.int32)
-        n = lib().orc_encode_chunk(self._h, _p(buf, c_uint8), len(data), _p(out, c_int32))
+        fn = getattr(lib(), "orc_encode_chunk" + ("_" + form if form else ""))
+        n = fn(self._h, _p(buf, c_uint8), len(data), _p(out, c_int32))
         return out[:n].tolist()
+
+    @property
+    def well_formed(self):
+        return bool(lib().orc_model_well_formed(self._h))
 
     def encode_ordinary(self, data, pattern=PAT_CL100K):
         if isinstance(data, str):

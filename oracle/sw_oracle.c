@@ -19,6 +19,7 @@ struct orc_model {
   uint64_t* keys;  /* (a << 32) | b, UINT64_MAX = empty */
   int32_t* vals;
   uint64_t mask;
+  int well_formed; /* every value >= 256, unique and larger than both ids of its pair */
 };
 
 static uint64_t orc_mix(uint64_t x) {
@@ -43,8 +44,28 @@ orc_model* orc_model_new(const int32_t* pairs, const int32_t* vals, int64_t n) {
     m->keys[h] = key;          /* dict assignment: a later duplicate overwrites (base.py:147) */
     m->vals[h] = vals[i];
   }
+  /* well-formed? (over the dict's final values) */
+  m->well_formed = 1;
+  int32_t vmax = 0;
+  for (uint64_t h = 0; h <= m->mask; ++h) {
+    if (m->keys[h] == UINT64_MAX) continue;
+    const int32_t v = m->vals[h], a = (int32_t)(m->keys[h] >> 32), b = (int32_t)(uint32_t)m->keys[h];
+    if (v < 256 || v <= a || v <= b) m->well_formed = 0;
+    if (v > vmax) vmax = v;
+  }
+  if (m->well_formed) {
+    uint8_t* seen = (uint8_t*)calloc((size_t)vmax + 1, 1);
+    for (uint64_t h = 0; h <= m->mask && seen; ++h) {
+      if (m->keys[h] == UINT64_MAX) continue;
+      if (seen[m->vals[h]]++) m->well_formed = 0;
+    }
+    if (!seen) m->well_formed = 0;
+    free(seen);
+  }
   return m;
 }
+
+int orc_model_well_formed(const orc_model* m) { return m->well_formed; }
 
 void orc_model_free(orc_model* m) {
   if (!m) return;
@@ -234,7 +255,87 @@ int64_t orc_presplit(const uint8_t* s, int64_t n, int pattern, int64_t* starts, 
 /* ------------------------------------------------------------------------------------ */
 /* E3/E4: the merge loop over one chunk                                                  */
 /* ------------------------------------------------------------------------------------ */
+/* The same loop for a LONG chunk of a well-formed table, in O(n log n): a min-heap of the
+ * adjacent pairs keyed by (rank, position) over a linked list of the symbols.  Equal to the
+ * loop above (and so to the reference) for well-formed tables: ranks are unique, so the step
+ * of rank r takes exactly the occurrences of one pair, and every pair a merge creates holds
+ * the new id r and so ranks above r -- the heap pops all of step r's occurrences, left to
+ * right, before anything else; an occurrence whose left or right symbol was consumed by the
+ * previous one (the (a, a) overlap rule of base.py:29-35) no longer matches and is skipped.
+ * tests/test_oracle_golden.py checks it against the loop above on long chunks of every table. */
+typedef struct { int64_t rank, pos; int32_t a, b; } orc_hent;
+static int orc_hless(const orc_hent* x, const orc_hent* y) {
+  return x->rank < y->rank || (x->rank == y->rank && x->pos < y->pos);
+}
+static void orc_hpush(orc_hent* h, int64_t* n, orc_hent e) {
+  int64_t i = (*n)++;
+  while (i > 0) {
+    int64_t p = (i - 1) / 2;
+    if (!orc_hless(&e, &h[p])) break;
+    h[i] = h[p];
+    i = p;
+  }
+  h[i] = e;
+}
+static orc_hent orc_hpop(orc_hent* h, int64_t* n) {
+  orc_hent top = h[0], last = h[--(*n)];
+  int64_t i = 0;
+  for (;;) {
+    int64_t l = 2 * i + 1, r = l + 1, c = i;
+    const orc_hent* best = &last;
+    if (l < *n && orc_hless(&h[l], best)) { c = l; best = &h[l]; }
+    if (r < *n && orc_hless(&h[r], best)) { c = r; best = &h[r]; }
+    if (c == i) break;
+    h[i] = h[c];
+    i = c;
+  }
+  if (*n > 0) h[i] = last;
+  return top;
+}
+
+int64_t orc_encode_chunk_heap(const orc_model* m, const uint8_t* b, int64_t len, int32_t* out) {
+  int32_t* id = (int32_t*)malloc(sizeof(int32_t) * len);
+  int64_t* nx = (int64_t*)malloc(sizeof(int64_t) * len);
+  int64_t* pv = (int64_t*)malloc(sizeof(int64_t) * len);
+  orc_hent* h = (orc_hent*)malloc(sizeof(orc_hent) * (2 * len + 2));
+  int64_t nh = 0;
+  for (int64_t i = 0; i < len; ++i) { id[i] = b[i]; nx[i] = i + 1 < len ? i + 1 : -1; pv[i] = i - 1; }
+  for (int64_t i = 0; i + 1 < len; ++i) {
+    int64_t r = orc_model_get(m, id[i], id[i + 1]);
+    if (r >= 0) { orc_hent e = {r, i, id[i], id[i + 1]}; orc_hpush(h, &nh, e); }
+  }
+  while (nh > 0) {
+    orc_hent e = orc_hpop(h, &nh);
+    const int64_t i = e.pos, j = nx[i];
+    if (id[i] != e.a || j < 0 || id[j] != e.b || pv[i] == -2) continue;  /* stale */
+    id[i] = (int32_t)e.rank;                       /* merge (base.py:22-36) */
+    nx[i] = nx[j];
+    if (nx[j] >= 0) pv[nx[j]] = i;
+    pv[j] = -2;                                     /* j consumed */
+    id[j] = -1;
+    if (pv[i] >= 0) {
+      int64_t r = orc_model_get(m, id[pv[i]], id[i]);
+      if (r >= 0) { orc_hent f = {r, pv[i], id[pv[i]], id[i]}; orc_hpush(h, &nh, f); }
+    }
+    if (nx[i] >= 0) {
+      int64_t r = orc_model_get(m, id[i], id[nx[i]]);
+      if (r >= 0) { orc_hent f = {r, i, id[i], id[nx[i]]}; orc_hpush(h, &nh, f); }
+    }
+  }
+  int64_t n = 0;
+  for (int64_t i = 0; i >= 0; i = nx[i]) out[n++] = id[i];
+  free(id); free(nx); free(pv); free(h);
+  return n;
+}
+
+#define ORC_HEAP_MIN 256 /* chunks at least this long take the heap form (well-formed tables) */
+
 int64_t orc_encode_chunk(const orc_model* m, const uint8_t* b, int64_t len, int32_t* out) {
+  if (m->well_formed && len >= ORC_HEAP_MIN) return orc_encode_chunk_heap(m, b, len, out);
+  return orc_encode_chunk_naive(m, b, len, out);
+}
+
+int64_t orc_encode_chunk_naive(const orc_model* m, const uint8_t* b, int64_t len, int32_t* out) {
   int32_t* ids = out;
   int64_t n = len;
   for (int64_t i = 0; i < n; ++i) ids[i] = b[i];               /* chunk.encode("utf-8") */

@@ -33,6 +33,7 @@
 #include "capi.h"
 #include "hostpool.h"
 #include "kernels.h"
+#include "long_split.h"
 #include "presplit_kernel.h"
 #include "shredword_hip.h"
 #include "table.h"
@@ -75,9 +76,9 @@ struct sw_encoder {
   DevChunkTable chunks{};
   void* d_chunks = nullptr;
   int64_t n_chunk_entries = 0;
-  // split + verify for long chunks (k_merge_long_split): well-formed tables only
+  // split + verify for long chunks (long_split.h): well-formed tables only
   bool split_ok = false;              // values >= 256, unique, larger than both pair members
-  bool long_split = true;             // SW_OPT_LONG_SPLIT
+  bool long_split = true;             // SW_OPT_LONG_SPLIT (0: the wave loop per long chunk)
   uint2* d_inv = nullptr;             // merge value -> pair
   uint32_t n_inv = 0;
   int64_t max_launch = kMaxLaunchBytes;  // SW_OPT_MAX_LAUNCH_BYTES (sw_encode_batch splits above it)
@@ -107,8 +108,8 @@ struct sw_encoder {
   // they overlap (each alone leaves most of the chip idle), joined before k_tile_count
   bool merge_fork = true;             // SW_OPT_MERGE_STREAMS
   bool out16 = false;                 // SW_OPT_OUT_BITS 16: sw_encode_device writes uint16 ids
-  hipStream_t s_fork[3] = {nullptr, nullptr, nullptr};
-  hipEvent_t ev_fork = nullptr, ev_join[3] = {nullptr, nullptr, nullptr};
+  hipStream_t s_fork[2] = {nullptr, nullptr};
+  hipEvent_t ev_fork = nullptr, ev_join[2] = {nullptr, nullptr};
   sw::HostPool* pool = nullptr;
   // workspace
   int64_t cap_bytes = -1, cap_str = -1;
@@ -128,7 +129,11 @@ struct sw_encoder {
   uint32_t dmask = 0;
   uint4* d_dres = nullptr;            // dense result heads, one per table entry
   uint8_t* d_dcnt = nullptr;          // their id counts (<= 32), one byte per table entry
-  uint32_t* d_big = nullptr;          // chunks over kLongLds bytes: count, then their long-bucket indices
+  uint32_t* d_big = nullptr;          // chunks over kLongLds bytes: count, then their long-list indices
+  // long chunks by split + verify (long_split.h): per long chunk, per piece, piece ids, counters
+  void* d_lp = nullptr;               // one allocation, carved into LongArgs
+  LongArgs lp{};
+  int64_t* d_lpart = nullptr;         // scan partials for the piece / chunk scans
   bool dedupe = true;
   bool dedupe_exact = true;           // SW_OPT_DEDUPE_EXACT
   int64_t dedupe_slots = 0;           // SW_OPT_DEDUPE_SLOTS (0: automatic)
@@ -176,7 +181,9 @@ void free_workspace(sw_encoder* h) {
   h->d_bcnt = nullptr; h->d_boff = nullptr; h->d_qtotal = nullptr;
   (void)hipFree(h->d_dtab); (void)hipFree(h->d_tile_base); (void)hipFree(h->d_tile_cnt);
   (void)hipFree(h->d_dres); (void)hipFree(h->d_big); (void)hipFree(h->d_dcnt);
-  h->d_dres = nullptr; h->d_big = nullptr; h->d_dcnt = nullptr;
+  (void)hipFree(h->d_lp); (void)hipFree(h->d_lpart);
+  h->d_dres = nullptr; h->d_big = nullptr; h->d_dcnt = nullptr; h->d_lp = nullptr; h->d_lpart = nullptr;
+  h->lp = LongArgs{};
   (void)hipFree(h->d_total);
   h->d_scratch = nullptr; h->d_res = nullptr; h->d_pbits = nullptr; h->d_pcount = nullptr; h->d_part = nullptr;
   h->d_dtab = nullptr; h->d_tile_base = nullptr; h->d_tile_cnt = nullptr; h->d_total = nullptr;
@@ -231,6 +238,33 @@ int32_t ensure_workspace(sw_encoder* h, int64_t n_bytes) {
     h->dmask = (uint32_t)(slots - 1);
   }
   HIP_TRY(hipMalloc(&h->d_big, sizeof(uint32_t) * (nb / (kLongLds + 1) + 2)));  // (count + list)
+  {  // long_split.h: a long chunk has > kShort bytes; a piece >= kPieceW - 2 kCutHalf + 1 bytes, but a chunk's last
+    const int64_t lcap = nb / (kShort + 1) + 64, pcap = nb / 8 + 64;
+    const size_t bytes = 8 * (size_t)kLcAlloc + 4 * (size_t)lcap * 7 + 8 * (size_t)lcap  // chunks
+                         + 4 * (size_t)pcap * 11                                         // pieces, lists
+                         + 4 * (size_t)(nb + 64) + 4 * (size_t)pcap + 1024;             // ids, window list (+ alignment)
+    HIP_TRY(hipMalloc(&h->d_lp, bytes));
+    char* q = (char*)h->d_lp;
+    auto take = [&](size_t n) { char* r = q; q += (n + 15) & ~(size_t)15; return (void*)r; };
+    LongArgs& L = h->lp;
+    L.ctl = (int64_t*)take(8 * (size_t)kLcAlloc);
+    L.lpo = (int64_t*)take(8 * (size_t)lcap);
+    L.lstart = (uint32_t*)take(4 * (size_t)lcap); L.llen = (uint32_t*)take(4 * (size_t)lcap);
+    L.lnp = (uint32_t*)take(4 * (size_t)lcap); L.lfall = (uint32_t*)take(4 * (size_t)lcap);
+    L.flist = (uint32_t*)take(4 * (size_t)lcap);
+    L.wstart = (uint32_t*)take(4 * (size_t)lcap); L.wlen = (uint32_t*)take(4 * (size_t)lcap);
+    L.pbeg = (uint32_t*)take(4 * (size_t)pcap); L.pcnt = (uint32_t*)take(4 * (size_t)pcap);
+    L.pchunk = (uint32_t*)take(4 * (size_t)pcap); L.pflag = (uint32_t*)take(4 * (size_t)pcap);
+    L.pprev = (uint32_t*)take(4 * (size_t)pcap); L.pnext = (uint32_t*)take(4 * (size_t)pcap);
+    L.jlist[0] = (uint32_t*)take(4 * (size_t)pcap); L.jlist[1] = (uint32_t*)take(4 * (size_t)pcap);
+    L.clist = (uint32_t*)take(4 * (size_t)pcap); L.hlist = (uint32_t*)take(4 * (size_t)pcap);
+    L.pseen = (uint32_t*)take(4 * (size_t)pcap);
+    L.pid = (uint32_t*)take(4 * (size_t)(nb + 64));
+    L.wlist = (uint32_t*)take(4 * (size_t)pcap);
+    L.lcap = lcap;
+    L.pcap = pcap;
+    HIP_TRY(hipMalloc(&h->d_lpart, sizeof(int64_t) * kDscanGrid));
+  }
   HIP_TRY(hipMalloc(&h->d_tile_base, sizeof(int64_t) * n_tiles));
   HIP_TRY(hipMalloc(&h->d_tile_cnt, sizeof(uint32_t) * n_tiles));
   HIP_TRY(hipMalloc(&h->d_total, sizeof(int64_t)));
@@ -318,11 +352,15 @@ hipError_t launch_presplit(hipStream_t st, const uint8_t* d_bytes, int64_t n_byt
 
 // exclusive scan of cnt[0..n) into base, total into *total (three small kernels)
 hipError_t sw::launch_scan(hipStream_t st, const uint32_t* cnt, int64_t n, int64_t* part, int64_t* base,
-                           int64_t* total) {
+                           int64_t* total, const int64_t* n_dev) {
   const int64_t n_parts = (n + kScanBlock - 1) / kScanBlock;
-  hipLaunchKernelGGL(k_scan_reduce, dim3((unsigned)n_parts), dim3(kThreads), 0, st, cnt, n, part);
-  hipLaunchKernelGGL(k_scan_parts, dim3(1), dim3(1024), 0, st, part, n_parts, total);
-  hipLaunchKernelGGL(k_scan_apply, dim3((unsigned)n_parts), dim3(kThreads), 0, st, cnt, n, part, base);
+  if (n_parts == 0) {
+    (void)hipMemsetAsync(total, 0, sizeof(int64_t), st);
+    return hipGetLastError();
+  }
+  hipLaunchKernelGGL(k_scan_reduce, dim3((unsigned)n_parts), dim3(kThreads), 0, st, cnt, n, n_dev, part);
+  hipLaunchKernelGGL(k_scan_parts, dim3(1), dim3(1024), 0, st, part, n, n_dev, total);
+  hipLaunchKernelGGL(k_scan_apply, dim3((unsigned)n_parts), dim3(kThreads), 0, st, cnt, n, n_dev, part, base);
   return hipGetLastError();
 }
 int64_t sw::scan_block() { return kScanBlock; }
@@ -444,7 +482,7 @@ extern "C" void sw_encoder_destroy(sw_encoder* h) {
     delete h->pool;
     if (h->s_h2d) (void)hipStreamDestroy(h->s_h2d);
     if (h->s_d2h) (void)hipStreamDestroy(h->s_d2h);
-    for (int k = 0; k < 3; ++k) {
+    for (int k = 0; k < 2; ++k) {
       if (h->s_fork[k]) (void)hipStreamDestroy(h->s_fork[k]);
       if (h->ev_join[k]) (void)hipEventDestroy(h->ev_join[k]);
     }
@@ -567,6 +605,62 @@ extern "C" int32_t sw_encoder_phase_cycles(sw_encoder* h, double* out32, int32_t
 }
 
 namespace {
+// the long-chunk split + verify passes (long_split.h) on stream s: well-formed tables only
+template <bool kWide, bool k16>
+hipError_t launch_long_split(sw_encoder* h, hipStream_t s, const EncArgs& a) {
+  LongArgs& L = h->lp;
+  const dim3 g(kLpGrid), b(kThreads);
+  hipLaunchKernelGGL(k_dscan_reduce, dim3(kDscanGrid), b, 0, s, L.lnp, L.lcap, &L.ctl[kLcLong], h->d_lpart);
+  hipLaunchKernelGGL(k_dscan_parts, dim3(1), dim3(kDscanGrid), 0, s, h->d_lpart, &L.ctl[kLcPieces]);
+  hipLaunchKernelGGL(k_dscan_apply, dim3(kDscanGrid), b, 0, s, L.lnp, L.lcap, &L.ctl[kLcLong], h->d_lpart, L.lpo);
+  hipLaunchKernelGGL(k_lp_fill, g, b, 0, s, L);
+  hipLaunchKernelGGL((k_lp_encode<kWide, k16>), g, b, 0, s, a, L);  // (and round 0's junctions)
+  for (int r = 0; r < kLpRounds; ++r) {
+    hipLaunchKernelGGL(k_lp_heads, g, b, 0, s, L, r);
+    hipLaunchKernelGGL((k_lp_windows<kWide, k16>), g, b, 0, s, a, L, r);
+    hipLaunchKernelGGL((k_lp_bigwin<kWide, k16>), g, dim3(64), 0, s, a, L, r);
+    hipLaunchKernelGGL((k_lp_junctions<kWide>), g, b, 0, s, a, L, r + 1);  // (r + 1 == kLpRounds: the final check)
+  }
+  hipLaunchKernelGGL((k_lp_fallback<kWide, k16>), g, dim3(64), 0, s, a, L);
+  hipLaunchKernelGGL(k_lp_gather, g, b, 0, s, a, L);
+  return hipGetLastError();
+}
+
+// every long chunk (> kShort bytes) on stream s, listed from the queue (k_lp_prep): split +
+// verify over the whole GPU (long_split.h; well-formed tables), or the wave loop per chunk.
+// (Started from the bitmap right after the pre-split, beside k_classify, they only slowed it
+// down by as much: both fill the chip.  They run beside the merge kernels, which leave it
+// mostly idle.)
+template <bool kWide, bool k16>
+hipError_t launch_long(sw_encoder* h, hipStream_t s, const EncArgs& a, bool split) {
+  constexpr unsigned kLongGrid = 32768;  // k_merge_long_lds: a workgroup per long chunk (grid-stride past that)
+  LongArgs& L = h->lp;
+  hipError_t e = hipMemsetAsync(L.ctl, 0, sizeof(int64_t) * kLcAlloc, s);
+  if (e == hipSuccess) e = hipMemsetAsync(h->d_big, 0, sizeof(uint32_t), s);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(k_lp_prep, dim3(kLpPrepGrid), dim3(kThreads), 0, s, a, L, split ? (int64_t)kShort : INT64_MAX);
+  if (!split) {
+    hipLaunchKernelGGL((k_merge_long_lds<kWide, k16>), dim3(kLongGrid), dim3(64), 0, s, a);
+    hipLaunchKernelGGL((k_merge_long<kWide>), dim3(512), dim3(kThreads), 0, s, a);  // (over kLongLds bytes)
+    return hipGetLastError();
+  }
+  e = launch_long_split<kWide, k16>(h, s, a);
+#ifdef SW_LP_DEBUG
+  if (e == hipSuccess && getenv("SW_LP_DEBUG")) {
+    int64_t c[kLcAlloc];
+    (void)hipStreamSynchronize(s);
+    (void)hipMemcpy(c, L.ctl, sizeof(c), hipMemcpyDeviceToHost);
+    fprintf(stderr, "lp: long %lld pieces %lld fall %lld\n", (long long)c[kLcLong], (long long)c[kLcPieces],
+            (long long)c[kLcFall]);
+    for (int r = 0; r <= kLpRounds; ++r)
+      fprintf(stderr, "lp r%d: jun %lld conf %lld heads %lld big %lld big_bytes %lld big_max %lld\n", r,
+              (long long)c[kLcJun + r], (long long)c[kLcConf + r], (long long)c[kLcHead + r], (long long)c[kLcBig + r],
+              r < kLpRounds ? (long long)c[kLcDbg + r] : 0LL, r < kLpRounds ? (long long)c[kLcDbg + kLpRounds + r] : 0LL);
+  }
+#endif
+  return e;
+}
+
 // the device pipeline; d_out_ids is int32_t*, or uint16_t* when out16 (the table is ids16)
 int32_t encode_device(sw_encoder* h, const uint8_t* d_bytes, int64_t n_bytes, const int64_t* d_str_off, int64_t n_str,
                       const uint64_t* d_chunk_bits, void* d_out_ids, bool out16, int64_t* d_out_off, void* stream,
@@ -616,56 +710,50 @@ int32_t encode_device(sw_encoder* h, const uint8_t* d_bytes, int64_t n_bytes, co
     a.n_tiles = n_tiles; a.qtmp = h->d_res; a.bcnt = h->d_bcnt; a.boff = h->d_boff; a.q_total = h->d_qtotal;
     a.queue = h->d_queue; a.stamps = h->d_stamps;
     a.inv = h->d_inv; a.n_inv = h->n_inv; a.ids16 = h->ids16 ? 1u : 0u;
-    const bool split = h->split_ok && h->long_split;
+    a.lstart = h->lp.wstart; a.llen = h->lp.wlen; a.n_long = &h->lp.ctl[kLcWave]; a.lcap = h->lp.lcap;
+    const bool split = h->split_ok && h->long_split;  // (split + verify needs a well-formed table)
     if (h->dedupe) HIP_TRY(hipMemsetAsync(h->d_dtab, 0, sizeof(uint64_t) * ((size_t)a.dmask + 1), st));
-    HIP_TRY(hipMemsetAsync(h->d_big, 0, sizeof(uint32_t), st));
     hipLaunchKernelGGL(k_classify, dim3((unsigned)((n_tiles + kWaves - 1) / kWaves)), dim3(kThreads), 0, st, a);
     HIP_TRY(hipGetLastError());
     HIP_TRY(launch_scan(st, h->d_bcnt, kNumBuckets * n_tiles, h->d_part, h->d_boff, h->d_qtotal));
     hipLaunchKernelGGL(k_scatter, dim3((unsigned)((n_tiles + 3) / 4)), dim3(kThreads), 0, st, a);
     const dim3 pg(2048), pb(kThreads);  // persistent grid for the queue kernels
-    constexpr unsigned kLongGrid = 32768;  // k_merge_long_lds: a workgroup per long chunk (grid-stride past that)
-    // streams of the merge kernels: [0] buckets 17..32 B, [1] 9..16 B, [2] 2..8 B, [3] long
+    // streams of the merge kernels: [0] buckets 17..32 B, then 2..8 B, [1] 9..16 B, [3] long.  (Two
+    // forks only: streams beyond the process's hardware queues (4) share one and run in launch
+    // order, which put the long chunks behind a bucket.)
     hipStream_t ms[4] = {st, st, st, st};
     if (h->merge_fork) {
-      for (int k = 0; k < 3; ++k) {
+      for (int k = 0; k < 2; ++k) {
         if (!h->s_fork[k]) HIP_TRY(hipStreamCreateWithFlags(&h->s_fork[k], hipStreamNonBlocking));
         if (!h->ev_join[k]) HIP_TRY(hipEventCreateWithFlags(&h->ev_join[k], hipEventDisableTiming));
       }
       if (!h->ev_fork) HIP_TRY(hipEventCreateWithFlags(&h->ev_fork, hipEventDisableTiming));
       HIP_TRY(hipEventRecord(h->ev_fork, st));
-      for (int k = 0; k < 3; ++k) {
-        HIP_TRY(hipStreamWaitEvent(h->s_fork[k], h->ev_fork, 0));
-        ms[k + 1] = h->s_fork[k];
-      }
+      for (int k = 0; k < 2; ++k) HIP_TRY(hipStreamWaitEvent(h->s_fork[k], h->ev_fork, 0));
+      ms[1] = h->s_fork[0];
+      ms[3] = h->s_fork[1];
     }
+    if (h->table.wide) HIP_TRY((launch_long<true, false>(h, ms[3], a, split)));  // (the longest path: first)
+    else if (h->ids16) HIP_TRY((launch_long<false, true>(h, ms[3], a, split)));
+    else HIP_TRY((launch_long<false, false>(h, ms[3], a, split)));
     if (h->table.wide) {
       hipLaunchKernelGGL((k_merge_bucket<true, false, 32>), pg, pb, 0, ms[0], a, 8, 9);
       hipLaunchKernelGGL((k_merge_bucket<true, false, 16>), pg, pb, 0, ms[1], a, 5, 7);
       hipLaunchKernelGGL((k_merge_bucket<true, false, 8>), pg, pb, 0, ms[2], a, 3, 4);
       hipLaunchKernelGGL((k_merge_bucket<true, false, 4>), pg, pb, 0, ms[2], a, 0, 2);
-      if (split) hipLaunchKernelGGL((k_merge_long_split<true, false>), dim3(kLongGrid), dim3(64), 0, ms[3], a);
-      else hipLaunchKernelGGL((k_merge_long_lds<true, false>), dim3(kLongGrid), dim3(64), 0, ms[3], a);
-      hipLaunchKernelGGL((k_merge_long<true>), dim3(512), pb, 0, ms[3], a);
     } else if (h->ids16) {
       hipLaunchKernelGGL((k_merge_bucket<false, true, 32>), pg, pb, 0, ms[0], a, 8, 9);
       hipLaunchKernelGGL((k_merge_bucket<false, true, 16>), pg, pb, 0, ms[1], a, 5, 7);
       hipLaunchKernelGGL((k_merge_bucket<false, true, 8>), pg, pb, 0, ms[2], a, 3, 4);
       hipLaunchKernelGGL((k_merge_bucket<false, true, 4>), pg, pb, 0, ms[2], a, 0, 2);
-      if (split) hipLaunchKernelGGL((k_merge_long_split<false, true>), dim3(kLongGrid), dim3(64), 0, ms[3], a);
-      else hipLaunchKernelGGL((k_merge_long_lds<false, true>), dim3(kLongGrid), dim3(64), 0, ms[3], a);
-      hipLaunchKernelGGL((k_merge_long<false>), dim3(512), pb, 0, ms[3], a);
     } else {
       hipLaunchKernelGGL((k_merge_bucket<false, false, 32>), pg, pb, 0, ms[0], a, 8, 9);
       hipLaunchKernelGGL((k_merge_bucket<false, false, 16>), pg, pb, 0, ms[1], a, 5, 7);
       hipLaunchKernelGGL((k_merge_bucket<false, false, 8>), pg, pb, 0, ms[2], a, 3, 4);
       hipLaunchKernelGGL((k_merge_bucket<false, false, 4>), pg, pb, 0, ms[2], a, 0, 2);
-      if (split) hipLaunchKernelGGL((k_merge_long_split<false, false>), dim3(kLongGrid), dim3(64), 0, ms[3], a);
-      else hipLaunchKernelGGL((k_merge_long_lds<false, false>), dim3(kLongGrid), dim3(64), 0, ms[3], a);
-      hipLaunchKernelGGL((k_merge_long<false>), dim3(512), pb, 0, ms[3], a);
     }
     if (h->merge_fork) {
-      for (int k = 0; k < 3; ++k) {
+      for (int k = 0; k < 2; ++k) {
         HIP_TRY(hipEventRecord(h->ev_join[k], h->s_fork[k]));
         HIP_TRY(hipStreamWaitEvent(st, h->ev_join[k], 0));
       }

@@ -488,7 +488,12 @@ struct EncArgs {
   unsigned long long* stamps;  // SW_STAMPS builds: cycles per phase, summed
   const uint2* inv;          // [n_inv] merge value -> its pair (a, b); well-formed tables only
   uint32_t n_inv;
-  uint32_t* big_list;        // queued chunks over kLongLds bytes (their index in the long bucket)
+  // the long chunks (> kShort bytes) for the per-chunk kernels, listed by k_lp_prep (any order)
+  const uint32_t* lstart;    // first byte
+  const uint32_t* llen;      // bytes
+  const int64_t* n_long;     // how many (device)
+  int64_t lcap;              // list capacity
+  uint32_t* big_list;        // long chunks over kLongLds bytes (their index in the long list)
   uint32_t* big_count;       // ... how many (cleared per launch)
   uint32_t ids16;            // every id fits 16 bits (dres layout)
 };
@@ -803,7 +808,8 @@ __device__ __forceinline__ void classify_tile(const EncArgs& a, int64_t tile, ui
       if (queued) {
         const int64_t qi = t0 + nown + __popcll(pend & lt_mask);
         SW_STNT2(&a.qtmp[qi], (uint32_t)ls | ((uint32_t)k << kTileBits) | ((uint32_t)(len <= kShort ? len : 0) << (2 * kTileBits)));
-        SW_STNT2(&a.qtmp[qi + kTile / 2], did);
+        // (a long chunk has no dense result: the field carries its length, kNoDid if too long)
+        SW_STNT2(&a.qtmp[qi + kTile / 2], len > kShort ? (len < (int)kNoDid ? (uint32_t)len : kNoDid) : did);
       }
       nown += __popcll(pend);
       while (pend) {  // one ballot per bucket present
@@ -903,6 +909,12 @@ __device__ __forceinline__ void bucket_range(const EncArgs& a, int b_lo, int b_h
   *hi = (b_hi + 1 < kNumBuckets) ? a.boff[(int64_t)(b_hi + 1) * a.n_tiles] : *a.q_total;
 }
 
+// long chunks listed by k_lp_prep (clamped to the list's capacity)
+__device__ __forceinline__ int64_t long_count(const EncArgs& a) {
+  const int64_t v = *a.n_long;
+  return v < a.lcap ? (v < 0 ? 0 : v) : a.lcap;
+}
+
 // the chunk bytes [g, g + n) of the word-aligned input as N/4 zero-padded LE words
 template <int N>
 __device__ __forceinline__ void chunk_words(const uint32_t* words, int64_t last_word, int64_t g, int n,
@@ -996,11 +1008,11 @@ __global__ void __launch_bounds__(kThreads) k_merge_bucket(EncArgs a, int b_lo, 
 constexpr int kLongLds = 4096;
 
 // ---------------------------------------------------------------------------------------
-// Exact merge loop for one chunk of 33..kLongLds bytes, one wave, without compaction: lane j
-// owns positions [64j, 64j + 64) and keeps in registers their ALIVE mask (merged-away
-// positions die; "adjacent" means the next alive position), the smallest (rank, position) key
-// of its pairs and the mask of the positions holding that rank.  Per step of the reference
-// loop (base.py:10-36):
+// Exact merge loop for one chunk of up to kLongLds bytes, one wave, without compaction: lane j
+// owns the S positions [S j, S j + S), S = ceil(n / 64) (so every lane has work however short
+// the chunk), and keeps in registers their ALIVE mask (merged-away positions die; "adjacent"
+// means the next alive position), the smallest (rank, position) key of its pairs and the mask
+// of the positions holding that rank.  Per step of the reference loop (base.py:10-36):
 //   - the global minimum key is one wave min: the lowest rank, first occurrence (the pair of
 //     the earliest position with that rank, as min() over the first-occurrence-ordered stats);
 //   - its occurrences can only sit at positions of lanes whose minimum rank is that rank, in
@@ -1010,29 +1022,38 @@ constexpr int kLongLds = 4096;
 //     occurrences cannot overlap; for (a, a) the runs are resolved in position order, lane
 //     after lane;
 //   - the right partners die, and only the ranks of the new tokens and of their alive
-//     predecessors are looked up again; only the lanes whose positions changed recompute
-//     their minimum.
+//     predecessors are looked up again (eight lookups in flight per lane); only the lanes whose
+//     positions changed recompute their minimum.
 // So a step costs a few wave-wide operations plus the changed segments, not two passes over
-// the whole chunk.  id / rk live in LDS at lds_pos(p): a wave's reads of "position k of every
-// lane" hit 64 distinct banks.  Returns the surviving count; their ids are written to out.
+// the whole chunk.  Position p = S j + k lives in LDS at k * 64 + j: a wave's reads of "position
+// k of every lane" hit 64 distinct banks.  The chunk's bytes are read from src.  Returns the
+// surviving count; their ids are written to out.
 // ---------------------------------------------------------------------------------------
-__device__ __forceinline__ int lds_pos(int p) { return ((p & 63) << 6) | (p >> 6); }
-
 template <bool kWide, typename T>  // T: uint16_t when every id and value fits 16 bits (half the LDS)
-__device__ int seg_merge(const DevTable& t, T* id, T* rk, uint64_t* s_kill, uint64_t* s_dirty, int n, int lane,
-                         uint32_t* out) {
-  auto rank_at = [&](int p) -> uint32_t {  // (16-bit storage: 0xFFFF is +inf)
-    const uint32_t r = rk[lds_pos(p)];
+__device__ int seg_merge(const DevTable& t, const uint8_t* src, T* id, T* rk, uint64_t* s_kill, uint64_t* s_dirty,
+                         int n, int lane, uint32_t* out) {
+  const int S = n <= 64 ? 1 : (n + 63) >> 6;  // segment length (<= 64: n <= kLongLds)
+  const int base = lane * S;
+  auto own = [&](int k) -> int { return k * 64 + lane; };   // LDS index of my position base + k
+  auto at = [&](int p) -> int {                              // LDS index of any position p
+    if (p >= base && p < base + S) return own(p - base);
+    const int j = p / S;
+    return (p - j * S) * 64 + j;
+  };
+  auto rank_own = [&](int k) -> uint32_t {  // (16-bit storage: 0xFFFF is +inf)
+    const uint32_t r = rk[own(k)];
     return (sizeof(T) == 2 && r == 0xFFFFu) ? kInf : r;
   };
-  const int base = lane << 6;
   uint64_t am;
   {
-    const int c = n - base;
+    const int c = min(n - base, S);
     am = c >= 64 ? ~0ULL : c <= 0 ? 0ULL : ((1ULL << c) - 1ULL);
   }
+  for (int k = 0; k < S; ++k)
+    if (base + k < n) id[own(k)] = (T)src[base + k];
   s_kill[lane] = 0;
   s_dirty[lane] = 0;
+  wave_sync_mem();
   // exclusive scans over the lanes: first alive position after my segment (n: none), last
   // alive position before it (-1: none)
   int nxt_after = n, prv_before = -1;
@@ -1060,14 +1081,14 @@ __device__ int seg_merge(const DevTable& t, T* id, T* rk, uint64_t* s_kill, uint
     return m ? base + 63 - __builtin_clzll(m) : prv_before;
   };
   uint64_t smin = ~0ULL, mmask = 0;  // my minimum key (rank << 32 | position), its positions
-  auto seg_min = [&]() {  // (all 64 entries read 16 at a time, independent loads: one LDS wait per 16)
+  auto seg_min = [&]() {  // (16 entries read at a time, independent loads: one LDS wait per 16)
     smin = ~0ULL;
     mmask = 0;
 #pragma unroll 1
-    for (int k0 = 0; k0 < 64; k0 += 16) {
+    for (int k0 = 0; k0 < S; k0 += 16) {
       uint32_t rr[16];
 #pragma unroll
-      for (int u = 0; u < 16; ++u) rr[u] = rank_at(base + k0 + u);
+      for (int u = 0; u < 16; ++u) rr[u] = rank_own(k0 + u);
 #pragma unroll
       for (int u = 0; u < 16; ++u) {
         const int k = k0 + u;
@@ -1085,16 +1106,17 @@ __device__ int seg_merge(const DevTable& t, T* id, T* rk, uint64_t* s_kill, uint
   };
   scans();
   // initial ranks: every pair (p, p + 1), eight lookups in flight per lane
-  for (int k0 = 0; k0 < 64; k0 += 8) {
+  for (int k0 = 0; k0 < S; k0 += 8) {
     uint32_t r[8];
 #pragma unroll
     for (int u = 0; u < 8; ++u) {
-      const int p = base + k0 + u;
-      r[u] = p + 1 < n ? lookup<kWide>(t, id[lds_pos(p)], id[lds_pos(p + 1)]) : kInf;
+      const int k = k0 + u, p = base + k;
+      const int nx = k + 1 < S ? own(k + 1) : lane + 1;  // (the next segment's first position)
+      r[u] = (k < S && p + 1 < n) ? lookup<kWide>(t, id[own(k)], id[nx]) : kInf;
     }
 #pragma unroll
     for (int u = 0; u < 8; ++u)
-      if (base + k0 + u < n) rk[lds_pos(base + k0 + u)] = (T)r[u];
+      if (k0 + u < S && base + k0 + u < n) rk[own(k0 + u)] = (T)r[u];
   }
   seg_min();
   wave_sync_mem();
@@ -1103,19 +1125,19 @@ __device__ int seg_merge(const DevTable& t, T* id, T* rk, uint64_t* s_kill, uint
     const uint32_t r = (uint32_t)(key >> 32);
     if (r == kInf) break;
     const int pm = (int)(uint32_t)key;
-    // the pair at pm (lane pm >> 6 owns it)
-    const int lm = pm >> 6, km = pm & 63;
+    // the pair at pm (lane pm / S owns it)
+    const int lm = pm / S, km = pm - lm * S;
     const uint64_t am_m = __shfl(am, lm, 64);
     const int na_m = __shfl(nxt_after, lm, 64);
     const uint64_t mq = km == 63 ? 0ULL : (am_m & (~0ULL << (km + 1)));
-    const int qm = mq ? (lm << 6) + __builtin_ctzll(mq) : na_m;
-    const uint32_t p0 = id[lds_pos(pm)], p1 = id[lds_pos(qm)];
+    const int qm = mq ? lm * S + __builtin_ctzll(mq) : na_m;
+    const uint32_t p0 = id[km * 64 + lm], p1 = id[at(qm)];
     // my occurrences of (p0, p1): among my min-rank positions
     uint64_t take = 0;
     if ((uint32_t)(smin >> 32) == r) {
       for (uint64_t m = mmask; m; m &= m - 1) {
         const int k = __builtin_ctzll(m);
-        if ((uint32_t)id[lds_pos(base + k)] == p0 && (uint32_t)id[lds_pos(next_of(k))] == p1) take |= 1ULL << k;
+        if ((uint32_t)id[own(k)] == p0 && (uint32_t)id[at(next_of(k))] == p1) take |= 1ULL << k;
       }
     }
     if (p0 == p1) {  // runs of (a, a): left to right, a taken position consumes its next
@@ -1143,10 +1165,14 @@ __device__ int seg_merge(const DevTable& t, T* id, T* rk, uint64_t* s_kill, uint
     uint64_t kill = 0;
     for (uint64_t m = take; m; m &= m - 1) {
       const int k = __builtin_ctzll(m);
-      id[lds_pos(base + k)] = (T)r;
+      id[own(k)] = (T)r;
       const int nc = next_of(k);
-      if (nc < base + 64) kill |= 1ULL << (nc - base);
-      else __hip_atomic_fetch_or(&s_kill[nc >> 6], 1ULL << (nc & 63), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      if (nc < base + S) {
+        kill |= 1ULL << (nc - base);
+      } else {
+        const int j = nc / S;
+        __hip_atomic_fetch_or(&s_kill[j], 1ULL << (nc - j * S), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      }
     }
     wave_sync_mem();
     kill |= s_kill[lane];
@@ -1158,17 +1184,35 @@ __device__ int seg_merge(const DevTable& t, T* id, T* rk, uint64_t* s_kill, uint
     for (uint64_t m = take; m; m &= m - 1) {
       const int pv = prev_of(__builtin_ctzll(m));
       if (pv < 0) continue;
-      if (pv >= base) dirty |= 1ULL << (pv - base);
-      else __hip_atomic_fetch_or(&s_dirty[pv >> 6], 1ULL << (pv & 63), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      if (pv >= base) {
+        dirty |= 1ULL << (pv - base);
+      } else {
+        const int j = pv / S;
+        __hip_atomic_fetch_or(&s_dirty[j], 1ULL << (pv - j * S), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      }
     }
     wave_sync_mem();
     dirty |= s_dirty[lane];
     s_dirty[lane] = 0;
     dirty &= am;
-    for (uint64_t m = dirty; m; m &= m - 1) {
-      const int k = __builtin_ctzll(m);
-      const int nx = next_of(k);
-      rk[lds_pos(base + k)] = (T)(nx < n ? lookup<kWide>(t, id[lds_pos(base + k)], id[lds_pos(nx)]) : kInf);
+    for (uint64_t m = dirty; m;) {  // eight lookups in flight (branch-free: spare slots look up (0, 0))
+      int ks[8];
+      uint32_t rr[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const bool v = m != 0ULL;
+        const int k = v ? __builtin_ctzll(m) : 0;
+        m = v ? (m & (m - 1)) : m;
+        const int nx = v ? next_of(k) : n;
+        ks[u] = v ? k : -1;
+        const uint32_t x = v ? (uint32_t)id[own(k)] : 0u;
+        const uint32_t y = (v && nx < n) ? (uint32_t)id[at(nx)] : 0u;
+        rr[u] = lookup<kWide>(t, x, y);
+        rr[u] = nx < n ? rr[u] : kInf;
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+        if (ks[u] >= 0) rk[own(ks[u])] = (T)rr[u];
     }
     if (dirty | kill) seg_min();
     wave_sync_mem();
@@ -1177,7 +1221,7 @@ __device__ int seg_merge(const DevTable& t, T* id, T* rk, uint64_t* s_kill, uint
   const uint32_t cnt = (uint32_t)__popcll(am);
   const uint32_t incl = wave_incl_scan(cnt, lane);
   uint32_t o = incl - cnt;
-  for (uint64_t m = am; m; m &= m - 1) out[o++] = id[lds_pos(base + __builtin_ctzll(m))];
+  for (uint64_t m = am; m; m &= m - 1) out[o++] = id[own(__builtin_ctzll(m))];
   return (int)__shfl(incl, 63, 64);
 }
 
@@ -1190,20 +1234,15 @@ __global__ void __launch_bounds__(64) k_merge_long_lds(EncArgs a) {
   __shared__ T s_rk[kLongLds];
   __shared__ uint64_t s_kill[64], s_dirty[64];
   const int lane = threadIdx.x;
-  int64_t lo, hi;
-  bucket_range(a, kLongBucket, kLongBucket, &lo, &hi);
-  for (int64_t i = lo + blockIdx.x; i < hi; i += gridDim.x) {
-    const uint64_t e = a.queue[i];
-    const int64_t start = (int64_t)(e >> 33);
-    const int64_t len = next_set_bit(a.bits, a.n_words, start + 1, a.n_bytes) - start;
+  const int64_t n_long = long_count(a);
+  for (int64_t i = blockIdx.x; i < n_long; i += gridDim.x) {
+    const int64_t start = a.lstart[i], len = a.llen[i];
     if (len > kLongLds) {  // (k_merge_long, from the list)
-      if (lane == 0) a.big_list[atomicAdd(a.big_count, 1u)] = (uint32_t)(i - lo);
+      if (lane == 0) a.big_list[atomicAdd(a.big_count, 1u)] = (uint32_t)i;
       continue;
     }
-    for (int j = lane; j < len; j += 64) s_id[lds_pos(j)] = (T)a.bytes[start + j];
-    wave_sync_mem();
     uint32_t* gid = a.res + 2 * start + 1;
-    const int m = seg_merge<kWide, T>(a.table, s_id, s_rk, s_kill, s_dirty, (int)len, lane, gid);
+    const int m = seg_merge<kWide, T>(a.table, a.bytes + start, s_id, s_rk, s_kill, s_dirty, (int)len, lane, gid);
     if (lane == 0) gid[-1] = (uint32_t)m;
     wave_sync_mem();
   }
@@ -1223,20 +1262,15 @@ __global__ void __launch_bounds__(64) k_merge_long_lds(EncArgs a) {
 // before either token is replaced: R < a_{i+1} and R <= b_{j+1} (R == a_{i+1} means the same
 // (x, x) pair also ends A, and left to right takes A's occurrence first).  If no coexisting pair
 // of the two spines satisfies that, the joint encoding IS the concatenation; otherwise the two
-// pieces are joined into one window and encoded again, and its new neighbours are checked.
-// After kSplitRounds rounds (long (a,a) runs cascade) or for a window over kMaxWindow bytes the
-// whole chunk runs the wave loop (seg_merge).  Cut points are chosen where the byte pair ranks
-// highest (ideally not a merge at all), which leaves ~1% of the junctions in conflict.
+// pieces are joined into one window and encoded again, and its new neighbours are checked
+// (long_split.h runs this over all long chunks of a launch at once).  Cut points are chosen where
+// the byte pair ranks highest (ideally not a merge at all), which leaves ~2% of the junctions
+// in conflict.
 // ---------------------------------------------------------------------------------------
-constexpr int kPieceN = 16;                              // per-lane register loop size
-constexpr int kPieceW = kPieceN == 32 ? 24 : 12;                 // cut spacing
-constexpr int kCutHalf = kPieceN == 32 ? 4 : 2;                  // cuts in [W k - H, W k + H)
-constexpr int kMaxPieces = (kLongLds + kPieceW - 1) / kPieceW;   // 171 (342)
-constexpr int kJWords = (kMaxPieces + 63) / 64;                  // junction bitmask words
+constexpr int kPieceN = 16;  // per-lane register loop size
+constexpr int kPieceW = 12;  // cut spacing
+constexpr int kCutHalf = 2;  // cuts in [W k - H, W k + H)
 static_assert(kPieceW + 2 * kCutHalf - 1 <= kPieceN && kPieceW + kCutHalf <= kPieceN, "pieces fit the loop");
-constexpr int kSplitRounds = 6;
-constexpr int kBrkBatch = 8;                          // byte-pair lookups in flight per lane
-constexpr int kMaxWindow = 512;
 
 // May the joint encoding of two adjacent segments differ from their separate encodings?  a: the
 // left segment's last token, b: the right segment's first token (both encoded on their own).
@@ -1257,50 +1291,6 @@ __device__ __forceinline__ bool junction_conflict(const DevTable& t, const uint2
     if (ra) { na = a; a = pr.y; } else { nb = b; b = pr.x; }
   }
   return true;
-}
-
-// The exact loop (any table) on id[0..n) in LDS run by ONE lane, for the rare windows over 64
-// bytes: rk[0..n-1) holds the ranks of the pairs (i, i + 1) on entry (TINF = not a merge) and is
-// scratch after; merges are compacted in place.  Returns the count.
-template <bool kWide, typename T>
-__device__ int lane_merge_lds(const DevTable& t, T* id, T* rk, int n) {
-  constexpr uint32_t TINF = sizeof(T) == 2 ? 0xFFFFu : kInf;  // (16-bit storage: values <= 0xFFFD)
-  constexpr uint32_t TREC = TINF - 1;                          // "look up again"
-  while (n >= 2) {
-    uint32_t best = TINF;
-    int bp = -1;
-    for (int i = 0; i + 1 < n; ++i) {
-      const uint32_t r = rk[i];
-      if (r < best) { best = r; bp = i; }
-    }
-    if (bp < 0) break;
-    // every non-overlapping occurrence, left to right (none before bp: it is the first with
-    // the minimum rank)
-    const uint32_t p0 = id[bp], p1 = id[bp + 1];
-    int w = bp;
-    for (int i = bp; i < n;) {
-      if (i + 1 < n && id[i] == p0 && id[i + 1] == p1) {
-        id[w] = (T)best;
-        rk[w] = (T)TREC;
-        if (w > 0) rk[w - 1] = (T)TREC;
-        ++w;
-        i += 2;
-      } else {
-        id[w] = id[i];
-        rk[w] = rk[i];
-        ++w;
-        ++i;
-      }
-    }
-    n = w;
-    for (int i = bp > 0 ? bp - 1 : 0; i + 1 < n; ++i) {
-      if (rk[i] == TREC) {
-        const uint32_t r = lookup<kWide>(t, id[i], id[i + 1]);
-        rk[i] = (T)(r == kInf ? TINF : r);
-      }
-    }
-  }
-  return n;
 }
 
 // The exact loop (any table) on a window of n <= 64 ids held one per lane (lane = position):
@@ -1355,249 +1345,16 @@ __device__ uint64_t wave_merge64(const DevTable& t, uint32_t& id, uint32_t& rk, 
   return alive;
 }
 
-template <bool kWide, bool k16>
-__global__ void __launch_bounds__(64) k_merge_long_split(EncArgs a) {
-  typedef typename std::conditional<k16, uint16_t, uint32_t>::type T;
-  constexpr uint32_t TINF = k16 ? 0xFFFFu : kInf;  // (16-bit storage: values <= 0xFFFD)
-  __shared__ T s_id[kLongLds];    // bytes, then each piece's ids from its first position
-  __shared__ T s_rkw[kMaxWindow];  // pair ranks of the rare window over 64 ids (one lane's loop)
-  __shared__ uint16_t s_cut[2][kMaxPieces + 1];  // piece k = [cut[k], cut[k + 1]) (double-buffered)
-  __shared__ uint16_t s_cnt[2][kMaxPieces];      // its ids, at s_id[cut[k] ..)
-  __shared__ uint8_t s_win[kMaxPieces];          // piece k is a window to encode again
-  const int lane = threadIdx.x;
-  const uint64_t lt_mask = (lane == 0) ? 0ULL : (~0ULL >> (64 - lane));
-  const DevTable& tb = a.table;
-  int64_t lo, hi;
-  SW_STAMP_INIT;
-  bucket_range(a, kLongBucket, kLongBucket, &lo, &hi);
-  for (int64_t i = lo + blockIdx.x; i < hi; i += gridDim.x) {
-    const uint64_t e = a.queue[i];
-    const int64_t start = (int64_t)(e >> 33);
-    const int len = (int)(next_set_bit(a.bits, a.n_words, start + 1, a.n_bytes) - start);
-    if (len > kLongLds) {  // (k_merge_long, from the list)
-      if (lane == 0) a.big_list[atomicAdd(a.big_count, 1u)] = (uint32_t)(i - lo);
-      continue;
-    }
-    SW_STAMP(18);
-    SW_COUNT(20, 1);
-    SW_COUNT(21, len);
-#ifdef SW_STAMPS
-    const unsigned long long t_chunk0 = __builtin_readcyclecounter();
-    bool big_win = false;
-#endif
-    const uint8_t* src = a.bytes + start;
-    uint32_t* gid = a.res + 2 * start + 1;
-    for (int j = lane; j < len; j += 64) s_id[j] = (T)src[j];
-    wave_sync_mem();
-    // byte-pair ranks looked up where they are used (the input bytes are immutable): no
-    // chunk-sized rank array in LDS, so ~12 KB per wave and 3 waves per SIMD instead of 1.75
-    auto brk = [&](int p) -> uint32_t { return lookup<kWide>(tb, src[p], src[p + 1]); };
-    int cur = 0;
-    int P = (len + kPieceW - 1) / kPieceW;
-    if (lane == 0) { s_cut[0][0] = 0; s_cut[0][P] = (uint16_t)len; }
-    wave_sync_mem();
-    // cut k (1 <= k < P) at the position in [W k - H, W k + H) whose byte pair ranks highest
-    for (int k = 1 + lane; k < P; k += 64) {
-      const int c0 = k * kPieceW - kCutHalf;
-      int best = c0;
-      uint32_t br = brk(c0 - 1);
-#pragma unroll
-      for (int u = 1; u < 2 * kCutHalf; ++u) {
-        const uint32_t r = c0 + u < len ? brk(c0 + u - 1) : 0u;
-        if (r > br) { br = r; best = c0 + u; }
-      }
-      s_cut[0][k] = (uint16_t)best;
-    }
-    wave_sync_mem();
-    SW_STAMP(12);
-    // every piece on its own (one lane each, in registers; initial ranks from s_brk)
-    for (int k = lane; k < P; k += 64) {
-      const int c = s_cut[0][k], n = s_cut[0][k + 1] - c;
-      uint32_t id[kPieceN], rk[kPieceN];
-#pragma unroll
-      for (int j = 0; j < kPieceN; ++j) {
-        id[j] = j < n ? (uint32_t)s_id[c + j] : 0u;
-        rk[j] = j + 1 < n ? brk(c + j) : kInf;
-      }
-      const uint32_t alive = lane_merge_reg_loop<kWide, k16, kPieceN>(tb, id, rk, n);
-      int m = 0;
-#pragma unroll
-      for (int j = 0; j < kPieceN; ++j)
-        if ((alive >> j) & 1u) s_id[c + m++] = (T)id[j];
-      s_cnt[0][k] = (uint16_t)m;
-    }
-    wave_sync_mem();
-    SW_STAMP(13);
-    // junction k (between pieces k - 1 and k) is bit k - 1
-    uint64_t conf[kJWords];
-#pragma unroll
-    for (int g = 0; g < kJWords; ++g) {
-      const int k = 1 + 64 * g + lane;
-      bool c = false;
-      if (k < P) c = junction_conflict<kWide>(tb, a.inv, a.n_inv, s_id[s_cut[0][k - 1] + s_cnt[0][k - 1] - 1],
-                                              s_id[s_cut[0][k]]);
-      conf[g] = __ballot(c);
-    }
-    auto cbit = [&](int j) -> bool {  // (selects: no dynamically indexed registers)
-      uint64_t w = conf[0];
-#pragma unroll
-      for (int g = 1; g < kJWords; ++g) w = (j >> 6) == g ? conf[g] : w;
-      return (w >> (j & 63)) & 1ULL;
-    };
-    auto any_conf = [&]() -> bool {
-      uint64_t o = 0;
-#pragma unroll
-      for (int g = 0; g < kJWords; ++g) o |= conf[g];
-      return o != 0ULL;
-    };
-    bool fall = false;
-    SW_STAMP(14);
-#ifdef SW_STAMPS
-    {
-      int nc = 0;
-      for (int g = 0; g < kJWords; ++g) nc += __popcll(conf[g]);
-      SW_COUNT(22, nc);
-    }
-#endif
-    for (int round = 0; any_conf(); ++round) {
-      if (round == kSplitRounds) { fall = true; break; }
-      SW_COUNT(23, 1);
-      // join the pieces across conflicting junctions; a joined piece is a window to encode again
-      const uint16_t* cut = s_cut[cur];
-      const uint16_t* cnt = s_cnt[cur];
-      uint16_t* ncut = s_cut[cur ^ 1];
-      uint16_t* ncnt = s_cnt[cur ^ 1];
-      int np = 0;
-      uint64_t wins[kJWords];
-#pragma unroll
-      for (int g = 0; g < kJWords; ++g) {
-        const int k = 64 * g + lane;
-        const bool keep = k < P && (k == 0 || !cbit(k - 1));
-        const bool win = keep && k + 1 < P && cbit(k);
-        const uint64_t km = __ballot(keep);
-        const int idx = np + __popcll(km & lt_mask);
-        if (keep) {
-          ncut[idx] = cut[k];
-          ncnt[idx] = cnt[k];
-          s_win[idx] = win ? 1 : 0;
-        }
-        np += __popcll(km);
-      }
-      if (lane == 0) ncut[np] = (uint16_t)len;
-      cur ^= 1;
-      P = np;
-      wave_sync_mem();
-      // the windows, one after the other, each by the whole wave (bytes again, ranks from s_brk)
-#pragma unroll
-      for (int g = 0; g < kJWords; ++g) {
-        const int j = 64 * g + lane;
-        wins[g] = __ballot(j < P && s_win[j]);
-      }
-#pragma unroll
-      for (int g = 0; g < kJWords; ++g) {
-        for (uint64_t wm = wins[g]; wm; wm &= wm - 1) {
-          const int j = 64 * g + __builtin_ctzll(wm);
-          const int c = ncut[j], n = ncut[j + 1] - c;
-          if (n > kMaxWindow) { fall = true; break; }
-          if (n > 64) {  // (rare) one lane, in LDS; the window's byte-pair ranks are restored after
-            SW_COUNT(27, 1);
-#ifdef SW_STAMPS
-            big_win = true;
-#endif
-            for (int q = lane; q < n - 1; q += 64) {
-              const uint32_t r = lookup<kWide>(tb, src[c + q], src[c + q + 1]);
-              s_rkw[q] = (T)(r == kInf ? TINF : r);
-            }
-            wave_sync_mem();
-            if (lane == 0) {
-              for (int q = 0; q < n; ++q) s_id[c + q] = (T)src[c + q];
-              ncnt[j] = (uint16_t)lane_merge_lds<kWide, T>(tb, s_id + c, s_rkw, n);
-            }
-            wave_sync_mem();
-            continue;
-          }
-          uint32_t id = lane < n ? (uint32_t)src[c + lane] : 0u;
-          uint32_t rk = lane + 1 < n ? brk(c + lane) : kInf;
-          const uint64_t al = wave_merge64<kWide>(tb, id, rk, n, lane);
-          wave_sync_mem();  // (every lane's reads of the window's old ids precede the stores)
-          if ((al >> lane) & 1ULL) s_id[c + __popcll(al & lt_mask)] = (T)id;
-          if (lane == 0) ncnt[j] = (uint16_t)__popcll(al);
-        }
-        if (fall) break;
-      }
-      if (fall) break;
-      wave_sync_mem();
-      // only the junctions next to a window can have changed
-#pragma unroll
-      for (int g = 0; g < kJWords; ++g) {
-        const int k = 1 + 64 * g + lane;
-        bool c = false;
-        if (k < P && (s_win[k - 1] || s_win[k]))
-          c = junction_conflict<kWide>(tb, a.inv, a.n_inv, s_id[ncut[k - 1] + ncnt[k - 1] - 1], s_id[ncut[k]]);
-        conf[g] = __ballot(c);
-      }
-    }
-    SW_STAMP(15);
-    if (fall) {  // the whole chunk in the wave loop
-      SW_COUNT(24, 1);
-      SW_COUNT(25, len);
-      SW_COUNT(26, len > 1024 ? 1 : 0);
-      wave_sync_mem();
-      for (int j = lane; j < len; j += 64) gid[j] = src[j];
-      wave_sync_mem();
-      const int64_t m = coop_merge<kWide>(tb, gid, gid + len, len, lane);
-      if (lane == 0) gid[-1] = (uint32_t)m;
-      wave_sync_mem();
-      SW_STAMP(16);
-      continue;
-    }
-    // the pieces' ids in order: gathered into s_brk, then stored coalesced
-    const uint16_t* cut = s_cut[cur];
-    const uint16_t* cnt = s_cnt[cur];
-    int total = 0;
-    wave_sync_mem();
-#pragma unroll
-    for (int g = 0; g < kJWords; ++g) {
-      const int k = 64 * g + lane;
-      const uint32_t c = k < P ? cnt[k] : 0u;
-      const uint32_t incl = wave_incl_scan(c, lane);
-      const int o = total + (int)(incl - c);
-      if (k < P) {
-        const int b = cut[k];
-        for (uint32_t q = 0; q < c; ++q) gid[o + q] = (uint32_t)s_id[b + q];
-      }
-      total += (int)__shfl(incl, 63, 64);
-    }
-    wave_sync_mem();
-    if (lane == 0) gid[-1] = (uint32_t)total;
-    wave_sync_mem();
-    SW_STAMP(17);
-#ifdef SW_STAMPS
-    if (threadIdx.x == 0) {
-      const unsigned long long dt = __builtin_readcyclecounter() - t_chunk0;
-      atomicMax(&a.stamps[19 * 64], dt);
-      if (len > 1024) { atomicAdd(&a.stamps[28 * 64], dt); atomicAdd(&a.stamps[29 * 64], 1ULL); }
-      if (big_win) { atomicAdd(&a.stamps[30 * 64], dt); atomicAdd(&a.stamps[31 * 64], 1ULL); }
-    }
-#endif
-  }
-}
-
 template <bool kWide>
 __global__ void __launch_bounds__(kThreads) k_merge_long(EncArgs a) {
   SW_STAMP_INIT;
   const int64_t gw = ((int64_t)blockIdx.x * kThreads + threadIdx.x) >> 6;
   const int64_t n_waves = ((int64_t)gridDim.x * kThreads) >> 6;
   const int lane = threadIdx.x & 63;
-  int64_t lo, hi;
-  bucket_range(a, kLongBucket, kLongBucket, &lo, &hi);
-  const uint32_t n_big = *a.big_count;  // (listed by k_merge_long_split / k_merge_long_lds)
+  const uint32_t n_big = *a.big_count;  // (listed by k_merge_long_lds)
   for (int64_t b = gw; b < (int64_t)n_big; b += n_waves) {
-    const int64_t i = lo + a.big_list[b];
-    const uint64_t e = a.queue[i];
-    const int64_t start = (int64_t)(e >> 33);
-    const int64_t end = next_set_bit(a.bits, a.n_words, start + 1, a.n_bytes);
-    const int64_t len = end - start;
+    const int64_t i = a.big_list[b];
+    const int64_t start = a.lstart[i], len = a.llen[i];
     uint32_t* gid = a.res + 2 * start + 1;  // ids: len words, then ranks: len - 1 words
     uint32_t* grk = gid + len;
     for (int64_t j = lane; j < len; j += 64) gid[j] = a.bytes[start + j];
@@ -1630,7 +1387,21 @@ __global__ void k_tile_strings(const int64_t* str_off, int64_t n_str, int64_t n_
 constexpr int kScanPer = 16;                      // tiles per thread in the scan kernels
 constexpr int kScanBlock = kThreads * kScanPer;   // tiles per scan block
 
-__global__ void __launch_bounds__(kThreads) k_scan_reduce(const uint32_t* cnt, int64_t n, int64_t* part) {
+// (n_dev: when not null the count is min(n, *n_dev), read on the device -- a grid sized for a
+// capacity n whose blocks past the live count return at once)
+__device__ __forceinline__ int64_t scan_count(int64_t n, const int64_t* n_dev) {
+  if (!n_dev) return n;
+  const int64_t d = *n_dev;
+  return d < n ? (d < 0 ? 0 : d) : n;
+}
+
+__global__ void __launch_bounds__(kThreads) k_scan_reduce(const uint32_t* cnt, int64_t n_max, const int64_t* n_dev,
+                                                          int64_t* part) {
+  const int64_t n = scan_count(n_max, n_dev);
+  if ((int64_t)blockIdx.x * kScanBlock >= n) {
+    if (threadIdx.x == 0) part[blockIdx.x] = 0;
+    return;
+  }
   const int64_t base = (int64_t)blockIdx.x * kScanBlock + (int64_t)threadIdx.x * kScanPer;
   uint64_t s = 0;
   for (int k = 0; k < kScanPer; ++k)
@@ -1647,8 +1418,9 @@ __global__ void __launch_bounds__(kThreads) k_scan_reduce(const uint32_t* cnt, i
   }
 }
 
-__global__ void __launch_bounds__(1024) k_scan_parts(int64_t* part, int64_t n_parts, int64_t* total) {
+__global__ void __launch_bounds__(1024) k_scan_parts(int64_t* part, int64_t n_max, const int64_t* n_dev, int64_t* total) {
   __shared__ int64_t sh[1024];
+  const int64_t n_parts = (scan_count(n_max, n_dev) + kScanBlock - 1) / kScanBlock;
   int64_t carry = 0;
   for (int64_t base = 0; base < n_parts; base += 1024) {
     const int64_t i = base + threadIdx.x;
@@ -1668,8 +1440,10 @@ __global__ void __launch_bounds__(1024) k_scan_parts(int64_t* part, int64_t n_pa
   if (threadIdx.x == 0) *total = carry;
 }
 
-__global__ void __launch_bounds__(kThreads) k_scan_apply(const uint32_t* cnt, int64_t n, const int64_t* part,
-                                                         int64_t* base_out) {
+__global__ void __launch_bounds__(kThreads) k_scan_apply(const uint32_t* cnt, int64_t n_max, const int64_t* n_dev,
+                                                         const int64_t* part, int64_t* base_out) {
+  const int64_t n = scan_count(n_max, n_dev);
+  if ((int64_t)blockIdx.x * kScanBlock >= n) return;
   const int64_t base = (int64_t)blockIdx.x * kScanBlock + (int64_t)threadIdx.x * kScanPer;
   uint32_t v[kScanPer];
   uint64_t s = 0;
@@ -1695,6 +1469,88 @@ __global__ void __launch_bounds__(kThreads) k_scan_apply(const uint32_t* cnt, in
   for (int k = 0; k < kScanPer; ++k) {
     if (base + k < n) base_out[base + k] = run;
     run += v[k];
+  }
+}
+
+// The same scan over a count that lives in device memory (n = min(*n_dev, n_max)), on a fixed grid
+// of kDscanGrid blocks whatever the capacity: block b scans the b-th of kDscanGrid equal ranges.
+constexpr int kDscanGrid = 512;
+__device__ __forceinline__ void dscan_range(int64_t n, int64_t* lo, int64_t* hi) {
+  const int64_t per = ((n + kDscanGrid - 1) / kDscanGrid + kScanBlock - 1) / kScanBlock * kScanBlock;
+  *lo = min((int64_t)blockIdx.x * per, n);
+  *hi = min(*lo + per, n);
+}
+
+__global__ void __launch_bounds__(kThreads) k_dscan_reduce(const uint32_t* cnt, int64_t n_max, const int64_t* n_dev,
+                                                           int64_t* part) {
+  int64_t lo, hi;
+  dscan_range(scan_count(n_max, n_dev), &lo, &hi);
+  uint64_t s = 0;
+  for (int64_t i = lo + threadIdx.x; i < hi; i += kThreads) s += cnt[i];
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off, 64);
+  __shared__ uint64_t sw[kThreads / 64];
+  if ((threadIdx.x & 63) == 0) sw[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint64_t t = 0;
+    for (int k = 0; k < kThreads / 64; ++k) t += sw[k];
+    part[blockIdx.x] = (int64_t)t;
+  }
+}
+
+__global__ void __launch_bounds__(kDscanGrid) k_dscan_parts(int64_t* part, int64_t* total) {
+  __shared__ int64_t sh[kDscanGrid];
+  const int64_t v = part[threadIdx.x];
+  sh[threadIdx.x] = v;
+  __syncthreads();
+  for (int off = 1; off < kDscanGrid; off <<= 1) {
+    const int64_t y = threadIdx.x >= off ? sh[threadIdx.x - off] : 0;
+    __syncthreads();
+    sh[threadIdx.x] += y;
+    __syncthreads();
+  }
+  part[threadIdx.x] = sh[threadIdx.x] - v;
+  if (threadIdx.x == kDscanGrid - 1) *total = sh[threadIdx.x];
+}
+
+__global__ void __launch_bounds__(kThreads) k_dscan_apply(const uint32_t* cnt, int64_t n_max, const int64_t* n_dev,
+                                                          const int64_t* part, int64_t* base_out) {
+  int64_t lo, hi;
+  dscan_range(scan_count(n_max, n_dev), &lo, &hi);
+  __shared__ uint64_t sw[kThreads / 64];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  int64_t carry = part[blockIdx.x];
+  for (int64_t t0 = lo; t0 < hi; t0 += kScanBlock) {  // kScanPer consecutive items per thread
+    const int64_t base = t0 + (int64_t)threadIdx.x * kScanPer;
+    uint32_t v[kScanPer];
+    uint64_t s = 0;
+#pragma unroll
+    for (int k = 0; k < kScanPer; ++k) {
+      v[k] = base + k < hi ? cnt[base + k] : 0u;
+      s += v[k];
+    }
+    uint64_t x = s;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+      const uint64_t y = __shfl_up(x, off, 64);
+      if (lane >= off) x += y;
+    }
+    if (lane == 63) sw[wid] = x;
+    __syncthreads();
+    uint64_t wb = 0, tot = 0;
+    for (int k = 0; k < kThreads / 64; ++k) {
+      if (k < wid) wb += sw[k];
+      tot += sw[k];
+    }
+    __syncthreads();
+    int64_t run = carry + (int64_t)(wb + x - s);
+#pragma unroll
+    for (int k = 0; k < kScanPer; ++k) {
+      if (base + k < hi) base_out[base + k] = run;
+      run += v[k];
+    }
+    carry += (int64_t)tot;
   }
 }
 

@@ -236,10 +236,16 @@ def test_long_split_vs_oracle(model):
     t.pattern = ""
 
 
-def test_long_split_stress_corpus_vs_oracle():
+@pytest.mark.parametrize("mode", [1, 0])
+def test_long_split_stress_corpus_vs_oracle(mode):
     buf, off = corpus.synth(123, corpus.STRESS, 30000, 600)
     t = tok_for("bl50k.model")
-    assert_same(t.encode_packed(buf, off), oracle_encode(t.merges, buf, off, "cl100k"))
+    L, h = _lib.lib(), t._encoder()
+    _lib.check(L.sw_encoder_set_option(h, _lib.SW_OPT_LONG_SPLIT, mode))
+    try:
+        assert_same(t.encode_packed(buf, off), oracle_encode(t.merges, buf, off, "cl100k"))
+    finally:
+        L.sw_encoder_set_option(h, _lib.SW_OPT_LONG_SPLIT, 1)
 
 
 @pytest.mark.parametrize("seed", range(4))

@@ -79,3 +79,26 @@ def test_oracle_matches_reference_at_scale(name):
         blk = np.ascontiguousarray(ids[ids_off[s0]:ids_off[s1]], dtype="<i4")
         assert len(blk) == cnt, "block %d: %d ids, the reference %d" % (k, len(blk), cnt)
         assert hashlib.sha256(blk.tobytes()).hexdigest() == digest, "block %d (strings %d..%d)" % (k, s0, s1)
+
+
+@pytest.mark.parametrize("model", ["toy500.model", "bl32k.model", "bl50k.model"])
+def test_oracle_heap_form_equals_reference_loop(model):
+    """The oracle's O(n log n) form for long chunks of well-formed tables (orc_encode_chunk_heap)
+    gives exactly the reference loop's ids (orc_encode_chunk_naive, base.py:10-36 step by step)
+    on long chunks of every kind: letter runs, (a, a) runs, whitespace runs, mixed text, raw bytes."""
+    import random
+
+    m = oracle.OracleModel(load_model_merges(model))
+    assert m.well_formed
+    rng = random.Random(21)
+    cases = []
+    for n in (256, 300, 700, 1500, 4096):
+        cases.append(bytes(rng.choice(b"abcdefghijklmnopqrstuvwxyz") for _ in range(n)))
+        cases.append(bytes(rng.choice(b"etaoin shrdlu") for _ in range(n)))
+        cases.append(bytes([rng.choice(b"ab")]) * n)
+        cases.append(b"".join(bytes([c]) * rng.randint(1, 40) for c in rng.choices(b"a ze\n", k=n))[:n])
+        cases.append(bytes(rng.randrange(256) for _ in range(n)))
+        cases.append(("Hello world, 中文字符 😀 " * (n // 20 + 1)).encode()[:n])
+    for c in cases:
+        assert m.encode_chunk(c, "heap") == m.encode_chunk(c, "naive"), (model, len(c), c[:40])
+        assert m.encode_chunk(c) == m.encode_chunk(c, "naive")

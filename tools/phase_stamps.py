@@ -33,20 +33,7 @@ names = {0: "classify: stage+enum", 1: "classify: lookups", 7: "classify: dedupe
          3: "classify: strings",
          4: "merge N<16 (blk)", 5: "merge N>=16 (blk)", 6: "merge long (blk)",
          8: "compact: prologue loads", 9: "compact: slots+gathers", 10: "compact: scan+stores", 11: "compact: strings"}
-if kind == corpus.STRESS:
-    names.update({18: "long-split: loop/skip", 12: "long-split: cuts", 13: "long-split: pieces",
-                  14: "long-split: junctions", 15: "long-split: rounds", 16: "long-split: fallback",
-                  17: "long-split: output"})
 tot = sum(out[i] for i in names)
 print("kind=%s bytes=%d chunks=%d tiles=%d kernel_ms=%.3f" % (model, len(buf), nch, tiles, tok.last_stats.ms_kernels))
 for i, nm in names.items():
     print("%-26s %12.0f cycles/tile-equiv  %5.1f%%" % (nm, out[i] / tiles / reps, 100 * out[i] / tot))
-if kind == corpus.STRESS:
-    ch = out[20] / reps
-    print("long-split per launch: chunks %.0f, bytes %.0f, conflicts(round 0) %.0f, rounds %.0f, fallbacks %.0f "
-          "(%.0f bytes, %.0f over 1 KiB), windows over 64 B %.0f; cycles per chunk: %s" % (
-              ch, out[21] / reps, out[22] / reps, out[23] / reps, out[24] / reps, out[25] / reps, out[26] / reps,
-              out[27] / reps, {names[i]: round(out[i] / reps / max(ch, 1)) for i in (12, 13, 14, 15, 16, 17)}))
-    print("long-split (non-fallback chunks): max cycles per chunk %.0f; chunks over 1 KiB: %.0f, mean cycles %.0f; "
-          "chunks with a window over 64 B: %.0f, mean cycles %.0f" % (
-              out[19], out[29] / reps, out[28] / max(out[29], 1), out[31] / reps, out[30] / max(out[31], 1)))

@@ -238,8 +238,8 @@ int32_t ensure_workspace(sw_encoder* h, int64_t n_bytes) {
     h->dmask = (uint32_t)(slots - 1);
   }
   HIP_TRY(hipMalloc(&h->d_big, sizeof(uint32_t) * (nb / (kLongLds + 1) + 2)));  // (count + list)
-  {  // long_split.h: a long chunk has > kShort bytes; a piece >= kPieceW - 2 kCutHalf + 1 bytes, but a chunk's last
-    const int64_t lcap = nb / (kShort + 1) + 64, pcap = nb / 8 + 64;
+  {  // long_split.h: a long chunk has > kShort bytes and ceil(len / kPieceW) pieces
+    const int64_t lcap = nb / (kShort + 1) + 64, pcap = nb / kPieceW + lcap;  // (ceil(len / W) pieces a chunk)
     const size_t bytes = 8 * (size_t)kLcAlloc + 4 * (size_t)lcap * 7 + 8 * (size_t)lcap  // chunks
                          + 4 * (size_t)pcap * 11                                         // pieces, lists
                          + 4 * (size_t)(nb + 64) + 4 * (size_t)pcap + 1024;             // ids, window list (+ alignment)

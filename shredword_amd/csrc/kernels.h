@@ -1267,7 +1267,7 @@ __global__ void __launch_bounds__(64) k_merge_long_lds(EncArgs a) {
 // the byte pair ranks highest (ideally not a merge at all), which leaves ~2% of the junctions
 // in conflict.
 // ---------------------------------------------------------------------------------------
-constexpr int kPieceN = 16;  // per-lane register loop size
+constexpr int kPieceN = 16;  // per-lane register loop size (12-byte loops with 8-byte pieces: C5 106.9 -> 104.1 GB/s)
 constexpr int kPieceW = 12;  // cut spacing
 constexpr int kCutHalf = 2;  // cuts in [W k - H, W k + H)
 static_assert(kPieceW + 2 * kCutHalf - 1 <= kPieceN && kPieceW + kCutHalf <= kPieceN, "pieces fit the loop");

@@ -209,13 +209,8 @@ __device__ __forceinline__ void lp_holes(const LongArgs& L, uint32_t beg, int m,
 // own: lane 0 encodes the piece before them again, so every junction (piece - 1, piece) is
 // checked by the lane of its right piece with its left neighbour's last id from the next lane
 // down.  Conflicts are listed for round 0.
-#ifdef SW_LP_WAVES  // (A/B builds: a minimum occupancy for k_lp_encode, the register budget it implies)
-#define SW_LP_ENC_ATTR __attribute__((amdgpu_waves_per_eu(SW_LP_WAVES)))
-#else
-#define SW_LP_ENC_ATTR
-#endif
 template <bool kWide, bool k16>
-__global__ void __launch_bounds__(kThreads) SW_LP_ENC_ATTR k_lp_encode(EncArgs a, LongArgs L) {
+__global__ void __launch_bounds__(kThreads) k_lp_encode(EncArgs a, LongArgs L) {
   const int64_t np = lp_count(&L.ctl[kLcPieces], L.pcap);
   const int lane = threadIdx.x & 63;
   const uint64_t lt_mask = (lane == 0) ? 0ULL : (~0ULL >> (64 - lane));

@@ -20,6 +20,7 @@
 
 #include <algorithm>
 #include <array>
+#include <atomic>
 #include <chrono>
 #include <cstdint>
 #include <cstdio>
@@ -29,6 +30,8 @@
 #include <thread>
 #include <unordered_map>
 #include <vector>
+
+#include <hipcub/hipcub.hpp>
 
 #include "capi.h"
 #include "shredword_hip.h"
@@ -69,6 +72,23 @@ __device__ __forceinline__ uint64_t slot_of(Slot* tab, uint64_t mask, uint64_t k
     }
     if (cur == key) return i;
     i = (i + 1) & mask;
+  }
+}
+
+// slot_of with the first candidate's key already loaded (cur = tab[i].key, i = the key's home)
+__device__ __forceinline__ uint64_t slot_of_from(Slot* tab, uint64_t mask, uint64_t key, uint64_t i,
+                                                 unsigned long long cur, uint32_t* used, unsigned long long* n_used) {
+  for (;;) {
+    if (cur == kEmpty) {
+      cur = atomicCAS(&tab[i].key, kEmpty, (unsigned long long)key);
+      if (cur == kEmpty) {
+        used[atomicAdd(n_used, 1ULL)] = (uint32_t)i;
+        return i;
+      }
+    }
+    if (cur == key) return i;
+    i = (i + 1) & mask;
+    cur = tab[i].key;
   }
 }
 
@@ -124,37 +144,43 @@ __global__ void k_bloom_init(const int32_t* ids, const int64_t* woff, const int3
   bloom[w] = f;
 }
 
-__global__ void k_merge_words(int32_t* ids, const int64_t* woff, int32_t* len, const uint64_t* wcnt, uint64_t* bloom,
-                              int64_t nw, int32_t A, int32_t B, int32_t X, Slot* tab, uint64_t mask, uint32_t* used,
-                              unsigned long long* n_used) {
-  const int64_t w = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (w >= nw) return;
+// (bl, base, L, wcw: the word's filter, start, live length and count, loaded by the caller)
+__device__ __forceinline__ bool merge_word_pre(int32_t* ids, int32_t* len, uint64_t* bloom, int64_t w, uint64_t bl,
+                                               int64_t base, int L, uint64_t wcw, int32_t A, int32_t B, int32_t X,
+                                               Slot* tab, uint64_t mask, uint32_t* used, unsigned long long* n_used) {
   const uint64_t need = sym_bit(A) | sym_bit(B);
-  if ((bloom[w] & need) != need) return;
-  const int64_t base = woff[w];
+  if ((bl & need) != need) return false;
   int32_t* s = ids + base;
-  const int L = len[w];
   int r = 0;
   while (r + 1 < L && !(s[r] == A && s[r + 1] == B)) ++r;  // (most words: read only)
-  if (r + 1 >= L) return;
-  const long long wc = (long long)wcnt[w];
+  if (r + 1 >= L) return false;
+  const long long wc = (long long)wcw;
   unsigned long long call = 4ULL * (unsigned long long)base;
-  auto add = [&](uint64_t h, long long d) {
-    const uint64_t i = slot_of(tab, mask, h, used, n_used);
-    atomicAdd(&tab[i].val, (unsigned long long)d);
-    atomicMin(&tab[i].first, call++);
+  // an occurrence's (up to) four changes, in the reference's call order: their home slots' keys
+  // are loaded together (one memory round trip instead of four), then each is resolved
+  auto add4 = [&](bool left, int32_t pv, bool right, int32_t nx) {
+    uint64_t h[4], home[4];
+    unsigned long long cur[4];
+    const bool on[4] = {left, left, right, right};
+    h[0] = phash(pv, A); h[1] = phash(pv, X); h[2] = phash(B, nx); h[3] = phash(X, nx);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      home[k] = mix64(h[k]) & mask;
+      cur[k] = on[k] ? tab[home[k]].key : 0ULL;
+    }
+    const long long d[4] = {-wc, wc, -wc, wc};
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      if (!on[k]) continue;
+      const uint64_t i = slot_of_from(tab, mask, h[k], home[k], cur[k], used, n_used);
+      atomicAdd(&tab[i].val, (unsigned long long)d[k]);
+      atomicMin(&tab[i].first, call++);
+    }
   };
   int o = r;
   while (r < L) {
     if (r + 1 < L && s[r] == A && s[r + 1] == B) {
-      if (o > 0) {
-        add(phash(s[o - 1], A), -wc);
-        add(phash(s[o - 1], X), wc);
-      }
-      if (r + 2 < L) {
-        add(phash(B, s[r + 2]), -wc);
-        add(phash(X, s[r + 2]), wc);
-      }
+      add4(o > 0, o > 0 ? s[o - 1] : 0, r + 2 < L, r + 2 < L ? s[r + 2] : 0);
       s[o++] = X;
       r += 2;
     } else {
@@ -165,6 +191,149 @@ __global__ void k_merge_words(int32_t* ids, const int64_t* woff, int32_t* len, c
   uint64_t f = 0;
   for (int k = 0; k < o; ++k) f |= sym_bit(s[k]);
   bloom[w] = f;
+  return true;
+}
+
+__device__ __forceinline__ bool merge_word(int32_t* ids, const int64_t* woff, int32_t* len, const uint64_t* wcnt,
+                                           uint64_t* bloom, int64_t w, int32_t A, int32_t B, int32_t X, Slot* tab,
+                                           uint64_t mask, uint32_t* used, unsigned long long* n_used) {
+  const uint64_t need = sym_bit(A) | sym_bit(B);
+  const uint64_t bl = bloom[w];
+  if ((bl & need) != need) return false;
+  return merge_word_pre(ids, len, bloom, w, bl, woff[w], len[w], wcnt[w], A, B, X, tab, mask, used, n_used);
+}
+
+// the rewrite of every word containing (A, B): one thread per word
+__global__ void __launch_bounds__(kBlock) k_merge_words(int32_t* ids, const int64_t* woff, int32_t* len,
+                                                        const uint64_t* wcnt, uint64_t* bloom, int64_t nw, int32_t A,
+                                                        int32_t B, int32_t X, Slot* tab, uint64_t mask, uint32_t* used,
+                                                        unsigned long long* n_used) {
+  const int64_t w = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (w < nw) merge_word(ids, woff, len, wcnt, bloom, w, A, B, X, tab, mask, used, n_used);
+}
+
+__device__ __forceinline__ void merge_cand(int32_t* ids, const int64_t* woff, int32_t* len, const uint64_t* wcnt,
+                                           uint64_t* bloom, const uint32_t* c0, int64_t n0, const uint32_t* c1,
+                                           int64_t n1, const uint32_t* c2, int64_t n2, uint32_t* stamp, uint32_t seq,
+                                           int32_t A, int32_t B, int32_t X, Slot* tab, uint64_t mask, uint32_t* used,
+                                           unsigned long long* n_used, uint32_t* pool, unsigned long long* pool_n,
+                                           uint64_t pool_cap, unsigned int* overflow, int64_t i) {
+  bool done = false;
+  uint32_t w = 0;
+  if (i < n0 + n1 + n2) {
+    w = i < n0 ? c0[i] : i < n0 + n1 ? c1[i - n0] : c2[i - n0 - n1];
+    // the word's filter, start, length and count loaded beside the stamp claim (one round trip,
+    // not three: only the claimant uses them, and nothing else rewrites the word in this step)
+    const uint64_t bl = bloom[w];
+    const int64_t base = woff[w];
+    const int L = len[w];
+    const uint64_t wcw = wcnt[w];
+    if (atomicExch(&stamp[w], seq) != seq)
+      done = merge_word_pre(ids, len, bloom, w, bl, base, L, wcw, A, B, X, tab, mask, used, n_used);
+  }
+  const uint64_t m = __ballot(done);  // (one pool append per wave)
+  if (!m) return;
+  const int lane = threadIdx.x & 63;
+  unsigned long long base = 0;
+  if (lane == __builtin_ctzll(m)) base = atomicAdd(pool_n, (unsigned long long)__popcll(m));
+  base = __shfl(base, __builtin_ctzll(m), 64);
+  if (done) {
+    const uint64_t k = base + __popcll(m & ((1ULL << lane) - 1ULL));
+    if (k < pool_cap) pool[k] = w;
+    else atomicOr(overflow, 1u);
+  }
+}
+
+// Per-pair word lists: the words that can hold (A, B) at a merge are those where A and B were
+// adjacent in the loaded corpus (`init`: every adjacent pair's words, sorted by pair), those
+// where the merge that created A rewrote something, and those where B's did (`pool`: the words
+// each merge rewrote, in merge order) -- a merge only ever makes pairs with the token it creates.
+// One thread per candidate (three ranges); a word listed twice is taken once (its stamp).
+__global__ void __launch_bounds__(kBlock) k_merge_cand(int32_t* ids, const int64_t* woff, int32_t* len,
+                                                       const uint64_t* wcnt, uint64_t* bloom, const uint32_t* c0,
+                                                       int64_t n0, const uint32_t* c1, int64_t n1, const uint32_t* c2,
+                                                       int64_t n2, uint32_t* stamp, uint32_t seq, int32_t A, int32_t B,
+                                                       int32_t X, Slot* tab, uint64_t mask, uint32_t* used,
+                                                       unsigned long long* n_used, uint32_t* pool,
+                                                       unsigned long long* pool_n, uint64_t pool_cap,
+                                                       unsigned int* overflow) {
+  merge_cand(ids, woff, len, wcnt, bloom, c0, n0, c1, n1, c2, n2, stamp, seq, A, B, X, tab, mask, used, n_used, pool,
+             pool_n, pool_cap, overflow, (int64_t)blockIdx.x * blockDim.x + threadIdx.x);
+}
+
+// the initial pair -> words list: every adjacent pair's key and its word (then sorted by key)
+__global__ void k_pair_words(const int32_t* ids, const int64_t* woff, const int32_t* len, int64_t nw,
+                             uint64_t* keys, uint32_t* words) {
+  const int64_t w = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (w >= nw) return;
+  const int64_t base = woff[w];
+  for (int k = 0, L = len[w]; k + 1 < L; ++k) {  // (entry base + k - w: every word's first position skipped)
+    keys[base + k - w] = ((uint64_t)(uint32_t)ids[base + k] << 32) | (uint32_t)ids[base + k + 1];
+    words[base + k - w] = (uint32_t)w;
+  }
+}
+
+// a merge step's changes, by ONE workgroup after k_merge_words: the claimed slots, densely (the
+// first `hcap` straight into host-coherent memory), cleared with their counter; then the record
+// count and the step's sequence number for the host, which spins on it instead of synchronising
+// the stream.  (One workgroup: a grid would need a device-scope fence per block to know when all
+// are done, which on a multi-XCD part costs more than the whole step.)
+__device__ __forceinline__ void collect_step(Slot* tab, const uint32_t* used, unsigned long long* n_used, Slot* out,
+                                             Slot* hout, unsigned long long* hcount, unsigned long long* hseq,
+                                             unsigned long long seq, uint64_t hcap, const unsigned long long* pool_n,
+                                             const unsigned int* overflow) {
+  const uint64_t n = __hip_atomic_load(n_used, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  for (uint64_t i = threadIdx.x; i < n; i += blockDim.x) {
+    Slot& sl = tab[used[i]];
+    Slot v;  // (atomic loads: the slots were updated by atomics of other workgroups)
+    v.key = __hip_atomic_load(&sl.key, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    v.val = __hip_atomic_load(&sl.val, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    v.first = __hip_atomic_load(&sl.first, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (i < hcap) hout[i] = v;
+    else out[i] = v;
+    sl.key = kEmpty;
+    sl.val = 0;
+    sl.first = ~0ULL;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    *n_used = 0;
+    hcount[0] = n;
+    hcount[2] = __hip_atomic_load(pool_n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // (words rewritten so far,
+    hcount[3] = __hip_atomic_load(overflow, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // list overflow)
+    __threadfence_system();
+    __hip_atomic_store(hseq, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+}
+
+__global__ void __launch_bounds__(1024) k_collect_step(Slot* tab, const uint32_t* used, unsigned long long* n_used,
+                                                       Slot* out, Slot* hout, unsigned long long* hcount,
+                                                       unsigned long long* hseq, unsigned long long seq, uint64_t hcap,
+                                                       const unsigned long long* pool_n, const unsigned int* overflow) {
+  collect_step(tab, used, n_used, out, hout, hcount, hseq, seq, hcap, pool_n, overflow);
+}
+
+// a merge over few candidates (<= kFuseBlocks workgroups) in ONE launch: the candidates, then the
+// last workgroup to finish (a ticket after a device-scope fence: a few fences, not thousands)
+// collects the changes and publishes them
+constexpr unsigned kFuseBlocks = 16;
+__global__ void __launch_bounds__(kBlock) k_merge_cand_fused(
+    int32_t* ids, const int64_t* woff, int32_t* len, const uint64_t* wcnt, uint64_t* bloom, const uint32_t* c0,
+    int64_t n0, const uint32_t* c1, int64_t n1, const uint32_t* c2, int64_t n2, uint32_t* stamp, uint32_t seq, int32_t A,
+    int32_t B, int32_t X, Slot* tab, uint64_t mask, uint32_t* used, unsigned long long* n_used, uint32_t* pool,
+    unsigned long long* pool_n, uint64_t pool_cap, unsigned int* overflow, unsigned int* ticket, Slot* out, Slot* hout,
+    unsigned long long* hcount, unsigned long long* hseq, unsigned long long hseq_val, uint64_t hcap) {
+  merge_cand(ids, woff, len, wcnt, bloom, c0, n0, c1, n1, c2, n2, stamp, seq, A, B, X, tab, mask, used, n_used, pool,
+             pool_n, pool_cap, overflow, (int64_t)blockIdx.x * blockDim.x + threadIdx.x);
+  __shared__ bool last;
+  __threadfence();
+  __syncthreads();
+  if (threadIdx.x == 0) last = atomicAdd(ticket, 1u) == gridDim.x - 1;
+  __syncthreads();
+  if (!last) return;
+  __threadfence();
+  if (threadIdx.x == 0) *ticket = 0;
+  collect_step(tab, used, n_used, out, hout, hcount, hseq, hseq_val, hcap, pool_n, overflow);
 }
 
 // the table's claimed slots, densely (the first `hcap` also into host-mapped memory, with the
@@ -187,6 +356,138 @@ __global__ void k_collect(Slot* tab, const uint32_t* used, const unsigned long l
     t.key = kEmpty;
     t.val = 0;
     t.first = ~0ULL;
+  }
+}
+
+// final token frequencies over the rewritten corpus (bpe_save :703-712; negative ids skipped)
+__global__ void k_tok_freq(const int32_t* ids, const int64_t* woff, const int32_t* len, const uint64_t* wcnt, int64_t nw,
+                           int64_t n_tok, unsigned long long* freq) {
+  const int64_t w = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (w >= nw) return;
+  const unsigned long long c = wcnt[w];
+  for (int k = 0, L = len[w]; k < L; ++k) {
+    const int32_t id = ids[woff[w] + k];
+    if (id >= 0 && id < n_tok) atomicAdd(&freq[id], c);
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// corpus load on the device (bpe_load_corpus, bpe.cpp:208-297): words = maximal runs of
+// non-delimiter bytes, counted per distinct word (first occurrence = smallest offset), ordered
+// as the reference's StrMap iterates (djb2 & 4095 bucket, then first occurrence), the character
+// histogram over the distinct words, then the symbols written in that order
+// ---------------------------------------------------------------------------------------------
+__device__ __forceinline__ bool d_delim(uint8_t c) { return c == ' ' || c == '\t' || c == '\r' || c == '\n'; }
+
+// word starts (a non-delimiter after a delimiter or at 0); a NUL byte anywhere sets *bad
+__global__ void k_word_flags(const uint8_t* text, int64_t n, uint8_t* flags, unsigned int* bad) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const uint8_t c = text[i];
+    if (c == 0) atomicOr(bad, 1u);
+    flags[i] = (!d_delim(c) && (i == 0 || d_delim(text[i - 1]))) ? 1 : 0;
+  }
+}
+
+__device__ __forceinline__ uint64_t d_word_hash(const uint8_t* p, int64_t n) {  // FNV-1a 64 + finaliser
+  uint64_t h = 1469598103934665603ULL;
+  for (int64_t i = 0; i < n; ++i) h = (h ^ p[i]) * 1099511628211ULL;
+  h ^= h >> 29;
+  h *= 0xbf58476d1ce4e5b9ULL;
+  return h ^ (h >> 32);
+}
+
+__global__ void k_iota(uint32_t* v, int64_t n) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    v[i] = (uint32_t)i;
+}
+
+// every word occurrence's 64-bit hash (the sort key) and start
+__global__ void k_word_hash(const uint8_t* text, int64_t n, const int64_t* starts, const int64_t* n_words,
+                            uint64_t* keys, uint64_t* vals) {
+  const int64_t nwd = *n_words;
+  for (int64_t w = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; w < nwd; w += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t s = starts[w];
+    int64_t e = s;
+    while (e < n && !d_delim(text[e])) ++e;
+    keys[w] = d_word_hash(text + s, e - s);
+    vals[w] = (uint64_t)s;
+  }
+}
+
+// after the (stable) sort by hash: run heads (an occurrence whose hash differs from the one before)
+__global__ void k_run_heads(const uint64_t* skeys, int64_t m, int64_t* head) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < m; i += (int64_t)gridDim.x * blockDim.x)
+    head[i] = (i == 0 || skeys[i] != skeys[i - 1]) ? i : 0;
+}
+
+// exactness: every occurrence equals its run's first occurrence byte for byte (a 64-bit hash
+// collision between two distinct words sets *bad, and the load falls back to the host)
+__global__ void k_word_verify(const uint8_t* text, int64_t n, const uint64_t* svals, const int64_t* headidx, int64_t m,
+                              unsigned int* bad) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < m; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t s = (int64_t)svals[i], r = (int64_t)svals[headidx[i]];
+    if (s == r) continue;
+    int64_t q = 0;
+    while (s + q < n && r + q < n && !d_delim(text[s + q]) && text[s + q] == text[r + q]) ++q;
+    const bool end_s = s + q >= n || d_delim(text[s + q]), end_r = r + q >= n || d_delim(text[r + q]);
+    if (!(end_s && end_r)) atomicOr(bad, 1u);
+  }
+}
+
+// the distinct words (one per run): first occurrence (the run's first: the sort is stable and
+// the occurrences were in corpus order), count, length, and the StrMap order key (djb2 & 4095,
+// then the first occurrence: hash.cpp:29-53, 61-72)
+__global__ void k_word_runs(const uint8_t* text, int64_t n, const uint64_t* svals, const int64_t* roff,
+                            const int64_t* n_runs, uint64_t* first, uint64_t* cnt, uint32_t* wlen, uint64_t* keys) {
+  const int64_t nd = *n_runs;
+  for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < nd; r += (int64_t)gridDim.x * blockDim.x) {
+    const uint64_t f = svals[roff[r]];
+    uint64_t h = 5381;
+    int64_t e = (int64_t)f;
+    while (e < n && !d_delim(text[e])) {
+      h = (h << 5) + h + text[e];
+      ++e;
+    }
+    first[r] = f;
+    cnt[r] = (uint64_t)(roff[r + 1] - roff[r]);
+    wlen[r] = (uint32_t)(e - (int64_t)f);
+    keys[r] = ((h & 4095u) << 52) | f;
+  }
+}
+
+// the character histogram over the distinct words (histogram.cpp:30-36: each distinct word's
+// bytes once), per block in LDS; and each word's length and count in StrMap order
+__global__ void k_word_hist(const uint8_t* text, const uint64_t* first, const uint32_t* wlen, const uint64_t* cnt,
+                            const uint32_t* order, int64_t nd, unsigned long long* hist, int64_t* len_out,
+                            int32_t* len32, uint64_t* cnt_out) {
+  __shared__ unsigned int h[256];
+  for (int c = threadIdx.x; c < 256; c += blockDim.x) h[c] = 0;
+  __syncthreads();
+  for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < nd; j += (int64_t)gridDim.x * blockDim.x) {
+    const uint32_t r = order[j];
+    const uint64_t f = first[r];
+    const uint32_t L = wlen[r];
+    for (uint32_t q = 0; q < L; ++q) atomicAdd(&h[text[f + q]], 1u);
+    len_out[j] = L;
+    len32[j] = (int32_t)L;
+    cnt_out[j] = cnt[r];
+  }
+  __syncthreads();
+  for (int c = threadIdx.x; c < 256; c += blockDim.x)
+    if (h[c]) atomicAdd(&hist[c], (unsigned long long)h[c]);
+}
+
+// the symbols: word j's bytes through the coverage map, at woff[j]
+__global__ void k_word_ids(const uint8_t* text, const uint64_t* first, const uint32_t* wlen, const uint32_t* order,
+                           const int64_t* woff, int64_t nd, const int32_t* map, int32_t* ids) {
+  __shared__ int32_t m[256];
+  for (int c = threadIdx.x; c < 256; c += blockDim.x) m[c] = map[c];
+  __syncthreads();
+  for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < nd; j += (int64_t)gridDim.x * blockDim.x) {
+    const uint32_t r = order[j];
+    const uint64_t f = first[r];
+    int32_t* d = ids + woff[j];
+    for (uint32_t q = 0, L = wlen[r]; q < L; ++q) d[q] = m[text[f + q]];
   }
 }
 
@@ -237,47 +538,49 @@ struct PairInfo {
 };
 
 // pair -> PairInfo, open addressing (the BIMap's role, hash.cpp:104-130; its iteration order
-// only matters for the heap seed, which is sorted explicitly)
+// only matters for the heap seed, which is sorted explicitly).  Key and value in one 24-byte
+// entry (one cache miss a lookup); prefetch() lets the change pass issue its misses early.
 class PairMap {
  public:
   explicit PairMap(size_t n) { rehash(n); }
   PairInfo& operator[](uint64_t key) {  // get or create (freq 0, version 0)
-    if (2 * (n_ + 1) > keys_.size()) rehash(keys_.size());
+    if (2 * (n_ + 1) > e_.size()) rehash(e_.size());
     size_t i = slot(key);
-    if (keys_[i] != key) {
-      keys_[i] = key;
-      vals_[i] = PairInfo{};
+    if (e_[i].key != key) {
+      e_[i].key = key;
+      e_[i].v = PairInfo{};
       ++n_;
     }
-    return vals_[i];
+    return e_[i].v;
   }
+  void prefetch(uint64_t key) const { __builtin_prefetch(&e_[(size_t)mix(key) & (e_.size() - 1)], 1); }
 
  private:
+  struct E {
+    uint64_t key;
+    PairInfo v;
+  };
   static uint64_t mix(uint64_t x) {
     x ^= x >> 33;
     x *= 0xff51afd7ed558ccdULL;
     return x ^ (x >> 33);
   }
   size_t slot(uint64_t key) const {
-    size_t i = (size_t)mix(key) & (keys_.size() - 1);
-    while (keys_[i] != key && keys_[i] != kEmpty) i = (i + 1) & (keys_.size() - 1);
+    size_t i = (size_t)mix(key) & (e_.size() - 1);
+    while (e_[i].key != key && e_[i].key != kEmpty) i = (i + 1) & (e_.size() - 1);
     return i;
   }
   void rehash(size_t n) {
     size_t cap = 1024;
     while (cap < 2 * n) cap <<= 1;
-    std::vector<uint64_t> ok;
-    std::vector<PairInfo> ov;
-    ok.swap(keys_);
-    ov.swap(vals_);
-    keys_.assign(cap, kEmpty);
-    vals_.assign(cap, PairInfo{});
+    std::vector<E> old;
+    old.swap(e_);
+    e_.assign(cap, E{kEmpty, PairInfo{}});
     n_ = 0;
-    for (size_t i = 0; i < ok.size(); ++i)
-      if (ok[i] != kEmpty) (*this)[ok[i]] = ov[i];
+    for (const E& x : old)
+      if (x.key != kEmpty) (*this)[x.key] = x.v;
   }
-  std::vector<uint64_t> keys_;
-  std::vector<PairInfo> vals_;
+  std::vector<E> e_;
   size_t n_ = 0;
 };
 
@@ -310,12 +613,15 @@ struct sw_trainer {
   sw_train_config cfg{};
   int device = 0;
   hipStream_t st = nullptr;
-  // corpus (host copy of the initial symbols; the device copy is rewritten by training)
-  std::vector<int32_t> ids;
-  std::vector<int64_t> woff;
-  std::vector<int32_t> wlen;
-  std::vector<uint64_t> wcnt;
+  // the loaded corpus, on the device (training rewrites copies of ids and len): every distinct
+  // word's symbols back to back in StrMap order, its offset, length and count
+  int32_t* d_ids0 = nullptr;
+  int64_t* d_woff0 = nullptr;
+  int32_t* d_len0 = nullptr;
+  uint64_t* d_wcnt0 = nullptr;
+  int64_t nw = 0, ns = 0;
   bool loaded = false;
+  bool host_load = false;             // the last load took the host path (SW_TRAIN_HOST_LOAD, or a hash collision)
   // results
   std::vector<int32_t> merges;   // 3 per merge
   std::vector<uint64_t> tok_freq;
@@ -337,11 +643,31 @@ struct sw_trainer {
   Slot* h_out_dev = nullptr;      // (their device-side addresses)
   unsigned long long* h_nused_dev = nullptr;
   int64_t out_cap = 0;
+  // merge steps (k_merge_words + k_collect_step): device counter, and host-coherent records + count + sequence
+  unsigned long long* d_step_used = nullptr;
+  // per-pair word lists (k_merge_cand): the initial pair -> words list, the rewritten-words pool
+  uint32_t* d_pwords = nullptr;
+  unsigned int* d_ticket = nullptr;
+  uint32_t* d_stamp = nullptr;
+  uint32_t* d_pool = nullptr;
+  unsigned long long* d_pool_n = nullptr;
+  unsigned int* d_overflow = nullptr;
+  Slot* h_rec = nullptr;
+  unsigned long long* h_cnt = nullptr;   // [0] record count, [1] sequence number
+  Slot* h_rec_dev = nullptr;
+  unsigned long long* h_cnt_dev = nullptr;
 };
 
 namespace {
 
 constexpr int64_t kPinnedRecords = 4096;  // change records fetched with the count (more: a second copy)
+
+void free_corpus(sw_trainer* t) {
+  (void)hipFree(t->d_ids0); (void)hipFree(t->d_woff0); (void)hipFree(t->d_len0); (void)hipFree(t->d_wcnt0);
+  t->d_ids0 = nullptr; t->d_woff0 = nullptr; t->d_len0 = nullptr; t->d_wcnt0 = nullptr;
+  t->nw = t->ns = 0;
+  t->loaded = false;
+}
 
 void free_device(sw_trainer* t) {
   (void)hipFree(t->d_ids); (void)hipFree(t->d_woff); (void)hipFree(t->d_len); (void)hipFree(t->d_wcnt);
@@ -349,6 +675,14 @@ void free_device(sw_trainer* t) {
   t->d_bloom = nullptr;
   (void)hipFree(t->d_tab); (void)hipFree(t->d_out); (void)hipFree(t->d_used); (void)hipFree(t->d_nused);
   (void)hipHostFree(t->h_out); (void)hipHostFree(t->h_nused);
+  (void)hipFree(t->d_step_used);
+  (void)hipFree(t->d_pwords); (void)hipFree(t->d_stamp); (void)hipFree(t->d_pool); (void)hipFree(t->d_pool_n);
+  (void)hipFree(t->d_overflow); (void)hipFree(t->d_ticket);
+  t->d_ticket = nullptr;
+  t->d_pwords = nullptr; t->d_stamp = nullptr; t->d_pool = nullptr; t->d_pool_n = nullptr; t->d_overflow = nullptr;
+  (void)hipHostFree(t->h_rec); (void)hipHostFree(t->h_cnt);
+  t->d_step_used = nullptr; t->h_rec = nullptr; t->h_cnt = nullptr;
+  t->h_rec_dev = nullptr; t->h_cnt_dev = nullptr;
   t->d_ids = nullptr; t->d_woff = nullptr; t->d_len = nullptr; t->d_wcnt = nullptr; t->d_tab = nullptr;
   t->d_out = nullptr; t->d_used = nullptr; t->d_nused = nullptr; t->h_out = nullptr; t->h_nused = nullptr;
   t->h_out_dev = nullptr; t->h_nused_dev = nullptr;
@@ -420,6 +754,22 @@ inline uint64_t word_hash(const uint8_t* p, int64_t n) {  // FNV-1a 64, then a f
 
 // bpe_load_corpus (bpe.cpp:208-297) restated over a buffer: the text's ranges are counted by
 // host threads in parallel (the first occurrence of a word = its smallest offset), then merged
+// character coverage (bpe.cpp:256-279): chars in StrMap order ((c + 165) & 255), stable by
+// count, the first (size_t)(n * coverage) kept; the others map to unk_id
+void coverage_map(const uint64_t (&ch)[256], const sw_train_config& cfg, int32_t (&map)[256]) {
+  std::vector<int> chars;
+  for (int b = 0; b < 256; ++b) {
+    const int c = (b + 91) & 255;
+    if (ch[c]) chars.push_back(c);
+  }
+  std::stable_sort(chars.begin(), chars.end(), [&](int x, int y) { return ch[x] > ch[y]; });
+  float cov = cfg.character_coverage;
+  if (!(cov > 0.0f && cov < 1.0f)) cov = 0.995f;
+  const size_t keep = (size_t)((float)chars.size() * cov);
+  for (int c = 0; c < 256; ++c) map[c] = cfg.unk_id;
+  for (size_t k = 0; k < keep && k < chars.size(); ++k) map[chars[k]] = chars[k];
+}
+
 int32_t load_words(sw_trainer* t, const uint8_t* text, int64_t n) {
   if (n > 0 && std::memchr(text, 0, (size_t)n)) return sw::set_error(SW_ERR_ARG, "sw_trainer: the corpus holds NUL bytes");
   const int T = (int)std::max<int64_t>(1, std::min<int64_t>({16, (int64_t)std::thread::hardware_concurrency(),
@@ -515,47 +865,201 @@ int32_t load_words(sw_trainer* t, const uint8_t* text, int64_t n) {
       std::sort(order.begin() + start[b], order.begin() + start[b + 1],
                 [&](int64_t x, int64_t y) { return first[(size_t)x] < first[(size_t)y]; });
   });
-  // character coverage (bpe.cpp:256-279): chars in StrMap order ((c + 165) & 255), stable by
-  // count, the first (size_t)(n * coverage) kept
   uint64_t ch[256] = {0};
   for (const auto& a : chs)
     for (int c = 0; c < 256; ++c) ch[c] += a[(size_t)c];
-  std::vector<int> chars;
-  for (int b = 0; b < 256; ++b) {
-    const int c = (b + 91) & 255;
-    if (ch[c]) chars.push_back(c);
-  }
-  std::stable_sort(chars.begin(), chars.end(), [&](int x, int y) { return ch[x] > ch[y]; });
-  float cov = t->cfg.character_coverage;
-  if (!(cov > 0.0f && cov < 1.0f)) cov = 0.995f;
-  const size_t keep = (size_t)((float)chars.size() * cov);
   int32_t map[256];
-  for (int c = 0; c < 256; ++c) map[c] = t->cfg.unk_id;
-  for (size_t k = 0; k < keep && k < chars.size(); ++k) map[chars[k]] = chars[k];
-  // symbols, words in corpus order (filled by the threads)
-  t->woff.assign((size_t)nw, 0);
-  t->wlen.assign((size_t)nw, 0);
-  t->wcnt.assign((size_t)nw, 0);
+  coverage_map(ch, t->cfg, map);
+  // symbols, words in StrMap order (filled by the threads), then onto the device
+  std::vector<int64_t> woff((size_t)nw);
+  std::vector<int32_t> wlen((size_t)nw);
+  std::vector<uint64_t> wcnt((size_t)nw);
   int64_t total = 0;
   for (int64_t r = 0; r < nw; ++r) {
     const int64_t k = order[(size_t)r];
-    t->woff[(size_t)r] = total;
-    t->wlen[(size_t)r] = (int32_t)wlen0[(size_t)k];
-    t->wcnt[(size_t)r] = counts[(size_t)k];
+    woff[(size_t)r] = total;
+    wlen[(size_t)r] = (int32_t)wlen0[(size_t)k];
+    wcnt[(size_t)r] = counts[(size_t)k];
     total += wlen0[(size_t)k];
   }
-  t->ids.assign((size_t)total, 0);
+  std::vector<int32_t> ids((size_t)total);
   run([&](int p) {
     for (int64_t r = nw * p / T, e = nw * (p + 1) / T; r < e; ++r) {
       const int64_t k = order[(size_t)r];
       const uint8_t* w = text + woff0[(size_t)k];
-      int32_t* d = t->ids.data() + t->woff[(size_t)r];
+      int32_t* d = ids.data() + woff[(size_t)r];
       for (int64_t q = 0; q < wlen0[(size_t)k]; ++q) d[q] = map[w[q]];
     }
   });
+  free_corpus(t);
+  SW_HIP_TRY(hipMalloc(&t->d_ids0, sizeof(int32_t) * std::max<int64_t>(total, 1)));
+  SW_HIP_TRY(hipMalloc(&t->d_woff0, sizeof(int64_t) * std::max<int64_t>(nw, 1)));
+  SW_HIP_TRY(hipMalloc(&t->d_len0, sizeof(int32_t) * std::max<int64_t>(nw, 1)));
+  SW_HIP_TRY(hipMalloc(&t->d_wcnt0, sizeof(uint64_t) * std::max<int64_t>(nw, 1)));
+  if (total) SW_HIP_TRY(hipMemcpy(t->d_ids0, ids.data(), sizeof(int32_t) * total, hipMemcpyHostToDevice));
+  if (nw) {
+    SW_HIP_TRY(hipMemcpy(t->d_woff0, woff.data(), sizeof(int64_t) * nw, hipMemcpyHostToDevice));
+    SW_HIP_TRY(hipMemcpy(t->d_len0, wlen.data(), sizeof(int32_t) * nw, hipMemcpyHostToDevice));
+    SW_HIP_TRY(hipMemcpy(t->d_wcnt0, wcnt.data(), sizeof(uint64_t) * nw, hipMemcpyHostToDevice));
+  }
+  t->nw = nw;
+  t->ns = total;
+  t->host_load = true;
   t->loaded = true;
   t->merges.clear();
   t->tok_freq.clear();
+  return SW_OK;
+}
+
+// device temporaries freed together
+struct TempBufs {
+  std::vector<void*> p;
+  ~TempBufs() { for (void* x : p) (void)hipFree(x); }
+  template <typename T>
+  hipError_t get(T** out, size_t bytes) {
+    void* q = nullptr;
+    const hipError_t e = hipMalloc(&q, std::max<size_t>(bytes, 16));
+    if (e == hipSuccess) p.push_back(q);
+    *out = (T*)q;
+    return e;
+  }
+};
+
+// bpe_load_corpus on the device (the kernels above); returns 1 when a 64-bit hash collision
+// between two distinct words makes it give way to the host path
+int32_t load_words_device(sw_trainer* t, const uint8_t* text, int64_t n) {
+  hipStream_t st = t->st;
+  TempBufs b;  // (temporaries, freed on every return)
+  uint8_t* d_text;
+  uint8_t* d_flags;
+  int64_t *d_starts, *d_cnt;
+  unsigned int* d_bad;
+  SW_HIP_TRY(b.get(&d_text, (size_t)n));
+  SW_HIP_TRY(b.get(&d_flags, (size_t)n));
+  SW_HIP_TRY(b.get(&d_cnt, 4 * sizeof(int64_t)));
+  SW_HIP_TRY(b.get(&d_bad, sizeof(unsigned int)));
+  SW_HIP_TRY(hipMemsetAsync(d_bad, 0, sizeof(unsigned int), st));
+  if (n) SW_HIP_TRY(hipMemcpyAsync(d_text, text, (size_t)n, hipMemcpyHostToDevice, st));
+  const unsigned g = 4096;
+  hipLaunchKernelGGL(k_word_flags, dim3(g), dim3(kBlock), 0, st, d_text, n, d_flags, d_bad);
+  // word starts (in corpus order)
+  size_t tmp_bytes = 0;
+  hipcub::CountingInputIterator<int64_t> pos(0);
+  SW_HIP_TRY(hipcub::DeviceSelect::Flagged(nullptr, tmp_bytes, pos, d_flags, (int64_t*)nullptr, d_cnt, n, st));
+  void* d_tmp;
+  SW_HIP_TRY(b.get(&d_tmp, tmp_bytes));
+  // (an upper bound of the word count without a round trip: at most one word per 2 bytes + 1)
+  const int64_t wmax = n / 2 + 1;
+  SW_HIP_TRY(b.get(&d_starts, sizeof(int64_t) * (size_t)wmax));
+  SW_HIP_TRY(hipcub::DeviceSelect::Flagged(d_tmp, tmp_bytes, pos, d_flags, d_starts, d_cnt, n, st));
+  int64_t nwords = 0;
+  unsigned int bad = 0;
+  SW_HIP_TRY(hipMemcpyAsync(&nwords, d_cnt, sizeof(int64_t), hipMemcpyDeviceToHost, st));
+  SW_HIP_TRY(hipMemcpyAsync(&bad, d_bad, sizeof(unsigned int), hipMemcpyDeviceToHost, st));
+  SW_HIP_TRY(hipStreamSynchronize(st));
+  if (bad) return sw::set_error(SW_ERR_ARG, "sw_trainer: the corpus holds NUL bytes");
+  // distinct words: the occurrences sorted by hash (stable: corpus order within a run), one
+  // run per distinct word, every occurrence checked against its run's first
+  const int64_t m = nwords;
+  uint64_t *d_hk, *d_hk2, *d_hv, *d_hv2;
+  int64_t *d_head, *d_roff, *d_rcnt64;
+  SW_HIP_TRY(b.get(&d_hk, sizeof(uint64_t) * (size_t)std::max<int64_t>(m, 1)));
+  SW_HIP_TRY(b.get(&d_hk2, sizeof(uint64_t) * (size_t)std::max<int64_t>(m, 1)));
+  SW_HIP_TRY(b.get(&d_hv, sizeof(uint64_t) * (size_t)std::max<int64_t>(m, 1)));
+  SW_HIP_TRY(b.get(&d_hv2, sizeof(uint64_t) * (size_t)std::max<int64_t>(m, 1)));
+  hipLaunchKernelGGL(k_word_hash, dim3(g), dim3(kBlock), 0, st, d_text, n, d_starts, d_cnt, d_hk, d_hv);
+  size_t tb1 = 0;
+  SW_HIP_TRY(hipcub::DeviceRadixSort::SortPairs(nullptr, tb1, d_hk, d_hk2, d_hv, d_hv2, (int)m, 0, 64, st));
+  void* d_tmp1;
+  SW_HIP_TRY(b.get(&d_tmp1, tb1));
+  SW_HIP_TRY(hipcub::DeviceRadixSort::SortPairs(d_tmp1, tb1, d_hk, d_hk2, d_hv, d_hv2, (int)m, 0, 64, st));
+  int64_t* d_headidx;
+  SW_HIP_TRY(b.get(&d_head, sizeof(int64_t) * (size_t)std::max<int64_t>(m, 1)));
+  SW_HIP_TRY(b.get(&d_headidx, sizeof(int64_t) * (size_t)std::max<int64_t>(m, 1)));
+  hipLaunchKernelGGL(k_run_heads, dim3(g), dim3(kBlock), 0, st, d_hk2, m, d_head);
+  size_t tb2 = 0;  // (every occurrence's run head: a max-scan of the head positions)
+  SW_HIP_TRY(hipcub::DeviceScan::InclusiveScan(nullptr, tb2, d_head, d_headidx, hipcub::Max(), (int)m, st));
+  void* d_tmp2;
+  SW_HIP_TRY(b.get(&d_tmp2, tb2));
+  SW_HIP_TRY(hipcub::DeviceScan::InclusiveScan(d_tmp2, tb2, d_head, d_headidx, hipcub::Max(), (int)m, st));
+  hipLaunchKernelGGL(k_word_verify, dim3(g), dim3(kBlock), 0, st, d_text, n, d_hv2, d_headidx, m, d_bad);
+  // runs: their lengths (counts), then offsets
+  uint64_t* d_ukeys;
+  SW_HIP_TRY(b.get(&d_ukeys, sizeof(uint64_t) * (size_t)std::max<int64_t>(m, 1)));
+  SW_HIP_TRY(b.get(&d_rcnt64, sizeof(int64_t) * (size_t)(m + 1)));
+  SW_HIP_TRY(b.get(&d_roff, sizeof(int64_t) * (size_t)(m + 1)));
+  size_t tb3 = 0;
+  SW_HIP_TRY(hipcub::DeviceRunLengthEncode::Encode(nullptr, tb3, d_hk2, d_ukeys, d_rcnt64, d_cnt + 1, (int)m, st));
+  void* d_tmp3;
+  SW_HIP_TRY(b.get(&d_tmp3, tb3));
+  SW_HIP_TRY(hipcub::DeviceRunLengthEncode::Encode(d_tmp3, tb3, d_hk2, d_ukeys, d_rcnt64, d_cnt + 1, (int)m, st));
+  int64_t nd = 0;
+  SW_HIP_TRY(hipMemcpyAsync(&nd, d_cnt + 1, sizeof(int64_t), hipMemcpyDeviceToHost, st));
+  SW_HIP_TRY(hipMemcpyAsync(&bad, d_bad, sizeof(unsigned int), hipMemcpyDeviceToHost, st));
+  SW_HIP_TRY(hipStreamSynchronize(st));
+  if (bad) return 1;  // (a hash collision: the host path)
+  SW_HIP_TRY(hipMemsetAsync(d_rcnt64 + nd, 0, sizeof(int64_t), st));
+  size_t tb4 = 0;
+  SW_HIP_TRY(hipcub::DeviceScan::ExclusiveSum(nullptr, tb4, d_rcnt64, d_roff, (int)(nd + 1), st));
+  void* d_tmp4;
+  SW_HIP_TRY(b.get(&d_tmp4, tb4));
+  SW_HIP_TRY(hipcub::DeviceScan::ExclusiveSum(d_tmp4, tb4, d_rcnt64, d_roff, (int)(nd + 1), st));
+  // StrMap order
+  uint64_t *d_first, *d_wcnt, *d_keys, *d_keys2;
+  uint32_t *d_wlen, *d_ridx, *d_order;
+  SW_HIP_TRY(b.get(&d_first, sizeof(uint64_t) * (size_t)std::max<int64_t>(nd, 1)));
+  SW_HIP_TRY(b.get(&d_wcnt, sizeof(uint64_t) * (size_t)std::max<int64_t>(nd, 1)));
+  SW_HIP_TRY(b.get(&d_wlen, sizeof(uint32_t) * (size_t)std::max<int64_t>(nd, 1)));
+  SW_HIP_TRY(b.get(&d_keys, sizeof(uint64_t) * (size_t)std::max<int64_t>(nd, 1)));
+  SW_HIP_TRY(b.get(&d_keys2, sizeof(uint64_t) * (size_t)std::max<int64_t>(nd, 1)));
+  SW_HIP_TRY(b.get(&d_ridx, sizeof(uint32_t) * (size_t)std::max<int64_t>(nd, 1)));
+  SW_HIP_TRY(b.get(&d_order, sizeof(uint32_t) * (size_t)std::max<int64_t>(nd, 1)));
+  hipLaunchKernelGGL(k_word_runs, dim3(g), dim3(kBlock), 0, st, d_text, n, d_hv2, d_roff, d_cnt + 1, d_first, d_wcnt,
+                     d_wlen, d_keys);
+  hipLaunchKernelGGL(k_iota, dim3(g), dim3(kBlock), 0, st, d_ridx, nd);
+  size_t tb5 = 0;
+  SW_HIP_TRY(hipcub::DeviceRadixSort::SortPairs(nullptr, tb5, d_keys, d_keys2, d_ridx, d_order, (int)nd, 0, 64, st));
+  void* d_tmp5;
+  SW_HIP_TRY(b.get(&d_tmp5, tb5));
+  SW_HIP_TRY(hipcub::DeviceRadixSort::SortPairs(d_tmp5, tb5, d_keys, d_keys2, d_ridx, d_order, (int)nd, 0, 64, st));
+  // histogram, lengths, counts; then the offsets
+  unsigned long long* d_hist;
+  int64_t* d_len64;
+  SW_HIP_TRY(b.get(&d_hist, 256 * sizeof(unsigned long long)));
+  SW_HIP_TRY(b.get(&d_len64, sizeof(int64_t) * (size_t)std::max<int64_t>(nd, 1) + sizeof(int64_t)));
+  free_corpus(t);
+  SW_HIP_TRY(hipMalloc(&t->d_woff0, sizeof(int64_t) * (size_t)std::max<int64_t>(nd + 1, 1)));
+  SW_HIP_TRY(hipMalloc(&t->d_len0, sizeof(int32_t) * (size_t)std::max<int64_t>(nd, 1)));
+  SW_HIP_TRY(hipMalloc(&t->d_wcnt0, sizeof(uint64_t) * (size_t)std::max<int64_t>(nd, 1)));
+  SW_HIP_TRY(hipMemsetAsync(d_hist, 0, 256 * sizeof(unsigned long long), st));
+  SW_HIP_TRY(hipMemsetAsync(d_len64 + nd, 0, sizeof(int64_t), st));
+  hipLaunchKernelGGL(k_word_hist, dim3(g), dim3(kBlock), 0, st, d_text, d_first, d_wlen, d_wcnt, d_order, nd, d_hist,
+                     d_len64, t->d_len0, t->d_wcnt0);
+  size_t tb6 = 0;
+  SW_HIP_TRY(hipcub::DeviceScan::ExclusiveSum(nullptr, tb6, d_len64, t->d_woff0, (int)(nd + 1), st));
+  void* d_tmp6;
+  SW_HIP_TRY(b.get(&d_tmp6, tb6));
+  SW_HIP_TRY(hipcub::DeviceScan::ExclusiveSum(d_tmp6, tb6, d_len64, t->d_woff0, (int)(nd + 1), st));
+  unsigned long long hist[256];
+  int64_t total = 0;
+  SW_HIP_TRY(hipMemcpyAsync(hist, d_hist, sizeof(hist), hipMemcpyDeviceToHost, st));
+  SW_HIP_TRY(hipMemcpyAsync(&total, t->d_woff0 + nd, sizeof(int64_t), hipMemcpyDeviceToHost, st));
+  SW_HIP_TRY(hipStreamSynchronize(st));
+  uint64_t ch[256];
+  for (int c = 0; c < 256; ++c) ch[c] = hist[c];
+  int32_t map[256];
+  coverage_map(ch, t->cfg, map);
+  int32_t* d_map;
+  SW_HIP_TRY(b.get(&d_map, sizeof(map)));
+  SW_HIP_TRY(hipMemcpyAsync(d_map, map, sizeof(map), hipMemcpyHostToDevice, st));
+  SW_HIP_TRY(hipMalloc(&t->d_ids0, sizeof(int32_t) * (size_t)std::max<int64_t>(total, 1)));
+  hipLaunchKernelGGL(k_word_ids, dim3(g), dim3(kBlock), 0, st, d_text, d_first, d_wlen, d_order, t->d_woff0, nd, d_map,
+                     t->d_ids0);
+  SW_HIP_TRY(hipGetLastError());
+  SW_HIP_TRY(hipStreamSynchronize(st));  // (the temporaries are freed on return)
+  t->nw = nd;
+  t->ns = total;
+  t->host_load = false;
   return SW_OK;
 }
 
@@ -579,10 +1083,36 @@ int32_t collect(sw_trainer* t, std::vector<Slot>* out) {
   return SW_OK;
 }
 
+// the host side of k_collect_step: spin on the step's sequence number in host-coherent memory
+// (no stream synchronisation), then take the records; bounded, so a failed launch is reported
+int32_t wait_step(sw_trainer* t, unsigned long long seq, std::vector<Slot>* out) {
+  volatile unsigned long long* vs = t->h_cnt + 1;
+  const auto t0 = std::chrono::steady_clock::now();
+  for (uint64_t spin = 0; *vs != seq; ++spin) {
+    if ((spin & 0xFFFF) == 0xFFFF) {
+      const hipError_t e = hipStreamQuery(t->st);
+      if (e != hipSuccess && e != hipErrorNotReady)
+        return sw::set_error(SW_ERR_HIP, std::string("sw_trainer_train: merge step: ") + hipGetErrorString(e));
+      if (e == hipSuccess && *vs != seq)
+        return sw::set_error(SW_ERR_HIP, "sw_trainer_train: merge step finished without publishing its records");
+      if (ms_since(t0) > 60000.0) return sw::set_error(SW_ERR_HIP, "sw_trainer_train: merge step timed out");
+    }
+  }
+  std::atomic_thread_fence(std::memory_order_acquire);
+  const int64_t n = (int64_t)((volatile unsigned long long*)t->h_cnt)[0];
+  out->assign(t->h_rec, t->h_rec + std::min(n, kPinnedRecords));
+  if (n > kPinnedRecords) {
+    out->resize((size_t)n);
+    SW_HIP_TRY(hipMemcpy(out->data() + kPinnedRecords, t->d_out + kPinnedRecords, sizeof(Slot) * (n - kPinnedRecords),
+                         hipMemcpyDeviceToHost));
+  }
+  return SW_OK;
+}
+
 int64_t train(sw_trainer* t) {
   using clk = std::chrono::steady_clock;
   const auto t_up = clk::now();
-  const int64_t nw = (int64_t)t->wlen.size(), ns = (int64_t)t->ids.size();
+  const int64_t nw = t->nw, ns = t->ns;
   uint64_t min_freq = t->cfg.min_pair_freq ? t->cfg.min_pair_freq : 2000;  // MIN_PAIR_FREQ (bpe.cpp:128-130)
   free_device(t);
   // tables: room for twice the distinct pairs a pass can touch (<= symbols; a merge's changes
@@ -605,13 +1135,21 @@ int64_t train(sw_trainer* t) {
   SW_HIP_TRY(hipHostMalloc(&t->h_out, sizeof(Slot) * kPinnedRecords, hipHostMallocMapped));
   SW_HIP_TRY(hipHostMalloc(&t->h_nused, sizeof(unsigned long long), hipHostMallocMapped));
   SW_HIP_TRY(hipHostGetDevicePointer((void**)&t->h_out_dev, t->h_out, 0));
+  SW_HIP_TRY(hipMalloc(&t->d_step_used, sizeof(unsigned long long)));
+  SW_HIP_TRY(hipMemsetAsync(t->d_step_used, 0, sizeof(unsigned long long), t->st));
+  SW_HIP_TRY(hipHostMalloc(&t->h_rec, sizeof(Slot) * kPinnedRecords, hipHostMallocMapped | hipHostMallocCoherent));
+  SW_HIP_TRY(hipHostMalloc(&t->h_cnt, 4 * sizeof(unsigned long long), hipHostMallocMapped | hipHostMallocCoherent));
+  for (int k = 0; k < 4; ++k) t->h_cnt[k] = 0;
+  SW_HIP_TRY(hipHostGetDevicePointer((void**)&t->h_rec_dev, t->h_rec, 0));
+  SW_HIP_TRY(hipHostGetDevicePointer((void**)&t->h_cnt_dev, t->h_cnt, 0));
   SW_HIP_TRY(hipHostGetDevicePointer((void**)&t->h_nused_dev, t->h_nused, 0));
   t->pass = 0;
-  if (ns) SW_HIP_TRY(hipMemcpyAsync(t->d_ids, t->ids.data(), sizeof(int32_t) * ns, hipMemcpyHostToDevice, t->st));
+  // the working copies of the loaded corpus (training rewrites ids and len in place)
+  if (ns) SW_HIP_TRY(hipMemcpyAsync(t->d_ids, t->d_ids0, sizeof(int32_t) * ns, hipMemcpyDeviceToDevice, t->st));
   if (nw) {
-    SW_HIP_TRY(hipMemcpyAsync(t->d_woff, t->woff.data(), sizeof(int64_t) * nw, hipMemcpyHostToDevice, t->st));
-    SW_HIP_TRY(hipMemcpyAsync(t->d_len, t->wlen.data(), sizeof(int32_t) * nw, hipMemcpyHostToDevice, t->st));
-    SW_HIP_TRY(hipMemcpyAsync(t->d_wcnt, t->wcnt.data(), sizeof(uint64_t) * nw, hipMemcpyHostToDevice, t->st));
+    SW_HIP_TRY(hipMemcpyAsync(t->d_woff, t->d_woff0, sizeof(int64_t) * nw, hipMemcpyDeviceToDevice, t->st));
+    SW_HIP_TRY(hipMemcpyAsync(t->d_len, t->d_len0, sizeof(int32_t) * nw, hipMemcpyDeviceToDevice, t->st));
+    SW_HIP_TRY(hipMemcpyAsync(t->d_wcnt, t->d_wcnt0, sizeof(uint64_t) * nw, hipMemcpyDeviceToDevice, t->st));
   }
   SW_HIP_TRY(hipMemsetAsync(t->d_nused, 0, 2 * sizeof(unsigned long long), t->st));
   hipLaunchKernelGGL(k_init, dim3(2048), dim3(kBlock), 0, t->st, t->d_tab, cap);
@@ -642,6 +1180,62 @@ int64_t train(sw_trainer* t) {
   MaxHeap heap;
   heap.d.reserve(seeds.size() * 2 + 16);
   for (const Seed& s : seeds) heap.push(s.a, s.b, s.freq, 0);
+  // per-pair word lists (k_merge_cand): the loaded corpus's adjacent pairs sorted by pair, their
+  // distinct keys and run lengths on the host; SW_TRAIN_FULL_SCAN=1 keeps every merge on the
+  // word filters of all words instead (A/B, tests)
+  const char* fs_env = std::getenv("SW_TRAIN_FULL_SCAN");
+  bool lists = !(fs_env && fs_env[0] == '1') && ns > nw;
+  std::vector<uint64_t> ukeys;
+  std::vector<int64_t> uoff;
+  std::vector<std::pair<uint64_t, uint64_t>> touched;  // per merge: its rewritten words in the pool
+  const int64_t pool_cap = ns + 64;                    // (every rewrite shortens its word: <= ns in all)
+  if (lists) {
+    const int64_t np = ns - nw;
+    TempBufs b;
+    uint64_t *d_k, *d_k2;
+    uint32_t* d_w;
+    int64_t* d_nrun;
+    SW_HIP_TRY(b.get(&d_k, sizeof(uint64_t) * np));
+    SW_HIP_TRY(b.get(&d_k2, sizeof(uint64_t) * np));
+    SW_HIP_TRY(b.get(&d_w, sizeof(uint32_t) * np));
+    SW_HIP_TRY(hipMalloc(&t->d_pwords, sizeof(uint32_t) * np));
+    hipLaunchKernelGGL(k_pair_words, dim3(grid), dim3(kBlock), 0, t->st, t->d_ids, t->d_woff, t->d_len, nw, d_k, d_w);
+    size_t tb = 0;
+    SW_HIP_TRY(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, d_k, d_k2, d_w, t->d_pwords, (int)np, 0, 64, t->st));
+    void* d_tmp;
+    SW_HIP_TRY(b.get(&d_tmp, tb));
+    SW_HIP_TRY(hipcub::DeviceRadixSort::SortPairs(d_tmp, tb, d_k, d_k2, d_w, t->d_pwords, (int)np, 0, 64, t->st));
+    uint64_t* d_u;
+    int64_t* d_c;
+    SW_HIP_TRY(b.get(&d_u, sizeof(uint64_t) * np));
+    SW_HIP_TRY(b.get(&d_c, sizeof(int64_t) * np));
+    SW_HIP_TRY(b.get(&d_nrun, sizeof(int64_t)));
+    size_t tb2 = 0;
+    SW_HIP_TRY(hipcub::DeviceRunLengthEncode::Encode(nullptr, tb2, d_k2, d_u, d_c, d_nrun, (int)np, t->st));
+    void* d_tmp2;
+    SW_HIP_TRY(b.get(&d_tmp2, tb2));
+    SW_HIP_TRY(hipcub::DeviceRunLengthEncode::Encode(d_tmp2, tb2, d_k2, d_u, d_c, d_nrun, (int)np, t->st));
+    int64_t nrun = 0;
+    SW_HIP_TRY(hipMemcpyAsync(&nrun, d_nrun, sizeof(int64_t), hipMemcpyDeviceToHost, t->st));
+    SW_HIP_TRY(hipStreamSynchronize(t->st));
+    ukeys.resize((size_t)nrun);
+    std::vector<int64_t> cnt((size_t)nrun);
+    SW_HIP_TRY(hipMemcpy(ukeys.data(), d_u, sizeof(uint64_t) * nrun, hipMemcpyDeviceToHost));
+    SW_HIP_TRY(hipMemcpy(cnt.data(), d_c, sizeof(int64_t) * nrun, hipMemcpyDeviceToHost));
+    uoff.resize((size_t)nrun + 1);
+    uoff[0] = 0;
+    for (int64_t k = 0; k < nrun; ++k) uoff[(size_t)k + 1] = uoff[(size_t)k] + cnt[(size_t)k];
+    SW_HIP_TRY(hipMalloc(&t->d_stamp, sizeof(uint32_t) * nw));
+    SW_HIP_TRY(hipMalloc(&t->d_pool, sizeof(uint32_t) * pool_cap));
+    SW_HIP_TRY(hipMalloc(&t->d_pool_n, sizeof(unsigned long long)));
+    SW_HIP_TRY(hipMalloc(&t->d_overflow, sizeof(unsigned int)));
+    SW_HIP_TRY(hipMalloc(&t->d_ticket, sizeof(unsigned int)));
+    SW_HIP_TRY(hipMemsetAsync(t->d_ticket, 0, sizeof(unsigned int), t->st));
+    SW_HIP_TRY(hipMemsetAsync(t->d_stamp, 0, sizeof(uint32_t) * nw, t->st));
+    SW_HIP_TRY(hipMemsetAsync(t->d_pool_n, 0, sizeof(unsigned long long), t->st));
+    SW_HIP_TRY(hipMemsetAsync(t->d_overflow, 0, sizeof(unsigned int), t->st));
+    SW_HIP_TRY(hipStreamSynchronize(t->st));  // (the temporaries are freed on leaving this block)
+  }
   t->stats[2] = ms_since(t_cnt);
 
   // merges (bpe_train / bpe_merge_batch: batch boundaries do not change the result)
@@ -649,26 +1243,96 @@ int64_t train(sw_trainer* t) {
   t->merges.clear();
   double dev_ms = 0, host_ms = 0;
   struct Change { uint32_t bucket; uint64_t first; uint64_t h; int64_t delta; };
-  std::vector<Change> ch;
+  std::vector<Change> ch, ch2;
+  std::vector<uint32_t> bstart(1025), bfill(1024);
   int64_t nm = 0;
+  unsigned long long seq = 0;
+  uint64_t n_pops = 0, n_changes = 0, n_pushes = 0;  // (SW_TRAIN_DEBUG)
+  double launch_ms = 0;
   while (nm < target && !heap.d.empty()) {
     const HeapEntry top = heap.pop();
+    ++n_pops;
     PairInfo& pi = info[pkey(top.a, top.b)];
     if (top.version != pi.version) continue;  // stale
     if (pi.freq < min_freq) continue;
     const int32_t A = top.a, B = top.b, X = (int32_t)(256 + nm);
     const auto t0 = clk::now();
-    hipLaunchKernelGGL(k_merge_words, dim3(grid), dim3(kBlock), 0, t->st, t->d_ids, t->d_woff, t->d_len, t->d_wcnt,
-                       t->d_bloom, nw,
-                       A, B, X, t->d_tab, t->tab_mask, t->d_used, t->d_nused + (t->pass & 1));
-    if (int32_t rc = collect(t, &rec)) return rc;
+    ++seq;
+    if (lists) {  // the candidate words: the initial list of (A, B), the words A's and B's merges rewrote
+      const uint64_t key = pkey(A, B);
+      const auto it = std::lower_bound(ukeys.begin(), ukeys.end(), key);
+      int64_t o0 = 0, n0 = 0, o1 = 0, n1 = 0, o2 = 0, n2 = 0;
+      if (it != ukeys.end() && *it == key) {
+        const size_t k = (size_t)(it - ukeys.begin());
+        o0 = uoff[k];
+        n0 = uoff[k + 1] - uoff[k];
+      }
+      if (A >= 256 && A - 256 < nm) { o1 = (int64_t)touched[(size_t)(A - 256)].first; n1 = (int64_t)touched[(size_t)(A - 256)].second; }
+      if (B >= 256 && B - 256 < nm && B != A) {
+        o2 = (int64_t)touched[(size_t)(B - 256)].first;
+        n2 = (int64_t)touched[(size_t)(B - 256)].second;
+      }
+      const int64_t nc = n0 + n1 + n2;
+      const unsigned g = (unsigned)std::max<int64_t>((nc + kBlock - 1) / kBlock, 1);
+      if (g <= kFuseBlocks) {  // (one launch)
+        hipLaunchKernelGGL(k_merge_cand_fused, dim3(g), dim3(kBlock), 0, t->st, t->d_ids, t->d_woff, t->d_len,
+                           t->d_wcnt, t->d_bloom, t->d_pwords + o0, n0, t->d_pool + o1, n1, t->d_pool + o2, n2,
+                           t->d_stamp, (uint32_t)seq, A, B, X, t->d_tab, t->tab_mask, t->d_used, t->d_step_used,
+                           t->d_pool, t->d_pool_n, (uint64_t)pool_cap, t->d_overflow, t->d_ticket, t->d_out,
+                           t->h_rec_dev, t->h_cnt_dev, t->h_cnt_dev + 1, seq, (uint64_t)kPinnedRecords);
+      } else {
+        hipLaunchKernelGGL(k_merge_cand, dim3(g), dim3(kBlock), 0, t->st, t->d_ids, t->d_woff, t->d_len, t->d_wcnt,
+                           t->d_bloom, t->d_pwords + o0, n0, t->d_pool + o1, n1, t->d_pool + o2, n2, t->d_stamp,
+                           (uint32_t)seq, A, B, X, t->d_tab, t->tab_mask, t->d_used, t->d_step_used, t->d_pool,
+                           t->d_pool_n, (uint64_t)pool_cap, t->d_overflow);
+        hipLaunchKernelGGL(k_collect_step, dim3(1), dim3(1024), 0, t->st, t->d_tab, t->d_used, t->d_step_used,
+                           t->d_out, t->h_rec_dev, t->h_cnt_dev, t->h_cnt_dev + 1, seq, (uint64_t)kPinnedRecords,
+                           t->d_pool_n, t->d_overflow);
+      }
+    } else {
+      hipLaunchKernelGGL(k_merge_words, dim3(grid), dim3(kBlock), 0, t->st, t->d_ids, t->d_woff, t->d_len, t->d_wcnt,
+                         t->d_bloom, nw, A, B, X, t->d_tab, t->tab_mask, t->d_used, t->d_step_used);
+      hipLaunchKernelGGL(k_collect_step, dim3(1), dim3(1024), 0, t->st, t->d_tab, t->d_used, t->d_step_used, t->d_out,
+                         t->h_rec_dev, t->h_cnt_dev, t->h_cnt_dev + 1, seq, (uint64_t)kPinnedRecords, t->d_step_used,
+                         (const unsigned int*)t->d_step_used);  // (full scan: no pool; these two fields unused)
+    }
+    SW_HIP_TRY(hipGetLastError());
+    {
+      const auto t_issued = clk::now();
+      launch_ms += std::chrono::duration<double, std::milli>(t_issued - t0).count();
+      if (int32_t rc = wait_step(t, seq, &rec)) return rc;
+    }
+    if (lists) {
+      const uint64_t pn = ((volatile unsigned long long*)t->h_cnt)[2];
+      const uint64_t before = touched.empty() ? 0 : touched.back().first + touched.back().second;
+      if (((volatile unsigned long long*)t->h_cnt)[3]) lists = false;  // (cannot happen: <= ns rewrites)
+      touched.emplace_back(before, pn - before);
+    }
     const auto t1 = clk::now();
     dev_ms += std::chrono::duration<double, std::milli>(t1 - t0).count();
     // FreqChangeMap order: hash % 1024 ascending, newest first within a bucket
     ch.clear();
-    for (const Slot& s : rec) ch.push_back(Change{(uint32_t)(s.key % 1024u), s.first, s.key, (int64_t)s.val});
-    std::sort(ch.begin(), ch.end(),
-              [](const Change& x, const Change& y) { return x.bucket != y.bucket ? x.bucket < y.bucket : x.first > y.first; });
+    for (const Slot& s : rec) {
+      ch.push_back(Change{(uint32_t)(s.key % 1024u), s.first, s.key, (int64_t)s.val});
+      info.prefetch(pkey((int32_t)(s.key >> 32), (int32_t)(s.key & 0xFFFFFFFFu)));
+    }
+    n_changes += ch.size();
+    if (ch.size() <= 256) {
+      std::sort(ch.begin(), ch.end(),
+                [](const Change& x, const Change& y) { return x.bucket != y.bucket ? x.bucket < y.bucket : x.first > y.first; });
+    } else {  // (many changes: a counting sort by bucket, then each bucket's few by first call)
+      std::fill(bstart.begin(), bstart.end(), 0u);
+      for (const Change& c : ch) bstart[c.bucket + 1]++;
+      for (int q = 0; q < 1024; ++q) bstart[q + 1] += bstart[q];
+      ch2.resize(ch.size());
+      std::copy(bstart.begin(), bstart.begin() + 1024, bfill.begin());
+      for (const Change& c : ch) ch2[bfill[c.bucket]++] = c;
+      for (int q = 0; q < 1024; ++q)
+        if (bstart[q + 1] - bstart[q] > 1)
+          std::sort(ch2.begin() + bstart[q], ch2.begin() + bstart[q + 1],
+                    [](const Change& x, const Change& y) { return x.first > y.first; });
+      ch.swap(ch2);
+    }
     for (const Change& c : ch) {
       const int32_t pa = (int32_t)(c.h >> 32), pb = (int32_t)(c.h & 0xFFFFFFFFu);
       if (pa == A && pb == B) continue;
@@ -682,6 +1346,7 @@ int64_t train(sw_trainer* t) {
       if (q.freq >= min_freq) {
         q.version++;
         heap.push(pa, pb, q.freq, q.version);
+        ++n_pushes;
       }
     }
     PairInfo& done = info[pkey(A, B)];
@@ -693,21 +1358,31 @@ int64_t train(sw_trainer* t) {
     ++nm;
     host_ms += ms_since(t1);
   }
+  if (const char* dbg = std::getenv("SW_TRAIN_DEBUG"); dbg && dbg[0] == '1')
+    std::fprintf(stderr, "sw_trainer: %lld merges, %llu heap pops, %llu change records, %llu heap pushes, heap %zu, "
+                 "launch calls %.1f ms\n", (long long)nm, (unsigned long long)n_pops, (unsigned long long)n_changes,
+                 (unsigned long long)n_pushes, heap.d.size(), launch_ms);
   t->stats[3] = dev_ms;
   t->stats[4] = host_ms;
   t->stats[5] = (double)nm;
   t->stats[6] = (double)nw;
   t->stats[7] = (double)ns;
-  // final token frequencies over the rewritten corpus (bpe_save :703-712; negative ids skipped)
-  std::vector<int32_t> ids((size_t)ns), len((size_t)nw);
-  if (ns) SW_HIP_TRY(hipMemcpy(ids.data(), t->d_ids, sizeof(int32_t) * ns, hipMemcpyDeviceToHost));
-  if (nw) SW_HIP_TRY(hipMemcpy(len.data(), t->d_len, sizeof(int32_t) * nw, hipMemcpyDeviceToHost));
+  // final token frequencies over the rewritten corpus (bpe_save :703-712; negative ids skipped),
+  // on the device
   t->tok_freq.assign((size_t)(256 + nm), 0);
-  for (int64_t w = 0; w < nw; ++w)
-    for (int32_t k = 0; k < len[(size_t)w]; ++k) {
-      const int32_t id = ids[(size_t)(t->woff[(size_t)w] + k)];
-      if (id >= 0 && id < 256 + nm) t->tok_freq[(size_t)id] += t->wcnt[(size_t)w];
-    }
+  unsigned long long* d_freq = nullptr;
+  SW_HIP_TRY(hipMalloc(&d_freq, sizeof(unsigned long long) * (size_t)(256 + nm)));
+  struct FreeOnExit {
+    void* p;
+    ~FreeOnExit() { (void)hipFree(p); }
+  } free_freq{d_freq};
+  SW_HIP_TRY(hipMemsetAsync(d_freq, 0, sizeof(unsigned long long) * (size_t)(256 + nm), t->st));
+  if (nw) hipLaunchKernelGGL(k_tok_freq, dim3(grid), dim3(kBlock), 0, t->st, t->d_ids, t->d_woff, t->d_len, t->d_wcnt,
+                             nw, (int64_t)(256 + nm), d_freq);
+  SW_HIP_TRY(hipGetLastError());
+  SW_HIP_TRY(hipMemcpyAsync(t->tok_freq.data(), d_freq, sizeof(uint64_t) * (size_t)(256 + nm), hipMemcpyDeviceToHost,
+                            t->st));
+  SW_HIP_TRY(hipStreamSynchronize(t->st));
   free_device(t);
   return nm;
 }
@@ -736,14 +1411,23 @@ extern "C" void sw_trainer_destroy(sw_trainer* t) {
   if (!t) return;
   DeviceGuard g(t->device);
   free_device(t);
+  free_corpus(t);
   if (t->st) (void)hipStreamDestroy(t->st);
   delete t;
 }
 
 extern "C" int32_t sw_trainer_load_text(sw_trainer* t, const uint8_t* text, int64_t n) {
   if (!t || n < 0 || (n > 0 && !text)) return sw::set_error(SW_ERR_ARG, "sw_trainer_load_text: bad arguments");
+  DeviceGuard g(t->device);
   const auto t0 = std::chrono::steady_clock::now();
-  const int32_t rc = load_words(t, text, n);
+  t->merges.clear();
+  t->tok_freq.clear();
+  // the device path; the host threads when asked (SW_TRAIN_HOST_LOAD=1, for A/B and tests) or
+  // when two distinct words share a 64-bit hash
+  const char* env = std::getenv("SW_TRAIN_HOST_LOAD");
+  int32_t rc = (env && env[0] == '1') ? 1 : load_words_device(t, text, n);
+  if (rc == 1) rc = load_words(t, text, n);
+  t->loaded = rc == SW_OK;
   t->stats[0] = ms_since(t0);
   return rc;
 }
@@ -753,9 +1437,15 @@ extern "C" int32_t sw_trainer_load_corpus(sw_trainer* t, const char* path) {
   FILE* f = std::fopen(path, "rb");
   if (!f) return sw::set_error(SW_ERR_ARG, std::string("sw_trainer_load_corpus: cannot open ") + path);
   std::vector<uint8_t> buf;
+  if (std::fseek(f, 0, SEEK_END) == 0) {  // (one read of the whole file when its size is known)
+    const long sz = std::ftell(f);
+    if (sz > 0) buf.resize((size_t)sz);
+    std::rewind(f);
+    buf.resize(std::fread(buf.data(), 1, buf.size(), f));
+  }
   uint8_t tmp[1 << 16];
   size_t got;
-  while ((got = std::fread(tmp, 1, sizeof(tmp), f)) > 0) buf.insert(buf.end(), tmp, tmp + got);
+  while ((got = std::fread(tmp, 1, sizeof(tmp), f)) > 0) buf.insert(buf.end(), tmp, tmp + got);  // (pipes)
   std::fclose(f);
   return sw_trainer_load_text(t, buf.data(), (int64_t)buf.size());
 }

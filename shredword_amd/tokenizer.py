@@ -132,6 +132,39 @@ class Tokenizer(BaseTokenizer):
         if d:
             _lib.lib().sw_decoder_destroy(d)
 
+    # ---------------------------------------------------------------- training
+    def train(self, text, vocab_size, verbose=False, min_pair_freq=2, character_coverage=0.9999, unk_id=-1):
+        """Learn `vocab_size - 256` merges from `text` on the GPU (BaseTokenizer.train, abstract in
+        the reference, base.py:107; the trainer is shredword's C++ one, bpe.cpp, restated in
+        csrc/train.hip: words split at ' \\t\\r\\n', bytes below the character coverage mapped to
+        `unk_id`).  The merges replace this tokenizer's (special tokens are kept); merges built on
+        a negative `unk_id` are left out (no byte sequence can produce them).  Returns the number
+        of merges learned, which is smaller when no pair reaches `min_pair_freq` any more."""
+        from .trainer import BPETrainer
+        if vocab_size < 256:
+            raise ValueError("vocab_size must be at least 256 (the byte alphabet)")
+        t = BPETrainer(target_vocab_size=vocab_size, unk_id=unk_id, character_coverage=character_coverage,
+                       min_pair_freq=min_pair_freq, device=self.device)
+        try:
+            t.load_text(text)
+            n = t.train()
+            rows = t.merges
+            freq = t.token_freq if verbose else None
+        finally:
+            t.destroy()
+        made, merges = set(range(256)), {}
+        for a, b, v in rows.tolist():
+            if a in made and b in made:
+                merges[(a, b)] = v
+                made.add(v)
+        self.merges = merges
+        self.vocab = build_vocab(self.merges, self.special_tokens)
+        if verbose:
+            for k, ((a, b), v) in enumerate(merges.items()):
+                print("merge %d/%d: (%d, %d) -> %d (%r) had %d occurrences at the end" % (
+                    k + 1, len(merges), a, b, v, self.vocab[v], int(freq[v]) if v < len(freq) else 0))
+        return n
+
     # ---------------------------------------------------------------- device table
     def _encoder(self):
         key = (id(self._merges), self._merges.version, self.device)

@@ -13,8 +13,15 @@ from test_train_oracle import INDEX, golden, recipe_text
 pytestmark = pytest.mark.gpu
 
 
+@pytest.mark.parametrize("mode", ["default", "host_load", "full_scan"])
 @pytest.mark.parametrize("entry", INDEX, ids=[e["name"] for e in INDEX])
-def test_gpu_trainer_matches_reference(entry):
+def test_gpu_trainer_matches_reference(entry, mode, monkeypatch):
+    """Bit-exact with the reference trainer (merges and final token frequencies): the corpus
+    loaded on the device and every merge over its pair's word lists (the default); loaded by the
+    host threads (SW_TRAIN_HOST_LOAD=1, the path a 64-bit word-hash collision takes); every merge
+    over all words' filters (SW_TRAIN_FULL_SCAN=1)."""
+    monkeypatch.setenv("SW_TRAIN_HOST_LOAD", "1" if mode == "host_load" else "0")
+    monkeypatch.setenv("SW_TRAIN_FULL_SCAN", "1" if mode == "full_scan" else "0")
     text = recipe_text(entry["corpus"])
     target, unk, cov, minf = entry["config"]
     t = sa.BPETrainer(target, unk, cov, minf)
@@ -107,3 +114,30 @@ def test_gpu_trainer_negative_unk_matches_oracle():
     sample = b" ".join(words[:50]).decode()
     assert tok.decode(tok.encode(sample)) == sample
     tok.close()
+
+
+def test_tokenizer_train():
+    """Tokenizer.train (BaseTokenizer.train, abstract in the reference, base.py:107) drives the
+    GPU trainer: the merges are the trainer's (equal to the oracle's), the vocabulary follows,
+    and the trained tokenizer round-trips text, special tokens kept."""
+    rng = np.random.default_rng(5)
+    words = ["".join(rng.choice(list("abcdeé "), size=rng.integers(1, 9))) for _ in range(3000)]
+    text = " ".join(words) + "\n"
+    tok = sa.Tokenizer(device=0)
+    tok.special_tokens = {"<|end|>": 100000}
+    n = tok.train(text, 256 + 120, min_pair_freq=2, character_coverage=0.9999, unk_id=-1)
+    assert 0 < n <= 120 and len(tok.merges) <= n
+    exp_rows, _ = oracle.train(text.encode("utf-8"), 256 + 120, -1, 0.9999, 2)
+    assert n == len(exp_rows)
+    made, exp = set(range(256)), []
+    for a, b, v in exp_rows.tolist():  # (merges built on the negative UNK id left out)
+        if a in made and b in made:
+            exp.append((a, b, v))
+            made.add(v)
+    assert [(a, b, v) for (a, b), v in tok.merges.items()] == exp
+    for (a, b), v in tok.merges.items():
+        assert tok.vocab[v] == tok.vocab[a] + tok.vocab[b]
+    assert tok.special_tokens == {"<|end|>": 100000}
+    s = "abc dé ea<|end|> bad"
+    assert tok.decode(tok.encode(s)) == s
+    assert len(tok.encode("abcde abcde")) < len("abcde abcde".encode("utf-8"))

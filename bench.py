@@ -207,10 +207,12 @@ def main():
     side = torch.cuda.Stream(dev) if gather else None
     done_ev = [None for _ in outs]
     n_step = [0]
+    host_t = {"encode": 0.0, "gathers": 0.0, "reassembly": 0.0}  # (SW_BENCH_HOST_TIMES=1: host time per call)
 
     def step():
         slot = n_step[0] % len(outs)
         n_step[0] += 1
+        h0 = time.perf_counter()
         if done_ev[slot] is not None:
             torch.cuda.current_stream(dev).wait_event(done_ev[slot])
             done_ev[slot] = None
@@ -218,11 +220,15 @@ def main():
         _lib.check(L.sw_encode_device(h, d_buf.data_ptr(), n_bytes, d_off.data_ptr(), n_str,
                                       d_bits.data_ptr() if host_ps else None, o_ids.data_ptr(), o_off.data_ptr(),
                                       stream, None))
+        h1 = time.perf_counter()
+        host_t["encode"] += h1 - h0
         if not gather:
             return
         # steps 1-3: one counts all-gather, padded id and offset all-gathers (RCCL)
         works, res = shard.reassemble(o_ids, o_off, None, dev, concat=False, width=width, width_s=width_s,
                                       id_bits=id_bits, async_op=True)
+        h2 = time.perf_counter()
+        host_t["gathers"] += h2 - h1
         side.wait_stream(torch.cuda.current_stream(dev))
         with torch.cuda.stream(side):  # step 4 once the gathers have landed
             for w in works:
@@ -231,6 +237,7 @@ def main():
             ev = torch.cuda.Event()
             ev.record(side)
         done_ev[slot] = ev
+        host_t["reassembly"] += time.perf_counter() - h2
         if not overlap:
             torch.cuda.current_stream(dev).wait_event(ev)
             done_ev[slot] = None
@@ -248,12 +255,19 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
+    for k in host_t:
+        host_t[k] = 0.0
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
+    t_issued = time.perf_counter()
     finish()
     torch.cuda.synchronize()
     t1 = time.perf_counter()
+    if os.environ.get("SW_BENCH_HOST_TIMES") == "1":
+        sys.stderr.write("host ms per step: %s, all issued after %.3f ms of %.3f\n" % (
+            {k: round(v * 1e3 / args.steps, 3) for k, v in host_t.items()}, (t_issued - t0) * 1e3 / args.steps,
+            (t1 - t0) * 1e3 / args.steps))
     if world > 1:
         dist.barrier()
     k_ms = L.sw_encoder_last_kernel_ms(h)

@@ -82,7 +82,7 @@ def reassemble(local_ids, local_off, group=None, device=None, concat=True, width
     dev = device if device is not None else local_ids.device
     mine = torch.empty(2, dtype=torch.int64, device=dev)
     mine[0:1] = local_off[-1:].to(device=dev, dtype=torch.int64)
-    mine[1] = local_off.numel() - 1
+    mine[1:2].fill_(local_off.numel() - 1)  # (a fill kernel: `mine[1] = n` copies from pageable host memory, synchronously)
     both = torch.empty(2 * world, dtype=torch.int64, device=dev)
     gather(both, mine)  # [count_0, n_str_0, count_1, ...]
     counts, n_strs = both[0::2], both[1::2]

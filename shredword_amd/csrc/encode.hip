@@ -125,7 +125,7 @@ struct sw_encoder {
   int64_t* d_boff = nullptr;          // its exclusive scan
   int64_t* d_qtotal = nullptr;
   unsigned long long* d_stamps = nullptr;  // SW_STAMPS builds
-  uint64_t* d_dtab = nullptr;         // chunk dedupe table
+  uint64_t* d_dtab = nullptr;         // chunk dedupe table (two words per entry)
   uint32_t dmask = 0;
   uint4* d_dres = nullptr;            // dense result heads, one per table entry
   uint8_t* d_dcnt = nullptr;          // their id counts (<= 32), one byte per table entry
@@ -232,7 +232,7 @@ int32_t ensure_workspace(sw_encoder* h, int64_t n_bytes) {
      // result head per entry
     int64_t slots = 64;
     while (slots < nb / 64 && slots < (1LL << 22)) slots <<= 1;
-    HIP_TRY(hipMalloc(&h->d_dtab, sizeof(uint64_t) * slots));
+    HIP_TRY(hipMalloc(&h->d_dtab, 2 * sizeof(uint64_t) * slots));  // (16-byte entries)
     HIP_TRY(hipMalloc(&h->d_dres, sizeof(uint4) * slots));
     HIP_TRY(hipMalloc(&h->d_dcnt, slots));
     h->dmask = (uint32_t)(slots - 1);
@@ -712,7 +712,7 @@ int32_t encode_device(sw_encoder* h, const uint8_t* d_bytes, int64_t n_bytes, co
     a.inv = h->d_inv; a.n_inv = h->n_inv; a.ids16 = h->ids16 ? 1u : 0u;
     a.lstart = h->lp.wstart; a.llen = h->lp.wlen; a.n_long = &h->lp.ctl[kLcWave]; a.lcap = h->lp.lcap;
     const bool split = h->split_ok && h->long_split;  // (split + verify needs a well-formed table)
-    if (h->dedupe) HIP_TRY(hipMemsetAsync(h->d_dtab, 0, sizeof(uint64_t) * ((size_t)a.dmask + 1), st));
+    if (h->dedupe) HIP_TRY(hipMemsetAsync(h->d_dtab, 0, 2 * sizeof(uint64_t) * ((size_t)a.dmask + 1), st));
     hipLaunchKernelGGL(k_classify, dim3((unsigned)((n_tiles + kWaves - 1) / kWaves)), dim3(kThreads), 0, st, a);
     HIP_TRY(hipGetLastError());
     HIP_TRY(launch_scan(st, h->d_bcnt, kNumBuckets * n_tiles, h->d_part, h->d_boff, h->d_qtotal));
@@ -742,6 +742,11 @@ int32_t encode_device(sw_encoder* h, const uint8_t* d_bytes, int64_t n_bytes, co
       hipLaunchKernelGGL((k_merge_bucket<true, false, 16>), pg, pb, 0, ms[1], a, 5, 7);
       hipLaunchKernelGGL((k_merge_bucket<true, false, 8>), pg, pb, 0, ms[2], a, 3, 4);
       hipLaunchKernelGGL((k_merge_bucket<true, false, 4>), pg, pb, 0, ms[1], a, 0, 2);
+    } else if (h->ids16 && h->split_ok) {  // (a well-formed table: the rank-matching loop)
+      hipLaunchKernelGGL((k_merge_bucket<false, true, 32, true>), pg, pb, 0, ms[0], a, 8, 9);
+      hipLaunchKernelGGL((k_merge_bucket<false, true, 16, true>), pg, pb, 0, ms[1], a, 5, 7);
+      hipLaunchKernelGGL((k_merge_bucket<false, true, 8, true>), pg, pb, 0, ms[2], a, 3, 4);
+      hipLaunchKernelGGL((k_merge_bucket<false, true, 4, true>), pg, pb, 0, ms[1], a, 0, 2);
     } else if (h->ids16) {
       hipLaunchKernelGGL((k_merge_bucket<false, true, 32>), pg, pb, 0, ms[0], a, 8, 9);
       hipLaunchKernelGGL((k_merge_bucket<false, true, 16>), pg, pb, 0, ms[1], a, 5, 7);

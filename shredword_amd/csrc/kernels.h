@@ -64,7 +64,8 @@ __host__ __device__ inline uint32_t slot_did(int32_t v) { return (uint32_t)(-(in
 // need no second read.  A reference list entry (rlist) is p or kRlDense | d.
 constexpr uint32_t kRlDense = 0x80000000u;
 constexpr uint32_t kNoDid = 0x7FFFFFFu;    // (27-bit dense result field of a queue entry: none)
-constexpr int kDdExactMax = 7;             // dedupe keys of <= this many bytes are exact (no verification)
+constexpr int kDdExactMax = 14;            // dedupe keys of <= this many bytes are exact (no verification)
+constexpr int kDdExactW0 = 7;              // ... of which this many fit the entry's first word
 
 // streaming accesses (read or written once per launch) carry the non-temporal hint, so the
 // caches keep the randomly gathered merge results instead
@@ -366,7 +367,85 @@ __device__ __forceinline__ uint32_t lane_merge_reg_loop(const DevTable& t, uint3
   return alive;
 }
 
-template <bool kWide, bool k16, int N>
+// The same loop for a WELL-FORMED table with 16-bit ids (every trained table; SW_INFO_SPLIT):
+// a value names exactly one pair, so the winning pair's occurrences are the alive slots whose
+// rank equals it (no id compares, no fetch of the pair's ids), and the ranks are kept as
+// min-ready keys rank << 5 | slot (rank 0xFFFF: no pair -- a dead slot or the last one), so a
+// step's argmin is one min per slot.  About a quarter fewer VALU instructions per step.
+template <bool kWide, int N>
+__device__ __forceinline__ uint32_t lane_merge_reg_loop_wf(const DevTable& t, uint32_t (&id)[N], uint32_t (&rk)[N], int n,
+                                                           int* iters = nullptr) {
+  constexpr uint32_t NONE = 0xFFFFFFFFu;  // no right neighbour
+  constexpr uint32_t KINF = 0xFFFFu << 5;
+  uint32_t rid[N];
+#pragma unroll
+  for (int k = 0; k < N; ++k) {
+    rid[k] = (k + 1 < n) ? id[(k + 1) % N] : NONE;
+    rk[k] = ((k + 1 < n) ? (min(rk[k], 0xFFFFu) << 5) : KINF) | (uint32_t)k;
+  }
+  uint32_t alive = (n >= 32) ? 0xFFFFFFFFu : ((1u << n) - 1u);
+  int it = 0;
+  while (true) {
+    uint32_t best = 0xFFFFFFFFu;
+#pragma unroll
+    for (int k = 0; k < N; ++k) best = min(best, rk[k]);
+    const uint32_t nv = best >> 5;
+    if (nv >= 0xFFFFu) break;
+    ++it;
+    // left-to-right: every non-overlapping occurrence of the winning pair (base.py:29-35)
+    bool took = false;
+    uint32_t changed = 0;
+#pragma unroll
+    for (int k = 0; k < N; ++k) {
+      const bool al = (alive >> k) & 1u;
+      const bool consume = al && took;
+      const bool match = al && !took && (rk[k] >> 5) == nv;
+      alive = consume ? (alive & ~(1u << k)) : alive;
+      id[k] = match ? nv : id[k];
+      changed |= match ? (1u << k) : 0u;
+      took = al ? match : took;
+    }
+    // right-to-left: new right neighbours; dead slots and the last alive one get no pair; pairs
+    // touching a new token need a new rank
+    uint32_t carry = NONE, need = 0;
+    bool carry_chg = false;
+#pragma unroll
+    for (int k = N - 1; k >= 0; --k) {
+      const bool al = (alive >> k) & 1u;
+      const bool chg = (changed >> k) & 1u;
+      rid[k] = al ? carry : rid[k];
+      need |= (al && carry != NONE && (chg || carry_chg)) ? (1u << k) : 0u;
+      rk[k] = (!al || carry == NONE) ? (KINF | (uint32_t)k) : rk[k];
+      carry = al ? id[k] : carry;
+      carry_chg = al ? chg : carry_chg;
+    }
+    while (need) {  // two lookups in flight per round
+      const int j1 = __ffs(need) - 1;
+      need &= need - 1;
+      const int j2 = need ? __ffs(need) - 1 : j1;
+      need &= need - 1;
+      uint32_t a1 = 0, b1 = 0, a2 = 0, b2 = 0;
+#pragma unroll
+      for (int k = 0; k < N; ++k) {
+        a1 = (k == j1) ? id[k] : a1;
+        b1 = (k == j1) ? rid[k] : b1;
+        a2 = (k == j2) ? id[k] : a2;
+        b2 = (k == j2) ? rid[k] : b2;
+      }
+      const uint32_t k1 = (min(lookup<kWide>(t, a1, b1), 0xFFFFu) << 5) | (uint32_t)j1;
+      const uint32_t k2 = (min(lookup<kWide>(t, a2, b2), 0xFFFFu) << 5) | (uint32_t)j2;
+#pragma unroll
+      for (int k = 0; k < N; ++k) {
+        rk[k] = (k == j1) ? k1 : rk[k];
+        rk[k] = (k == j2) ? k2 : rk[k];
+      }
+    }
+  }
+  if (iters) *iters = it;
+  return alive;
+}
+
+template <bool kWide, bool k16, int N, bool kWF = false>
 __device__ __forceinline__ uint32_t lane_merge_reg(const DevTable& t, uint32_t (&id)[N], int n, int* iters = nullptr) {
   uint32_t rk[N];
   // initial ranks: four lookups in flight at a time (sched barriers cap the live registers)
@@ -378,7 +457,8 @@ __device__ __forceinline__ uint32_t lane_merge_reg(const DevTable& t, uint32_t (
     for (int k = g; k < g + 4 && k < N; ++k) rk[k] = (k + 1 < n) ? rk[k] : kInf;
     __builtin_amdgcn_sched_barrier(0);
   }
-  return lane_merge_reg_loop<kWide, k16, N>(t, id, rk, n, iters);
+  if constexpr (kWF && k16 && !kWide) return lane_merge_reg_loop_wf<kWide, N>(t, id, rk, n, iters);
+  else return lane_merge_reg_loop<kWide, k16, N>(t, id, rk, n, iters);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -478,7 +558,7 @@ struct EncArgs {
   const int64_t* boff;       // [kNumBuckets * n_tiles] exclusive scan of bcnt (bucket-major)
   const int64_t* q_total;    // queued chunks in all
   uint64_t* queue;           // dense merge queue, bucket-major: start << 33 | len << 27 | dense result
-  uint64_t* dtab;            // chunk dedupe table (dedupe_claim), dmask + 1 entries
+  uint64_t* dtab;            // chunk dedupe table (dedupe_claim), dmask + 1 entries of two words
   uint32_t dmask;
   uint32_t dfp_mask;         // fingerprint bits in use (all 26 except in collision tests)
   uint32_t dedupe;           // 0: every queued chunk runs its own merge loop
@@ -531,9 +611,11 @@ __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t x, int lane) {
 // Batch-wide dedupe of queued chunks (in k_classify).  Real text repeats its multi-token words
 // endlessly, and a chunk's encoding depends on its bytes alone, so the merge loop needs to run
 // once per DISTINCT chunk of the launch.  The table (cleared before every launch) holds one
-// word per claimed chunk, 8 candidates per chunk in one 64-byte line:
-//   exact keys, chunks of <= 7 bytes:  bytes | length << 56 | 1 << 63
-//   longer chunks:                     26-bit fingerprint << 37 | length << 31 | position
+// 16-byte entry per claimed chunk, 8 candidates per chunk in one 128-byte line; the first word
+// is claimed with a CAS:
+//   exact keys, chunks of <= 14 bytes:  bytes 0..6 | length << 56 | 1 << 63, and for 8..14 bytes
+//                                       a second word bytes 7..13 | 1 << 63 (stored after the claim)
+//   longer chunks:                      26-bit fingerprint << 37 | length << 31 | position
 // The first occurrence claims an entry with a CAS and is merged; its result head lands in
 // dres at the entry's index, which every later occurrence refers to (slot_dref): nothing has to
 // be read back from the claimant.  Exact keys decide equality by themselves; a fingerprint match
@@ -560,22 +642,36 @@ __device__ __forceinline__ DdOut dedupe_claim(const EncArgs& a, const uint32_t* 
   }
   const uint32_t h2 = (h ^ (h >> 16)) * 0x7FEB352Du;
   const bool exact = n <= (int)a.dexact;
-  const uint64_t tag = exact ? ((uint64_t)u[0] | ((uint64_t)u[1] << 32) | ((uint64_t)n << 56) | kDdExact)
+  const bool ex2 = exact && n > kDdExactW0;  // (the key's bytes 7.. live in the entry's second word)
+  const uint64_t tag = exact ? ((uint64_t)u[0] | ((uint64_t)(u[1] & 0xFFFFFFu) << 32) | ((uint64_t)n << 56) | kDdExact)
                              : ((uint64_t)((h2 >> 6) & a.dfp_mask & 0x3FFFFFFu) << 37 | (uint64_t)n << 31);
   const uint64_t mine = exact ? tag : (tag | (uint64_t)start);
+  // bytes 7..13 and a marker bit (a written second word is never 0)
+  const uint64_t mine1 = ((uint64_t)(u[1] >> 24) | ((uint64_t)u[2] << 8) | ((uint64_t)(u[3] & 0xFFFFu) << 40)) | kDdExact;
   const uint32_t grp = h & a.dmask & ~7u;
   for (int j = 0; j < 8; ++j) {
     const uint32_t idx = grp | ((h2 + j) & 7u);
-    unsigned long long* p = (unsigned long long*)a.dtab + idx;
-    // an entry changes once (0 -> final), so a cached plain load is safe: a stale 0 only sends
-    // this lane to the CAS, which returns the live value
-    uint64_t cur = *p;
+    unsigned long long* p = (unsigned long long*)a.dtab + 2 * (int64_t)idx;
+    // an entry's words change once each (0 -> final), so a cached plain load is safe: a stale 0
+    // first word only sends this lane to the CAS, which returns the live value; a stale 0 second
+    // word is re-read with an atomic (the live value), and one still 0 (its claimant has not
+    // stored it yet) counts as a different key -- this chunk then takes another entry or merges
+    // on its own, neither of which can change a result
+    const u32x4 q = *(const u32x4*)p;
+    uint64_t cur = (uint64_t)q[0] | ((uint64_t)q[1] << 32);
     if (cur == 0) {
       cur = atomicCAS(p, 0ULL, (unsigned long long)mine);
-      if (cur == 0) return DdOut{1, idx};  // claimed: this chunk is merged and shared
+      if (cur == 0) {  // claimed: this chunk is merged and shared
+        if (ex2) __hip_atomic_store(p + 1, (unsigned long long)mine1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        return DdOut{1, idx};
+      }
     }
     if (exact) {
-      if (cur == mine) return DdOut{2, idx};
+      if (cur != mine) continue;
+      if (!ex2) return DdOut{2, idx};
+      uint64_t w1 = (uint64_t)q[2] | ((uint64_t)q[3] << 32);
+      if (w1 == 0) w1 = __hip_atomic_fetch_or(p + 1, 0ULL, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (w1 == mine1) return DdOut{2, idx};
       continue;
     }
     if ((cur & ~0x7FFFFFFFULL) != tag) continue;
@@ -934,7 +1030,7 @@ __device__ __forceinline__ void chunk_words(const uint32_t* words, int64_t last_
 }
 
 // merge loop for the queue entry e of this lane (act); result at res[2 * start ..)
-template <bool kWide, bool k16, int N>
+template <bool kWide, bool k16, int N, bool kWF>
 __device__ __forceinline__ void merge_entry(const EncArgs& a, const uint32_t* words, int64_t last_word, int64_t mis,
                                             uint64_t e, bool act) {
   const int64_t start = (int64_t)(e >> 33);
@@ -947,7 +1043,7 @@ __device__ __forceinline__ void merge_entry(const EncArgs& a, const uint32_t* wo
   for (int q = 0; q < N / 4; ++q)
 #pragma unroll
     for (int r = 0; r < 4; ++r) id[4 * q + r] = (u[q] >> (8 * r)) & 0xFFu;
-  const uint32_t alive = lane_merge_reg<kWide, k16, N>(a.table, id, n);
+  const uint32_t alive = lane_merge_reg<kWide, k16, N, kWF>(a.table, id, n);
   if (!act) return;
   uint32_t* dst = a.res + 2 * start;
   int m = 0;
@@ -982,7 +1078,7 @@ __device__ __forceinline__ void merge_entry(const EncArgs& a, const uint32_t* wo
 // k_merge_bucket<N>: queued chunks of buckets [b_lo, b_hi] (length <= N), one per lane;
 // persistent grid-stride over 64-entry batches of the bucket-major queue
 // ---------------------------------------------------------------------------------------
-template <bool kWide, bool k16, int N>
+template <bool kWide, bool k16, int N, bool kWF = false>  // kWF: a well-formed table (lane_merge_reg_loop_wf)
 __global__ void __launch_bounds__(kThreads) k_merge_bucket(EncArgs a, int b_lo, int b_hi) {
   SW_STAMP_INIT;
   const int64_t gw = ((int64_t)blockIdx.x * kThreads + threadIdx.x) >> 6;  // global wave id
@@ -995,7 +1091,7 @@ __global__ void __launch_bounds__(kThreads) k_merge_bucket(EncArgs a, int b_lo, 
   const int64_t last_word = (mis + a.n_bytes - 1) >> 2;  // last word holding input bytes
   for (int64_t base = lo + gw * 64; base < hi; base += n_waves * 64) {
     const int64_t i = base + lane;
-    merge_entry<kWide, k16, N>(a, words, last_word, mis, i < hi ? a.queue[i] : 0, i < hi);
+    merge_entry<kWide, k16, N, kWF>(a, words, last_word, mis, i < hi ? a.queue[i] : 0, i < hi);
   }
 #ifdef SW_STAMPS
   SW_STAMP(N >= 16 ? 5 : 4);
@@ -1588,8 +1684,32 @@ __device__ __forceinline__ uint32_t ref_count(const EncArgs& a, uint32_t r) {
   return dn ? c8 : c32;
 }
 
+// Staged result heads: k_tile_count gathers the head of each of a tile's first kHeadCap
+// references (in reference-list order, which is the order of the tile's reference slots) into
+// the unused upper half of the tile's reference-list region (a tile has at most kTile / 2
+// references, and kHeadCap 16-byte heads fill the other kTile / 2 words), so k_compact reads
+// them as one coalesced run loaded beside its slots instead of gathering them after the slots
+// arrive: one dependent round trip less per tile, and each head is gathered once, not twice
+constexpr int kHeadCap = kTile / 2 * 4 / 16;  // 256
+static_assert(kTile / 2 * 4 >= kHeadCap * 16, "staged heads fit the reference list's upper half");
+__device__ __forceinline__ uint4* tile_heads(const EncArgs& a, int64_t t) {
+  return (uint4*)(a.rlist + t * kTile + kTile / 2);
+}
+// the head of a reference-list entry (dense result or the position of a merged chunk) and its
+// id count
+__device__ __forceinline__ uint4 rl_head(const EncArgs& a, uint32_t r) {
+  const bool dn = (r & kRlDense) != 0;
+  const uint32_t* src = dn ? (const uint32_t*)(a.dres + (r & ~kRlDense)) : a.res + 2 * (int64_t)r;
+  uint4 q;
+  __builtin_memcpy(&q, src, sizeof(q));
+  return q;
+}
+__device__ __forceinline__ uint32_t rl_head_count(const EncArgs& a, uint32_t r, uint4 q) {
+  return ((r & kRlDense) != 0 && a.ids16) ? (q.x & 0xFFFFu) : q.x;
+}
+
 // k_tile_count: kTcTiles tiles per wave, their first 64 list entries and sizes loaded together,
-// then their counts: one dependent round trip serves kTcTiles tiles (a tile holds ~58
+// then their heads: one dependent round trip serves kTcTiles tiles (a tile holds ~58
 // references on prose, so one wave per tile spent most of its life waiting)
 constexpr int kTcTiles = 2;
 __global__ void __launch_bounds__(kThreads) k_tile_count(EncArgs a) {
@@ -1605,13 +1725,26 @@ __global__ void __launch_bounds__(kThreads) k_tile_count(EncArgs a) {
     C[k] = (int)a.tile_slots[t];
     nr[k] = (int)a.tile_nref[t];
   }
+  uint4 q0[kTcTiles];
 #pragma unroll
-  for (int k = 0; k < kTcTiles; ++k) c[k] = lane < nr[k] ? ref_count(a, p0[k]) : 0u;
+  for (int k = 0; k < kTcTiles; ++k) q0[k] = lane < nr[k] ? rl_head(a, p0[k]) : make_uint4(0, 0, 0, 0);
+#pragma unroll
+  for (int k = 0; k < kTcTiles; ++k) {
+    c[k] = lane < nr[k] ? rl_head_count(a, p0[k], q0[k]) : 0u;
+    if (tb + k < a.n_tiles && lane < nr[k]) tile_heads(a, tb + k)[lane] = q0[k];
+  }
 #pragma unroll
   for (int k = 0; k < kTcTiles; ++k) {
     const uint32_t* rl = a.rlist + min(tb + k, a.n_tiles - 1) * kTile;
-    for (int i0 = 64; i0 < nr[k]; i0 += 64)  // (long lists: the rest a round at a time)
-      if (i0 + lane < nr[k]) c[k] += ref_count(a, SW_LDNT2(&rl[i0 + lane]));
+    for (int i0 = 64; i0 < nr[k]; i0 += 64) {  // (long lists: the rest a round at a time)
+      const int i = i0 + lane;
+      if (i < nr[k]) {
+        const uint32_t r = SW_LDNT2(&rl[i]);
+        const uint4 q = rl_head(a, r);
+        c[k] += rl_head_count(a, r, q);
+        if (i < kHeadCap && tb + k < a.n_tiles) tile_heads(a, tb + k)[i] = q;
+      }
+    }
   }
 #pragma unroll
   for (int k = 0; k < kTcTiles; ++k) {
@@ -1653,27 +1786,39 @@ __device__ __forceinline__ void compact_tile(const EncArgs& a, int64_t t, int64_
   const int sj = has_s ? (int)s_cj : -1;
   const bool many = s_hi - s_lo > 64;  // rare: slot offsets go through scratch instead
   uint32_t s_off = 0, carry = 0;
+  // the first group's slots and the tile's first kRefCap staged heads (k_tile_count) load beside
+  // the tile's slot count: nothing waits for C or for the slots before the heads are asked for
+  int32_t v0[R];
+#pragma unroll
+  for (int u = 0; u < R; ++u) v0[u] = SW_LDNT(&src[(u << 6) + lane]);
+  const uint4* heads = tile_heads(a, t);
+  uint4 hq[kRefCap / 64];
+#pragma unroll
+  for (int k = 0; k < kRefCap / 64; ++k) {
+    const u32x4 x = SW_LDNT((const u32x4*)&heads[64 * k + lane]);
+    hq[k] = make_uint4(x[0], x[1], x[2], x[3]);
+  }
+#pragma unroll
+  for (int k = 0; k < kRefCap / 64; ++k) s_rq[64 * k + lane] = hq[k];
+  (void)s_rp;
 #ifdef SW_STAMPS
   if (sj == -12345) s_off = 1;  // (forces the string loads to land here in stamp builds)
   SW_STAMP(8);
 #endif
+  uint32_t gref = 0;  // wave-uniform: references of the tile before this group
   for (int r0 = 0; r0 * 64 < C; r0 += R) {
     int32_t v[R];
 #pragma unroll
-    for (int u = 0; u < R; ++u) v[u] = SW_LDNT(&src[min(((r0 + u) << 6) + lane, kTile - 1)]);
-    // dense list of the group's references (their index in the list per round and lane)
+    for (int u = 0; u < R; ++u) v[u] = r0 == 0 ? v0[u] : SW_LDNT(&src[min(((r0 + u) << 6) + lane, kTile - 1)]);
+    // each reference's index in the tile's reference list (= the staged heads' order)
     uint32_t ridx[R];
-    int nref = 0;  // wave-uniform
 #pragma unroll
     for (int u = 0; u < R; ++u) {
       const bool ref = ((r0 + u) << 6) + lane < C && v[u] < 0;
       const uint64_t mk = __ballot(ref);
-      ridx[u] = (uint32_t)(nref + __popcll(mk & lt_mask));
-      if (ref && ridx[u] < (uint32_t)kRefCap) s_rp[ridx[u]] = (uint32_t)v[u];
-      nref += __popcll(mk);
+      ridx[u] = gref + (uint32_t)__popcll(mk & lt_mask);
+      gref += (uint32_t)__popcll(mk);
     }
-    wave_sync_mem();
-    for (int i = lane; i < min(nref, kRefCap); i += 64) s_rq[i] = ref_head(a, (int32_t)s_rp[i]);
     wave_sync_mem();
     SW_STAMP(9);
     const uint32_t gbase = carry;  // the group's first id, tile-relative
@@ -1685,7 +1830,9 @@ __device__ __forceinline__ void compact_tile(const EncArgs& a, int64_t t, int64_
       const bool valid = j < C;
       const bool ref = valid && v[u] < 0;
       uint4 q = make_uint4(0, 0, 0, 0);
-      if (ref) q = ridx[u] < (uint32_t)kRefCap ? s_rq[ridx[u]] : ref_head(a, v[u]);
+      if (ref) {  // staged heads: the first kRefCap from LDS, then straight from the staging area
+        q = ridx[u] < (uint32_t)kRefCap ? s_rq[ridx[u]] : ridx[u] < (uint32_t)kHeadCap ? heads[ridx[u]] : ref_head(a, v[u]);
+      }
       const bool dense = ref && slot_is_dref(v[u]);
       const bool d16 = dense && a.ids16 != 0;
       const uint32_t m = ref ? (dense ? (q.x & 0xFFFFu) : q.x) : (valid ? 1u : 0u);

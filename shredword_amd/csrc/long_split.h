@@ -242,7 +242,7 @@ __global__ void __launch_bounds__(kThreads) k_lp_encode(EncArgs a, LongArgs L) {
     for (int q = 0; q < kPieceN / 4; ++q)
 #pragma unroll
       for (int r = 0; r < 4; ++r) id[4 * q + r] = (u[q] >> (8 * r)) & 0xFFu;
-    const uint32_t alive = lane_merge_reg<kWide, k16, kPieceN>(a.table, id, n);
+    const uint32_t alive = lane_merge_reg<kWide, k16, kPieceN, true>(a.table, id, n);
     uint32_t first = 0, last = 0;
     int m = 0;
 #pragma unroll
@@ -379,7 +379,7 @@ __global__ void __launch_bounds__(kThreads) k_lp_windows(EncArgs a, LongArgs L, 
     for (int q = 0; q < kShort / 4; ++q)
 #pragma unroll
       for (int b = 0; b < 4; ++b) id[4 * q + b] = (u[q] >> (8 * b)) & 0xFFu;
-    const uint32_t alive = lane_merge_reg<kWide, k16, kShort>(a.table, id, act ? n : 0);
+    const uint32_t alive = lane_merge_reg<kWide, k16, kShort, true>(a.table, id, act ? n : 0);
     if (!act) continue;
     uint32_t m = 0;
 #pragma unroll

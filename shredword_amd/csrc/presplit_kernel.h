@@ -129,6 +129,11 @@ __global__ void __launch_bounds__(kPbThreads, 4) k_presplit_bits(PbArgs g, int p
   const int64_t b0 = (int64_t)blockIdx.x * kPbBlock, c0 = b0 / psb::kChunk;
   const int64_t n_chunks = (g.n_bytes + psb::kChunk - 1) / psb::kChunk;
   const bool cl = pattern == 0;
+  // this thread's 40 bytes are asked for first: they arrive while the string starts below are
+  // looked up and staged (otherwise step 1 would issue them only after that round trip)
+  psb::RegBytes by;
+  const int64_t cm = c0 + tid;
+  if (pattern != 2 && cm < n_chunks) pb_load40(g, 32 * cm, by.w);
   // 0. string starts of [b0 - kPbPre, b0 + kPbBlock + 64) (the batch end is str_off[n_str])
   for (int i = tid; i < kPbSsWords; i += kPbThreads) s_ss[i] = 0;
   __syncthreads();
@@ -155,11 +160,9 @@ __global__ void __launch_bounds__(kPbThreads, 4) k_presplit_bits(PbArgs g, int p
   // 1. class masks of the block's chunks c0 .. c0 + 255 (40 bytes each straight from global
   //    memory: staging the block through LDS measured slower)
   {
-    const int64_t c = c0 + tid;
+    const int64_t c = cm;
     psb::Masks m{};
     if (c < n_chunks) {
-      psb::RegBytes by;
-      pb_load40(g, 32 * c, by.w);
       const uint64_t s = (uint64_t)src.ss_at(32 * c - 4) | ((uint64_t)(src.ss_at(32 * c + 28) & 0xFFu) << 32);
       m = psb::classify(by, s, UcdClass{}, cl);
     }

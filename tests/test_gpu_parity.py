@@ -271,13 +271,14 @@ def test_dedupe_table_pressure_and_collisions(slots, fp_bits, exact):
 
 
 def test_dedupe_exact_key_prefix_collisions():
-    """Chunks equal in their first 7 bytes and length but not after (exact keys up to 7 bytes,
-    fingerprint keys beyond) must stay apart, each sharing only its own result, in a one-group
-    table where they all meet."""
+    """Chunks equal in their first 7 (or 14) bytes and length but not after (exact keys up to 14
+    bytes, the first 7 in the entry's claimed word and the rest in its second word; fingerprint
+    keys beyond) must stay apart, each sharing only its own result, in a one-group table where
+    they all meet."""
     rng = np.random.default_rng(11)
-    stems = [" abcdefg", " qwertyu", " zxcvbnm"]
+    stems = [" abcdefg", " qwertyu", " zxcvbnm", " abcdefghijklm", " abcdefghijklz"]
     words = [st + "".join(chr(0x61 + int(c)) for c in rng.integers(0, 26, size=k))
-             for st in stems for k in (0, 1, 2, 3, 4) for _ in range(6)]
+             for st in stems for k in (0, 1, 2, 3, 4, 7) for _ in range(6)]
     texts = ["".join(rng.choice(words, size=40)) for _ in range(300)]
     buf, off = pack([x.encode() for x in texts])
     t = tok_for("bl32k.model")

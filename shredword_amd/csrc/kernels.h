@@ -576,6 +576,7 @@ struct EncArgs {
   uint32_t* big_list;        // long chunks over kLongLds bytes (their index in the long list)
   uint32_t* big_count;       // ... how many (cleared per launch)
   uint32_t ids16;            // every id fits 16 bits (dres layout)
+  uint16_t* tdefer;          // [n_tiles] k_presplit_classify: the deferred last chunk's start in the tile, or 0xFFFF
 };
 
 #ifdef SW_STAMPS
@@ -743,9 +744,15 @@ constexpr int kWinWords = kWin / 4 + 8;
 // function of (tile, base) (compact_tile) the compiler fits 78 VGPRs, 6 waves, no spill: 1.11 ->
 // 0.95 ms (profiles/r2_k.md).
 #define SW_CLS_ATTR __attribute__((amdgpu_waves_per_eu(6, 6)))
-// one tile (the body of k_classify's tile loop)
+// one tile (the body of k_classify's tile loop).  kFused (k_presplit_classify): the tile's
+// chunk-start bits come from the pre-split of its 8 KiB block in LDS (s_bits: the block's 256
+// dwords, this tile's from 64 wv), and the end of the tile's last chunk is known only when the
+// next chunk start lies inside the block: otherwise that chunk is DEFERRED -- its slot and all
+// that follows from it are left to k_classify_deferred, and a.tdefer[tile] holds its start.
+template <bool kFused = false>
 __device__ __forceinline__ void classify_tile(const EncArgs& a, int64_t tile, uint32_t* s_b32, uint16_t* s_cstart,
-                                              uint16_t* s_qbuf) {
+                                              uint16_t* s_qbuf, const uint32_t* s_bits = nullptr, int wv = 0,
+                                              int64_t blk_end = 0) {
   SW_STAMP_INIT;
   const int lane = threadIdx.x & 63;
   const uint64_t lt_mask = (lane == 0) ? 0ULL : (~0ULL >> (64 - lane));
@@ -773,7 +780,13 @@ __device__ __forceinline__ void classify_tile(const EncArgs& a, int64_t tile, ui
     }
   }
   if (lane < 8) s_b32[kWin / 4 + lane] = 0;
-  const uint64_t bw = (lane < kTileWords && w0 + lane < a.n_words) ? SW_LDNT2(&a.bits[w0 + lane]) : 0ULL;
+  uint64_t bw = 0;
+  if constexpr (kFused) {  // word lane of the tile (lane 32: the next tile's first, if in the block)
+    const int q = 64 * wv + 2 * lane;
+    if (lane < kTileWords && q + 1 < kWaves * 64) bw = (uint64_t)s_bits[q] | ((uint64_t)s_bits[q + 1] << 32);
+  } else {
+    bw = (lane < kTileWords && w0 + lane < a.n_words) ? SW_LDNT2(&a.bits[w0 + lane]) : 0ULL;
+  }
   const int64_t s_first = a.tile_slo[tile];  // (prefetched: used by step 6)
 
   // 2. chunk starts in [t0, t1): lane w owns bitmap word w
@@ -813,12 +826,32 @@ __device__ __forceinline__ void classify_tile(const EncArgs& a, int64_t tile, ui
       last_end = min(q, a.n_bytes);
     } else if (C > 0) {
       // (a chunk running past the halo)
-      const int64_t q = next_set_bit(a.bits, a.n_words, t0 + 64 * kTileWords, a.n_bytes);
-      last_end = min(q, a.n_bytes);
+      if constexpr (kFused) {  // the block's later dwords, then: past the block, deferred
+        int64_t q = -1;
+        for (int i0 = 64 * wv + 2 * kTileWords; i0 < kWaves * 64 && q < 0; i0 += 64) {
+          const int i = i0 + lane;
+          const uint32_t x = i < kWaves * 64 ? s_bits[i] : 0u;
+          const uint64_t hm = __ballot(x != 0);
+          if (hm) {
+            const int src = __ffsll((long long)hm) - 1;
+            q = (blk_end - (int64_t)kWaves * kTile) + 32 * (int64_t)(i0 + src) + __ffs(__shfl((int)x, src, 64)) - 1;
+          }
+        }
+        last_end = q >= 0 ? min(q, a.n_bytes) : blk_end < a.n_bytes ? (int64_t)-1 : a.n_bytes;
+      } else {
+        const int64_t q = next_set_bit(a.bits, a.n_words, t0 + 64 * kTileWords, a.n_bytes);
+        last_end = min(q, a.n_bytes);
+      }
     }
   }
-  const int rel_end = (int)(last_end - t0);
   wave_sync_mem();
+  // kFused: a last chunk whose end is past the block is deferred (processed: Cp chunks)
+  const bool defer = kFused && last_end < 0;
+  const int Cp = defer ? C - 1 : C;
+  const int rel_end = defer ? (int)s_cstart[C - 1] : (int)(last_end - t0);
+  if constexpr (kFused) {
+    if (lane == 0) a.tdefer[tile] = defer ? (uint16_t)s_cstart[C - 1] : (uint16_t)0xFFFFu;
+  }
   SW_STAMP(0);
 
   // 3. settle single bytes and whole-chunk-table hits (their slots written here).  The rest
@@ -826,7 +859,7 @@ __device__ __forceinline__ void classify_tile(const EncArgs& a, int64_t tile, ui
   //    point their slot at the first occurrence's result, the others are queued for the merge
   //    kernels and counted per length bucket (lane b: bucket b).
   int32_t* dst = a.scratch + t0;
-  const int rounds = (C + 63) >> 6;
+  const int rounds = (Cp + 63) >> 6;
   const bool use_table = a.chunks.enabled != 0;
   const int64_t mis = (int64_t)((uintptr_t)a.bytes & 3);
   const uint32_t* gwords = (const uint32_t*)((uintptr_t)a.bytes - mis);
@@ -840,21 +873,21 @@ __device__ __forceinline__ void classify_tile(const EncArgs& a, int64_t tile, ui
     if (r0 < rounds) {
       uint32_t tok[kLookRounds];
       if (use_table) {
-        table_lookups<kLookRounds>(a.chunks, s_b32, s_cstart, C, rel_end, r0, lane, tok);
+        table_lookups<kLookRounds>(a.chunks, s_b32, s_cstart, Cp, rel_end, r0, lane, tok);
       } else {
 #pragma unroll
         for (int u = 0; u < kLookRounds; ++u) {  // (no table: single bytes only)
           const int k = ((r0 + u) << 6) + lane;
-          const bool valid = k < C;
+          const bool valid = k < Cp;
           const int ls = valid ? s_cstart[k] : 0;
-          const int end = (k + 1 < C) ? (int)s_cstart[k + 1] : rel_end;
+          const int end = (k + 1 < Cp) ? (int)s_cstart[k + 1] : rel_end;
           tok[u] = (valid && end - ls == 1) ? (s_b32[ls >> 2] >> (8 * (ls & 3))) & 0xFFu : kInf;
         }
       }
 #pragma unroll
       for (int u = 0; u < kLookRounds; ++u) {
         const int k = ((r0 + u) << 6) + lane;
-        const bool valid = k < C;
+        const bool valid = k < Cp;
         const bool queued = valid && tok[u] == kInf;
         if (valid && !queued) SW_STNT(&dst[k], (int32_t)tok[u]);
         const uint64_t mq = __ballot(queued);
@@ -876,7 +909,7 @@ __device__ __forceinline__ void classify_tile(const EncArgs& a, int64_t tile, ui
         if (64 * q + lane < nq) s_qbuf[64 * (q - 1) + lane] = rest[q - 1];
       nq = nq > 64 ? nq - 64 : 0;
       const int ls = act ? s_cstart[k] : 0;
-      const int end = (k + 1 < C) ? (int)s_cstart[k + 1] : rel_end;
+      const int end = (k + 1 < Cp) ? (int)s_cstart[k + 1] : rel_end;
       const int len = act ? end - ls : 0;
       DdOut dd{0, 0};
       if (act && a.dedupe && len <= kShort) {
@@ -1788,28 +1821,27 @@ __device__ __forceinline__ void compact_tile(const EncArgs& a, int64_t t, int64_
   uint32_t s_off = 0, carry = 0;
   // the first group's slots and the tile's first kRefCap staged heads (k_tile_count) load beside
   // the tile's slot count: nothing waits for C or for the slots before the heads are asked for
-  int32_t v0[R];
-#pragma unroll
-  for (int u = 0; u < R; ++u) v0[u] = SW_LDNT(&src[(u << 6) + lane]);
+  // (straight into LDS, no registers held: global_load_lds, lane i's 16 bytes to s_rq[64 k + i])
   const uint4* heads = tile_heads(a, t);
-  uint4 hq[kRefCap / 64];
+  const int nref_t = (int)a.tile_nref[t];  // (only the staged heads in use are read)
 #pragma unroll
-  for (int k = 0; k < kRefCap / 64; ++k) {
-    const u32x4 x = SW_LDNT((const u32x4*)&heads[64 * k + lane]);
-    hq[k] = make_uint4(x[0], x[1], x[2], x[3]);
-  }
-#pragma unroll
-  for (int k = 0; k < kRefCap / 64; ++k) s_rq[64 * k + lane] = hq[k];
+  for (int k = 0; k < kRefCap / 64; ++k)
+    if (64 * k + lane < nref_t)
+      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)&heads[64 * k + lane],
+                                       (__attribute__((address_space(3))) void*)&s_rq[64 * k], 16, 0, 0);
   (void)s_rp;
 #ifdef SW_STAMPS
   if (sj == -12345) s_off = 1;  // (forces the string loads to land here in stamp builds)
   SW_STAMP(8);
 #endif
   uint32_t gref = 0;  // wave-uniform: references of the tile before this group
-  for (int r0 = 0; r0 * 64 < C; r0 += R) {
+  // (the first group runs whatever C is -- its slots are loaded without waiting for C; a group
+  // past C does nothing)
+  int r0 = 0;
+  do {
     int32_t v[R];
 #pragma unroll
-    for (int u = 0; u < R; ++u) v[u] = r0 == 0 ? v0[u] : SW_LDNT(&src[min(((r0 + u) << 6) + lane, kTile - 1)]);
+    for (int u = 0; u < R; ++u) v[u] = SW_LDNT(&src[min(((r0 + u) << 6) + lane, kTile - 1)]);
     // each reference's index in the tile's reference list (= the staged heads' order)
     uint32_t ridx[R];
 #pragma unroll
@@ -1819,6 +1851,7 @@ __device__ __forceinline__ void compact_tile(const EncArgs& a, int64_t t, int64_
       ridx[u] = gref + (uint32_t)__popcll(mk & lt_mask);
       gref += (uint32_t)__popcll(mk);
     }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (the staged heads have landed in LDS)
     wave_sync_mem();
     SW_STAMP(9);
     const uint32_t gbase = carry;  // the group's first id, tile-relative
@@ -1831,7 +1864,7 @@ __device__ __forceinline__ void compact_tile(const EncArgs& a, int64_t t, int64_
       const bool ref = valid && v[u] < 0;
       uint4 q = make_uint4(0, 0, 0, 0);
       if (ref) {  // staged heads: the first kRefCap from LDS, then straight from the staging area
-        q = ridx[u] < (uint32_t)kRefCap ? s_rq[ridx[u]] : ridx[u] < (uint32_t)kHeadCap ? heads[ridx[u]] : ref_head(a, v[u]);
+        q = ridx[u] < (uint32_t)kRefCap ? s_rq[ridx[u]] : ref_head(a, v[u]);
       }
       const bool dense = ref && slot_is_dref(v[u]);
       const bool d16 = dense && a.ids16 != 0;
@@ -1891,7 +1924,8 @@ __device__ __forceinline__ void compact_tile(const EncArgs& a, int64_t t, int64_
     __builtin_amdgcn_s_waitcnt(0);
     SW_STAMP(10);
 #endif
-  }
+    r0 += R;
+  } while (r0 * 64 < C);
   if (has_s) a.out_off[my_s] = ~(base + (int64_t)(sj >= C ? carry : s_off));
   if (many) {
     wave_sync_mem();

@@ -211,12 +211,20 @@ def test_invalid_utf8_bytes():
 
 @pytest.mark.parametrize("kind,model", [(corpus.MIXED, "bl32k.model"), (corpus.STRESS, "bl50k.model")])
 def test_large_corpus_vs_oracle(kind, model):
-    """64 MB (MIXED) / 24 MB (STRESS) seeded corpora, bit-exact against the multithreaded oracle."""
+    """64 MB (MIXED) / 24 MB (STRESS) seeded corpora, bit-exact against the multithreaded oracle,
+    with the device pre-split fused into the classification (default: chunks deferred across
+    8 KiB blocks) and as two kernels."""
     n = 60000 if kind == corpus.MIXED else 40000
     buf, off = corpus.synth(99, kind, n, 1074 if kind == corpus.MIXED else 600)
     t = tok_for(model)
-    got = gpu_encode(t, buf, off)
-    assert_same(got, oracle_encode(t.merges, buf, off, "cl100k"))
+    exp = oracle_encode(t.merges, buf, off, "cl100k")
+    L, h = _lib.lib(), t._encoder()
+    try:
+        for fused in (1, 0):
+            _lib.check(L.sw_encoder_set_option(h, _lib.SW_OPT_FUSED_PRESPLIT, fused))
+            assert_same(gpu_encode(t, buf, off), exp)
+    finally:
+        L.sw_encoder_set_option(h, _lib.SW_OPT_FUSED_PRESPLIT, 1)
 
 
 def test_device_api_with_torch_buffers():

@@ -28,6 +28,11 @@ import numpy as np
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
+# Hardware queues of this process (read by HIP at its first call, which comes later): the step
+# uses up to five streams -- the launch stream, the two merge forks, RCCL's and the reassembly's.
+# With HIP's default of 4 two of them shared one queue and ran in launch order, so the next
+# batch's encode queued behind the previous batch's reassembly (profiles/r3f_gw1_trace.md).
+os.environ["GPU_MAX_HW_QUEUES"] = "8"
 
 METRIC = "encoded MB/s (input bytes) + Mtokens/s at 32k merges, 1/2/4/8 MI355X vs CPU ref"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (/opt/skills/guides/MI355X_MICROARCH.md)
@@ -61,8 +66,6 @@ def parse():
     ap.add_argument("--dedupe-slots", type=int, default=0, help="A/B only: cap the dedupe table (power of two)")
     ap.add_argument("--no-dedupe-exact", action="store_true", help="A/B only: fingerprint keys for every chunk")
     ap.add_argument("--no-merge-streams", action="store_true", help="A/B only: merge kernels one after another")
-    ap.add_argument("--no-fused", action="store_true",
-                    help="A/B only: device pre-split and chunk classification as two kernels (same results)")
     ap.add_argument("--pipe-dma", action="store_true", help="A/B only: e2e pipeline copies by DMA, not kernels")
     ap.add_argument("--pipe-depth", type=int, default=0, help="A/B only: e2e pipeline runs in flight (2..4)")
     ap.add_argument("--pipe-run-mb", type=int, default=0, help="A/B only: e2e pipeline run size (MiB)")
@@ -143,8 +146,6 @@ def main():
         _lib.check(L.sw_encoder_set_option(h, _lib.SW_OPT_DEDUPE_EXACT, 0))
     if args.no_merge_streams:
         _lib.check(L.sw_encoder_set_option(h, _lib.SW_OPT_MERGE_STREAMS, 0))
-    if args.no_fused:
-        _lib.check(L.sw_encoder_set_option(h, _lib.SW_OPT_FUSED_PRESPLIT, 0))
     if args.pipe_dma:
         _lib.check(L.sw_encoder_set_option(h, _lib.SW_OPT_PIPE_COPY_KERNELS, 0))
     if args.pipe_depth:
@@ -209,6 +210,7 @@ def main():
         finals = [(torch.empty(world * width, dtype=torch.int32, device=dev),
                    torch.empty(world * width_s + 1, dtype=torch.int64, device=dev)) for _ in outs]
     side = torch.cuda.Stream(dev) if gather else None
+    gbufs = [{} for _ in outs]  # the gathers' receive buffers, one set per batch in flight (no allocation in the step)
     done_ev = [None for _ in outs]
     n_step = [0]
     host_t = {"encode": 0.0, "gathers": 0.0, "reassembly": 0.0}  # (SW_BENCH_HOST_TIMES=1: host time per call)
@@ -230,7 +232,7 @@ def main():
             return
         # steps 1-3: one counts all-gather, padded id and offset all-gathers (RCCL)
         works, res = shard.reassemble(o_ids, o_off, None, dev, concat=False, width=width, width_s=width_s,
-                                      id_bits=id_bits, async_op=True)
+                                      id_bits=id_bits, async_op=True, bufs=gbufs[slot])
         h2 = time.perf_counter()
         host_t["gathers"] += h2 - h1
         side.wait_stream(torch.cuda.current_stream(dev))

@@ -143,11 +143,6 @@ int32_t sw_encoder_reserve(sw_encoder* h, int64_t max_bytes, int64_t max_strings
  *                          16-bit transport: no conversion pass, half the output bytes.
  *                          sw_encode_batch is not affected (host results are int32). */
 #define SW_OPT_OUT_BITS 16
-/*   SW_OPT_FUSED_PRESPLIT  1 (default): sw_encode_device's device pre-split and the chunk
- *                          classification run as one kernel (the pre-split bits of each 8 KiB
- *                          block go to its classification through LDS); 0: two kernels.  Same
- *                          results either way. */
-#define SW_OPT_FUSED_PRESPLIT 17
 int32_t sw_encoder_set_option(sw_encoder* h, int32_t option, int64_t value);
 
 /* Encoder facts (sw_encoder_get_info): distinct merges, whole-chunk table entries, whether the

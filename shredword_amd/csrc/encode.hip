@@ -35,7 +35,6 @@
 #include "kernels.h"
 #include "long_split.h"
 #include "presplit_kernel.h"
-#include "fused_kernel.h"
 #include "shredword_hip.h"
 #include "table.h"
 
@@ -108,7 +107,6 @@ struct sw_encoder {
   // the merge kernels of different length buckets are independent: forked onto these streams
   // they overlap (each alone leaves most of the chip idle), joined before k_tile_count
   bool merge_fork = true;             // SW_OPT_MERGE_STREAMS
-  bool fused_presplit = true;         // SW_OPT_FUSED_PRESPLIT
   bool out16 = false;                 // SW_OPT_OUT_BITS 16: sw_encode_device writes uint16 ids
   hipStream_t s_fork[2] = {nullptr, nullptr};
   hipEvent_t ev_fork = nullptr, ev_join[2] = {nullptr, nullptr};
@@ -121,14 +119,13 @@ struct sw_encoder {
   int64_t* d_tile_slo = nullptr;
   uint32_t* d_tile_slots = nullptr;
   uint32_t* d_tile_nref = nullptr;
-  uint16_t* d_tdefer = nullptr;        // k_presplit_classify's deferred chunk per tile
   uint32_t* d_rlist = nullptr;
   uint64_t* d_queue = nullptr;        // dense merge queue (bucket-major)
   uint32_t* d_bcnt = nullptr;         // [kNumBuckets * n_tiles] queued chunks per (bucket, tile)
   int64_t* d_boff = nullptr;          // its exclusive scan
   int64_t* d_qtotal = nullptr;
   unsigned long long* d_stamps = nullptr;  // SW_STAMPS builds
-  uint64_t* d_dtab = nullptr;         // chunk dedupe table (two words per entry)
+  uint64_t* d_dtab = nullptr;         // chunk dedupe table
   uint32_t dmask = 0;
   uint4* d_dres = nullptr;            // dense result heads, one per table entry
   uint8_t* d_dcnt = nullptr;          // their id counts (<= 32), one byte per table entry
@@ -178,9 +175,9 @@ struct DeviceGuard {
 void free_workspace(sw_encoder* h) {
   (void)hipFree(h->d_scratch); (void)hipFree(h->d_res); (void)hipFree(h->d_pbits); (void)hipFree(h->d_pcount); (void)hipFree(h->d_part);
   (void)hipFree(h->d_tile_slo); (void)hipFree(h->d_stamps);
-  (void)hipFree(h->d_tile_slots); (void)hipFree(h->d_tile_nref); (void)hipFree(h->d_tdefer); (void)hipFree(h->d_rlist); (void)hipFree(h->d_queue); (void)hipFree(h->d_bcnt); (void)hipFree(h->d_boff);
+  (void)hipFree(h->d_tile_slots); (void)hipFree(h->d_tile_nref); (void)hipFree(h->d_rlist); (void)hipFree(h->d_queue); (void)hipFree(h->d_bcnt); (void)hipFree(h->d_boff);
   (void)hipFree(h->d_qtotal);
-  h->d_tile_slo = nullptr; h->d_stamps = nullptr; h->d_tile_slots = nullptr; h->d_tile_nref = nullptr; h->d_tdefer = nullptr; h->d_rlist = nullptr; h->d_queue = nullptr;
+  h->d_tile_slo = nullptr; h->d_stamps = nullptr; h->d_tile_slots = nullptr; h->d_tile_nref = nullptr; h->d_rlist = nullptr; h->d_queue = nullptr;
   h->d_bcnt = nullptr; h->d_boff = nullptr; h->d_qtotal = nullptr;
   (void)hipFree(h->d_dtab); (void)hipFree(h->d_tile_base); (void)hipFree(h->d_tile_cnt);
   (void)hipFree(h->d_dres); (void)hipFree(h->d_big); (void)hipFree(h->d_dcnt);
@@ -224,7 +221,6 @@ int32_t ensure_workspace(sw_encoder* h, int64_t n_bytes) {
   HIP_TRY(hipMalloc(&h->d_tile_slo, sizeof(int64_t) * n_tiles));
   HIP_TRY(hipMalloc(&h->d_tile_slots, sizeof(uint32_t) * n_tiles));
   HIP_TRY(hipMalloc(&h->d_tile_nref, sizeof(uint32_t) * n_tiles));
-  HIP_TRY(hipMalloc(&h->d_tdefer, sizeof(uint16_t) * n_tiles));
   HIP_TRY(hipMalloc(&h->d_rlist, sizeof(uint32_t) * n_tiles * kTile));
   // queued chunks have >= 2 bytes: at most nb / 2 of them
   HIP_TRY(hipMalloc(&h->d_queue, sizeof(uint64_t) * (nb / 2 + 64)));
@@ -236,7 +232,7 @@ int32_t ensure_workspace(sw_encoder* h, int64_t n_bytes) {
      // result head per entry
     int64_t slots = 64;
     while (slots < nb / 64 && slots < (1LL << 22)) slots <<= 1;
-    HIP_TRY(hipMalloc(&h->d_dtab, 2 * sizeof(uint64_t) * slots));  // (16-byte entries)
+    HIP_TRY(hipMalloc(&h->d_dtab, sizeof(uint64_t) * slots));
     HIP_TRY(hipMalloc(&h->d_dres, sizeof(uint4) * slots));
     HIP_TRY(hipMalloc(&h->d_dcnt, slots));
     h->dmask = (uint32_t)(slots - 1);
@@ -529,7 +525,6 @@ extern "C" int32_t sw_encoder_set_option(sw_encoder* h, int32_t option, int64_t 
     case SW_OPT_LONG_SPLIT: h->long_split = value != 0; return SW_OK;
     case SW_OPT_PIPE_COPY_KERNELS: h->pipe_kcopy = value != 0; return SW_OK;
     case SW_OPT_MERGE_STREAMS: h->merge_fork = value != 0; return SW_OK;
-    case SW_OPT_FUSED_PRESPLIT: h->fused_presplit = value != 0; return SW_OK;
     case SW_OPT_OUT_BITS:
       if (value != 16 && value != 32) return fail(SW_ERR_ARG, "SW_OPT_OUT_BITS: 16 or 32");
       if (value == 16 && !h->ids16) return fail(SW_ERR_ARG, "SW_OPT_OUT_BITS 16: a table id does not fit 16 bits");
@@ -695,10 +690,8 @@ int32_t encode_device(sw_encoder* h, const uint8_t* d_bytes, int64_t n_bytes, co
   if (n_tiles > 0)  // (the pre-split and k_classify start from each tile's first string)
     hipLaunchKernelGGL(k_tile_strings, dim3((unsigned)((n_tiles + 255) / 256)), dim3(256), 0, st, d_str_off, n_str,
                        n_tiles, h->d_tile_slo);
-  // the full path pre-splits on the device: in k_presplit_classify below (fused), or first
-  const bool fused = n_tiles > 0 && !d_chunk_bits && h->fused_presplit;
-  if (n_tiles > 0 && !d_chunk_bits) {
-    if (!fused) HIP_TRY(launch_presplit(st, d_bytes, n_bytes, d_str_off, n_str, h->pattern, h->d_pbits, h->d_tile_slo));
+  if (n_tiles > 0 && !d_chunk_bits) {  // the full path: device pre-split first
+    HIP_TRY(launch_presplit(st, d_bytes, n_bytes, d_str_off, n_str, h->pattern, h->d_pbits, h->d_tile_slo));
     d_chunk_bits = h->d_pbits;
   }
   if (n_tiles > 0) {
@@ -716,19 +709,11 @@ int32_t encode_device(sw_encoder* h, const uint8_t* d_bytes, int64_t n_bytes, co
     a.out_off = d_out_off; a.tile_slo = h->d_tile_slo;
     a.n_tiles = n_tiles; a.qtmp = h->d_res; a.bcnt = h->d_bcnt; a.boff = h->d_boff; a.q_total = h->d_qtotal;
     a.queue = h->d_queue; a.stamps = h->d_stamps;
-    a.inv = h->d_inv; a.n_inv = h->n_inv; a.ids16 = h->ids16 ? 1u : 0u; a.tdefer = h->d_tdefer;
+    a.inv = h->d_inv; a.n_inv = h->n_inv; a.ids16 = h->ids16 ? 1u : 0u;
     a.lstart = h->lp.wstart; a.llen = h->lp.wlen; a.n_long = &h->lp.ctl[kLcWave]; a.lcap = h->lp.lcap;
     const bool split = h->split_ok && h->long_split;  // (split + verify needs a well-formed table)
-    if (h->dedupe) HIP_TRY(hipMemsetAsync(h->d_dtab, 0, 2 * sizeof(uint64_t) * ((size_t)a.dmask + 1), st));
-    if (fused) {  // pre-split + classification of each 8 KiB block, then the chunks left across blocks
-      const PbArgs g{d_bytes, n_bytes, d_str_off, n_str, h->d_tile_slo};
-      hipLaunchKernelGGL(k_presplit_classify, dim3((unsigned)((n_bytes + kPbBlock - 1) / kPbBlock)), dim3(kPbThreads), 0,
-                         st, g, (int)h->pattern, (uint32_t*)h->d_pbits, a);
-      hipLaunchKernelGGL(k_classify_deferred, dim3((unsigned)((n_tiles + kThreads - 1) / kThreads)), dim3(kThreads), 0,
-                         st, a);
-    } else {
-      hipLaunchKernelGGL(k_classify, dim3((unsigned)((n_tiles + kWaves - 1) / kWaves)), dim3(kThreads), 0, st, a);
-    }
+    if (h->dedupe) HIP_TRY(hipMemsetAsync(h->d_dtab, 0, sizeof(uint64_t) * ((size_t)a.dmask + 1), st));
+    hipLaunchKernelGGL(k_classify, dim3((unsigned)((n_tiles + kWaves - 1) / kWaves)), dim3(kThreads), 0, st, a);
     HIP_TRY(hipGetLastError());
     HIP_TRY(launch_scan(st, h->d_bcnt, kNumBuckets * n_tiles, h->d_part, h->d_boff, h->d_qtotal));
     hipLaunchKernelGGL(k_scatter, dim3((unsigned)((n_tiles + 3) / 4)), dim3(kThreads), 0, st, a);

@@ -64,8 +64,7 @@ __host__ __device__ inline uint32_t slot_did(int32_t v) { return (uint32_t)(-(in
 // need no second read.  A reference list entry (rlist) is p or kRlDense | d.
 constexpr uint32_t kRlDense = 0x80000000u;
 constexpr uint32_t kNoDid = 0x7FFFFFFu;    // (27-bit dense result field of a queue entry: none)
-constexpr int kDdExactMax = 14;            // dedupe keys of <= this many bytes are exact (no verification)
-constexpr int kDdExactW0 = 7;              // ... of which this many fit the entry's first word
+constexpr int kDdExactMax = 7;             // dedupe keys of <= this many bytes are exact (no verification)
 
 // streaming accesses (read or written once per launch) carry the non-temporal hint, so the
 // caches keep the randomly gathered merge results instead
@@ -558,7 +557,7 @@ struct EncArgs {
   const int64_t* boff;       // [kNumBuckets * n_tiles] exclusive scan of bcnt (bucket-major)
   const int64_t* q_total;    // queued chunks in all
   uint64_t* queue;           // dense merge queue, bucket-major: start << 33 | len << 27 | dense result
-  uint64_t* dtab;            // chunk dedupe table (dedupe_claim), dmask + 1 entries of two words
+  uint64_t* dtab;            // chunk dedupe table (dedupe_claim), dmask + 1 entries
   uint32_t dmask;
   uint32_t dfp_mask;         // fingerprint bits in use (all 26 except in collision tests)
   uint32_t dedupe;           // 0: every queued chunk runs its own merge loop
@@ -576,7 +575,6 @@ struct EncArgs {
   uint32_t* big_list;        // long chunks over kLongLds bytes (their index in the long list)
   uint32_t* big_count;       // ... how many (cleared per launch)
   uint32_t ids16;            // every id fits 16 bits (dres layout)
-  uint16_t* tdefer;          // [n_tiles] k_presplit_classify: the deferred last chunk's start in the tile, or 0xFFFF
 };
 
 #ifdef SW_STAMPS
@@ -612,11 +610,9 @@ __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t x, int lane) {
 // Batch-wide dedupe of queued chunks (in k_classify).  Real text repeats its multi-token words
 // endlessly, and a chunk's encoding depends on its bytes alone, so the merge loop needs to run
 // once per DISTINCT chunk of the launch.  The table (cleared before every launch) holds one
-// 16-byte entry per claimed chunk, 8 candidates per chunk in one 128-byte line; the first word
-// is claimed with a CAS:
-//   exact keys, chunks of <= 14 bytes:  bytes 0..6 | length << 56 | 1 << 63, and for 8..14 bytes
-//                                       a second word bytes 7..13 | 1 << 63 (stored after the claim)
-//   longer chunks:                      26-bit fingerprint << 37 | length << 31 | position
+// word per claimed chunk, 8 candidates per chunk in one 64-byte line:
+//   exact keys, chunks of <= 7 bytes:  bytes | length << 56 | 1 << 63
+//   longer chunks:                     26-bit fingerprint << 37 | length << 31 | position
 // The first occurrence claims an entry with a CAS and is merged; its result head lands in
 // dres at the entry's index, which every later occurrence refers to (slot_dref): nothing has to
 // be read back from the claimant.  Exact keys decide equality by themselves; a fingerprint match
@@ -643,36 +639,22 @@ __device__ __forceinline__ DdOut dedupe_claim(const EncArgs& a, const uint32_t* 
   }
   const uint32_t h2 = (h ^ (h >> 16)) * 0x7FEB352Du;
   const bool exact = n <= (int)a.dexact;
-  const bool ex2 = exact && n > kDdExactW0;  // (the key's bytes 7.. live in the entry's second word)
-  const uint64_t tag = exact ? ((uint64_t)u[0] | ((uint64_t)(u[1] & 0xFFFFFFu) << 32) | ((uint64_t)n << 56) | kDdExact)
+  const uint64_t tag = exact ? ((uint64_t)u[0] | ((uint64_t)u[1] << 32) | ((uint64_t)n << 56) | kDdExact)
                              : ((uint64_t)((h2 >> 6) & a.dfp_mask & 0x3FFFFFFu) << 37 | (uint64_t)n << 31);
   const uint64_t mine = exact ? tag : (tag | (uint64_t)start);
-  // bytes 7..13 and a marker bit (a written second word is never 0)
-  const uint64_t mine1 = ((uint64_t)(u[1] >> 24) | ((uint64_t)u[2] << 8) | ((uint64_t)(u[3] & 0xFFFFu) << 40)) | kDdExact;
   const uint32_t grp = h & a.dmask & ~7u;
   for (int j = 0; j < 8; ++j) {
     const uint32_t idx = grp | ((h2 + j) & 7u);
-    unsigned long long* p = (unsigned long long*)a.dtab + 2 * (int64_t)idx;
-    // an entry's words change once each (0 -> final), so a cached plain load is safe: a stale 0
-    // first word only sends this lane to the CAS, which returns the live value; a stale 0 second
-    // word is re-read with an atomic (the live value), and one still 0 (its claimant has not
-    // stored it yet) counts as a different key -- this chunk then takes another entry or merges
-    // on its own, neither of which can change a result
-    const u32x4 q = *(const u32x4*)p;
-    uint64_t cur = (uint64_t)q[0] | ((uint64_t)q[1] << 32);
+    unsigned long long* p = (unsigned long long*)a.dtab + idx;
+    // an entry changes once (0 -> final), so a cached plain load is safe: a stale 0 only sends
+    // this lane to the CAS, which returns the live value
+    uint64_t cur = *p;
     if (cur == 0) {
       cur = atomicCAS(p, 0ULL, (unsigned long long)mine);
-      if (cur == 0) {  // claimed: this chunk is merged and shared
-        if (ex2) __hip_atomic_store(p + 1, (unsigned long long)mine1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        return DdOut{1, idx};
-      }
+      if (cur == 0) return DdOut{1, idx};  // claimed: this chunk is merged and shared
     }
     if (exact) {
-      if (cur != mine) continue;
-      if (!ex2) return DdOut{2, idx};
-      uint64_t w1 = (uint64_t)q[2] | ((uint64_t)q[3] << 32);
-      if (w1 == 0) w1 = __hip_atomic_fetch_or(p + 1, 0ULL, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (w1 == mine1) return DdOut{2, idx};
+      if (cur == mine) return DdOut{2, idx};
       continue;
     }
     if ((cur & ~0x7FFFFFFFULL) != tag) continue;
@@ -744,15 +726,9 @@ constexpr int kWinWords = kWin / 4 + 8;
 // function of (tile, base) (compact_tile) the compiler fits 78 VGPRs, 6 waves, no spill: 1.11 ->
 // 0.95 ms (profiles/r2_k.md).
 #define SW_CLS_ATTR __attribute__((amdgpu_waves_per_eu(6, 6)))
-// one tile (the body of k_classify's tile loop).  kFused (k_presplit_classify): the tile's
-// chunk-start bits come from the pre-split of its 8 KiB block in LDS (s_bits: the block's 256
-// dwords, this tile's from 64 wv), and the end of the tile's last chunk is known only when the
-// next chunk start lies inside the block: otherwise that chunk is DEFERRED -- its slot and all
-// that follows from it are left to k_classify_deferred, and a.tdefer[tile] holds its start.
-template <bool kFused = false>
+// one tile (the body of k_classify's tile loop)
 __device__ __forceinline__ void classify_tile(const EncArgs& a, int64_t tile, uint32_t* s_b32, uint16_t* s_cstart,
-                                              uint16_t* s_qbuf, const uint32_t* s_bits = nullptr, int wv = 0,
-                                              int64_t blk_end = 0) {
+                                              uint16_t* s_qbuf) {
   SW_STAMP_INIT;
   const int lane = threadIdx.x & 63;
   const uint64_t lt_mask = (lane == 0) ? 0ULL : (~0ULL >> (64 - lane));
@@ -780,13 +756,7 @@ __device__ __forceinline__ void classify_tile(const EncArgs& a, int64_t tile, ui
     }
   }
   if (lane < 8) s_b32[kWin / 4 + lane] = 0;
-  uint64_t bw = 0;
-  if constexpr (kFused) {  // word lane of the tile (lane 32: the next tile's first, if in the block)
-    const int q = 64 * wv + 2 * lane;
-    if (lane < kTileWords && q + 1 < kWaves * 64) bw = (uint64_t)s_bits[q] | ((uint64_t)s_bits[q + 1] << 32);
-  } else {
-    bw = (lane < kTileWords && w0 + lane < a.n_words) ? SW_LDNT2(&a.bits[w0 + lane]) : 0ULL;
-  }
+  const uint64_t bw = (lane < kTileWords && w0 + lane < a.n_words) ? SW_LDNT2(&a.bits[w0 + lane]) : 0ULL;
   const int64_t s_first = a.tile_slo[tile];  // (prefetched: used by step 6)
 
   // 2. chunk starts in [t0, t1): lane w owns bitmap word w
@@ -826,32 +796,12 @@ __device__ __forceinline__ void classify_tile(const EncArgs& a, int64_t tile, ui
       last_end = min(q, a.n_bytes);
     } else if (C > 0) {
       // (a chunk running past the halo)
-      if constexpr (kFused) {  // the block's later dwords, then: past the block, deferred
-        int64_t q = -1;
-        for (int i0 = 64 * wv + 2 * kTileWords; i0 < kWaves * 64 && q < 0; i0 += 64) {
-          const int i = i0 + lane;
-          const uint32_t x = i < kWaves * 64 ? s_bits[i] : 0u;
-          const uint64_t hm = __ballot(x != 0);
-          if (hm) {
-            const int src = __ffsll((long long)hm) - 1;
-            q = (blk_end - (int64_t)kWaves * kTile) + 32 * (int64_t)(i0 + src) + __ffs(__shfl((int)x, src, 64)) - 1;
-          }
-        }
-        last_end = q >= 0 ? min(q, a.n_bytes) : blk_end < a.n_bytes ? (int64_t)-1 : a.n_bytes;
-      } else {
-        const int64_t q = next_set_bit(a.bits, a.n_words, t0 + 64 * kTileWords, a.n_bytes);
-        last_end = min(q, a.n_bytes);
-      }
+      const int64_t q = next_set_bit(a.bits, a.n_words, t0 + 64 * kTileWords, a.n_bytes);
+      last_end = min(q, a.n_bytes);
     }
   }
+  const int rel_end = (int)(last_end - t0);
   wave_sync_mem();
-  // kFused: a last chunk whose end is past the block is deferred (processed: Cp chunks)
-  const bool defer = kFused && last_end < 0;
-  const int Cp = defer ? C - 1 : C;
-  const int rel_end = defer ? (int)s_cstart[C - 1] : (int)(last_end - t0);
-  if constexpr (kFused) {
-    if (lane == 0) a.tdefer[tile] = defer ? (uint16_t)s_cstart[C - 1] : (uint16_t)0xFFFFu;
-  }
   SW_STAMP(0);
 
   // 3. settle single bytes and whole-chunk-table hits (their slots written here).  The rest
@@ -859,7 +809,7 @@ __device__ __forceinline__ void classify_tile(const EncArgs& a, int64_t tile, ui
   //    point their slot at the first occurrence's result, the others are queued for the merge
   //    kernels and counted per length bucket (lane b: bucket b).
   int32_t* dst = a.scratch + t0;
-  const int rounds = (Cp + 63) >> 6;
+  const int rounds = (C + 63) >> 6;
   const bool use_table = a.chunks.enabled != 0;
   const int64_t mis = (int64_t)((uintptr_t)a.bytes & 3);
   const uint32_t* gwords = (const uint32_t*)((uintptr_t)a.bytes - mis);
@@ -873,21 +823,21 @@ __device__ __forceinline__ void classify_tile(const EncArgs& a, int64_t tile, ui
     if (r0 < rounds) {
       uint32_t tok[kLookRounds];
       if (use_table) {
-        table_lookups<kLookRounds>(a.chunks, s_b32, s_cstart, Cp, rel_end, r0, lane, tok);
+        table_lookups<kLookRounds>(a.chunks, s_b32, s_cstart, C, rel_end, r0, lane, tok);
       } else {
 #pragma unroll
         for (int u = 0; u < kLookRounds; ++u) {  // (no table: single bytes only)
           const int k = ((r0 + u) << 6) + lane;
-          const bool valid = k < Cp;
+          const bool valid = k < C;
           const int ls = valid ? s_cstart[k] : 0;
-          const int end = (k + 1 < Cp) ? (int)s_cstart[k + 1] : rel_end;
+          const int end = (k + 1 < C) ? (int)s_cstart[k + 1] : rel_end;
           tok[u] = (valid && end - ls == 1) ? (s_b32[ls >> 2] >> (8 * (ls & 3))) & 0xFFu : kInf;
         }
       }
 #pragma unroll
       for (int u = 0; u < kLookRounds; ++u) {
         const int k = ((r0 + u) << 6) + lane;
-        const bool valid = k < Cp;
+        const bool valid = k < C;
         const bool queued = valid && tok[u] == kInf;
         if (valid && !queued) SW_STNT(&dst[k], (int32_t)tok[u]);
         const uint64_t mq = __ballot(queued);
@@ -909,7 +859,7 @@ __device__ __forceinline__ void classify_tile(const EncArgs& a, int64_t tile, ui
         if (64 * q + lane < nq) s_qbuf[64 * (q - 1) + lane] = rest[q - 1];
       nq = nq > 64 ? nq - 64 : 0;
       const int ls = act ? s_cstart[k] : 0;
-      const int end = (k + 1 < Cp) ? (int)s_cstart[k + 1] : rel_end;
+      const int end = (k + 1 < C) ? (int)s_cstart[k + 1] : rel_end;
       const int len = act ? end - ls : 0;
       DdOut dd{0, 0};
       if (act && a.dedupe && len <= kShort) {
@@ -1717,32 +1667,8 @@ __device__ __forceinline__ uint32_t ref_count(const EncArgs& a, uint32_t r) {
   return dn ? c8 : c32;
 }
 
-// Staged result heads: k_tile_count gathers the head of each of a tile's first kHeadCap
-// references (in reference-list order, which is the order of the tile's reference slots) into
-// the unused upper half of the tile's reference-list region (a tile has at most kTile / 2
-// references, and kHeadCap 16-byte heads fill the other kTile / 2 words), so k_compact reads
-// them as one coalesced run loaded beside its slots instead of gathering them after the slots
-// arrive: one dependent round trip less per tile, and each head is gathered once, not twice
-constexpr int kHeadCap = kTile / 2 * 4 / 16;  // 256
-static_assert(kTile / 2 * 4 >= kHeadCap * 16, "staged heads fit the reference list's upper half");
-__device__ __forceinline__ uint4* tile_heads(const EncArgs& a, int64_t t) {
-  return (uint4*)(a.rlist + t * kTile + kTile / 2);
-}
-// the head of a reference-list entry (dense result or the position of a merged chunk) and its
-// id count
-__device__ __forceinline__ uint4 rl_head(const EncArgs& a, uint32_t r) {
-  const bool dn = (r & kRlDense) != 0;
-  const uint32_t* src = dn ? (const uint32_t*)(a.dres + (r & ~kRlDense)) : a.res + 2 * (int64_t)r;
-  uint4 q;
-  __builtin_memcpy(&q, src, sizeof(q));
-  return q;
-}
-__device__ __forceinline__ uint32_t rl_head_count(const EncArgs& a, uint32_t r, uint4 q) {
-  return ((r & kRlDense) != 0 && a.ids16) ? (q.x & 0xFFFFu) : q.x;
-}
-
 // k_tile_count: kTcTiles tiles per wave, their first 64 list entries and sizes loaded together,
-// then their heads: one dependent round trip serves kTcTiles tiles (a tile holds ~58
+// then their counts: one dependent round trip serves kTcTiles tiles (a tile holds ~58
 // references on prose, so one wave per tile spent most of its life waiting)
 constexpr int kTcTiles = 2;
 __global__ void __launch_bounds__(kThreads) k_tile_count(EncArgs a) {
@@ -1758,26 +1684,13 @@ __global__ void __launch_bounds__(kThreads) k_tile_count(EncArgs a) {
     C[k] = (int)a.tile_slots[t];
     nr[k] = (int)a.tile_nref[t];
   }
-  uint4 q0[kTcTiles];
 #pragma unroll
-  for (int k = 0; k < kTcTiles; ++k) q0[k] = lane < nr[k] ? rl_head(a, p0[k]) : make_uint4(0, 0, 0, 0);
-#pragma unroll
-  for (int k = 0; k < kTcTiles; ++k) {
-    c[k] = lane < nr[k] ? rl_head_count(a, p0[k], q0[k]) : 0u;
-    if (tb + k < a.n_tiles && lane < nr[k]) tile_heads(a, tb + k)[lane] = q0[k];
-  }
+  for (int k = 0; k < kTcTiles; ++k) c[k] = lane < nr[k] ? ref_count(a, p0[k]) : 0u;
 #pragma unroll
   for (int k = 0; k < kTcTiles; ++k) {
     const uint32_t* rl = a.rlist + min(tb + k, a.n_tiles - 1) * kTile;
-    for (int i0 = 64; i0 < nr[k]; i0 += 64) {  // (long lists: the rest a round at a time)
-      const int i = i0 + lane;
-      if (i < nr[k]) {
-        const uint32_t r = SW_LDNT2(&rl[i]);
-        const uint4 q = rl_head(a, r);
-        c[k] += rl_head_count(a, r, q);
-        if (i < kHeadCap && tb + k < a.n_tiles) tile_heads(a, tb + k)[i] = q;
-      }
-    }
+    for (int i0 = 64; i0 < nr[k]; i0 += 64)  // (long lists: the rest a round at a time)
+      if (i0 + lane < nr[k]) c[k] += ref_count(a, SW_LDNT2(&rl[i0 + lane]));
   }
 #pragma unroll
   for (int k = 0; k < kTcTiles; ++k) {
@@ -1819,39 +1732,27 @@ __device__ __forceinline__ void compact_tile(const EncArgs& a, int64_t t, int64_
   const int sj = has_s ? (int)s_cj : -1;
   const bool many = s_hi - s_lo > 64;  // rare: slot offsets go through scratch instead
   uint32_t s_off = 0, carry = 0;
-  // the first group's slots and the tile's first kRefCap staged heads (k_tile_count) load beside
-  // the tile's slot count: nothing waits for C or for the slots before the heads are asked for
-  // (straight into LDS, no registers held: global_load_lds, lane i's 16 bytes to s_rq[64 k + i])
-  const uint4* heads = tile_heads(a, t);
-  const int nref_t = (int)a.tile_nref[t];  // (only the staged heads in use are read)
-#pragma unroll
-  for (int k = 0; k < kRefCap / 64; ++k)
-    if (64 * k + lane < nref_t)
-      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)&heads[64 * k + lane],
-                                       (__attribute__((address_space(3))) void*)&s_rq[64 * k], 16, 0, 0);
-  (void)s_rp;
 #ifdef SW_STAMPS
   if (sj == -12345) s_off = 1;  // (forces the string loads to land here in stamp builds)
   SW_STAMP(8);
 #endif
-  uint32_t gref = 0;  // wave-uniform: references of the tile before this group
-  // (the first group runs whatever C is -- its slots are loaded without waiting for C; a group
-  // past C does nothing)
-  int r0 = 0;
-  do {
+  for (int r0 = 0; r0 * 64 < C; r0 += R) {
     int32_t v[R];
 #pragma unroll
     for (int u = 0; u < R; ++u) v[u] = SW_LDNT(&src[min(((r0 + u) << 6) + lane, kTile - 1)]);
-    // each reference's index in the tile's reference list (= the staged heads' order)
+    // dense list of the group's references (their index in the list per round and lane)
     uint32_t ridx[R];
+    int nref = 0;  // wave-uniform
 #pragma unroll
     for (int u = 0; u < R; ++u) {
       const bool ref = ((r0 + u) << 6) + lane < C && v[u] < 0;
       const uint64_t mk = __ballot(ref);
-      ridx[u] = gref + (uint32_t)__popcll(mk & lt_mask);
-      gref += (uint32_t)__popcll(mk);
+      ridx[u] = (uint32_t)(nref + __popcll(mk & lt_mask));
+      if (ref && ridx[u] < (uint32_t)kRefCap) s_rp[ridx[u]] = (uint32_t)v[u];
+      nref += __popcll(mk);
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (the staged heads have landed in LDS)
+    wave_sync_mem();
+    for (int i = lane; i < min(nref, kRefCap); i += 64) s_rq[i] = ref_head(a, (int32_t)s_rp[i]);
     wave_sync_mem();
     SW_STAMP(9);
     const uint32_t gbase = carry;  // the group's first id, tile-relative
@@ -1863,9 +1764,7 @@ __device__ __forceinline__ void compact_tile(const EncArgs& a, int64_t t, int64_
       const bool valid = j < C;
       const bool ref = valid && v[u] < 0;
       uint4 q = make_uint4(0, 0, 0, 0);
-      if (ref) {  // staged heads: the first kRefCap from LDS, then straight from the staging area
-        q = ridx[u] < (uint32_t)kRefCap ? s_rq[ridx[u]] : ref_head(a, v[u]);
-      }
+      if (ref) q = ridx[u] < (uint32_t)kRefCap ? s_rq[ridx[u]] : ref_head(a, v[u]);
       const bool dense = ref && slot_is_dref(v[u]);
       const bool d16 = dense && a.ids16 != 0;
       const uint32_t m = ref ? (dense ? (q.x & 0xFFFFu) : q.x) : (valid ? 1u : 0u);
@@ -1924,8 +1823,7 @@ __device__ __forceinline__ void compact_tile(const EncArgs& a, int64_t t, int64_
     __builtin_amdgcn_s_waitcnt(0);
     SW_STAMP(10);
 #endif
-    r0 += R;
-  } while (r0 * 64 < C);
+  }
   if (has_s) a.out_off[my_s] = ~(base + (int64_t)(sj >= C ? carry : s_off));
   if (many) {
     wave_sync_mem();

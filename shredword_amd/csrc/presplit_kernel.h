@@ -122,20 +122,13 @@ struct PbSrc {  // psb::carries' view: the block's chunks from LDS, the others c
   }
 };
 
-// The pre-split of one kPbBlock block by its kPbThreads threads: returns this thread's 32
-// chunk-start bits (0 past the batch) and stores them as one dword of bits32.  Every thread of the
-// block must call it (it holds block barriers); s_m / s_ss: the block's LDS.
-__device__ __forceinline__ uint32_t presplit_block(const PbArgs& g, int pattern, uint32_t* bits32,
-                                                   uint32_t (*s_m)[kPbChunks], uint32_t* s_ss) {
+__global__ void __launch_bounds__(kPbThreads, 4) k_presplit_bits(PbArgs g, int pattern, uint32_t* bits32) {
+  __shared__ uint32_t s_m[9][kPbChunks];
+  __shared__ uint32_t s_ss[kPbSsWords];
   const int tid = threadIdx.x;
   const int64_t b0 = (int64_t)blockIdx.x * kPbBlock, c0 = b0 / psb::kChunk;
   const int64_t n_chunks = (g.n_bytes + psb::kChunk - 1) / psb::kChunk;
   const bool cl = pattern == 0;
-  // this thread's 40 bytes are asked for first: they arrive while the string starts below are
-  // looked up and staged (otherwise step 1 would issue them only after that round trip)
-  psb::RegBytes by;
-  const int64_t c = c0 + tid;
-  if (pattern != 2 && c < n_chunks) pb_load40(g, 32 * c, by.w);
   // 0. string starts of [b0 - kPbPre, b0 + kPbBlock + 64) (the batch end is str_off[n_str])
   for (int i = tid; i < kPbSsWords; i += kPbThreads) s_ss[i] = 0;
   __syncthreads();
@@ -149,46 +142,45 @@ __device__ __forceinline__ uint32_t presplit_block(const PbArgs& g, int pattern,
   }
   __syncthreads();
   PbSrc src{g, s_m, s_ss, c0, b0, n_chunks, cl};
-  uint32_t r = 0;
   if (pattern == 2) {  // the chunks are the strings
-    if (c < n_chunks) r = src.ss(c);
-  } else {
-    // 1. class masks of the block's chunks c0 .. c0 + 255 (40 bytes each straight from global
-    //    memory: staging the block through LDS measured slower)
-    {
-      psb::Masks m{};
-      if (c < n_chunks) {
-        const uint64_t s = (uint64_t)src.ss_at(32 * c - 4) | ((uint64_t)(src.ss_at(32 * c + 28) & 0xFFu) << 32);
-        m = psb::classify(by, s, UcdClass{}, cl);
-      }
-      s_m[0][tid] = m.L; s_m[1][tid] = m.N; s_m[2][tid] = m.C; s_m[3][tid] = m.P; s_m[4][tid] = m.H;
-      s_m[5][tid] = m.A; s_m[6][tid] = m.X; s_m[7][tid] = m.K1; s_m[8][tid] = m.K2;
-    }
-    __syncthreads();
-    // 2. this thread's chunk
+    const int64_t c = c0 + tid;
     if (c < n_chunks) {
-      const psb::Masks m0 = src.get(c - 1), m1 = src.get(c), m2 = src.get(c + 1);
-      const uint64_t ssw = (uint64_t)src.ss_at(32 * c - 16) | ((uint64_t)src.ss_at(32 * c + 16) << 32);
-      uint32_t need = 0;
-      r = psb::rules(m0, m1, m2, ssw, cl, psb::Carry{}, &need);
-      if (need) {
-        const psb::Carry cy = psb::carries(src, c, need);
-        r = psb::rules(m0, m1, m2, ssw, cl, cy, &need);
-      }
+      uint32_t r = src.ss(c);
+      if (32 * c + 32 > g.n_bytes) r &= (1u << (g.n_bytes - 32 * c)) - 1u;
+      bits32[c] = r;
+      if (c == n_chunks - 1 && (c & 1) == 0) bits32[c + 1] = 0;  // (the last word's upper half)
     }
+    return;
   }
-  if (c < n_chunks) {
-    if (32 * c + 32 > g.n_bytes) r &= (1u << (g.n_bytes - 32 * c)) - 1u;
-    bits32[c] = r;
-    if (c == n_chunks - 1 && (c & 1) == 0) bits32[c + 1] = 0;  // (the last word's upper half)
+  // 1. class masks of the block's chunks c0 .. c0 + 255 (40 bytes each straight from global
+  //    memory: staging the block through LDS measured slower)
+  {
+    const int64_t c = c0 + tid;
+    psb::Masks m{};
+    if (c < n_chunks) {
+      psb::RegBytes by;
+      pb_load40(g, 32 * c, by.w);
+      const uint64_t s = (uint64_t)src.ss_at(32 * c - 4) | ((uint64_t)(src.ss_at(32 * c + 28) & 0xFFu) << 32);
+      m = psb::classify(by, s, UcdClass{}, cl);
+    }
+    s_m[0][tid] = m.L; s_m[1][tid] = m.N; s_m[2][tid] = m.C; s_m[3][tid] = m.P; s_m[4][tid] = m.H;
+    s_m[5][tid] = m.A; s_m[6][tid] = m.X; s_m[7][tid] = m.K1; s_m[8][tid] = m.K2;
   }
-  return r;
-}
-
-__global__ void __launch_bounds__(kPbThreads, 4) k_presplit_bits(PbArgs g, int pattern, uint32_t* bits32) {
-  __shared__ uint32_t s_m[9][kPbChunks];
-  __shared__ uint32_t s_ss[kPbSsWords];
-  (void)presplit_block(g, pattern, bits32, s_m, s_ss);
+  __syncthreads();
+  // 2. this thread's chunk
+  const int64_t c = c0 + tid;
+  if (c >= n_chunks) return;
+  const psb::Masks m0 = src.get(c - 1), m1 = src.get(c), m2 = src.get(c + 1);
+  const uint64_t ssw = (uint64_t)src.ss_at(32 * c - 16) | ((uint64_t)src.ss_at(32 * c + 16) << 32);
+  uint32_t need = 0;
+  uint32_t r = psb::rules(m0, m1, m2, ssw, cl, psb::Carry{}, &need);
+  if (need) {
+    const psb::Carry cy = psb::carries(src, c, need);
+    r = psb::rules(m0, m1, m2, ssw, cl, cy, &need);
+  }
+  if (32 * c + 32 > g.n_bytes) r &= (1u << (g.n_bytes - 32 * c)) - 1u;
+  bits32[c] = r;
+  if (c == n_chunks - 1 && (c & 1) == 0) bits32[c + 1] = 0;  // (the last word's upper half)
 }
 
 // number of set bits (chunks) in the bitmap

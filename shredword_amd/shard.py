@@ -42,7 +42,7 @@ def shard_of(buf, str_off, lo, hi):
 
 
 def reassemble(local_ids, local_off, group=None, device=None, concat=True, width=None, width_s=None, id_bits=32,
-               async_op=False):
+               async_op=False, bufs=None):
     """Collective reassembly of per-rank encodes (steps 1-4 above) on every rank.
 
     local_ids: torch int32 [>= local count] on `device` (or int16 holding each id's low 16 bits, e.g.
@@ -66,7 +66,13 @@ def reassemble(local_ids, local_off, group=None, device=None, concat=True, width
     been waited on, in order (Work.wait(): with RCCL the caller's stream waits, the host does
     not; the last work folds the width check into the flag check_bounds reads).  The next
     batch's encode can run meanwhile -- the reassembly of batch k overlaps the encode of batch
-    k + 1; local_ids / local_off must not be rewritten before the wait."""
+    k + 1; local_ids / local_off must not be rewritten before the wait.
+    bufs (with both widths): a dict the call keeps its device buffers in and reuses on the next
+    call with the same dict -- a step loop then allocates nothing.  (A fresh 0.5 GB receive buffer
+    per step went to hipMalloc while the previous one was still in use on the reassembly's
+    stream, and that allocation waited for the device: the next encode could not be issued until
+    the previous reassembly had finished.)  The caller must not reuse a dict before the
+    previous call's buffers are consumed (one dict per batch in flight)."""
     import torch
     import torch.distributed as dist
 
@@ -80,10 +86,18 @@ def reassemble(local_ids, local_off, group=None, device=None, concat=True, width
         if async_op:
             works.append(w)
     dev = device if device is not None else local_ids.device
-    mine = torch.empty(2, dtype=torch.int64, device=dev)
+
+    def buf(name, n, dtype):  # a device buffer, from `bufs` when the caller keeps them
+        if bufs is None:
+            return torch.empty(n, dtype=dtype, device=dev)
+        b = bufs.get(name)
+        if b is None or b.numel() != n or b.dtype != dtype or b.device != dev:
+            b = bufs[name] = torch.empty(n, dtype=dtype, device=dev)
+        return b
+    mine = buf("mine", 2, torch.int64)
     mine[0:1] = local_off[-1:].to(device=dev, dtype=torch.int64)
     mine[1:2].fill_(local_off.numel() - 1)  # (a fill kernel: `mine[1] = n` copies from pageable host memory, synchronously)
-    both = torch.empty(2 * world, dtype=torch.int64, device=dev)
+    both = buf("both", 2 * world, torch.int64)
     gather(both, mine)  # [count_0, n_str_0, count_1, ...]
     counts, n_strs = both[0::2], both[1::2]
     if width is None or width_s is None:  # the one host synchronisation: the gathers' sizes
@@ -109,7 +123,7 @@ def reassemble(local_ids, local_off, group=None, device=None, concat=True, width
         k = min(width, local_ids.numel())
         # (16 bits: the low 16 bits of each id, two's-complement truncation of the int32 value)
         send[:k] = local_ids[:k].to(device=dev, dtype=torch.int32).to(want)
-    recv = torch.empty(world * width, dtype=want, device=dev)
+    recv = buf("recv", world * width, want)
     if wide:
         gather(recv, send)
     else:  # moved as bytes (RCCL and gloo have no 16-bit integer type; an all-gather only copies)
@@ -120,7 +134,7 @@ def reassemble(local_ids, local_off, group=None, device=None, concat=True, width
     else:
         send_o = torch.zeros(width_s, dtype=torch.int64, device=dev)
         send_o[:min(m, width_s)] = local_off[:min(m, width_s)].to(device=dev, dtype=torch.int64)
-    recv_o = torch.empty(world * width_s, dtype=torch.int64, device=dev)
+    recv_o = buf("recv_o", world * width_s, torch.int64)
     gather(recv_o, send_o)
     if not concat:
         res = (recv, counts, width, recv_o, n_strs, width_s)

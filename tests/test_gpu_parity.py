@@ -211,20 +211,12 @@ def test_invalid_utf8_bytes():
 
 @pytest.mark.parametrize("kind,model", [(corpus.MIXED, "bl32k.model"), (corpus.STRESS, "bl50k.model")])
 def test_large_corpus_vs_oracle(kind, model):
-    """64 MB (MIXED) / 24 MB (STRESS) seeded corpora, bit-exact against the multithreaded oracle,
-    with the device pre-split fused into the classification (default: chunks deferred across
-    8 KiB blocks) and as two kernels."""
+    """64 MB (MIXED) / 24 MB (STRESS) seeded corpora, bit-exact against the multithreaded oracle."""
     n = 60000 if kind == corpus.MIXED else 40000
     buf, off = corpus.synth(99, kind, n, 1074 if kind == corpus.MIXED else 600)
     t = tok_for(model)
-    exp = oracle_encode(t.merges, buf, off, "cl100k")
-    L, h = _lib.lib(), t._encoder()
-    try:
-        for fused in (1, 0):
-            _lib.check(L.sw_encoder_set_option(h, _lib.SW_OPT_FUSED_PRESPLIT, fused))
-            assert_same(gpu_encode(t, buf, off), exp)
-    finally:
-        L.sw_encoder_set_option(h, _lib.SW_OPT_FUSED_PRESPLIT, 1)
+    got = gpu_encode(t, buf, off)
+    assert_same(got, oracle_encode(t.merges, buf, off, "cl100k"))
 
 
 def test_device_api_with_torch_buffers():
@@ -279,10 +271,9 @@ def test_dedupe_table_pressure_and_collisions(slots, fp_bits, exact):
 
 
 def test_dedupe_exact_key_prefix_collisions():
-    """Chunks equal in their first 7 (or 14) bytes and length but not after (exact keys up to 14
-    bytes, the first 7 in the entry's claimed word and the rest in its second word; fingerprint
-    keys beyond) must stay apart, each sharing only its own result, in a one-group table where
-    they all meet."""
+    """Chunks equal in their first 7 (or 14) bytes and length but not after (exact keys up to 7
+    bytes, fingerprint keys beyond) must stay apart, each sharing only its own result, in a
+    one-group table where they all meet."""
     rng = np.random.default_rng(11)
     stems = [" abcdefg", " qwertyu", " zxcvbnm", " abcdefghijklm", " abcdefghijklz"]
     words = [st + "".join(chr(0x61 + int(c)) for c in rng.integers(0, 26, size=k))

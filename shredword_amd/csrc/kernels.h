@@ -444,6 +444,112 @@ __device__ __forceinline__ uint32_t lane_merge_reg_loop_wf(const DevTable& t, ui
   return alive;
 }
 
+// the initial ranks of slots g .. g + 3 are in registers before any later slot's lookups issue
+// (lane_merge_lds_wf: the compiler otherwise hoisted all N lookups -- 8 registers each in
+// flight -- to the front: 239 VGPRs at N = 32, 132 with this)
+template <int N>
+__device__ __forceinline__ void rank_group_done(uint32_t (&rk)[N], int g) {
+  if constexpr (N >= 4) {
+    asm volatile("" : "+v"(rk[g]), "+v"(rk[g + 1]), "+v"(rk[g + 2]), "+v"(rk[g + 3])::"memory");
+  } else {
+    asm volatile("" ::: "memory");
+  }
+}
+
+// Alive-set arithmetic on a lane's position mask A (bit k: position k holds a token):
+// next_alive(A, S): for each position of S (a subset of A) the next alive position after it
+// (none past bit 31): the bits just above S, carried through the gaps of A by one addition.
+__device__ __forceinline__ uint32_t next_alive(uint32_t A, uint32_t S) {
+  const uint32_t T = S << 1, G = ~A;
+  return (T & A) | ((G + (T & G)) & A);
+}
+__device__ __forceinline__ uint32_t prev_alive(uint32_t A, uint32_t S) {
+  return __builtin_bitreverse32(next_alive(__builtin_bitreverse32(A), __builtin_bitreverse32(S)));
+}
+
+// The merge loop for a WELL-FORMED table with 16-bit ids, with the ids in LDS and the pairs'
+// ranks in registers as min-ready keys (rank << 5 | slot), every step done on bit masks:
+//   - the winning rank: one min per slot;
+//   - its occurrences M: the slots whose key has that rank (a value names one pair);
+//   - their right partners: next_alive(A, M).  Occurrences overlap only for an (a, a) pair
+//     (two adjacent occurrences of one pair are a, a, a); then they are taken left to right,
+//     each one removing its partner, as merge() does (base.py:29-35);
+//   - the partners die, the occurrences take the new id (LDS stores at their slots), and only the
+//     pairs of the occurrences and of the alive slots before them are looked up again.
+// So a step costs a few instructions per slot (the min, the rank compare, the key updates)
+// instead of two sweeps that carry ids along, and the ids hold no registers.  s_id: this wave's
+// ids, slot k of lane l at s_id[64 k + l] (a wave's accesses to one slot hit 64 banks).
+// Returns the alive mask; the surviving ids are s_id[64 k + lane] for its set bits, in order.
+template <bool kWide, int N>
+__device__ __forceinline__ uint32_t lane_merge_lds_wf(const DevTable& t, const uint32_t (&u)[N / 4], int n,
+                                                      uint32_t* s_id, int lane) {
+  static_assert(N <= 32, "alive masks are 32 bits");
+  constexpr uint32_t KINF = 0xFFFFu << 5;
+  uint32_t rk[N];
+#pragma unroll
+  for (int k = 0; k < N; ++k) s_id[64 * k + lane] = (u[k >> 2] >> (8 * (k & 3))) & 0xFFu;
+  // initial ranks: four lookups in flight at a time (sched barriers cap the live registers)
+#pragma unroll
+  for (int g = 0; g < N; g += 4) {
+#pragma unroll
+    for (int k = g; k < g + 4 && k < N; ++k) {
+      const uint32_t b0 = (u[k >> 2] >> (8 * (k & 3))) & 0xFFu;
+      const uint32_t b1 = (k + 1 < N) ? (u[(k + 1) >> 2] >> (8 * ((k + 1) & 3))) & 0xFFu : 0u;
+      rk[k] = lookup<kWide>(t, b0, b1);
+    }
+#pragma unroll
+    for (int k = g; k < g + 4 && k < N; ++k) rk[k] = ((k + 1 < n) ? (min(rk[k], 0xFFFFu) << 5) : KINF) | (uint32_t)k;
+    rank_group_done<N>(rk, g);
+  }
+  uint32_t alive = (n >= 32) ? 0xFFFFFFFFu : ((1u << n) - 1u);
+  while (true) {
+    uint32_t best = 0xFFFFFFFFu;
+#pragma unroll
+    for (int k = 0; k < N; ++k) best = min(best, rk[k]);
+    const uint32_t nv = best >> 5;
+    if (nv >= 0xFFFFu) break;
+    const uint32_t bound = (nv + 1) << 5;  // (every key is >= best: rank nv <=> key < bound)
+    uint32_t m0 = 0;
+#pragma unroll
+    for (int k = 0; k < N; ++k) m0 |= (rk[k] < bound ? 1u : 0u) << k;
+    uint32_t match = m0, cons = next_alive(alive, m0);
+    if (cons & m0) {  // an (a, a) pair with adjacent occurrences: left to right
+      match = 0;
+      for (uint32_t av = m0; av;) {
+        const uint32_t s = av & (0u - av);
+        match |= s;
+        av &= ~(s | next_alive(alive, s));
+      }
+      cons = next_alive(alive, match);
+    }
+    alive &= ~cons;
+    for (uint32_t m = match; m; m &= m - 1) s_id[64 * (__ffs(m) - 1) + lane] = nv;
+    // a partner that was the last alive slot leaves its occurrence without a right neighbour
+    const uint32_t last = 1u << (31 - __clz(alive));
+    const uint32_t kill = cons | (match & last);
+    uint32_t need = (match | prev_alive(alive, match)) & alive & ~last;
+#pragma unroll
+    for (int k = 0; k < N; ++k) rk[k] = ((kill >> k) & 1u) ? (KINF | (uint32_t)k) : rk[k];
+    while (need) {  // two lookups in flight per round
+      const int j1 = __ffs(need) - 1;
+      need &= need - 1;
+      const int j2 = need ? __ffs(need) - 1 : j1;
+      need &= need - 1;
+      const int x1 = __ffs(next_alive(alive, 1u << j1)) - 1, x2 = __ffs(next_alive(alive, 1u << j2)) - 1;
+      const uint32_t a1 = s_id[64 * j1 + lane], b1 = s_id[64 * x1 + lane];
+      const uint32_t a2 = s_id[64 * j2 + lane], b2 = s_id[64 * x2 + lane];
+      const uint32_t k1 = (min(lookup<kWide>(t, a1, b1), 0xFFFFu) << 5) | (uint32_t)j1;
+      const uint32_t k2 = (min(lookup<kWide>(t, a2, b2), 0xFFFFu) << 5) | (uint32_t)j2;
+#pragma unroll
+      for (int k = 0; k < N; ++k) {
+        rk[k] = (k == j1) ? k1 : rk[k];
+        rk[k] = (k == j2) ? k2 : rk[k];
+      }
+    }
+  }
+  return alive;
+}
+
 template <bool kWide, bool k16, int N, bool kWF = false>
 __device__ __forceinline__ uint32_t lane_merge_reg(const DevTable& t, uint32_t (&id)[N], int n, int* iters = nullptr) {
   uint32_t rk[N];
@@ -1013,25 +1119,44 @@ __device__ __forceinline__ void chunk_words(const uint32_t* words, int64_t last_
 }
 
 // merge loop for the queue entry e of this lane (act); result at res[2 * start ..)
+// (kLds: the well-formed 16-bit loop with the ids in LDS, lane_merge_lds_wf; s_id: the wave's ids)
 template <bool kWide, bool k16, int N, bool kWF>
 __device__ __forceinline__ void merge_entry(const EncArgs& a, const uint32_t* words, int64_t last_word, int64_t mis,
-                                            uint64_t e, bool act) {
+                                            uint64_t e, bool act, uint32_t* s_id) {
+  constexpr bool kLds = kWF && k16 && !kWide;
   const int64_t start = (int64_t)(e >> 33);
   const int n = act ? (int)((e >> 27) & 63u) : 0;
   const uint32_t did = (uint32_t)e & kNoDid;
   uint32_t u[N / 4];
   chunk_words<N>(words, last_word, start + mis, n, u);
-  uint32_t id[N];
+  const int lane = threadIdx.x & 63;
+  uint32_t id[kLds ? 1 : N];
+  uint32_t alive;
+  if constexpr (kLds) {
+    alive = lane_merge_lds_wf<kWide, N>(a.table, u, n, s_id, lane);
+  } else {
 #pragma unroll
-  for (int q = 0; q < N / 4; ++q)
+    for (int q = 0; q < N / 4; ++q)
 #pragma unroll
-    for (int r = 0; r < 4; ++r) id[4 * q + r] = (u[q] >> (8 * r)) & 0xFFu;
-  const uint32_t alive = lane_merge_reg<kWide, k16, N, kWF>(a.table, id, n);
+      for (int r = 0; r < 4; ++r) id[4 * q + r] = (u[q] >> (8 * r)) & 0xFFu;
+    alive = lane_merge_reg<kWide, k16, N, kWF>(a.table, id, n);
+  }
   if (!act) return;
   uint32_t* dst = a.res + 2 * start;
   int m = 0;
   // the dense result head (the first 7 ids as 16 bits, or 3 as 32 bits; see dres)
   uint32_t h0 = 0, h1 = 0, h2 = 0, h3 = 0;
+  if constexpr (kLds) {
+    for (uint32_t al = alive; al; al &= al - 1) {
+      const uint32_t x = s_id[64 * (__ffs(al) - 1) + lane];
+      dst[1 + m] = x;
+      h0 |= m == 0 ? x << 16 : 0u;
+      h1 |= m == 1 ? x : m == 2 ? x << 16 : 0u;
+      h2 |= m == 3 ? x : m == 4 ? x << 16 : 0u;
+      h3 |= m == 5 ? x : m == 6 ? x << 16 : 0u;
+      ++m;
+    }
+  } else {
 #pragma unroll
   for (int k = 0; k < N; ++k) {
     if ((alive >> k) & 1u) {
@@ -1049,6 +1174,7 @@ __device__ __forceinline__ void merge_entry(const EncArgs& a, const uint32_t* wo
       ++m;
     }
   }
+  }
   dst[0] = (uint32_t)m;
   if (did != kNoDid) {
     if (k16) a.dres[did] = make_uint4((uint32_t)m | h0, m <= 7 ? h1 : (uint32_t)start, h2, h3);
@@ -1061,7 +1187,7 @@ __device__ __forceinline__ void merge_entry(const EncArgs& a, const uint32_t* wo
 // k_merge_bucket<N>: queued chunks of buckets [b_lo, b_hi] (length <= N), one per lane;
 // persistent grid-stride over 64-entry batches of the bucket-major queue
 // ---------------------------------------------------------------------------------------
-template <bool kWide, bool k16, int N, bool kWF = false>  // kWF: a well-formed table (lane_merge_reg_loop_wf)
+template <bool kWide, bool k16, int N, bool kWF = false>  // kWF: a well-formed table (lane_merge_lds_wf)
 __global__ void __launch_bounds__(kThreads) k_merge_bucket(EncArgs a, int b_lo, int b_hi) {
   SW_STAMP_INIT;
   const int64_t gw = ((int64_t)blockIdx.x * kThreads + threadIdx.x) >> 6;  // global wave id
@@ -1072,9 +1198,12 @@ __global__ void __launch_bounds__(kThreads) k_merge_bucket(EncArgs a, int b_lo, 
   const int64_t mis = (int64_t)((uintptr_t)a.bytes & 3);
   const uint32_t* words = (const uint32_t*)((uintptr_t)a.bytes - mis);
   const int64_t last_word = (mis + a.n_bytes - 1) >> 2;  // last word holding input bytes
+  constexpr bool kLds = kWF && k16 && !kWide;
+  __shared__ uint32_t s_ids[kLds ? kWaves * 64 * N : 1];  // (lane_merge_lds_wf: the waves' ids)
+  uint32_t* s_id = s_ids + (kLds ? (threadIdx.x >> 6) * 64 * N : 0);
   for (int64_t base = lo + gw * 64; base < hi; base += n_waves * 64) {
     const int64_t i = base + lane;
-    merge_entry<kWide, k16, N, kWF>(a, words, last_word, mis, i < hi ? a.queue[i] : 0, i < hi);
+    merge_entry<kWide, k16, N, kWF>(a, words, last_word, mis, i < hi ? a.queue[i] : 0, i < hi, s_id);
   }
 #ifdef SW_STAMPS
   SW_STAMP(N >= 16 ? 5 : 4);

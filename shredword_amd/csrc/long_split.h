@@ -211,8 +211,11 @@ __device__ __forceinline__ void lp_holes(const LongArgs& L, uint32_t beg, int m,
 // down.  Conflicts are listed for round 0.
 template <bool kWide, bool k16>
 __global__ void __launch_bounds__(kThreads) k_lp_encode(EncArgs a, LongArgs L) {
+  constexpr bool kLds = k16 && !kWide;
+  __shared__ uint32_t s_ids[kLds ? kWaves * 64 * kPieceN : 1];  // (lane_merge_lds_wf: the waves' ids)
   const int64_t np = lp_count(&L.ctl[kLcPieces], L.pcap);
   const int lane = threadIdx.x & 63;
+  uint32_t* s_id = s_ids + (kLds ? (threadIdx.x >> 6) * 64 * kPieceN : 0);
   const uint64_t lt_mask = (lane == 0) ? 0ULL : (~0ULL >> (64 - lane));
   const int64_t mis = (int64_t)((uintptr_t)a.bytes & 3);
   const uint32_t* words = (const uint32_t*)((uintptr_t)a.bytes - mis);
@@ -237,21 +240,32 @@ __global__ void __launch_bounds__(kThreads) k_lp_encode(EncArgs a, LongArgs L) {
     const int n = act ? b1 - b0 : 0;
     uint32_t u[kPieceN / 4];
     chunk_words<kPieceN>(words, last_word, (int64_t)beg + mis, n, u);
-    uint32_t id[kPieceN];
-#pragma unroll
-    for (int q = 0; q < kPieceN / 4; ++q)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) id[4 * q + r] = (u[q] >> (8 * r)) & 0xFFu;
-    const uint32_t alive = lane_merge_reg<kWide, k16, kPieceN, true>(a.table, id, n);
     uint32_t first = 0, last = 0;
     int m = 0;
-#pragma unroll
-    for (int k = 0; k < kPieceN; ++k) {
-      if ((alive >> k) & 1u) {
-        if (own) L.pid[beg + m] = id[k];
-        first = m == 0 ? id[k] : first;
-        last = id[k];
+    if constexpr (kLds) {  // (16-bit ids: the loop with the ids in LDS)
+      const uint32_t alive = lane_merge_lds_wf<kWide, kPieceN>(a.table, u, n, s_id, lane);
+      for (uint32_t al = alive; al; al &= al - 1) {
+        const uint32_t x = s_id[64 * (__ffs(al) - 1) + lane];
+        if (own) L.pid[beg + m] = x;
+        first = m == 0 ? x : first;
+        last = x;
         ++m;
+      }
+    } else {
+      uint32_t id[kPieceN];
+#pragma unroll
+      for (int q = 0; q < kPieceN / 4; ++q)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) id[4 * q + r] = (u[q] >> (8 * r)) & 0xFFu;
+      const uint32_t alive = lane_merge_reg<kWide, k16, kPieceN, true>(a.table, id, n);
+#pragma unroll
+      for (int k = 0; k < kPieceN; ++k) {
+        if ((alive >> k) & 1u) {
+          if (own) L.pid[beg + m] = id[k];
+          first = m == 0 ? id[k] : first;
+          last = id[k];
+          ++m;
+        }
       }
     }
     const uint32_t x = (uint32_t)__shfl_up((int)last, 1, 64);
@@ -349,6 +363,10 @@ __device__ __forceinline__ void lp_absorb(const LongArgs& L, uint32_t j, uint32_
 // the windows of round r, one lane each: <= kShort bytes encoded in registers, longer listed
 template <bool kWide, bool k16>
 __global__ void __launch_bounds__(kThreads) k_lp_windows(EncArgs a, LongArgs L, int r) {
+  constexpr bool kLds = k16 && !kWide;
+  __shared__ uint32_t s_ids[kLds ? kWaves * 64 * kShort : 1];  // (lane_merge_lds_wf: the waves' ids)
+  const int lane = threadIdx.x & 63;
+  uint32_t* s_id = s_ids + (kLds ? (threadIdx.x >> 6) * 64 * kShort : 0);
   const int64_t nh = lp_count(&L.ctl[kLcHead + r], L.pcap), np = lp_count(&L.ctl[kLcPieces], L.pcap);
   const int64_t mis = (int64_t)((uintptr_t)a.bytes & 3);
   const uint32_t* words = (const uint32_t*)((uintptr_t)a.bytes - mis);
@@ -374,17 +392,23 @@ __global__ void __launch_bounds__(kThreads) k_lp_windows(EncArgs a, LongArgs L, 
     if (!__ballot(act)) continue;
     uint32_t u[kShort / 4];
     chunk_words<kShort>(words, last_word, (int64_t)beg + mis, act ? n : 0, u);
-    uint32_t id[kShort];
-#pragma unroll
-    for (int q = 0; q < kShort / 4; ++q)
-#pragma unroll
-      for (int b = 0; b < 4; ++b) id[4 * q + b] = (u[q] >> (8 * b)) & 0xFFu;
-    const uint32_t alive = lane_merge_reg<kWide, k16, kShort, true>(a.table, id, act ? n : 0);
-    if (!act) continue;
     uint32_t m = 0;
+    if constexpr (kLds) {  // (16-bit ids: the loop with the ids in LDS)
+      const uint32_t alive = lane_merge_lds_wf<kWide, kShort>(a.table, u, act ? n : 0, s_id, lane);
+      if (!act) continue;
+      for (uint32_t al = alive; al; al &= al - 1) L.pid[beg + m++] = s_id[64 * (__ffs(al) - 1) + lane];
+    } else {
+      uint32_t id[kShort];
 #pragma unroll
-    for (int k = 0; k < kShort; ++k)
-      if ((alive >> k) & 1u) L.pid[beg + m++] = id[k];
+      for (int q = 0; q < kShort / 4; ++q)
+#pragma unroll
+        for (int b = 0; b < 4; ++b) id[4 * q + b] = (u[q] >> (8 * b)) & 0xFFu;
+      const uint32_t alive = lane_merge_reg<kWide, k16, kShort, true>(a.table, id, act ? n : 0);
+      if (!act) continue;
+#pragma unroll
+      for (int k = 0; k < kShort; ++k)
+        if ((alive >> k) & 1u) L.pid[beg + m++] = id[k];
+    }
     lp_holes(L, beg, (int)m, n);
     lp_absorb(L, j, last, m, r);
   }

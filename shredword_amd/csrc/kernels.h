@@ -488,7 +488,7 @@ __device__ __forceinline__ uint32_t lane_merge_lds_wf(const DevTable& t, const u
   uint32_t rk[N];
 #pragma unroll
   for (int k = 0; k < N; ++k) s_id[64 * k + lane] = (u[k >> 2] >> (8 * (k & 3))) & 0xFFu;
-  // initial ranks: four lookups in flight at a time (sched barriers cap the live registers)
+  // initial ranks: four lookups in flight at a time
 #pragma unroll
   for (int g = 0; g < N; g += 4) {
 #pragma unroll
@@ -1120,15 +1120,14 @@ __device__ __forceinline__ void chunk_words(const uint32_t* words, int64_t last_
 
 // merge loop for the queue entry e of this lane (act); result at res[2 * start ..)
 // (kLds: the well-formed 16-bit loop with the ids in LDS, lane_merge_lds_wf; s_id: the wave's ids)
+// (u: the chunk's bytes, chunk_words<N> of the entry -- loaded by the caller, a batch ahead)
 template <bool kWide, bool k16, int N, bool kWF>
-__device__ __forceinline__ void merge_entry(const EncArgs& a, const uint32_t* words, int64_t last_word, int64_t mis,
-                                            uint64_t e, bool act, uint32_t* s_id) {
+__device__ __forceinline__ void merge_entry(const EncArgs& a, const uint32_t (&u)[N / 4], uint64_t e, bool act,
+                                            uint32_t* s_id) {
   constexpr bool kLds = kWF && k16 && !kWide;
   const int64_t start = (int64_t)(e >> 33);
   const int n = act ? (int)((e >> 27) & 63u) : 0;
   const uint32_t did = (uint32_t)e & kNoDid;
-  uint32_t u[N / 4];
-  chunk_words<N>(words, last_word, start + mis, n, u);
   const int lane = threadIdx.x & 63;
   uint32_t id[kLds ? 1 : N];
   uint32_t alive;
@@ -1201,9 +1200,18 @@ __global__ void __launch_bounds__(kThreads) k_merge_bucket(EncArgs a, int b_lo, 
   constexpr bool kLds = kWF && k16 && !kWide;
   __shared__ uint32_t s_ids[kLds ? kWaves * 64 * N : 1];  // (lane_merge_lds_wf: the waves' ids)
   uint32_t* s_id = s_ids + (kLds ? (threadIdx.x >> 6) * 64 * N : 0);
+  // software-pipelined: the next batch's queue entry and chunk bytes load before this batch's
+  // merge loop runs (two dependent round trips per batch off the critical path)
+  int64_t i = lo + gw * 64 + lane;
+  uint64_t e = i < hi ? a.queue[i] : 0;
   for (int64_t base = lo + gw * 64; base < hi; base += n_waves * 64) {
-    const int64_t i = base + lane;
-    merge_entry<kWide, k16, N, kWF>(a, words, last_word, mis, i < hi ? a.queue[i] : 0, i < hi, s_id);
+    uint32_t u[N / 4];
+    chunk_words<N>(words, last_word, (int64_t)(e >> 33) + mis, i < hi ? (int)((e >> 27) & 63u) : 0, u);
+    const int64_t i2 = i + n_waves * 64;
+    const uint64_t e2 = i2 < hi ? a.queue[i2] : 0;
+    merge_entry<kWide, k16, N, kWF>(a, u, e, i < hi, s_id);
+    i = i2;
+    e = e2;
   }
 #ifdef SW_STAMPS
   SW_STAMP(N >= 16 ? 5 : 4);

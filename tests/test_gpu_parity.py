@@ -179,6 +179,40 @@ def test_random_illformed_tables(seed):
         assert_same(gpu_encode(t, buf, off), oracle_encode(merges, buf, off, pat))
 
 
+@pytest.mark.parametrize("seed", range(8))
+def test_random_wellformed_tables(seed):
+    """Random WELL-FORMED tables (every value new, >= 256 and larger than its pair's members)
+    take the bit-mask merge loop with the ids in LDS (kernels.h lane_merge_lds_wf) in every
+    merge bucket and in the long chunks' pieces and windows: a 3-letter alphabet with many (a, a)
+    pairs (runs resolved left to right, base.py:29-35), chunks of every length 1..40 and a few
+    long ones, against the oracle."""
+    r = random.Random(100 + seed)
+    alpha = list(b"abc")
+    ids = list(alpha)
+    merges = {}
+    nxt = 256
+    for _ in range(r.randint(20, 400)):
+        a, b = r.choice(ids), r.choice(ids)
+        if r.random() < 0.3:
+            b = a  # (a, a) pairs
+        if (a, b) in merges:
+            continue
+        merges[(a, b)] = nxt
+        ids.append(nxt)
+        nxt += 1
+    datas = [bytes(r.choice(b"abc") for _ in range(n)) for n in range(0, 41) for _ in range(20)]
+    datas += [bytes(r.choice(b"aab") for _ in range(r.randint(33, 3000))) for _ in range(20)]
+    datas += [b"a" * n for n in range(1, 70)]
+    buf, off = pack(datas)
+    t = sa.Tokenizer()
+    t.merges = merges
+    L = _lib.lib()
+    assert L.sw_encoder_get_info(t._encoder(), _lib.SW_INFO_IDS16) == 1
+    assert L.sw_encoder_get_info(t._encoder(), _lib.SW_INFO_SPLIT) == 1
+    t.pattern = PAT_STR["none"]
+    assert_same(gpu_encode(t, buf, off), oracle_encode(merges, buf, off, "none"))
+
+
 def test_wide_ids_table():
     """Ids > 65535 (e.g. vocabularies past 64k): the 16-byte-slot table path."""
     base = load_model_merges("bl32k.model")

@@ -243,14 +243,18 @@ def test_invalid_utf8_bytes():
         t.pattern = ""
 
 
-@pytest.mark.parametrize("kind,model", [(corpus.MIXED, "bl32k.model"), (corpus.STRESS, "bl50k.model")])
-def test_large_corpus_vs_oracle(kind, model):
-    """64 MB (MIXED) / 24 MB (STRESS) seeded corpora, bit-exact against the multithreaded oracle."""
+@pytest.mark.parametrize("kind,model,pattern", [(corpus.MIXED, "bl32k.model", "cl100k"),
+                                               (corpus.STRESS, "bl50k.model", "cl100k"),
+                                               (corpus.MIXED, "bl32k.model", "gpt2")])
+def test_large_corpus_vs_oracle(kind, model, pattern):
+    """64 MB (MIXED) / 24 MB (STRESS) seeded corpora, bit-exact against the multithreaded oracle;
+    the GPT-2 pattern's device pre-split at 64 MB too (checked against the oracle directly, not
+    only against the host pre-split)."""
     n = 60000 if kind == corpus.MIXED else 40000
     buf, off = corpus.synth(99, kind, n, 1074 if kind == corpus.MIXED else 600)
-    t = tok_for(model)
+    t = tok_for(model, pattern)
     got = gpu_encode(t, buf, off)
-    assert_same(got, oracle_encode(t.merges, buf, off, "cl100k"))
+    assert_same(got, oracle_encode(t.merges, buf, off, pattern))
 
 
 def test_device_api_with_torch_buffers():

@@ -865,23 +865,26 @@ __device__ __forceinline__ void classify_tile(const EncArgs& a, int64_t tile, ui
   const uint64_t bw = (lane < kTileWords && w0 + lane < a.n_words) ? SW_LDNT2(&a.bits[w0 + lane]) : 0ULL;
   const int64_t s_first = a.tile_slo[tile];  // (prefetched: used by step 6)
 
-  // 2. chunk starts in [t0, t1): lane w owns bitmap word w
-  constexpr int nw_tile = kTile / 64;
-  uint64_t myword = 0;
-  if (lane < nw_tile) {
-    myword = bw;
-    const int64_t lim = t1 - (t0 + 64 * lane);  // bits at or beyond t1 belong to the next tile
-    if (lim <= 0) myword = 0;
-    else if (lim < 64) myword &= (1ULL << lim) - 1;
+  // 2. chunk starts in [t0, t1): lane l owns bits 32 l .. 32 l + 31 of the tile (half of bitmap
+  //    word l / 2: all 64 lanes enumerate, half as many starts each as with a word per lane)
+  static_assert(kTile == 64 * 32, "a tile's bits are 64 lanes x 32");
+  uint32_t myhalf;
+  {
+    const uint32_t lo = (uint32_t)__shfl((int)(uint32_t)bw, lane >> 1, 64);
+    const uint32_t hi = (uint32_t)__shfl((int)(uint32_t)(bw >> 32), lane >> 1, 64);
+    myhalf = (lane & 1) ? hi : lo;
+    const int64_t lim = t1 - (t0 + 32 * lane);  // bits at or beyond t1 belong to the next tile
+    if (lim <= 0) myhalf = 0;
+    else if (lim < 32) myhalf &= (1u << lim) - 1u;
   }
-  const uint32_t cnt = (uint32_t)__popcll(myword);
+  const uint32_t cnt = (uint32_t)__popc(myhalf);
   const uint32_t incl = wave_incl_scan(cnt, lane);
   const int C = (int)__shfl(incl, 63, 64);
   {
-    uint64_t x = myword;
+    uint32_t x = myhalf;
     uint32_t k = incl - cnt;
     while (x) {
-      s_cstart[k++] = (uint16_t)(64 * lane + __ffsll((long long)x) - 1);
+      s_cstart[k++] = (uint16_t)(32 * lane + __ffs(x) - 1);
       x &= x - 1;
     }
   }

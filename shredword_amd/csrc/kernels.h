@@ -738,6 +738,7 @@ __device__ __forceinline__ DdOut dedupe_claim(const EncArgs& a, const uint32_t* 
   uint32_t h = 0x9E3779B9u ^ ((uint32_t)n << 24);
 #pragma unroll
   for (int q = 0; q < kShort / 4; ++q) {
+    if (!__ballot(q < nw)) break;  // (no lane has word q: the wave stops at its longest chunk)
     if (q < nw) {
       h = (h ^ u[q]) * 0x85EBCA77u;
       h ^= h >> 13;

@@ -1945,10 +1945,20 @@ __device__ __forceinline__ void compact_tile(const EncArgs& a, int64_t t, int64_
         const int64_t pL = (int64_t)__shfl((long long)p, L, 64);
         const uint32_t oL = (uint32_t)__shfl((int)o, L, 64), mL = (uint32_t)__shfl((int)m, L, 64);
         const uint32_t loL = oL - gbase;
-        for (uint32_t k = 3 + lane; k < mL; k += 64) {
-          const int32_t id = (int32_t)a.res[2 * pL + 1 + k];
-          if (loL + k < (uint32_t)kOutCapW) s_out[loL + k] = id;
-          else dst[oL + k] = (OutT)id;
+        for (uint32_t k0 = 3; k0 < mL; k0 += 256) {  // (four loads in flight per lane, then the stores)
+          int32_t id[4];
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const uint32_t k = k0 + 64 * q + lane;
+            id[q] = k < mL ? (int32_t)a.res[2 * pL + 1 + k] : 0;
+          }
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const uint32_t k = k0 + 64 * q + lane;
+            if (k >= mL) break;
+            if (loL + k < (uint32_t)kOutCapW) s_out[loL + k] = id[q];
+            else dst[oL + k] = (OutT)id[q];
+          }
         }
       }
       const uint32_t got = (uint32_t)__shfl((int)o, sj & 63, 64);

@@ -1937,7 +1937,14 @@ __device__ __forceinline__ void compact_tile(const EncArgs& a, int64_t t, int64_
           if (hm > 1) put(1, q.z);
           if (hm > 2) put(2, q.w);
         }
-        for (uint32_t k = hm; k < mm; ++k) put(k, a.res[2 * p + 1 + k]);
+        for (uint32_t k0 = hm; k0 < mm; k0 += 4) {  // (four loads in flight, then their stores)
+          uint32_t x[4];
+#pragma unroll
+          for (int q = 0; q < 4; ++q) x[q] = k0 + q < mm ? a.res[2 * p + 1 + k0 + q] : 0u;
+#pragma unroll
+          for (int q = 0; q < 4; ++q)
+            if (k0 + q < mm) put(k0 + q, x[q]);
+        }
       }
       // long results (C5: whole 4 KiB chunks): one coalesced copy by the whole wave each
       for (uint64_t lm = __ballot(ref && m > kLaneCopy); lm; lm &= lm - 1) {

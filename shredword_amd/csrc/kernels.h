@@ -1893,7 +1893,15 @@ __device__ __forceinline__ void compact_tile(const EncArgs& a, int64_t t, int64_
       nref += __popcll(mk);
     }
     wave_sync_mem();
-    for (int i = lane; i < min(nref, kRefCap); i += 64) s_rq[i] = ref_head(a, (int32_t)s_rp[i]);
+    {  // (both gathers of a group in flight before either lands in LDS)
+      static_assert(kRefCap == 128, "two gathers per lane");
+      const int nr = min(nref, kRefCap);
+      uint4 q0 = make_uint4(0, 0, 0, 0), q1 = make_uint4(0, 0, 0, 0);
+      if (lane < nr) q0 = ref_head(a, (int32_t)s_rp[lane]);
+      if (lane + 64 < nr) q1 = ref_head(a, (int32_t)s_rp[lane + 64]);
+      if (lane < nr) s_rq[lane] = q0;
+      if (lane + 64 < nr) s_rq[lane + 64] = q1;
+    }
     wave_sync_mem();
     SW_STAMP(9);
     const uint32_t gbase = carry;  // the group's first id, tile-relative

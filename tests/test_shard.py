@@ -97,6 +97,19 @@ def _rank_main(rank, world, port, fixture, model, result_dir):
             got_off.append(torch.tensor([disp]))
             ok = ok and np.array_equal(torch.cat(got_ids).numpy(), d["ids"])
             ok = ok and np.array_equal(torch.cat(got_off).numpy(), d["ids_off"])
+        # receive buffers kept across calls (bufs, as bench.py's step loop does): the second call
+        # lands in the first call's tensors, and both compact to the whole batch
+        keep, ptr = {}, None
+        for rep in range(2):
+            works, res = shard.reassemble(t_ids, t_off, None, torch.device("cpu"), concat=False, width=len(buf),
+                                          width_s=len(off), id_bits=32, async_op=True, bufs=keep)
+            for w in works:
+                w.wait()
+            ok = ok and (ptr is None or res[0].data_ptr() == ptr)
+            ptr = res[0].data_ptr()
+            out_ids, out_off = shard.compact(res, 32)
+            ok = ok and np.array_equal(out_ids[:len(d["ids"])].numpy(), d["ids"])
+            ok = ok and np.array_equal(out_off[:len(d["ids_off"])].numpy(), d["ids_off"])
         shard.check_bounds()
         try:  # async needs the bounds (no host synchronisation allowed)
             shard.reassemble(t_ids, t_off, None, torch.device("cpu"), concat=False, async_op=True)

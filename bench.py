@@ -66,6 +66,8 @@ def parse():
     ap.add_argument("--dedupe-slots", type=int, default=0, help="A/B only: cap the dedupe table (power of two)")
     ap.add_argument("--no-dedupe-exact", action="store_true", help="A/B only: fingerprint keys for every chunk")
     ap.add_argument("--no-merge-streams", action="store_true", help="A/B only: merge kernels one after another")
+    ap.add_argument("--no-fused", action="store_true",
+                    help="A/B only: the device pre-split as its own kernel before k_classify (same results)")
     ap.add_argument("--pipe-dma", action="store_true", help="A/B only: e2e pipeline copies by DMA, not kernels")
     ap.add_argument("--pipe-depth", type=int, default=0, help="A/B only: e2e pipeline runs in flight (2..4)")
     ap.add_argument("--pipe-run-mb", type=int, default=0, help="A/B only: e2e pipeline run size (MiB)")
@@ -146,6 +148,8 @@ def main():
         _lib.check(L.sw_encoder_set_option(h, _lib.SW_OPT_DEDUPE_EXACT, 0))
     if args.no_merge_streams:
         _lib.check(L.sw_encoder_set_option(h, _lib.SW_OPT_MERGE_STREAMS, 0))
+    if args.no_fused:
+        _lib.check(L.sw_encoder_set_option(h, _lib.SW_OPT_FUSED_PRESPLIT, 0))
     if args.pipe_dma:
         _lib.check(L.sw_encoder_set_option(h, _lib.SW_OPT_PIPE_COPY_KERNELS, 0))
     if args.pipe_depth:

@@ -136,7 +136,11 @@ int32_t sw_encoder_reserve(sw_encoder* h, int64_t max_bytes, int64_t max_strings
  *                          run side by side on forked streams (joined before the counts); 0: one
  *                          after another on the launch stream.  Results identical. */
 #define SW_OPT_MERGE_STREAMS 13
-/* (options 14 and 15 were A/B knobs of round 2, removed: set_option rejects them) */
+/*   SW_OPT_FUSED_PRESPLIT  1 (default): the device pre-split of sw_encode_device (no caller bitmap) runs
+ *                          inside the classification kernel (k_split_classify: the input is read once,
+ *                          the bitmap is not read back); 0: as its own kernel first.  Results identical. */
+#define SW_OPT_FUSED_PRESPLIT 14
+/* (option 15 was an A/B knob of round 2, removed: set_option rejects it) */
 /*   SW_OPT_OUT_BITS        32 (default): sw_encode_device writes int32 ids; 16: it writes uint16
  *                          ids (d_out_ids is then a uint16_t*; only for tables whose every id
  *                          fits, SW_INFO_IDS16 -- SW_ERR_ARG otherwise).  The multi-GPU driver's

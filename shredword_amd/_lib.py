@@ -29,6 +29,7 @@ SW_OPT_DEDUPE_EXACT = 10
 SW_OPT_PIPE_COPY_KERNELS = 11
 SW_OPT_PIPE_DEPTH = 12
 SW_OPT_MERGE_STREAMS = 13
+SW_OPT_FUSED_PRESPLIT = 14
 SW_OPT_OUT_BITS = 16
 SW_INFO_MERGES, SW_INFO_CHUNK_ENTRIES, SW_INFO_WIDE_TABLE, SW_INFO_IDS16, SW_INFO_SPLIT = 1, 2, 3, 4, 5
 

@@ -35,6 +35,7 @@
 #include "kernels.h"
 #include "long_split.h"
 #include "presplit_kernel.h"
+#include "split_classify.h"
 #include "shredword_hip.h"
 #include "table.h"
 
@@ -140,6 +141,8 @@ struct sw_encoder {
   int32_t pattern = SW_PAT_CL100K;    // SW_OPT_PATTERN: device pre-split of sw_encode_device(bits = NULL)
   bool host_presplit = false;         // SW_OPT_HOST_PRESPLIT: sw_encode_batch pre-splits on the host
   uint64_t* d_pbits = nullptr;        // [n_bytes / 64] device pre-split bitmap
+  uint32_t* d_edge = nullptr;         // [kEdgeWords][n_tiles + 1] k_edges: the tile boundaries' masks and words
+  bool fused_presplit = true;         // SW_OPT_FUSED_PRESPLIT: the device pre-split inside k_split_classify
   unsigned long long* d_pcount = nullptr;
   uint32_t dedupe_fp_mask = (1u << 26) - 1;
   uint32_t* d_tile_cnt = nullptr;
@@ -173,7 +176,7 @@ struct DeviceGuard {
 };
 
 void free_workspace(sw_encoder* h) {
-  (void)hipFree(h->d_scratch); (void)hipFree(h->d_res); (void)hipFree(h->d_pbits); (void)hipFree(h->d_pcount); (void)hipFree(h->d_part);
+  (void)hipFree(h->d_scratch); (void)hipFree(h->d_res); (void)hipFree(h->d_pbits); (void)hipFree(h->d_edge); (void)hipFree(h->d_pcount); (void)hipFree(h->d_part);
   (void)hipFree(h->d_tile_slo); (void)hipFree(h->d_stamps);
   (void)hipFree(h->d_tile_slots); (void)hipFree(h->d_tile_nref); (void)hipFree(h->d_rlist); (void)hipFree(h->d_queue); (void)hipFree(h->d_bcnt); (void)hipFree(h->d_boff);
   (void)hipFree(h->d_qtotal);
@@ -185,7 +188,7 @@ void free_workspace(sw_encoder* h) {
   h->d_dres = nullptr; h->d_big = nullptr; h->d_dcnt = nullptr; h->d_lp = nullptr; h->d_lpart = nullptr;
   h->lp = LongArgs{};
   (void)hipFree(h->d_total);
-  h->d_scratch = nullptr; h->d_res = nullptr; h->d_pbits = nullptr; h->d_pcount = nullptr; h->d_part = nullptr;
+  h->d_scratch = nullptr; h->d_res = nullptr; h->d_pbits = nullptr; h->d_edge = nullptr; h->d_pcount = nullptr; h->d_part = nullptr;
   h->d_dtab = nullptr; h->d_tile_base = nullptr; h->d_tile_cnt = nullptr; h->d_total = nullptr;
   h->cap_bytes = -1; h->cap_str = -1;
 }
@@ -269,6 +272,7 @@ int32_t ensure_workspace(sw_encoder* h, int64_t n_bytes) {
   HIP_TRY(hipMalloc(&h->d_tile_cnt, sizeof(uint32_t) * n_tiles));
   HIP_TRY(hipMalloc(&h->d_total, sizeof(int64_t)));
   HIP_TRY(hipMalloc(&h->d_pbits, sizeof(uint64_t) * ((nb + 63) / 64)));
+  HIP_TRY(hipMalloc(&h->d_edge, sizeof(uint32_t) * kEdgeWords * (n_tiles + 1)));
   HIP_TRY(hipMalloc(&h->d_pcount, sizeof(unsigned long long)));
 #ifdef SW_STAMPS
   HIP_TRY(hipMalloc(&h->d_stamps, sizeof(unsigned long long) * 32 * 64));  // 64 copies per counter
@@ -525,6 +529,7 @@ extern "C" int32_t sw_encoder_set_option(sw_encoder* h, int32_t option, int64_t 
     case SW_OPT_LONG_SPLIT: h->long_split = value != 0; return SW_OK;
     case SW_OPT_PIPE_COPY_KERNELS: h->pipe_kcopy = value != 0; return SW_OK;
     case SW_OPT_MERGE_STREAMS: h->merge_fork = value != 0; return SW_OK;
+    case SW_OPT_FUSED_PRESPLIT: h->fused_presplit = value != 0; return SW_OK;
     case SW_OPT_OUT_BITS:
       if (value != 16 && value != 32) return fail(SW_ERR_ARG, "SW_OPT_OUT_BITS: 16 or 32");
       if (value == 16 && !h->ids16) return fail(SW_ERR_ARG, "SW_OPT_OUT_BITS 16: a table id does not fit 16 bits");
@@ -690,8 +695,11 @@ int32_t encode_device(sw_encoder* h, const uint8_t* d_bytes, int64_t n_bytes, co
   if (n_tiles > 0)  // (the pre-split and k_classify start from each tile's first string)
     hipLaunchKernelGGL(k_tile_strings, dim3((unsigned)((n_tiles + 255) / 256)), dim3(256), 0, st, d_str_off, n_str,
                        n_tiles, h->d_tile_slo);
-  if (n_tiles > 0 && !d_chunk_bits) {  // the full path: device pre-split first
-    HIP_TRY(launch_presplit(st, d_bytes, n_bytes, d_str_off, n_str, h->pattern, h->d_pbits, h->d_tile_slo));
+  // the full path (no caller bitmap): the device pre-split, fused into the classification
+  // (k_edges + k_split_classify) or as its own kernel first (SW_OPT_FUSED_PRESPLIT 0)
+  const bool fused = n_tiles > 0 && !d_chunk_bits && h->fused_presplit;
+  if (n_tiles > 0 && !d_chunk_bits) {
+    if (!fused) HIP_TRY(launch_presplit(st, d_bytes, n_bytes, d_str_off, n_str, h->pattern, h->d_pbits, h->d_tile_slo));
     d_chunk_bits = h->d_pbits;
   }
   if (n_tiles > 0) {
@@ -713,7 +721,15 @@ int32_t encode_device(sw_encoder* h, const uint8_t* d_bytes, int64_t n_bytes, co
     a.lstart = h->lp.wstart; a.llen = h->lp.wlen; a.n_long = &h->lp.ctl[kLcWave]; a.lcap = h->lp.lcap;
     const bool split = h->split_ok && h->long_split;  // (split + verify needs a well-formed table)
     if (h->dedupe) HIP_TRY(hipMemsetAsync(h->d_dtab, 0, sizeof(uint64_t) * ((size_t)a.dmask + 1), st));
-    hipLaunchKernelGGL(k_classify, dim3((unsigned)((n_tiles + kWaves - 1) / kWaves)), dim3(kThreads), 0, st, a);
+    if (fused) {
+      const PbArgs pg{d_bytes, n_bytes, d_str_off, n_str, h->d_tile_slo};
+      hipLaunchKernelGGL(k_edges, dim3((unsigned)((n_tiles + 1 + 255) / 256)), dim3(256), 0, st, pg, n_tiles,
+                         (int)h->pattern, h->d_edge);
+      hipLaunchKernelGGL(k_split_classify, dim3((unsigned)((n_tiles + kWaves - 1) / kWaves)), dim3(kThreads), 0, st, a,
+                         pg, (int)h->pattern, (const uint32_t*)h->d_edge, (uint32_t*)h->d_pbits);
+    } else {
+      hipLaunchKernelGGL(k_classify, dim3((unsigned)((n_tiles + kWaves - 1) / kWaves)), dim3(kThreads), 0, st, a);
+    }
     HIP_TRY(hipGetLastError());
     HIP_TRY(launch_scan(st, h->d_bcnt, kNumBuckets * n_tiles, h->d_part, h->d_boff, h->d_qtotal));
     hipLaunchKernelGGL(k_scatter, dim3((unsigned)((n_tiles + 3) / 4)), dim3(kThreads), 0, st, a);

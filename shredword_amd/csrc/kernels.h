@@ -833,12 +833,17 @@ constexpr int kWinWords = kWin / 4 + 8;
 // function of (tile, base) (compact_tile) the compiler fits 78 VGPRs, 6 waves, no spill: 1.11 ->
 // 0.95 ms (profiles/r2_k.md).
 #define SW_CLS_ATTR __attribute__((amdgpu_waves_per_eu(6, 6)))
-// one tile (the body of k_classify's tile loop)
+// (a last chunk that runs more than kShort bytes past its tile, end unknown to the tile: long,
+// its length found from the complete bitmap by k_lp_prep)
+constexpr int kRelEndLong = 1 << 30;
+__device__ __forceinline__ void classify_chunks(const EncArgs& a, int64_t tile, const uint32_t* s_b32,
+                                                uint16_t* s_cstart, uint16_t* s_qbuf, uint32_t myhalf, int rel_end,
+                                                int64_t s_first);
+
+// one tile (the body of k_classify's tile loop): the chunk starts from the uploaded bitmap
 __device__ __forceinline__ void classify_tile(const EncArgs& a, int64_t tile, uint32_t* s_b32, uint16_t* s_cstart,
                                               uint16_t* s_qbuf) {
-  SW_STAMP_INIT;
   const int lane = threadIdx.x & 63;
-  const uint64_t lt_mask = (lane == 0) ? 0ULL : (~0ULL >> (64 - lane));
   const int64_t t0 = tile * kTile;
   const int64_t t1 = min(t0 + (int64_t)kTile, a.n_bytes);
   const int64_t w0 = t0 >> 6;
@@ -878,17 +883,6 @@ __device__ __forceinline__ void classify_tile(const EncArgs& a, int64_t tile, ui
     if (lim <= 0) myhalf = 0;
     else if (lim < 32) myhalf &= (1u << lim) - 1u;
   }
-  const uint32_t cnt = (uint32_t)__popc(myhalf);
-  const uint32_t incl = wave_incl_scan(cnt, lane);
-  const int C = (int)__shfl(incl, 63, 64);
-  {
-    uint32_t x = myhalf;
-    uint32_t k = incl - cnt;
-    while (x) {
-      s_cstart[k++] = (uint16_t)(32 * lane + __ffs(x) - 1);
-      x &= x - 1;
-    }
-  }
   // end of the last chunk, tile-relative: the first chunk start at or after t1 (staged halo
   // word first; a launch is < 2^31 bytes, so tile-relative positions fit an int)
   int64_t last_end = a.n_bytes;
@@ -904,13 +898,37 @@ __device__ __forceinline__ void classify_tile(const EncArgs& a, int64_t tile, ui
       const int src = __ffsll((long long)has) - 1;
       const int64_t q = t0 + 64 * (int64_t)src + __ffsll((long long)__shfl(hw, src, 64)) - 1;
       last_end = min(q, a.n_bytes);
-    } else if (C > 0) {
+    } else if (__ballot(myhalf != 0)) {
       // (a chunk running past the halo)
       const int64_t q = next_set_bit(a.bits, a.n_words, t0 + 64 * kTileWords, a.n_bytes);
       last_end = min(q, a.n_bytes);
     }
   }
-  const int rel_end = (int)(last_end - t0);
+  classify_chunks(a, tile, s_b32, s_cstart, s_qbuf, myhalf, (int)(last_end - t0), s_first);
+}
+
+// The tile's chunks from its chunk-start bits on: lane l holds bits 32 l .. 32 l + 31 of the tile
+// (cut at the tile's end), rel_end is the end of the tile's last chunk relative to t0 (or
+// kRelEndLong), s_b32 the tile's bytes from t0 in LDS (with kWin - kTile bytes of halo).
+__device__ __forceinline__ void classify_chunks(const EncArgs& a, int64_t tile, const uint32_t* s_b32,
+                                                uint16_t* s_cstart, uint16_t* s_qbuf, uint32_t myhalf, int rel_end,
+                                                int64_t s_first) {
+  SW_STAMP_INIT;
+  const int lane = threadIdx.x & 63;
+  const uint64_t lt_mask = (lane == 0) ? 0ULL : (~0ULL >> (64 - lane));
+  const int64_t t0 = tile * kTile;
+  const int64_t t1 = min(t0 + (int64_t)kTile, a.n_bytes);
+  const uint32_t cnt = (uint32_t)__popc(myhalf);
+  const uint32_t incl = wave_incl_scan(cnt, lane);
+  const int C = (int)__shfl(incl, 63, 64);
+  {
+    uint32_t x = myhalf;
+    uint32_t k = incl - cnt;
+    while (x) {
+      s_cstart[k++] = (uint16_t)(32 * lane + __ffs(x) - 1);
+      x &= x - 1;
+    }
+  }
   wave_sync_mem();
   SW_STAMP(0);
 

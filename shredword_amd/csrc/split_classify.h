@@ -1,0 +1,267 @@
+// The device pre-split fused into the classification: k_split_classify, one wave per 2 KiB tile,
+// computes the tile's chunk starts (apply_regex, shredword/base.py:38-58, the bit-parallel rules
+// of presplit_bits.h) from the tile's bytes staged once in LDS, and goes straight on to the
+// classification of its chunks (classify_chunks, kernels.h) -- the input is read once and the
+// chunk-start bitmap never makes a round trip through HBM before it is used.  The bitmap is
+// still written (one dword per lane, coalesced) for the later kernels that need a chunk's end
+// past its tile (k_lp_prep) and for sw_presplit_device's callers.
+//
+// A lane's rules read its neighbours' class masks: inside the tile they come from LDS; the two
+// the tile does not compute -- lane 0's left neighbour (the previous tile's last 32 bytes) and
+// lane 63's right one (the next tile's first 32 bytes) -- come from k_edges, a small pass over
+// the tile boundaries before it: per boundary b (byte 2048 b) the class masks of the 32 bytes
+// after it and the final chunk-start word of those 32 bytes (which lane 0 of tile b takes as its
+// own, and which tells tile b - 1 where its last chunk ends).  Included by encode.hip only.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "kernels.h"
+#include "presplit_bits.h"
+#include "presplit_kernel.h"
+
+namespace sw {
+
+constexpr int kEdgeWords = 10;  // per boundary: the 9 class masks of its first 32 bytes + their chunk starts
+
+// string-start bits of [p, p + 32) (bit k = byte p + k; the batch end n_bytes counts as one),
+// the search narrowed to the strings of p's tile by tile_slo (k_tile_strings)
+__device__ __forceinline__ uint32_t ss32_hint(const int64_t* str_off, int64_t n_str, int64_t n_bytes,
+                                              const int64_t* tile_slo, int64_t n_tiles, int64_t p) {
+  if (p > n_bytes) return 0u;
+  int64_t lo = 0, hi = 0;
+  if (p > 0) {
+    const int64_t t = p >> kTileBits;
+    lo = t < n_tiles ? tile_slo[t] : n_str;
+    hi = t + 1 < n_tiles ? tile_slo[t + 1] : n_str;
+  }
+  while (lo < hi) {  // first string starting at or after p (str_off[n_str] = n_bytes >= p)
+    const int64_t m = (lo + hi) >> 1;
+    if (str_off[m] < p) lo = m + 1; else hi = m;
+  }
+  uint32_t v = 0;
+  for (int64_t i = lo; i <= n_str; ++i) {
+    const int64_t o = str_off[i];
+    if (o >= p + 32) break;
+    v |= 1u << (o - p);
+  }
+  return v;
+}
+
+// psb::carries' view of the batch from global memory only (k_edges, and k_split_classify's walks
+// past its tile): every chunk classified from its 40 bytes
+struct GSrc {
+  PbArgs g;
+  int64_t n_tiles, n_chunks;
+  bool cl;
+  __device__ __forceinline__ uint32_t ss_at(int64_t q) const {
+    return ss32_hint(g.str_off, g.n_str, g.n_bytes, g.tile_slo, n_tiles, q);
+  }
+  __device__ __forceinline__ uint32_t ss(int64_t c) const { return ss_at(32 * c); }
+  __device__ __forceinline__ psb::Masks get(int64_t c) const {
+    if (c < 0 || c >= n_chunks) return psb::Masks{};
+    psb::RegBytes by;
+    pb_load40(g, 32 * c, by.w);
+    const uint64_t s = (uint64_t)ss_at(32 * c - 4) | ((uint64_t)(ss_at(32 * c + 28) & 0xFFu) << 32);
+    return psb::classify(by, s, UcdClass{}, cl);
+  }
+};
+
+// k_edges: per tile boundary b in [0, n_tiles] (byte 2048 b, chunk c = 64 b): the class masks of
+// chunk c and its final chunk-start word (zeros past the batch).  edge[k * (n_tiles + 1) + b].
+__global__ void __launch_bounds__(256) k_edges(PbArgs g, int64_t n_tiles, int pattern, uint32_t* edge) {
+  const int64_t b = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (b > n_tiles) return;
+  const int64_t n_chunks = (g.n_bytes + psb::kChunk - 1) / psb::kChunk;
+  const int64_t c = b << (kTileBits - 5);
+  const int64_t stride = n_tiles + 1;
+  const GSrc src{g, n_tiles, n_chunks, pattern == 0};
+  psb::Masks m1{};
+  uint32_t r = 0;
+  if (c < n_chunks) {
+    if (pattern == 2) {  // (the chunks are the strings)
+      r = src.ss(c);
+    } else {
+      const psb::Masks m0 = src.get(c - 1), m2 = src.get(c + 1);
+      m1 = src.get(c);
+      const uint64_t ssw = (uint64_t)src.ss_at(32 * c - 16) | ((uint64_t)src.ss_at(32 * c + 16) << 32);
+      uint32_t need = 0;
+      r = psb::rules(m0, m1, m2, ssw, pattern == 0, psb::Carry{}, &need);
+      if (need) {
+        const psb::Carry cy = psb::carries(src, c, need);
+        r = psb::rules(m0, m1, m2, ssw, pattern == 0, cy, &need);
+      }
+    }
+    if (32 * c + 32 > g.n_bytes) r &= (1u << (g.n_bytes - 32 * c)) - 1u;
+  }
+  edge[0 * stride + b] = m1.L; edge[1 * stride + b] = m1.N; edge[2 * stride + b] = m1.C;
+  edge[3 * stride + b] = m1.P; edge[4 * stride + b] = m1.H; edge[5 * stride + b] = m1.A;
+  edge[6 * stride + b] = m1.X; edge[7 * stride + b] = m1.K1; edge[8 * stride + b] = m1.K2;
+  edge[9 * stride + b] = r;
+}
+
+// per-wave LDS of k_split_classify
+constexpr int kScPre = 32;                         // bytes staged before the tile
+constexpr int kScWinWords = (kScPre + kWin) / 4 + 8;  // [t0 - 32, t0 + kWin) + a zero tail
+constexpr int kScSsPre = 64;                       // string-start bits staged from t0 - 64 ...
+constexpr int kScSsWords = (kScSsPre + kTile + 128) / 32;  // ... to t0 + kTile + 128
+struct ScMasks {
+  uint32_t m[9][66];       // class masks: chunk c0 + j at column j + 1; column 0 zeros (lane 0's left
+                           // neighbour, unused: k_edges has its word), column 65 the next tile's first
+  uint32_t ss[kScSsWords]; // string starts
+};
+union ScShared {           // the masks are dead once the tile's chunk starts are known
+  ScMasks pre;
+  uint16_t cstart[kTile + 2];
+};
+
+// psb::carries' view inside k_split_classify: the tile's masks from LDS, the rest from global memory
+struct FSrc {
+  GSrc gs;
+  const ScMasks* sm;
+  int64_t c0, t0;
+  __device__ __forceinline__ uint32_t ss_at(int64_t q) const {
+    const int64_t r = q - (t0 - kScSsPre);
+    if (r >= 0 && r + 32 <= (int64_t)kScSsWords * 32) {
+      const int wi = (int)(r >> 5), sh = (int)(r & 31);
+      const uint64_t two = (uint64_t)sm->ss[wi] | ((wi + 1 < kScSsWords ? (uint64_t)sm->ss[wi + 1] : 0ULL) << 32);
+      return (uint32_t)(two >> sh);
+    }
+    return gs.ss_at(q);
+  }
+  __device__ __forceinline__ uint32_t ss(int64_t c) const { return ss_at(32 * c); }
+  int64_t n_chunks;
+  __device__ __forceinline__ psb::Masks get(int64_t c) const {
+    const int64_t j = c - c0;
+    if (j >= 0 && j < 64 && c < gs.n_chunks) {
+      const int k = (int)j + 1;
+      return psb::Masks{sm->m[0][k], sm->m[1][k], sm->m[2][k], sm->m[3][k], sm->m[4][k],
+                        sm->m[5][k], sm->m[6][k], sm->m[7][k], sm->m[8][k]};
+    }
+    return gs.get(c);
+  }
+};
+
+// one tile: pre-split, then classify_chunks
+__device__ __forceinline__ void split_classify_tile(const EncArgs& a, const PbArgs& g, int pattern, const uint32_t* edge,
+                                                    uint32_t* bits32, int64_t tile, uint32_t* s_win, ScShared* sh,
+                                                    uint16_t* s_qbuf) {
+  const int lane = threadIdx.x & 63;
+  const int64_t t0 = tile * kTile;
+  const int64_t t1 = min(t0 + (int64_t)kTile, a.n_bytes);
+  const int64_t n_chunks = (a.n_bytes + psb::kChunk - 1) / psb::kChunk;
+  const int64_t c0 = tile << (kTileBits - 5), c = c0 + lane;
+  const int64_t stride = a.n_tiles + 1;
+  const bool cl = pattern == 0;
+  // 1. loads: the bytes [t0 - 32, t0 + kWin) into LDS, the edge words, the first strings
+  const int64_t wb = t0 - kScPre;
+  if (((uintptr_t)a.bytes & 15) == 0 && wb >= 0 && wb + kScPre + kWin <= a.n_bytes) {
+#pragma unroll
+    for (int q = 0; q < ((kScPre + kWin) / 16 + 63) / 64; ++q) {
+      const int i = lane + 64 * q;
+      if (i < (kScPre + kWin) / 16) {
+        const u32x4 x = SW_LDNT((const u32x4*)(a.bytes + wb + 16 * (int64_t)i));
+        *(uint4*)(s_win + 4 * i) = make_uint4(x[0], x[1], x[2], x[3]);
+      }
+    }
+  } else {
+    for (int i = lane; i < (kScPre + kWin) / 4; i += 64) {
+      const int64_t p = wb + 4 * (int64_t)i;
+      uint32_t v = 0;
+      for (int k = 0; k < 4; ++k) v |= (p + k >= 0 && p + k < a.n_bytes ? (uint32_t)a.bytes[p + k] : 0u) << (8 * k);
+      s_win[i] = v;
+    }
+  }
+  if (lane < 8) s_win[(kScPre + kWin) / 4 + lane] = 0;
+  const uint32_t r0 = edge[9 * stride + tile], r_next = edge[9 * stride + tile + 1];
+  ScMasks& sm = sh->pre;
+  if (lane < 9) sm.m[lane][65] = edge[lane * stride + tile + 1];  // (k_edges: the next tile's first chunk)
+  else if (lane < 18) sm.m[lane - 9][0] = 0u;
+  const int64_t s_first = a.tile_slo[tile];
+  // 2. string starts of [t0 - kScSsPre, t0 + kTile + 128) (the batch end, str_off[n_str], included)
+  for (int i = lane; i < kScSsWords; i += 64) sm.ss[i] = 0;
+  wave_sync_mem();
+  {
+    const int64_t first = tile > 0 ? a.tile_slo[tile - 1] : 0;  // (<= the first string past t0 - kScSsPre)
+    for (int64_t i0 = first; i0 <= a.n_str; i0 += 64) {
+      const int64_t i = i0 + lane;
+      int64_t r = (int64_t)kScSsWords * 32;
+      if (i <= a.n_str) r = a.str_off[i] - (t0 - kScSsPre);
+      if (r >= 0 && r < (int64_t)kScSsWords * 32) atomicOr(&sm.ss[r >> 5], 1u << (r & 31));
+      if (__ballot(r < (int64_t)kScSsWords * 32) != ~0ULL) break;  // (offsets ascend: past the window)
+    }
+  }
+  wave_sync_mem();
+  const FSrc src{GSrc{g, a.n_tiles, n_chunks, cl}, &sm, c0, t0, n_chunks};
+  // 3. this lane's chunk: class masks (to LDS, where the rules read them: nothing is held in
+  //    registers across the rare walk of psb::carries, which would otherwise cost ~60 VGPRs)
+  uint32_t r = 0;
+  if (pattern == 2) {  // the chunks are the strings
+    if (c < n_chunks) r = src.ss(c);
+  } else {
+    {
+      psb::Masks m1{};
+      if (c < n_chunks) {
+        psb::RegBytes by;
+        const uint32_t* w = s_win + (kScPre / 4 - 1) + 8 * lane;  // bytes [t0 + 32 lane - 4, +40)
+#pragma unroll
+        for (int i = 0; i < 10; ++i) by.w[i] = w[i];
+        const int64_t p = 32 * c;
+        const uint64_t s = (uint64_t)src.ss_at(p - 4) | ((uint64_t)(src.ss_at(p + 28) & 0xFFu) << 32);
+        m1 = psb::classify(by, s, UcdClass{}, cl);
+      }
+      const int k = lane + 1;
+      sm.m[0][k] = m1.L; sm.m[1][k] = m1.N; sm.m[2][k] = m1.C; sm.m[3][k] = m1.P; sm.m[4][k] = m1.H;
+      sm.m[5][k] = m1.A; sm.m[6][k] = m1.X; sm.m[7][k] = m1.K1; sm.m[8][k] = m1.K2;
+    }
+    wave_sync_mem();
+    auto col = [&](int k) {
+      return psb::Masks{sm.m[0][k], sm.m[1][k], sm.m[2][k], sm.m[3][k], sm.m[4][k], sm.m[5][k], sm.m[6][k], sm.m[7][k], sm.m[8][k]};
+    };
+    if (c < n_chunks) {
+      const int64_t p = 32 * c;
+      const uint64_t ssw = (uint64_t)src.ss_at(p - 16) | ((uint64_t)src.ss_at(p + 16) << 32);
+      uint32_t need = 0;
+      r = psb::rules(col(lane), col(lane + 1), col(lane + 2), ssw, cl, psb::Carry{}, &need);
+      if (lane == 0) {  // (k_edges has lane 0's word, from the previous tile's masks)
+        r = r0;
+        need = 0;
+      }
+      if (need) {
+        const psb::Carry cy = psb::carries(src, c, need);
+        asm volatile("" ::: "memory");  // (the masks re-read from LDS, not kept live across the walk)
+        r = psb::rules(col(lane), col(lane + 1), col(lane + 2), ssw, cl, cy, &need);
+      }
+    }
+  }
+  if (c < n_chunks) {
+    if (32 * c + 32 > a.n_bytes) r &= (1u << (a.n_bytes - 32 * c)) - 1u;
+    bits32[c] = r;
+    if (c == n_chunks - 1 && (c & 1) == 0) bits32[c + 1] = 0;  // (the last word's upper half)
+  }
+  // 4. the end of the tile's last chunk: the first chunk start of the next tile (k_edges)
+  int rel_end;
+  if (t1 >= a.n_bytes) rel_end = (int)(a.n_bytes - t0);
+  else if (r_next != 0) rel_end = kTile + __builtin_ctz(r_next);
+  else if (a.n_bytes <= t1 + 32) rel_end = (int)(a.n_bytes - t0);
+  else rel_end = kRelEndLong;
+  wave_sync_mem();  // (the masks' LDS becomes the chunk-start list)
+  classify_chunks(a, tile, s_win + kScPre / 4, sh->cstart, s_qbuf, r, rel_end, s_first);
+}
+
+#ifndef SW_SC_WAVES
+#define SW_SC_WAVES 6
+#endif
+__global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(SW_SC_WAVES, SW_SC_WAVES))) k_split_classify(EncArgs a, PbArgs g, int pattern,
+                                                                         const uint32_t* edge, uint32_t* bits32) {
+  __shared__ __attribute__((aligned(16))) uint32_t s_win_all[kWaves][kScWinWords];
+  __shared__ ScShared s_sh_all[kWaves];
+  __shared__ uint16_t s_qb_all[kWaves][kQBuf];
+  const int wv = threadIdx.x >> 6;
+  const int64_t tile = (int64_t)blockIdx.x * kWaves + wv;
+  if (tile < a.n_tiles)
+    split_classify_tile(a, g, pattern, edge, bits32, tile, s_win_all[wv], &s_sh_all[wv], s_qb_all[wv]);
+}
+
+}  // namespace sw

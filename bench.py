@@ -34,6 +34,8 @@ sys.path.insert(0, ROOT)
 # batch's encode queued behind the previous batch's reassembly (profiles/r3f_gw1_trace.md).
 os.environ["GPU_MAX_HW_QUEUES"] = "8"
 
+SPECIALS = {"<|endoftext|>": 50256, "<|fim_prefix|>": 50257, "<|fim_middle|>": 50258, "<|fim_suffix|>": 50259}
+LAUNCH_LIMIT = (1 << 30) - 64  # bytes of one sw_encode_device launch
 METRIC = "encoded MB/s (input bytes) + Mtokens/s at 32k merges, 1/2/4/8 MI355X vs CPU ref"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (/opt/skills/guides/MI355X_MICROARCH.md)
 
@@ -45,6 +47,14 @@ def parse():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--config", default="c3", choices=["c3", "c5"],
                     help="c3: 1 GiB MIXED + 32k merges (configs[1]/[2]); c5: stress, 50k merges")
+    ap.add_argument("--corpus", default=None, choices=["mixed", "stress", "entropy", "ascii"],
+                    help="override the config's corpus kind (entropy: low repetition, most multi-token chunks "
+                         "distinct -- the merge loop without the memoisation's help)")
+    ap.add_argument("--specials", type=float, default=0.0,
+                    help="C3 with special tokens: insert <|endoftext|> at every string's end and about this many "
+                         "others per KiB at random code-point boundaries; found (and, with --presplit host, "
+                         "pre-split) on the host threads, timed apart from the GPU step; the batch is cut to "
+                         "the 2^30 - 64-byte launch limit")
     ap.add_argument("--strings", type=int, default=None)
     ap.add_argument("--mean-len", type=int, default=None)
     ap.add_argument("--pattern", default="cl100k", choices=["cl100k", "gpt2"])
@@ -123,6 +133,9 @@ def main():
 
     c5 = args.config == "c5"
     kind = corpus.STRESS if c5 else corpus.MIXED
+    corpus_name = args.corpus or ("stress" if c5 else "mixed")
+    if args.corpus:
+        kind = {"mixed": corpus.MIXED, "stress": corpus.STRESS, "entropy": corpus.ENTROPY, "ascii": corpus.ASCII}[args.corpus]
     n_str = args.strings or (1_000_000 if not c5 else 1_000_000)
     mean = args.mean_len or (1074 if not c5 else 600)
     model = "bl50k.model" if c5 else "bl32k.model"
@@ -130,9 +143,28 @@ def main():
 
     t = time.time()
     buf, off = corpus.synth(1_000_003 + rank, kind, n_str, mean, n_threads=args.threads)
+    specials = None
+    sp_host = None
+    t_split = None
+    if args.specials > 0:  # C3 with special tokens (the corpus carries their text)
+        specials = dict(SPECIALS)
+        buf, off = corpus.splice_specials(buf, off, specials, per_kib=args.specials, end_special=0,
+                                          n_threads=args.threads)
+        k = int(np.searchsorted(off, LAUNCH_LIMIT, side="right")) - 1  # (one launch: cut whole strings)
+        buf, off = buf[:int(off[k])], off[:k + 1]
+        n_str = k
     host_ps = args.presplit == "host"
-    bits, n_chunks = corpus.presplit(buf, off, pat, n_threads=args.threads) if host_ps else (None, -1)
-    t_prep = time.time() - t
+    t_data = time.time() - t
+    t = time.time()
+    if specials:
+        sp_host = corpus.find_specials(buf, off, specials, n_threads=args.threads)
+    if host_ps:
+        bits, n_chunks = (corpus.presplit_specials(buf, off, sp_host[0], sp_host[1], pat, n_threads=args.threads)
+                          if specials else corpus.presplit(buf, off, pat, n_threads=args.threads))
+    else:
+        bits, n_chunks = None, -1
+    t_split = time.time() - t
+    t_prep = t_data + t_split
     n_bytes = int(off[-1])
 
     tok = Tokenizer(device=local)
@@ -168,19 +200,23 @@ def main():
     id_bits = 16 if tok.ids16 else 32  # (the ids cross xGMI as 16 bits when every id fits: SURVEY.md 8(e))
     # the multi-GPU step encodes straight into the transport's width (SW_OPT_OUT_BITS 16: no
     # conversion pass before the gather, half the output bytes); N=1 writes int32
-    out16 = gather and id_bits == 16
-    if out16:
-        _lib.check(L.sw_encoder_set_option(h, _lib.SW_OPT_OUT_BITS, 16))
+    out16 = gather and id_bits == 16 and not specials
     d_out = torch.empty(int(cap.item()), dtype=torch.int16 if out16 else torch.int32, device=dev)
     d_oo = torch.empty(n_str + 1, dtype=torch.int64, device=dev)
     stream = torch.cuda.current_stream(dev).cuda_stream
+    # per-call choices (sw_encode_ex): the caller's bitmap (None: device pre-split, C2), the ids'
+    # width, the special-token occurrences found on the host (uploaded once, like the bitmap)
+    ex = _lib.SwEncodeEx(d_bits.data_ptr() if host_ps else None, 16 if out16 else 32, None, None, None, 0)
+    d_sp = None
+    if specials:
+        d_sp = tuple(torch.from_numpy(np.ascontiguousarray(x)).to(dev) for x in sp_host)
+        ex.sp_pos, ex.sp_len, ex.sp_id, ex.n_sp = d_sp[0].data_ptr(), d_sp[1].data_ptr(), d_sp[2].data_ptr(), len(sp_host[0])
 
     def encode(n_tok_ptr=None):
-        _lib.check(L.sw_encode_device(h, d_buf.data_ptr(), n_bytes, d_off.data_ptr(), n_str,
-                                      d_bits.data_ptr() if host_ps else None,  # None: device pre-split (C2)
-                                      d_out.data_ptr(), d_oo.data_ptr(), stream, n_tok_ptr))
+        _lib.check(L.sw_encode_device_ex(h, d_buf.data_ptr(), n_bytes, d_off.data_ptr(), n_str, ctypes.byref(ex),
+                                         d_out.data_ptr(), d_oo.data_ptr(), stream, n_tok_ptr))
 
-    if not host_ps:  # chunk count for the report (outside the timed region)
+    if not host_ps and not specials:  # chunk count for the report (outside the timed region)
         tmp_bits = torch.empty((n_bytes + 63) // 64, dtype=torch.int64, device=dev)
         c = ctypes.c_int64()
         _lib.check(L.sw_presplit_device(h, d_buf.data_ptr(), n_bytes, d_off.data_ptr(), n_str, pat,
@@ -227,9 +263,8 @@ def main():
             torch.cuda.current_stream(dev).wait_event(done_ev[slot])
             done_ev[slot] = None
         o_ids, o_off = outs[slot]
-        _lib.check(L.sw_encode_device(h, d_buf.data_ptr(), n_bytes, d_off.data_ptr(), n_str,
-                                      d_bits.data_ptr() if host_ps else None, o_ids.data_ptr(), o_off.data_ptr(),
-                                      stream, None))
+        _lib.check(L.sw_encode_device_ex(h, d_buf.data_ptr(), n_bytes, d_off.data_ptr(), n_str, ctypes.byref(ex),
+                                         o_ids.data_ptr(), o_off.data_ptr(), stream, None))
         h1 = time.perf_counter()
         host_t["encode"] += h1 - h0
         if not gather:
@@ -324,7 +359,8 @@ def main():
 
     # roofline of the encode pipeline (all sw_encode_device kernels, HIP events), rank-local, per launch
     # bytes in + ids out + offsets in/out (+ the bitmap when it comes from the host, C3)
-    b_algo = n_bytes + 4 * n_tok + 16 * (n_str + 1) + ((n_bytes + 7) // 8 if host_ps else 0)
+    # (ids written as 16 bits by the N>1 step, out16: 2 bytes each)
+    b_algo = n_bytes + (2 if out16 else 4) * n_tok + 16 * (n_str + 1) + ((n_bytes + 7) // 8 if host_ps else 0)
     achieved = b_algo / (k_ms * 1e-3) / 1e9 if k_ms > 0 else None
     # traffic: HBM bytes per launch from the committed PMC profile of this same workload, if any
     traffic, traffic_x2, traffic_src, counters = None, None, None, None
@@ -333,7 +369,8 @@ def main():
             tj = json.load(f)
         if (tj.get("n_bytes") == n_bytes and tj.get("merges") == len(tok.merges) and tj.get("pattern") == args.pattern
                 and tj.get("chunk_table") == (not args.no_chunk_table) and tj.get("dedupe") == (not args.no_dedupe)
-                and tj.get("presplit", "host") == args.presplit):
+                and tj.get("presplit", "host") == args.presplit
+                and tj.get("corpus", "mixed") == corpus_name and tj.get("specials", 0.0) == args.specials):
             traffic, traffic_src = int(tj["traffic_bytes_per_launch"]), tj["source"]
             traffic_x2 = int(tj.get("traffic_bytes_per_launch_x2", 0)) or None
             counters = tj.get("counters")
@@ -356,23 +393,32 @@ def main():
     # buffers through sw_encode_batch (Tokenizer.encode_packed).  Reported beside, never `value`.
     e2e = None
     if rank == 0 and world == 1 and args.e2e_steps > 0:
-        tok.encode_packed(buf, off, bits)  # (its own device workspace, grown once)
-        dte = 0.0
-        for _ in range(args.e2e_steps):  # each call timed entry to return; the previous call's
-            ids_e = off_e = None          # result is released outside the timer (the caller's cost)
+        # the caller's output arrays, allocated and touched once (encode_packed(out=...)): a call then
+        # writes the ids into resident pages instead of faulting in a fresh 1 GB array
+        out_e = np.zeros(n_bytes, dtype=np.int32)
+        oo_e = np.zeros(n_str + 1, dtype=np.int64)
+        tok.encode_packed(buf, off, bits, specials=specials, out=out_e, out_off=oo_e)  # (workspace grown once)
+        dte = dfresh = 0.0
+        for _ in range(args.e2e_steps):  # each call timed entry to return
             te = time.perf_counter()
-            ids_e, off_e = tok.encode_packed(buf, off, bits)
+            ids_e, off_e = tok.encode_packed(buf, off, bits, specials=specials, out=out_e, out_off=oo_e)
             dte += time.perf_counter() - te
-        dte /= args.e2e_steps
         st = tok.last_stats
+        te = time.perf_counter()  # (one call into a fresh array, for comparison with earlier rounds)
+        f_ids, f_off = tok.encode_packed(buf, off, bits, specials=specials)
+        dfresh = time.perf_counter() - te
+        del f_ids, f_off
+        dte /= args.e2e_steps
         e2e = {"mb_s": round(n_bytes / dte / 1e6, 1), "ms": round(dte * 1e3, 2), "ms_h2d": round(st.ms_h2d, 2),
                "ms_kernels": round(st.ms_kernels, 2), "ms_d2h": round(st.ms_d2h, 2),
                "same_token_count": int(off_e[-1]) == n_tok, "steps": args.e2e_steps,
-               "host_buffers": "pageable numpy, sw_encode_batch",
+               "host_buffers": "pageable numpy in, caller-provided numpy out (encode_packed out=/out_off=), "
+                               "sw_encode_batch%s" % ("_ex (specials found on the host threads)" if specials else ""),
                "pcie_copies": "dma" if args.pipe_dma else "kernels",
-               "timing": "mean over calls, each from entry to return (output array allocated and "
-                         "first touched inside the call)"}
-        del ids_e, off_e
+               "timing": "mean over calls, each from entry to return, into the caller's resident output arrays",
+               "mb_s_fresh_output": round(n_bytes / dfresh / 1e6, 1),
+               "fresh_output_note": "one call with the output array allocated inside it (page faults included)"}
+        del ids_e, off_e, out_e, oo_e
 
     # parity spot-check + CPU baseline (rank 0, N=1 only): the oracle on a bounded prefix of the
     # same corpus; the GPU ids for that prefix must be bit-identical
@@ -406,11 +452,15 @@ def main():
         k = max(1, min(k, n_str))
         sbuf, soff = buf[:int(off[k])], off[:k + 1]
         om = oracle.OracleModel(tok.merges)
+        def cpu_encode(nt):
+            if specials:
+                return om.encode_batch_specials(sbuf, soff, specials, pat, n_threads=nt)
+            return om.encode_batch(sbuf, soff, pat, n_threads=nt)
         tc = time.perf_counter()
-        ids_cpu, ooff_cpu = om.encode_batch(sbuf, soff, pat, n_threads=1)
+        ids_cpu, ooff_cpu = cpu_encode(1)
         dt1 = time.perf_counter() - tc
         tc = time.perf_counter()
-        om.encode_batch(sbuf, soff, pat, n_threads=args.threads)
+        cpu_encode(args.threads)
         dtm = time.perf_counter() - tc
         got = d_out[:int(ooff_cpu[-1])].cpu().numpy()
         if out16:
@@ -430,14 +480,18 @@ def main():
             "warmup": args.warmup, "ms_per_step": round(ms_step, 4), "higher_is_better": True, "scaling": "weak",
             "vs_baseline": None, "dtype": "int32", "data": "synthetic",
             "config": {"workload": ("C5 stress, 50k merges" if c5 else
-                                    ("C3: configs[2], host %s pre-split, GPU merge loop" % args.pattern) if host_ps else
-                                    ("C2: configs[1] full path, 1 GiB MIXED UTF-8, 1M strings, GPU %s pre-split + "
-                                     "merge loop + id compaction" % args.pattern))
+                                    ("C3: configs[2], host %s pre-split%s, GPU merge loop" % (
+                                        args.pattern, " + special tokens on host" if specials else "")) if host_ps else
+                                    ("C2: configs[1] full path, 1 GiB %s UTF-8, %d strings, GPU %s pre-split + "
+                                     "merge loop + id compaction%s" % (
+                                         (args.corpus or "mixed").upper(), n_str, args.pattern,
+                                         " + special tokens (found on host)" if specials else "")))
                        + (" + RCCL all-gather of ids + reassembly (offsets rebased, ids widened to int32)"
                           if gather else ""),
                        "presplit": args.presplit,
                        "bytes_per_rank": n_bytes, "strings_per_rank": n_str, "merges": len(tok.merges),
                        "model": model, "pattern": args.pattern, "parallelism": "doc-shard x%d" % world,
+                       "corpus": corpus_name,
                        "gather_in_step": gather, "gather_overlaps_next_encode": overlap, "gather_id_bits": id_bits if gather else None,
                        "encode_out_bits": 16 if out16 else 32,
                        "chunk_table": not args.no_chunk_table,
@@ -452,6 +506,11 @@ def main():
             "reassembly_check": reassembly_ok,
             "e2e_pcie": e2e,
             "host_prep_s": round(t_prep, 2),
+            "host_split_s": round(t_split, 3) if (host_ps or specials) else None,
+            "host_split_note": ("host threads, outside the timed GPU step: special-token occurrences%s (%d threads)" % (
+                " + %s pre-split bitmap" % args.pattern if host_ps else "", args.threads)) if (host_ps or specials) else None,
+            "specials": ({"per_kib": args.specials, "occurrences": int(len(sp_host[0])), "tokens": SPECIALS,
+                          "end_of_string": "<|endoftext|>"} if specials else None),
         }
         print(json.dumps(line), flush=True)
     tok.close()

@@ -47,6 +47,7 @@ extern "C" {
 #define SW_CORPUS_ASCII 0
 #define SW_CORPUS_MIXED 1
 #define SW_CORPUS_STRESS 2
+#define SW_CORPUS_ENTROPY 3   /* low repetition: a flat Zipf over 1 M words in six scripts */
 
 typedef struct sw_encoder sw_encoder;
 
@@ -141,12 +142,8 @@ int32_t sw_encoder_reserve(sw_encoder* h, int64_t max_bytes, int64_t max_strings
  *                          the bitmap is not read back); 0: as its own kernel first.  Results identical. */
 #define SW_OPT_FUSED_PRESPLIT 14
 /* (option 15 was an A/B knob of round 2, removed: set_option rejects it) */
-/*   SW_OPT_OUT_BITS        32 (default): sw_encode_device writes int32 ids; 16: it writes uint16
- *                          ids (d_out_ids is then a uint16_t*; only for tables whose every id
- *                          fits, SW_INFO_IDS16 -- SW_ERR_ARG otherwise).  The multi-GPU driver's
- *                          16-bit transport: no conversion pass, half the output bytes.
- *                          sw_encode_batch is not affected (host results are int32). */
-#define SW_OPT_OUT_BITS 16
+/* (option 16, a persistent 16-bit output of sw_encode_device, was replaced by the per-call
+ * sw_encode_ex.out_bits: set_option rejects it; sw_encode_device always writes int32) */
 int32_t sw_encoder_set_option(sw_encoder* h, int32_t option, int64_t value);
 
 /* Encoder facts (sw_encoder_get_info): distinct merges, whole-chunk table entries, whether the
@@ -166,6 +163,35 @@ int64_t sw_encoder_get_info(const sw_encoder* h, int32_t what);
  * or a negative status. */
 int64_t sw_presplit_host(const uint8_t* bytes, const int64_t* str_off, int64_t n_str, int32_t pattern,
                          uint64_t* chunk_bits, int32_t n_threads);
+
+/* ---- special tokens (E1: special_tokens, shredword/base.py:103, saved/loaded at :120-121 /
+ * :142-144; the reference defines no split) ----------------------------------------------------
+ * The tokenizer's specials: their UTF-8 bytes[off[k] .. off[k+1]) and ids[k], in dict order.
+ * Build-defined rule (minbpe's): scanning a string left to right, the first position where some
+ * special matches starts an occurrence; at one position the first special in dict order wins;
+ * the scan goes on after it.  An occurrence is one chunk that encodes to the special's id, and
+ * the text between occurrences is encoded on its own (pre-split included).  Empty specials never
+ * match.  Occurrences never cross a string. */
+typedef struct sw_specials {
+  const uint8_t* bytes;
+  const int64_t* off;   /* [n + 1] */
+  const int32_t* ids;   /* [n] */
+  int64_t n;
+} sw_specials;
+
+/* The occurrences in the strings bytes[str_off[s] .. str_off[s+1]), found on host threads
+ * (n_threads <= 0: all, capped at 64): sp_pos[k] (byte offset relative to str_off[0],
+ * ascending), sp_len[k], sp_id[k].  cap == 0 only counts.  Returns the number of occurrences,
+ * SW_ERR_CAP if more than cap, or another negative status. */
+int64_t sw_find_specials_host(const uint8_t* bytes, const int64_t* str_off, int64_t n_str, const sw_specials* sp,
+                              int64_t* sp_pos, int32_t* sp_len, int32_t* sp_id, int64_t cap, int32_t n_threads);
+
+/* sw_presplit_host with special-token occurrences (as sw_find_specials_host gives them): the
+ * text between occurrences is pre-split on its own and each occurrence is one chunk.  Returns the
+ * chunk count or a negative status. */
+int64_t sw_presplit_host_specials(const uint8_t* bytes, const int64_t* str_off, int64_t n_str, int32_t pattern,
+                                  const int64_t* sp_pos, const int32_t* sp_len, int64_t n_sp, uint64_t* chunk_bits,
+                                  int32_t n_threads);
 
 /* ---- batched encode, host buffers (the Tokenizer.encode / encode_batch path) ------------
  * Encodes n_str strings (bytes[str_off[s] .. str_off[s+1])) and writes their ids
@@ -203,6 +229,36 @@ int32_t sw_presplit_device(sw_encoder* h, const uint8_t* d_bytes, int64_t n_byte
 int32_t sw_encode_device(sw_encoder* h, const uint8_t* d_bytes, int64_t n_bytes, const int64_t* d_str_off,
                          int64_t n_str, const uint64_t* d_chunk_bits, int32_t* d_out_ids, int64_t* d_out_off,
                          void* stream, int64_t* n_tokens_host);
+
+/* ---- the same with per-call choices ---------------------------------------------------------
+ * sw_encode_device with (ex == NULL: exactly sw_encode_device):
+ *   chunk_bits   as d_chunk_bits above (NULL: the device pre-splits with SW_OPT_PATTERN)
+ *   out_bits     32: d_out_ids is int32_t*; 16: uint16_t* -- the multi-GPU driver's 16-bit transport
+ *                (SW_INFO_IDS16 tables with every special id below 65536; SW_ERR_ARG otherwise)
+ *   sp_pos / sp_len / sp_id / n_sp   special-token occurrences (device arrays; sp_pos relative to
+ *                d_bytes, ascending, non-overlapping, each inside one string; n_sp == 0: none), as
+ *                sw_find_specials_host finds them: each is one chunk encoding to its id, and the
+ *                device pre-split treats its ends as string boundaries (a caller bitmap must already:
+ *                sw_presplit_host_specials) */
+typedef struct sw_encode_ex {
+  const uint64_t* chunk_bits;
+  int32_t out_bits;
+  const int64_t* sp_pos;
+  const int32_t* sp_len;
+  const int32_t* sp_id;
+  int64_t n_sp;
+} sw_encode_ex;
+int32_t sw_encode_device_ex(sw_encoder* h, const uint8_t* d_bytes, int64_t n_bytes, const int64_t* d_str_off,
+                            int64_t n_str, const sw_encode_ex* ex, void* d_out_ids, int64_t* d_out_off, void* stream,
+                            int64_t* n_tokens_host);
+
+/* sw_encode_batch with special tokens (specials NULL or empty: exactly sw_encode_batch): the
+ * occurrences are found on the host threads (sw_find_specials_host); the pre-split is the
+ * device's, or the host threads' with SW_OPT_HOST_PRESPLIT (chunk_bits from the caller must come
+ * from sw_presplit_host_specials on the same specials).  Host buffers; synchronous. */
+int32_t sw_encode_batch_ex(sw_encoder* h, const uint8_t* bytes, const int64_t* str_off, int64_t n_str, int32_t pattern,
+                           const uint64_t* chunk_bits, const sw_specials* specials, int32_t* out_ids, int64_t out_cap,
+                           int64_t* out_off, sw_stats* stats);
 
 /* ---- decode (build_vocab, shredword/base.py:60-79, and the byte join of a decode) --------
  * A decoder holds a vocabulary: token t's bytes are vocab_bytes[vocab_off[t] .. vocab_off[t+1])
@@ -267,6 +323,14 @@ int32_t sw_reassemble_device(const void* d_recv, int32_t id_bits, const int64_t*
  * the bytes (cap >= out_off[n_strings]).  Returns the total byte count or SW_ERR_*. */
 int64_t sw_synth_corpus(uint64_t seed, int32_t kind, int64_t n_strings, int64_t mean_len,
                         uint8_t* out_bytes, int64_t cap, int64_t* out_off, int32_t n_threads);
+
+/* A corpus (bytes, off[0..n_strings]) with special tokens inserted: about per_kib random ones per
+ * KiB of each string, each at a random code-point boundary, and sp's end_special-th one at every
+ * string's end (end_special < 0: none).  Two passes like sw_synth_corpus (out_bytes NULL: only the
+ * offsets).  Returns the total byte count or -1. */
+int64_t sw_synth_splice_specials(uint64_t seed, const uint8_t* bytes, const int64_t* off, int64_t n_strings,
+                                 const sw_specials* sp, double per_kib, int32_t end_special, uint8_t* out_bytes,
+                                 int64_t cap, int64_t* out_off, int32_t n_threads);
 
 #ifdef __cplusplus
 }

@@ -46,6 +46,10 @@ def lib():
         L.orc_encode_batch.restype = c_int64
         L.orc_encode_batch.argtypes = [c_void_p, POINTER(c_uint8), POINTER(c_int64), c_int64, c_int,
                                        POINTER(c_int32), POINTER(c_int64), c_int]
+        L.orc_encode_batch_specials.restype = c_int64
+        L.orc_encode_batch_specials.argtypes = [c_void_p, POINTER(c_uint8), POINTER(c_int64), c_int64, c_int,
+                                                POINTER(c_uint8), POINTER(c_int64), POINTER(c_int32), c_int64,
+                                                POINTER(c_int32), POINTER(c_int64), c_int]
         L.orc_encode_with_specials.restype = c_int64
         L.orc_encode_with_specials.argtypes = [c_void_p, POINTER(c_uint8), c_int64, c_int, POINTER(c_uint8),
                                                POINTER(c_int64), POINTER(c_int32), c_int64, POINTER(c_int32)]
@@ -115,6 +119,28 @@ class OracleModel:
             buf = np.zeros(1, np.uint8)
         t = lib().orc_encode_batch(self._h, _p(buf, c_uint8), _p(off, c_int64), n, pattern, _p(out, c_int32),
                                    _p(out_off, c_int64), n_threads)
+        assert t >= 0
+        return out[:t], out_off
+
+    def encode_batch_specials(self, buf, off, special_tokens, pattern=PAT_CL100K, n_threads=1):
+        """encode_batch with special tokens (dict str -> id, dict order), per string as
+        encode_with_specials -> (ids int32[total], out_off int64[n+1])."""
+        buf = np.ascontiguousarray(buf, dtype=np.uint8)
+        off = np.ascontiguousarray(off, dtype=np.int64)
+        names = [s.encode("utf-8") for s in special_tokens]
+        sb = np.frombuffer(b"".join(names) or b"\0", dtype=np.uint8)
+        so = np.zeros(len(names) + 1, dtype=np.int64)
+        np.cumsum([len(x) for x in names], out=so[1:])
+        sid = np.array(list(special_tokens.values()) or [0], dtype=np.int32)
+        n = len(off) - 1
+        total = int(off[-1] - off[0]) if n > 0 else 0
+        out = np.empty(max(total, 1), dtype=np.int32)
+        out_off = np.empty(n + 1, dtype=np.int64)
+        if buf.size == 0:
+            buf = np.zeros(1, np.uint8)
+        t = lib().orc_encode_batch_specials(self._h, _p(buf, c_uint8), _p(off, c_int64), n, pattern, _p(sb, c_uint8),
+                                            _p(so, c_int64), _p(sid, c_int32), len(names), _p(out, c_int32),
+                                            _p(out_off, c_int64), n_threads)
         assert t >= 0
         return out[:t], out_off
 

@@ -377,19 +377,29 @@ int64_t orc_encode_ordinary(const orc_model* m, const uint8_t* s, int64_t n, int
 typedef struct {
   const orc_model* m; const uint8_t* bytes; const int64_t* off; int64_t s0, s1; int pattern;
   int32_t* out; int64_t* cnt;
+  const uint8_t* spec_bytes; const int64_t* spec_off; const int32_t* spec_ids; int64_t n_spec;
 } orc_job;
 
 static void* orc_worker(void* p) {
   orc_job* j = (orc_job*)p;
   for (int64_t s = j->s0; s < j->s1; ++s) {
     int64_t a = j->off[s], e = j->off[s + 1];
-    j->cnt[s] = orc_encode_ordinary(j->m, j->bytes + a, e - a, j->pattern, j->out + a);
+    j->cnt[s] = j->n_spec > 0 ? orc_encode_with_specials(j->m, j->bytes + a, e - a, j->pattern, j->spec_bytes,
+                                                         j->spec_off, j->spec_ids, j->n_spec, j->out + a)
+                              : orc_encode_ordinary(j->m, j->bytes + a, e - a, j->pattern, j->out + a);
   }
   return NULL;
 }
 
 int64_t orc_encode_batch(const orc_model* m, const uint8_t* bytes, const int64_t* off, int64_t n_str,
                          int pattern, int32_t* out, int64_t* out_off, int n_threads) {
+  return orc_encode_batch_specials(m, bytes, off, n_str, pattern, NULL, NULL, NULL, 0, out, out_off, n_threads);
+}
+
+int64_t orc_encode_batch_specials(const orc_model* m, const uint8_t* bytes, const int64_t* off, int64_t n_str,
+                                  int pattern, const uint8_t* spec_bytes, const int64_t* spec_off,
+                                  const int32_t* spec_ids, int64_t n_spec, int32_t* out, int64_t* out_off,
+                                  int n_threads) {
   if (n_threads < 1) n_threads = 1;
   int64_t* cnt = (int64_t*)calloc(n_str > 0 ? n_str : 1, sizeof(int64_t));
   /* each string writes its ids at its own byte offset (tokens <= bytes), then compact */
@@ -401,7 +411,7 @@ int64_t orc_encode_batch(const orc_model* m, const uint8_t* bytes, const int64_t
   for (int t = 0; t < n_threads; ++t) {
     int64_t target = off[0] + total_bytes * (t + 1) / n_threads, s1 = s;
     while (s1 < n_str && (t == n_threads - 1 || off[s1 + 1] <= target)) ++s1;
-    jobs[t] = (orc_job){m, bytes, off, s, s1, pattern, out - off[0], cnt};
+    jobs[t] = (orc_job){m, bytes, off, s, s1, pattern, out - off[0], cnt, spec_bytes, spec_off, spec_ids, n_spec};
     s = s1;
   }
   for (int t = 1; t < n_threads; ++t) pthread_create(&th[t], NULL, orc_worker, &jobs[t]);

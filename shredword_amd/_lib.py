@@ -21,7 +21,7 @@ SW_OK = 0
 SW_ERR_ARG, SW_ERR_HIP, SW_ERR_ALLOC, SW_ERR_CAP, SW_ERR_NODEV = -1, -2, -3, -4, -5
 
 SW_PAT_CL100K, SW_PAT_GPT2, SW_PAT_NONE = 0, 1, 2
-SW_CORPUS_ASCII, SW_CORPUS_MIXED, SW_CORPUS_STRESS = 0, 1, 2
+SW_CORPUS_ASCII, SW_CORPUS_MIXED, SW_CORPUS_STRESS, SW_CORPUS_ENTROPY = 0, 1, 2, 3
 SW_OPT_CHUNK_TABLE, SW_OPT_DEDUPE, SW_OPT_DEDUPE_SLOTS, SW_OPT_DEDUPE_FP_BITS = 1, 2, 3, 4
 SW_OPT_PATTERN, SW_OPT_HOST_PRESPLIT, SW_OPT_LONG_SPLIT, SW_OPT_MAX_LAUNCH_BYTES = 5, 6, 7, 8
 SW_OPT_PIPE_RUN_BYTES = 9
@@ -30,7 +30,7 @@ SW_OPT_PIPE_COPY_KERNELS = 11
 SW_OPT_PIPE_DEPTH = 12
 SW_OPT_MERGE_STREAMS = 13
 SW_OPT_FUSED_PRESPLIT = 14
-SW_OPT_OUT_BITS = 16
+SW_OPT_OUT_BITS = 16  # (removed: set_option rejects it; 16-bit output is sw_encode_ex.out_bits, per call)
 SW_INFO_MERGES, SW_INFO_CHUNK_ENTRIES, SW_INFO_WIDE_TABLE, SW_INFO_IDS16, SW_INFO_SPLIT = 1, 2, 3, 4, 5
 
 
@@ -38,6 +38,17 @@ class SwStats(Structure):
     _fields_ = [("n_bytes", c_int64), ("n_chunks", c_int64), ("n_tokens", c_int64),
                 ("ms_presplit", c_double), ("ms_h2d", c_double), ("ms_kernels", c_double),
                 ("ms_d2h", c_double), ("ms_total", c_double)]
+
+
+class SwSpecials(Structure):
+    """sw_specials: the tokenizer's special tokens (UTF-8 bytes, offsets, ids; dict order)."""
+    _fields_ = [("bytes", POINTER(c_uint8)), ("off", POINTER(c_int64)), ("ids", POINTER(c_int32)), ("n", c_int64)]
+
+
+class SwEncodeEx(Structure):
+    """sw_encode_ex: per-call choices of sw_encode_device_ex (device pointers as integers)."""
+    _fields_ = [("chunk_bits", c_void_p), ("out_bits", c_int32), ("sp_pos", c_void_p), ("sp_len", c_void_p),
+                ("sp_id", c_void_p), ("n_sp", c_int64)]
 
 
 class TrainConfig(Structure):
@@ -91,6 +102,15 @@ _SIGNATURES = {
                                      POINTER(c_int64)]),
     "sw_encode_device": (c_int32, [c_void_p, c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_void_p,
                                    c_void_p, c_void_p, POINTER(c_int64)]),
+    "sw_encode_device_ex": (c_int32, [c_void_p, c_void_p, c_int64, c_void_p, c_int64, POINTER(SwEncodeEx), c_void_p,
+                                      c_void_p, c_void_p, POINTER(c_int64)]),
+    "sw_encode_batch_ex": (c_int32, [c_void_p, POINTER(c_uint8), POINTER(c_int64), c_int64, c_int32,
+                                     POINTER(c_uint64), POINTER(SwSpecials), POINTER(c_int32), c_int64,
+                                     POINTER(c_int64), POINTER(SwStats)]),
+    "sw_find_specials_host": (c_int64, [POINTER(c_uint8), POINTER(c_int64), c_int64, POINTER(SwSpecials),
+                                        POINTER(c_int64), POINTER(c_int32), POINTER(c_int32), c_int64, c_int32]),
+    "sw_presplit_host_specials": (c_int64, [POINTER(c_uint8), POINTER(c_int64), c_int64, c_int32, POINTER(c_int64),
+                                            POINTER(c_int32), c_int64, POINTER(c_uint64), c_int32]),
     "sw_encoder_set_option": (c_int32, [c_void_p, c_int32, c_int64]),
     "sw_encoder_get_info": (c_int64, [c_void_p, c_int32]),
     "sw_encoder_set_timing": (c_int32, [c_void_p, c_int32]),
@@ -108,6 +128,8 @@ _SIGNATURES = {
                                    c_void_p, POINTER(c_int64)]),
     "sw_synth_corpus": (c_int64, [c_uint64, c_int32, c_int64, c_int64, POINTER(c_uint8), c_int64,
                                   POINTER(c_int64), c_int32]),
+    "sw_synth_splice_specials": (c_int64, [c_uint64, POINTER(c_uint8), POINTER(c_int64), c_int64, POINTER(SwSpecials),
+                                           c_double, c_int32, POINTER(c_uint8), c_int64, POINTER(c_int64), c_int32]),
     # trainer (include/shredword_train.h)
     "sw_trainer_create": (c_int32, [POINTER(TrainConfig), c_int32, POINTER(c_void_p)]),
     "sw_trainer_destroy": (None, [c_void_p]),
@@ -150,6 +172,21 @@ def check(code):
         msg = lib().sw_last_error()
         raise ShredwordError(int(code), msg.decode("utf-8", "replace") if msg else "")
     return code
+
+
+def specials_struct(special_tokens):
+    """dict str -> id (dict order) -> (SwSpecials, keep-alive arrays)."""
+    import numpy as np
+    names = [s.encode("utf-8") for s in special_tokens]
+    sb = np.frombuffer(b"".join(names) or b"\0", dtype=np.uint8).copy()
+    so = np.zeros(len(names) + 1, dtype=np.int64)
+    np.cumsum([len(x) for x in names], out=so[1:])
+    ids = np.array(list(special_tokens.values()) or [0], dtype=np.int64)
+    if ids.size and (ids.min() < 0 or ids.max() > 2 ** 31 - 2):
+        raise ValueError("special token ids must be in [0, 2^31 - 2]")
+    sid = ids.astype(np.int32)
+    st = SwSpecials(ptr(sb, c_uint8), ptr(so, c_int64), ptr(sid, c_int32), len(names))
+    return st, (sb, so, sid)
 
 
 def ptr(arr, ctype):

@@ -9,6 +9,13 @@
 //                          digit runs, whitespace runs, contractions
 //   SW_CORPUS_STRESS (C5)  Zipf string lengths 4..4096 B, >=1% strings that are a single
 //                          4096-B letter run, long whitespace runs, (a,a) runs
+//   SW_CORPUS_ENTROPY      low-repetition text: a flat Zipf over 1 M words in six scripts (Latin
+//                          with accents, Cyrillic, Greek, CJK, Hangul, Devanagari), random casing,
+//                          digits inside words -- most multi-token chunks are distinct, so the
+//                          merge loop itself, not the memoisation, carries the encode
+//
+// sw_synth_splice_specials inserts special tokens into such a corpus (the C3 workload: a
+// document separator at every string's end and others at random code-point boundaries).
 #include <algorithm>
 #include <cmath>
 #include <cstdint>
@@ -96,6 +103,10 @@ struct Lexicon {
   int kind;
   Lexicon(uint64_t seed, int kind_) : kind(kind_) {
     Rng r(key(seed, 0xC0FFEE));
+    if (kind == SW_CORPUS_ENTROPY) {
+      build_entropy(r);
+      return;
+    }
     size_t n = kind == SW_CORPUS_ASCII ? 50000 : 200000;
     words.reserve(n);
     for (size_t i = 0; i < n; ++i) {
@@ -123,6 +134,31 @@ struct Lexicon {
     }
     std::vector<double> zw(n);
     for (size_t i = 0; i < n; ++i) zw[i] = 1.0 / std::pow((double)i + 2.7, 1.07);
+    zipf.build(zw);
+  }
+  // 1 M words, each in one script, 1..12 code points; letters cased at random (Latin, Cyrillic,
+  // Greek), a digit inside 8% of the words; a flat Zipf (exponent 0.75)
+  void build_entropy(Rng& r) {
+    const size_t n = 1000000;
+    words.reserve(n);
+    static const uint32_t kBase[] = {0x61, 0x430, 0x3B1, 0x4E00, 0xAC00, 0x915};
+    static const uint32_t kSpan[] = {26, 32, 25, 0x51A6, 11172, 37};
+    for (size_t i = 0; i < n; ++i) {
+      std::string w;
+      double u = r.uni();
+      const int script = u < 0.45 ? 0 : u < 0.62 ? 1 : u < 0.74 ? 2 : u < 0.86 ? 3 : u < 0.94 ? 4 : 5;
+      const int len = script >= 3 ? 1 + (int)r.below(4) : 2 + (int)r.below(11);
+      for (int k = 0; k < len; ++k) {
+        if (r.uni() < 0.01) { w += (char)('0' + r.below(10)); continue; }
+        if (script == 0 && r.uni() < 0.12) { put_utf8(w, kLatin1[r.below(20)]); continue; }
+        uint32_t cp = kBase[script] + r.below(kSpan[script]);
+        if (script <= 2 && r.uni() < 0.3) cp -= script == 0 ? 0x20 : script == 1 ? 0x20 : 0x20;  // upper case
+        put_utf8(w, cp);
+      }
+      words.push_back(std::move(w));
+    }
+    std::vector<double> zw(n);
+    for (size_t i = 0; i < n; ++i) zw[i] = 1.0 / std::pow((double)i + 2.7, 0.75);
     zipf.build(zw);
   }
 };
@@ -226,7 +262,8 @@ size_t string_len(int kind, Rng& r, double mean) {
 extern "C" int64_t sw_synth_corpus(uint64_t seed, int32_t kind, int64_t n_strings, int64_t mean_len,
                                    uint8_t* out_bytes, int64_t cap, int64_t* out_off, int32_t n_threads) {
   if (n_strings < 0 || mean_len < 1 || !out_off) return -1;
-  if (kind != SW_CORPUS_ASCII && kind != SW_CORPUS_MIXED && kind != SW_CORPUS_STRESS) return -1;
+  if (kind != SW_CORPUS_ASCII && kind != SW_CORPUS_MIXED && kind != SW_CORPUS_STRESS && kind != SW_CORPUS_ENTROPY)
+    return -1;
   // lengths first (cheap, serial, deterministic)
   out_off[0] = 0;
   for (int64_t i = 0; i < n_strings; ++i) {
@@ -255,6 +292,65 @@ extern "C" int64_t sw_synth_corpus(uint64_t seed, int32_t kind, int64_t n_string
         prose(lx, r, s, L, kind == SW_CORPUS_ASCII);
       }
       std::memcpy(out_bytes + out_off[i], s.data(), L);
+    }
+  };
+  std::vector<std::thread> th;
+  for (int t = 1; t < nt; ++t) th.emplace_back(work, t);
+  work(0);
+  for (auto& x : th) x.join();
+  return out_off[n_strings];
+}
+
+extern "C" int64_t sw_synth_splice_specials(uint64_t seed, const uint8_t* bytes, const int64_t* off, int64_t n_strings,
+                                           const sw_specials* sp, double per_kib, int32_t end_special,
+                                           uint8_t* out_bytes, int64_t cap, int64_t* out_off, int32_t n_threads) {
+  if (n_strings < 0 || !off || !out_off || !sp || sp->n <= 0 || !sp->bytes || !sp->off || per_kib < 0) return -1;
+  if (end_special >= sp->n) return -1;
+  if (n_strings > 0 && off[n_strings] > off[0] && !bytes) return -1;
+  // per string: how many random insertions (deterministic), and the bytes they add
+  auto plan = [&](int64_t i, Rng& r) -> int64_t {
+    const double want = (double)(off[i + 1] - off[i]) / 1024.0 * per_kib;
+    return (int64_t)want + (r.uni() < want - (double)(int64_t)want ? 1 : 0);
+  };
+  auto sp_len = [&](int64_t k) { return sp->off[k + 1] - sp->off[k]; };
+  out_off[0] = 0;
+  for (int64_t i = 0; i < n_strings; ++i) {
+    Rng r(key(seed, 3 * (uint64_t)i + 1));
+    int64_t add = end_special >= 0 ? sp_len(end_special) : 0;
+    for (int64_t c = plan(i, r); c > 0; --c) add += sp_len(r.below((uint32_t)sp->n));
+    out_off[i + 1] = out_off[i] + (off[i + 1] - off[i]) + add;
+  }
+  if (!out_bytes) return out_off[n_strings];
+  if (cap < out_off[n_strings]) return -1;
+  int nt = n_threads > 0 ? n_threads : (int)std::min(16u, std::max(1u, std::thread::hardware_concurrency()));
+  auto work = [&](int t) {
+    std::vector<std::pair<int64_t, int64_t>> ins;  // (position in the string, special)
+    for (int64_t i = t; i < n_strings; i += nt) {
+      Rng r(key(seed, 3 * (uint64_t)i + 1));
+      const int64_t n = plan(i, r);
+      ins.clear();
+      for (int64_t c = 0; c < n; ++c) ins.emplace_back(0, r.below((uint32_t)sp->n));
+      const uint8_t* src = bytes + off[i];
+      const int64_t L = off[i + 1] - off[i];
+      Rng q(key(seed, 3 * (uint64_t)i + 2));
+      for (auto& x : ins) {  // a random code-point boundary
+        int64_t p = L > 0 ? (int64_t)q.below((uint32_t)(L + 1)) : 0;
+        while (p > 0 && p < L && (src[p] & 0xC0) == 0x80) --p;
+        x.first = p;
+      }
+      std::stable_sort(ins.begin(), ins.end(), [](const auto& a, const auto& b) { return a.first < b.first; });
+      uint8_t* dst = out_bytes + out_off[i];
+      int64_t at = 0;
+      for (const auto& x : ins) {
+        std::memcpy(dst, src + at, (size_t)(x.first - at));
+        dst += x.first - at;
+        at = x.first;
+        std::memcpy(dst, sp->bytes + sp->off[x.second], (size_t)sp_len(x.second));
+        dst += sp_len(x.second);
+      }
+      std::memcpy(dst, src + at, (size_t)(L - at));
+      dst += L - at;
+      if (end_special >= 0) std::memcpy(dst, sp->bytes + sp->off[end_special], (size_t)sp_len(end_special));
     }
   };
   std::vector<std::thread> th;

@@ -98,6 +98,8 @@ struct sw_encoder {
     uint8_t* d_in = nullptr; int64_t* d_off = nullptr; uint64_t* d_bits = nullptr;
     int32_t* d_out = nullptr; int64_t* d_oo = nullptr; uint16_t* d_out16 = nullptr;
     int64_t* d_ntok = nullptr;  // this run's token count, kept apart from the shared workspace
+    int64_t* h_sp = nullptr; int64_t* d_sp = nullptr;  // special-token occurrences: pos | len, id (3 x cap_sp x 8 B)
+    int64_t cap_sp = 0;
     hipEvent_t e_in = nullptr, e_comp = nullptr, e_out = nullptr;
     int64_t cap_bytes = 0, cap_str = 0;
   } pipe[4];
@@ -108,7 +110,6 @@ struct sw_encoder {
   // the merge kernels of different length buckets are independent: forked onto these streams
   // they overlap (each alone leaves most of the chip idle), joined before k_tile_count
   bool merge_fork = true;             // SW_OPT_MERGE_STREAMS
-  bool out16 = false;                 // SW_OPT_OUT_BITS 16: sw_encode_device writes uint16 ids
   hipStream_t s_fork[2] = {nullptr, nullptr};
   hipEvent_t ev_fork = nullptr, ev_join[2] = {nullptr, nullptr};
   sw::HostPool* pool = nullptr;
@@ -118,6 +119,7 @@ struct sw_encoder {
   uint32_t* d_res = nullptr;          // [2 * n_bytes] merge results, double-spaced position space
   int64_t* d_part = nullptr;
   int64_t* d_tile_slo = nullptr;
+  int64_t* d_tile_sp = nullptr;       // first special-token occurrence at or after each tile
   uint32_t* d_tile_slots = nullptr;
   uint32_t* d_tile_nref = nullptr;
   uint32_t* d_rlist = nullptr;
@@ -155,6 +157,10 @@ struct sw_encoder {
   uint64_t* d_bits = nullptr;
   int32_t* d_out = nullptr;
   int64_t* d_out_off = nullptr;
+  int64_t sp_cap = 0;                 // special-token occurrences staged for sw_encode_batch_ex
+  int64_t* d_sp_pos = nullptr;
+  int32_t* d_sp_len = nullptr;
+  int32_t* d_sp_id = nullptr;
   // dominant-kernel timing: one event pair per launch since sw_encoder_set_timing(h, 1)
   bool timing = false;
   std::vector<hipEvent_t> ev_pool;
@@ -177,10 +183,10 @@ struct DeviceGuard {
 
 void free_workspace(sw_encoder* h) {
   (void)hipFree(h->d_scratch); (void)hipFree(h->d_res); (void)hipFree(h->d_pbits); (void)hipFree(h->d_edge); (void)hipFree(h->d_pcount); (void)hipFree(h->d_part);
-  (void)hipFree(h->d_tile_slo); (void)hipFree(h->d_stamps);
+  (void)hipFree(h->d_tile_slo); (void)hipFree(h->d_tile_sp); (void)hipFree(h->d_stamps);
   (void)hipFree(h->d_tile_slots); (void)hipFree(h->d_tile_nref); (void)hipFree(h->d_rlist); (void)hipFree(h->d_queue); (void)hipFree(h->d_bcnt); (void)hipFree(h->d_boff);
   (void)hipFree(h->d_qtotal);
-  h->d_tile_slo = nullptr; h->d_stamps = nullptr; h->d_tile_slots = nullptr; h->d_tile_nref = nullptr; h->d_rlist = nullptr; h->d_queue = nullptr;
+  h->d_tile_slo = nullptr; h->d_tile_sp = nullptr; h->d_stamps = nullptr; h->d_tile_slots = nullptr; h->d_tile_nref = nullptr; h->d_rlist = nullptr; h->d_queue = nullptr;
   h->d_bcnt = nullptr; h->d_boff = nullptr; h->d_qtotal = nullptr;
   (void)hipFree(h->d_dtab); (void)hipFree(h->d_tile_base); (void)hipFree(h->d_tile_cnt);
   (void)hipFree(h->d_dres); (void)hipFree(h->d_big); (void)hipFree(h->d_dcnt);
@@ -196,6 +202,8 @@ void free_workspace(sw_encoder* h) {
 void free_io(sw_encoder* h) {
   (void)hipFree(h->d_bytes); (void)hipFree(h->d_str_off); (void)hipFree(h->d_bits);
   (void)hipFree(h->d_out); (void)hipFree(h->d_out_off);
+  (void)hipFree(h->d_sp_pos); (void)hipFree(h->d_sp_len); (void)hipFree(h->d_sp_id);
+  h->d_sp_pos = nullptr; h->d_sp_len = nullptr; h->d_sp_id = nullptr; h->sp_cap = 0;
   h->d_bytes = nullptr; h->d_str_off = nullptr; h->d_bits = nullptr; h->d_out = nullptr; h->d_out_off = nullptr;
   h->io_bytes = -1; h->io_str = -1;
 }
@@ -206,6 +214,7 @@ void free_pipe(sw_encoder* h) {
     (void)hipHostFree(p.h_oo); (void)hipHostFree(p.h_ntok);
     (void)hipFree(p.d_in); (void)hipFree(p.d_off); (void)hipFree(p.d_bits); (void)hipFree(p.d_out); (void)hipFree(p.d_oo);
     (void)hipFree(p.d_out16); (void)hipFree(p.d_ntok);
+    (void)hipHostFree(p.h_sp); (void)hipFree(p.d_sp);
     if (p.e_in) (void)hipEventDestroy(p.e_in);
     if (p.e_comp) (void)hipEventDestroy(p.e_comp);
     if (p.e_out) (void)hipEventDestroy(p.e_out);
@@ -222,6 +231,7 @@ int32_t ensure_workspace(sw_encoder* h, int64_t n_bytes) {
   // (+ slack for k_compact's head reads; k_classify's tile-local queue, aliased here, takes whole tiles)
   HIP_TRY(hipMalloc(&h->d_res, sizeof(uint32_t) * std::max<int64_t>(2 * nb + 16, n_tiles * kTile)));
   HIP_TRY(hipMalloc(&h->d_tile_slo, sizeof(int64_t) * n_tiles));
+  HIP_TRY(hipMalloc(&h->d_tile_sp, sizeof(int64_t) * n_tiles));
   HIP_TRY(hipMalloc(&h->d_tile_slots, sizeof(uint32_t) * n_tiles));
   HIP_TRY(hipMalloc(&h->d_tile_nref, sizeof(uint32_t) * n_tiles));
   HIP_TRY(hipMalloc(&h->d_rlist, sizeof(uint32_t) * n_tiles * kTile));
@@ -530,11 +540,6 @@ extern "C" int32_t sw_encoder_set_option(sw_encoder* h, int32_t option, int64_t 
     case SW_OPT_PIPE_COPY_KERNELS: h->pipe_kcopy = value != 0; return SW_OK;
     case SW_OPT_MERGE_STREAMS: h->merge_fork = value != 0; return SW_OK;
     case SW_OPT_FUSED_PRESPLIT: h->fused_presplit = value != 0; return SW_OK;
-    case SW_OPT_OUT_BITS:
-      if (value != 16 && value != 32) return fail(SW_ERR_ARG, "SW_OPT_OUT_BITS: 16 or 32");
-      if (value == 16 && !h->ids16) return fail(SW_ERR_ARG, "SW_OPT_OUT_BITS 16: a table id does not fit 16 bits");
-      h->out16 = value == 16;
-      return SW_OK;
     case SW_OPT_PIPE_DEPTH:
       if (value < 2 || value > 4) return fail(SW_ERR_ARG, "pipeline depth: 2 .. 4");
       h->pipe_depth = (int)value;
@@ -666,13 +671,24 @@ hipError_t launch_long(sw_encoder* h, hipStream_t s, const EncArgs& a, bool spli
   return e;
 }
 
+// special-token occurrences of one launch, on the device (sw_encode_ex)
+struct DevSpecials {
+  const int64_t* pos = nullptr;
+  const int32_t* len = nullptr;
+  const int32_t* id = nullptr;
+  int64_t n = 0;
+};
+
 // the device pipeline; d_out_ids is int32_t*, or uint16_t* when out16 (the table is ids16)
 int32_t encode_device(sw_encoder* h, const uint8_t* d_bytes, int64_t n_bytes, const int64_t* d_str_off, int64_t n_str,
-                      const uint64_t* d_chunk_bits, void* d_out_ids, bool out16, int64_t* d_out_off, void* stream,
-                      int64_t* n_tokens_host) {
+                      const uint64_t* d_chunk_bits, const DevSpecials& sp, void* d_out_ids, bool out16,
+                      int64_t* d_out_off, void* stream, int64_t* n_tokens_host) {
   if (!h || n_bytes < 0 || n_str < 0 || !d_str_off || !d_out_off || (n_bytes > 0 && (!d_bytes || !d_out_ids)))
     return fail(SW_ERR_ARG, "sw_encode_device: bad arguments");
+  if (sp.n < 0 || (sp.n > 0 && (!sp.pos || !sp.len || !sp.id)))
+    return fail(SW_ERR_ARG, "sw_encode_device: bad special-token occurrences");
   if (out16 && !h->ids16) return fail(SW_ERR_ARG, "sw_encode_device: 16-bit output needs a table whose ids fit 16 bits");
+  if (out16 && sp.n > 0) return fail(SW_ERR_ARG, "sw_encode_device: 16-bit output with special tokens is not supported");
   if (n_bytes > kMaxLaunchBytes) return fail(SW_ERR_ARG, "sw_encode_device: n_bytes > 2^30 - 64 (split the batch)");
   DeviceGuard g(h->device);
   hipStream_t st = (hipStream_t)stream;  // (NULL: the null stream, as torch's default stream)
@@ -695,9 +711,14 @@ int32_t encode_device(sw_encoder* h, const uint8_t* d_bytes, int64_t n_bytes, co
   if (n_tiles > 0)  // (the pre-split and k_classify start from each tile's first string)
     hipLaunchKernelGGL(k_tile_strings, dim3((unsigned)((n_tiles + 255) / 256)), dim3(256), 0, st, d_str_off, n_str,
                        n_tiles, h->d_tile_slo);
+  const SpArgs spa{sp.pos, sp.len, sp.id, sp.n, h->d_tile_sp};
+  if (n_tiles > 0 && sp.n > 0)  // (... and their first special-token occurrence)
+    hipLaunchKernelGGL(k_tile_strings, dim3((unsigned)((n_tiles + 255) / 256)), dim3(256), 0, st, sp.pos, sp.n,
+                       n_tiles, h->d_tile_sp);
   // the full path (no caller bitmap): the device pre-split, fused into the classification
-  // (k_edges + k_split_classify) or as its own kernel first (SW_OPT_FUSED_PRESPLIT 0)
-  const bool fused = n_tiles > 0 && !d_chunk_bits && h->fused_presplit;
+  // (k_edges + k_split_classify) or as its own kernel first (SW_OPT_FUSED_PRESPLIT 0; special
+  // tokens always take the fused kernel)
+  const bool fused = n_tiles > 0 && !d_chunk_bits && (h->fused_presplit || sp.n > 0);
   if (n_tiles > 0 && !d_chunk_bits) {
     if (!fused) HIP_TRY(launch_presplit(st, d_bytes, n_bytes, d_str_off, n_str, h->pattern, h->d_pbits, h->d_tile_slo));
     d_chunk_bits = h->d_pbits;
@@ -719,16 +740,24 @@ int32_t encode_device(sw_encoder* h, const uint8_t* d_bytes, int64_t n_bytes, co
     a.queue = h->d_queue; a.stamps = h->d_stamps;
     a.inv = h->d_inv; a.n_inv = h->n_inv; a.ids16 = h->ids16 ? 1u : 0u;
     a.lstart = h->lp.wstart; a.llen = h->lp.wlen; a.n_long = &h->lp.ctl[kLcWave]; a.lcap = h->lp.lcap;
+    a.sp = spa;
     const bool split = h->split_ok && h->long_split;  // (split + verify needs a well-formed table)
     if (h->dedupe) HIP_TRY(hipMemsetAsync(h->d_dtab, 0, sizeof(uint64_t) * ((size_t)a.dmask + 1), st));
     if (fused) {
-      const PbArgs pg{d_bytes, n_bytes, d_str_off, n_str, h->d_tile_slo};
+      const PbArgs pg{d_bytes, n_bytes, d_str_off, n_str, h->d_tile_slo, spa};
       hipLaunchKernelGGL(k_edges, dim3((unsigned)((n_tiles + 1 + 255) / 256)), dim3(256), 0, st, pg, n_tiles,
                          (int)h->pattern, h->d_edge);
-      hipLaunchKernelGGL(k_split_classify, dim3((unsigned)((n_tiles + kWaves - 1) / kWaves)), dim3(kThreads), 0, st, a,
-                         pg, (int)h->pattern, (const uint32_t*)h->d_edge, (uint32_t*)h->d_pbits);
+      const dim3 gc((unsigned)((n_tiles + kWaves - 1) / kWaves));
+      if (sp.n > 0)
+        hipLaunchKernelGGL(k_split_classify<true>, gc, dim3(kThreads), 0, st, a, pg, (int)h->pattern,
+                           (const uint32_t*)h->d_edge, (uint32_t*)h->d_pbits);
+      else
+        hipLaunchKernelGGL(k_split_classify<false>, gc, dim3(kThreads), 0, st, a, pg, (int)h->pattern,
+                           (const uint32_t*)h->d_edge, (uint32_t*)h->d_pbits);
+    } else if (sp.n > 0) {
+      hipLaunchKernelGGL(k_classify<true>, dim3((unsigned)((n_tiles + kWaves - 1) / kWaves)), dim3(kThreads), 0, st, a);
     } else {
-      hipLaunchKernelGGL(k_classify, dim3((unsigned)((n_tiles + kWaves - 1) / kWaves)), dim3(kThreads), 0, st, a);
+      hipLaunchKernelGGL(k_classify<false>, dim3((unsigned)((n_tiles + kWaves - 1) / kWaves)), dim3(kThreads), 0, st, a);
     }
     HIP_TRY(hipGetLastError());
     HIP_TRY(launch_scan(st, h->d_bcnt, kNumBuckets * n_tiles, h->d_part, h->d_boff, h->d_qtotal));
@@ -815,8 +844,21 @@ int32_t encode_device(sw_encoder* h, const uint8_t* d_bytes, int64_t n_bytes, co
 extern "C" int32_t sw_encode_device(sw_encoder* h, const uint8_t* d_bytes, int64_t n_bytes, const int64_t* d_str_off,
                                     int64_t n_str, const uint64_t* d_chunk_bits, int32_t* d_out_ids,
                                     int64_t* d_out_off, void* stream, int64_t* n_tokens_host) {
-  return encode_device(h, d_bytes, n_bytes, d_str_off, n_str, d_chunk_bits, d_out_ids, h && h->out16, d_out_off, stream,
-                       n_tokens_host);
+  return encode_device(h, d_bytes, n_bytes, d_str_off, n_str, d_chunk_bits, DevSpecials{}, d_out_ids, false, d_out_off,
+                       stream, n_tokens_host);
+}
+
+extern "C" int32_t sw_encode_device_ex(sw_encoder* h, const uint8_t* d_bytes, int64_t n_bytes, const int64_t* d_str_off,
+                                       int64_t n_str, const sw_encode_ex* ex, void* d_out_ids, int64_t* d_out_off,
+                                       void* stream, int64_t* n_tokens_host) {
+  if (!ex)
+    return encode_device(h, d_bytes, n_bytes, d_str_off, n_str, nullptr, DevSpecials{}, d_out_ids, false, d_out_off,
+                         stream, n_tokens_host);
+  if (ex->out_bits != 16 && ex->out_bits != 32) return fail(SW_ERR_ARG, "sw_encode_device_ex: out_bits 16 or 32");
+  DevSpecials sp;
+  sp.pos = ex->sp_pos; sp.len = ex->sp_len; sp.id = ex->sp_id; sp.n = ex->n_sp;
+  return encode_device(h, d_bytes, n_bytes, d_str_off, n_str, ex->chunk_bits, sp, d_out_ids, ex->out_bits == 16,
+                       d_out_off, stream, n_tokens_host);
 }
 
 // ids to 16 bits for the device -> host copy (every id of an ids16 table fits)
@@ -832,10 +874,11 @@ __global__ void k_pack16(const int32_t* in, const int64_t* total, uint16_t* out)
 // buffers hipMalloc'd, so every segment starts 16-byte aligned.
 typedef unsigned int v4u32 __attribute__((ext_vector_type(4)));
 
+constexpr int kCopySegs = 6;
 struct CopySegs {
-  const uint8_t* src[3];
-  uint8_t* dst[3];
-  int64_t n[3];
+  const uint8_t* src[kCopySegs];
+  uint8_t* dst[kCopySegs];
+  int64_t n[kCopySegs];
 };
 
 __device__ inline void copy_seg(const uint8_t* src, uint8_t* dst, int64_t n, int64_t t, int64_t nt) {
@@ -848,7 +891,7 @@ __device__ inline void copy_seg(const uint8_t* src, uint8_t* dst, int64_t n, int
 
 __global__ void __launch_bounds__(256) k_copy_segs(CopySegs c) {
   const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x, nt = (int64_t)gridDim.x * blockDim.x;
-  for (int k = 0; k < 3; ++k)
+  for (int k = 0; k < kCopySegs; ++k)
     if (c.n[k] > 0) copy_seg(c.src[k], c.dst[k], c.n[k], t, nt);
 }
 
@@ -881,16 +924,33 @@ __global__ void __launch_bounds__(256) k_push_run(const int32_t* __restrict__ id
 
 namespace {
 
+// special-token occurrences of a host batch (positions relative to its first byte, ascending)
+struct HostSpecials {
+  const int64_t* pos = nullptr;
+  const int32_t* len = nullptr;
+  const int32_t* id = nullptr;
+  int64_t n = 0;
+  bool narrow = true;  // every id fits the 16-bit download (<= 0xFFFD)
+};
+
+// the occurrences inside bytes [a, b) of the batch: [*j0, *j1)
+void sp_range(const HostSpecials& sp, int64_t a, int64_t b, int64_t* j0, int64_t* j1) {
+  *j0 = std::lower_bound(sp.pos, sp.pos + sp.n, a) - sp.pos;
+  *j1 = std::lower_bound(sp.pos, sp.pos + sp.n, b) - sp.pos;
+}
+
 // sw_encode_batch for a large host batch: runs of whole strings (<= pipe_run bytes, or one longer
 // string) through two slots of pinned and device buffers.  Host thread: stage run k (pool copies
 // into pinned memory), enqueue its upload and encode, then drain run k - 1 (its 16/32-bit ids and
 // offsets to pinned memory, pool copies out to the caller) while run k encodes.
 int32_t encode_batch_pipelined(sw_encoder* h, const uint8_t* bytes, const int64_t* str_off, int64_t n_str,
-                               int32_t pattern, const uint64_t* chunk_bits, int32_t* out_ids, int64_t out_cap,
-                               int64_t* out_off, sw_stats* stats, std::chrono::steady_clock::time_point T0) {
+                               int32_t pattern, const uint64_t* chunk_bits, const HostSpecials& sp, int32_t* out_ids,
+                               int64_t out_cap, int64_t* out_off, sw_stats* stats,
+                               std::chrono::steady_clock::time_point T0) {
+  const bool narrow = h->ids16 && sp.narrow;  // (ids downloaded as 16 bits)
   const int64_t b0 = str_off[0];
   std::vector<std::pair<int64_t, int64_t>> runs;
-  int64_t max_b = 1, max_s = 1;
+  int64_t max_b = 1, max_s = 1, max_sp = 1;
   const int64_t run_cap = std::min(h->pipe_run, h->max_launch);  // (a run is one launch)
   for (int64_t s_lo = 0; s_lo < n_str;) {
     int64_t s_hi = s_lo + 1;
@@ -901,6 +961,11 @@ int32_t encode_batch_pipelined(sw_encoder* h, const uint8_t* bytes, const int64_
     runs.emplace_back(s_lo, s_hi);
     max_b = std::max(max_b, nb);
     max_s = std::max(max_s, s_hi - s_lo);
+    if (sp.n > 0) {
+      int64_t j0, j1;
+      sp_range(sp, str_off[s_lo] - str_off[0], str_off[s_hi] - str_off[0], &j0, &j1);
+      max_sp = std::max(max_sp, j1 - j0);
+    }
     s_lo = s_hi;
   }
   DeviceGuard g(h->device);
@@ -910,6 +975,13 @@ int32_t encode_batch_pipelined(sw_encoder* h, const uint8_t* bytes, const int64_
   const int64_t max_w = (max_b + 63) / 64 + 1;
   for (int slot = 0; slot < h->pipe_depth; ++slot) {
     auto& p = h->pipe[slot];
+    if (sp.n > 0 && p.cap_sp < max_sp) {
+      (void)hipHostFree(p.h_sp); (void)hipFree(p.d_sp);
+      p.h_sp = nullptr; p.d_sp = nullptr; p.cap_sp = 0;
+      HIP_TRY(hipHostMalloc(&p.h_sp, 3 * sizeof(int64_t) * max_sp, hipHostMallocDefault));
+      HIP_TRY(hipMalloc(&p.d_sp, 3 * sizeof(int64_t) * max_sp));
+      p.cap_sp = max_sp;
+    }
     if (p.cap_bytes >= max_b && p.cap_str >= max_s) continue;
     const int64_t cb = std::max(max_b, p.cap_bytes), cs = std::max(max_s, p.cap_str), cw = (cb + 63) / 64 + 1;
     (void)hipHostFree(p.h_in); (void)hipHostFree(p.h_off); (void)hipHostFree(p.h_bits); (void)hipHostFree(p.h_out);
@@ -955,6 +1027,7 @@ int32_t encode_batch_pipelined(sw_encoder* h, const uint8_t* bytes, const int64_
   sw::HostPool& pool = *h->pool;
   double ms_stage = 0, ms_drain = 0;
   int64_t done = 0;
+  int64_t p_nsp[4] = {0, 0, 0, 0};  // special-token occurrences staged per slot
   static const bool trace = std::getenv("SW_PIPE_TRACE") != nullptr;  // (diagnostic timeline)
   auto stamp = [&](const char* what, size_t k) {
     if (trace)
@@ -968,6 +1041,18 @@ int32_t encode_batch_pipelined(sw_encoder* h, const uint8_t* bytes, const int64_
     const uint8_t* src = bytes + a0;
     pool.parallel_for(nb, [&](int64_t lo, int64_t hi) { std::memcpy(p.h_in + lo, src + lo, (size_t)(hi - lo)); });
     for (int64_t j = 0; j <= s_hi - s_lo; ++j) p.h_off[j] = str_off[s_lo + j] - a0;
+    if (sp.n > 0) {  // the run's special-token occurrences, rebased: positions, then lengths and ids (int32)
+      int64_t j0, j1;
+      sp_range(sp, a0 - b0, a0 - b0 + nb, &j0, &j1);
+      const int64_t m = j1 - j0;
+      int32_t* l32 = (int32_t*)(p.h_sp + m);
+      for (int64_t j = 0; j < m; ++j) {
+        p.h_sp[j] = sp.pos[j0 + j] - (a0 - b0);
+        l32[j] = sp.len[j0 + j];
+        l32[m + j] = sp.id[j0 + j];
+      }
+      p_nsp[k % h->pipe_depth] = m;
+    }
     if (chunk_bits) {  // the run's bits, realigned to its first byte
       const int64_t g0 = a0 - b0, nw = (nb + 63) / 64, last_q = (str_off[n_str] - b0 - 1) / 64;
       pool.parallel_for(nw, [&](int64_t lo, int64_t hi) {
@@ -987,20 +1072,26 @@ int32_t encode_batch_pipelined(sw_encoder* h, const uint8_t* bytes, const int64_
     auto& p = h->pipe[k % h->pipe_depth];
     const int64_t s_lo = runs[k].first, s_hi = runs[k].second, nb = str_off[s_hi] - str_off[s_lo], ns = s_hi - s_lo;
     const int64_t n_bits = chunk_bits ? (int64_t)sizeof(uint64_t) * ((nb + 63) / 64) : 0;
+    const int64_t m_sp = sp.n > 0 ? p_nsp[k % h->pipe_depth] : 0, n_sp_bytes = 16 * m_sp;  // (8 + 4 + 4 B each)
     if (h->pipe_kcopy) {
-      const CopySegs c{{p.h_in, (const uint8_t*)p.h_off, (const uint8_t*)p.h_bits},
-                       {p.d_in, (uint8_t*)p.d_off, (uint8_t*)p.d_bits},
-                       {nb, (int64_t)sizeof(int64_t) * (ns + 1), n_bits}};
+      const CopySegs c{{p.h_in, (const uint8_t*)p.h_off, (const uint8_t*)p.h_bits, (const uint8_t*)p.h_sp, nullptr, nullptr},
+                       {p.d_in, (uint8_t*)p.d_off, (uint8_t*)p.d_bits, (uint8_t*)p.d_sp, nullptr, nullptr},
+                       {nb, (int64_t)sizeof(int64_t) * (ns + 1), n_bits, n_sp_bytes, 0, 0}};
       hipLaunchKernelGGL(k_copy_segs, dim3(128), dim3(256), 0, h->s_h2d, c);
       HIP_TRY(hipGetLastError());
     } else {
       HIP_TRY(hipMemcpyAsync(p.d_in, p.h_in, (size_t)nb, hipMemcpyHostToDevice, h->s_h2d));
       HIP_TRY(hipMemcpyAsync(p.d_off, p.h_off, sizeof(int64_t) * (ns + 1), hipMemcpyHostToDevice, h->s_h2d));
       if (chunk_bits) HIP_TRY(hipMemcpyAsync(p.d_bits, p.h_bits, (size_t)n_bits, hipMemcpyHostToDevice, h->s_h2d));
+      if (m_sp > 0) HIP_TRY(hipMemcpyAsync(p.d_sp, p.h_sp, (size_t)n_sp_bytes, hipMemcpyHostToDevice, h->s_h2d));
     }
     HIP_TRY(hipEventRecord(p.e_in, h->s_h2d));
     HIP_TRY(hipStreamWaitEvent(h->stream, p.e_in, 0));
-    const int32_t r = encode_device(h, p.d_in, nb, p.d_off, ns, chunk_bits ? p.d_bits : nullptr, p.d_out, false,
+    DevSpecials dsp;
+    if (m_sp > 0) {
+      dsp.pos = p.d_sp; dsp.len = (const int32_t*)(p.d_sp + m_sp); dsp.id = dsp.len + m_sp; dsp.n = m_sp;
+    }
+    const int32_t r = encode_device(h, p.d_in, nb, p.d_off, ns, chunk_bits ? p.d_bits : nullptr, dsp, p.d_out, false,
                                     p.d_oo, h->stream, nullptr);
     if (r) return r;
     if (count && nb > 0)
@@ -1008,7 +1099,7 @@ int32_t encode_batch_pipelined(sw_encoder* h, const uint8_t* bytes, const int64_
     if (h->pipe_kcopy) {
       // the download kernel runs on s_d2h beside the next run's encode, which rewrites d_total
       HIP_TRY(hipMemcpyAsync(p.d_ntok, h->d_total, sizeof(int64_t), hipMemcpyDeviceToDevice, h->stream));
-    } else if (h->ids16) {
+    } else if (narrow) {
       hipLaunchKernelGGL(k_pack16, dim3(2048), dim3(256), 0, h->stream, p.d_out, h->d_total, p.d_out16);
     }
     HIP_TRY(hipGetLastError());
@@ -1016,7 +1107,7 @@ int32_t encode_batch_pipelined(sw_encoder* h, const uint8_t* bytes, const int64_
     HIP_TRY(hipEventRecord(p.e_comp, h->stream));
     if (h->pipe_kcopy) {
       HIP_TRY(hipStreamWaitEvent(h->s_d2h, p.e_comp, 0));
-      hipLaunchKernelGGL(k_push_run, dim3(128), dim3(256), 0, h->s_d2h, p.d_out, p.d_ntok, h->ids16 ? 0 : 1,
+      hipLaunchKernelGGL(k_push_run, dim3(128), dim3(256), 0, h->s_d2h, p.d_out, p.d_ntok, narrow ? 0 : 1,
                          p.h_out, p.d_oo, ns + 1, p.h_oo);
       HIP_TRY(hipGetLastError());
       HIP_TRY(hipEventRecord(p.e_out, h->s_d2h));
@@ -1034,15 +1125,15 @@ int32_t encode_batch_pipelined(sw_encoder* h, const uint8_t* bytes, const int64_
     if (!h->pipe_kcopy) {
       HIP_TRY(hipStreamWaitEvent(h->s_d2h, p.e_comp, 0));
       if (nt > 0)
-        HIP_TRY(hipMemcpyAsync(p.h_out, h->ids16 ? (void*)p.d_out16 : (void*)p.d_out,
-                               (size_t)nt * (h->ids16 ? 2 : 4), hipMemcpyDeviceToHost, h->s_d2h));
+        HIP_TRY(hipMemcpyAsync(p.h_out, narrow ? (void*)p.d_out16 : (void*)p.d_out,
+                               (size_t)nt * (narrow ? 2 : 4), hipMemcpyDeviceToHost, h->s_d2h));
       HIP_TRY(hipMemcpyAsync(p.h_oo, p.d_oo, sizeof(int64_t) * (ns + 1), hipMemcpyDeviceToHost, h->s_d2h));
       HIP_TRY(hipEventRecord(p.e_out, h->s_d2h));
     }
     HIP_TRY(hipEventSynchronize(p.e_out));
     stamp("pushed", k);
     int32_t* dst = out_ids + done;
-    if (h->ids16) {
+    if (narrow) {
       const uint16_t* s16 = (const uint16_t*)p.h_out;
       pool.parallel_for(nt, [&](int64_t lo, int64_t hi) {
         for (int64_t i = lo; i < hi; ++i) dst[i] = (int32_t)s16[i];
@@ -1100,9 +1191,12 @@ int32_t encode_batch_pipelined(sw_encoder* h, const uint8_t* bytes, const int64_
 
 }  // namespace
 
-extern "C" int32_t sw_encode_batch(sw_encoder* h, const uint8_t* bytes, const int64_t* str_off, int64_t n_str,
-                                   int32_t pattern, const uint64_t* chunk_bits, int32_t* out_ids, int64_t out_cap,
-                                   int64_t* out_off, sw_stats* stats) {
+namespace {
+
+// sw_encode_batch(_ex) with the batch's special-token occurrences found (sp, relative to str_off[0])
+int32_t encode_batch_impl(sw_encoder* h, const uint8_t* bytes, const int64_t* str_off, int64_t n_str, int32_t pattern,
+                          const uint64_t* chunk_bits, const HostSpecials& sp, int32_t* out_ids, int64_t out_cap,
+                          int64_t* out_off, sw_stats* stats) {
   auto T0 = std::chrono::steady_clock::now();
   if (!h || !str_off || !out_off || n_str < 0) return fail(SW_ERR_ARG, "sw_encode_batch: bad arguments");
   const int64_t b0 = n_str > 0 ? str_off[0] : 0;
@@ -1114,7 +1208,8 @@ extern "C" int32_t sw_encode_batch(sw_encoder* h, const uint8_t* bytes, const in
   if (!chunk_bits && pattern != SW_PAT_CL100K && pattern != SW_PAT_GPT2 && pattern != SW_PAT_NONE)
     return fail(SW_ERR_ARG, "sw_encode_batch: bad pattern");
   if (h->pipe_run > 0 && n_bytes > 2 * h->pipe_run && !(h->host_presplit && !chunk_bits))
-    return encode_batch_pipelined(h, bytes, str_off, n_str, pattern, chunk_bits, out_ids, out_cap, out_off, stats, T0);
+    return encode_batch_pipelined(h, bytes, str_off, n_str, pattern, chunk_bits, sp, out_ids, out_cap, out_off, stats,
+                                  T0);
   if (n_bytes > h->max_launch) {
     // one device launch addresses < 2^30 bytes: encode runs of whole strings separately
     int64_t done = 0, s_lo = 0;
@@ -1136,8 +1231,18 @@ extern "C" int32_t sw_encode_batch(sw_encoder* h, const uint8_t* bytes, const in
         }
       }
       sw_stats st{};
-      int32_t rc = sw_encode_batch(h, bytes, str_off + s_lo, s_hi - s_lo, pattern, chunk_bits ? sub.data() : nullptr,
-                                   out_ids + done, out_cap - done, out_off + s_lo, &st);
+      HostSpecials ssp = sp;  // (the run's occurrences, rebased to its first byte)
+      int64_t j0 = 0, j1 = 0;
+      std::vector<int64_t> spos;
+      if (sp.n > 0) {
+        const int64_t g0 = str_off[s_lo] - b0;
+        sp_range(sp, g0, str_off[s_hi] - b0, &j0, &j1);
+        spos.resize((size_t)(j1 - j0));
+        for (int64_t j = j0; j < j1; ++j) spos[(size_t)(j - j0)] = sp.pos[j] - g0;
+        ssp.pos = spos.data(); ssp.len = sp.len + j0; ssp.id = sp.id + j0; ssp.n = j1 - j0;
+      }
+      int32_t rc = encode_batch_impl(h, bytes, str_off + s_lo, s_hi - s_lo, pattern, chunk_bits ? sub.data() : nullptr,
+                                     ssp, out_ids + done, out_cap - done, out_off + s_lo, &st);
       if (rc) return rc;
       for (int64_t s = s_lo; s <= s_hi; ++s) out_off[s] += done;
       done = out_off[s_hi];
@@ -1162,7 +1267,8 @@ extern "C" int32_t sw_encode_batch(sw_encoder* h, const uint8_t* bytes, const in
   if (!chunk_bits && !device_presplit) {
     own_bits.resize((size_t)std::max<int64_t>(n_words, 1));
     auto a = std::chrono::steady_clock::now();
-    n_chunks = sw_presplit_host(bytes, str_off, n_str, pattern, own_bits.data(), 0);
+    n_chunks = sp.n > 0 ? sw_presplit_host_specials(bytes, str_off, n_str, pattern, sp.pos, sp.len, sp.n, own_bits.data(), 0)
+                        : sw_presplit_host(bytes, str_off, n_str, pattern, own_bits.data(), 0);
     if (n_chunks < 0) return fail((int32_t)n_chunks, "sw_encode_batch: bad pattern or offsets");
     ms_pre = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - a).count();
     chunk_bits = own_bits.data();
@@ -1179,6 +1285,14 @@ extern "C" int32_t sw_encode_batch(sw_encoder* h, const uint8_t* bytes, const in
     HIP_TRY(hipMalloc(&h->d_out_off, sizeof(int64_t) * (ns + 1)));
     h->io_bytes = nb; h->io_str = ns;
   }
+  if (sp.n > h->sp_cap) {
+    (void)hipFree(h->d_sp_pos); (void)hipFree(h->d_sp_len); (void)hipFree(h->d_sp_id);
+    h->d_sp_pos = nullptr; h->d_sp_len = nullptr; h->d_sp_id = nullptr; h->sp_cap = 0;
+    HIP_TRY(hipMalloc(&h->d_sp_pos, sizeof(int64_t) * sp.n));
+    HIP_TRY(hipMalloc(&h->d_sp_len, sizeof(int32_t) * sp.n));
+    HIP_TRY(hipMalloc(&h->d_sp_id, sizeof(int32_t) * sp.n));
+    h->sp_cap = sp.n;
+  }
   std::vector<int64_t> rel((size_t)n_str + 1);
   for (int64_t s = 0; s <= n_str; ++s) rel[s] = n_str > 0 ? str_off[s] - b0 : 0;
   auto a = std::chrono::steady_clock::now();
@@ -1189,6 +1303,13 @@ extern "C" int32_t sw_encode_batch(sw_encoder* h, const uint8_t* bytes, const in
       HIP_TRY(hipMemcpyAsync(h->d_bits, chunk_bits, sizeof(uint64_t) * n_words, hipMemcpyHostToDevice, st));
   }
   HIP_TRY(hipMemcpyAsync(h->d_str_off, rel.data(), sizeof(int64_t) * (n_str + 1), hipMemcpyHostToDevice, st));
+  DevSpecials dsp;
+  if (sp.n > 0) {
+    HIP_TRY(hipMemcpyAsync(h->d_sp_pos, sp.pos, sizeof(int64_t) * sp.n, hipMemcpyHostToDevice, st));
+    HIP_TRY(hipMemcpyAsync(h->d_sp_len, sp.len, sizeof(int32_t) * sp.n, hipMemcpyHostToDevice, st));
+    HIP_TRY(hipMemcpyAsync(h->d_sp_id, sp.id, sizeof(int32_t) * sp.n, hipMemcpyHostToDevice, st));
+    dsp.pos = h->d_sp_pos; dsp.len = h->d_sp_len; dsp.id = h->d_sp_id; dsp.n = sp.n;
+  }
   HIP_TRY(hipStreamSynchronize(st));
   double ms_h2d = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - a).count();
   int64_t n_tok = 0;
@@ -1198,7 +1319,7 @@ extern "C" int32_t sw_encode_batch(sw_encoder* h, const uint8_t* bytes, const in
   h->ev_used = 0;
   const int32_t was_pattern = h->pattern;
   if (device_presplit) h->pattern = pattern;
-  int32_t rc = encode_device(h, h->d_bytes, n_bytes, h->d_str_off, n_str, device_presplit ? nullptr : h->d_bits,
+  int32_t rc = encode_device(h, h->d_bytes, n_bytes, h->d_str_off, n_str, device_presplit ? nullptr : h->d_bits, dsp,
                              h->d_out, false, h->d_out_off, st, &n_tok);
   h->pattern = was_pattern;
   if (rc == SW_OK && device_presplit && stats && n_bytes > 0) {  // chunk count for the stats
@@ -1230,6 +1351,40 @@ extern "C" int32_t sw_encode_batch(sw_encoder* h, const uint8_t* bytes, const in
     stats->ms_total = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - T0).count();
   }
   return SW_OK;
+}
+
+}  // namespace
+
+extern "C" int32_t sw_encode_batch(sw_encoder* h, const uint8_t* bytes, const int64_t* str_off, int64_t n_str,
+                                   int32_t pattern, const uint64_t* chunk_bits, int32_t* out_ids, int64_t out_cap,
+                                   int64_t* out_off, sw_stats* stats) {
+  return encode_batch_impl(h, bytes, str_off, n_str, pattern, chunk_bits, HostSpecials{}, out_ids, out_cap, out_off,
+                           stats);
+}
+
+extern "C" int32_t sw_encode_batch_ex(sw_encoder* h, const uint8_t* bytes, const int64_t* str_off, int64_t n_str,
+                                      int32_t pattern, const uint64_t* chunk_bits, const sw_specials* specials,
+                                      int32_t* out_ids, int64_t out_cap, int64_t* out_off, sw_stats* stats) {
+  if (!specials || specials->n == 0)
+    return encode_batch_impl(h, bytes, str_off, n_str, pattern, chunk_bits, HostSpecials{}, out_ids, out_cap, out_off,
+                             stats);
+  if (!h || !str_off || n_str < 0) return fail(SW_ERR_ARG, "sw_encode_batch_ex: bad arguments");
+  for (int64_t k = 0; k < specials->n; ++k)
+    if (specials->ids && (specials->ids[k] < 0 || specials->ids[k] == INT32_MAX))
+      return fail(SW_ERR_ARG, "sw_encode_batch_ex: special token ids must be in [0, 2^31 - 2]");
+  const int64_t cnt = sw_find_specials_host(bytes, str_off, n_str, specials, nullptr, nullptr, nullptr, 0, 0);
+  if (cnt < 0) return fail((int32_t)cnt, "sw_encode_batch_ex: bad special tokens or string offsets");
+  std::vector<int64_t> pos((size_t)std::max<int64_t>(cnt, 1));
+  std::vector<int32_t> len(pos.size()), id(pos.size());
+  if (cnt > 0) {
+    const int64_t got = sw_find_specials_host(bytes, str_off, n_str, specials, pos.data(), len.data(), id.data(), cnt, 0);
+    if (got != cnt) return fail(SW_ERR_ARG, "sw_encode_batch_ex: special-token scan");
+  }
+  HostSpecials sp;
+  sp.pos = pos.data(); sp.len = len.data(); sp.id = id.data(); sp.n = cnt;
+  for (int64_t k = 0; k < cnt; ++k)
+    if (id[(size_t)k] > 0xFFFD) sp.narrow = false;
+  return encode_batch_impl(h, bytes, str_off, n_str, pattern, chunk_bits, sp, out_ids, out_cap, out_off, stats);
 }
 
 extern "C" int32_t sw_encoder_last_counts(sw_encoder* h, int64_t* out4) {

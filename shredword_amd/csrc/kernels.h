@@ -640,6 +640,17 @@ __device__ __forceinline__ int64_t coop_merge(const DevTable& t, uint32_t* id, u
 // ---------------------------------------------------------------------------------------
 // arguments shared by the pipeline's kernels
 // ---------------------------------------------------------------------------------------
+// special-token occurrences of a launch (E1; sw_encode_ex): ascending, non-overlapping, each
+// inside one string and one chunk of its own; tile_sp[t]: the first one starting at or after
+// tile t's first byte (k_tile_strings)
+struct SpArgs {
+  const int64_t* pos;
+  const int32_t* len;
+  const int32_t* id;
+  int64_t n;
+  const int64_t* tile_sp;
+};
+
 struct EncArgs {
   const uint8_t* bytes;
   int64_t n_bytes;
@@ -681,6 +692,7 @@ struct EncArgs {
   uint32_t* big_list;        // long chunks over kLongLds bytes (their index in the long list)
   uint32_t* big_count;       // ... how many (cleared per launch)
   uint32_t ids16;            // every id fits 16 bits (dres layout)
+  SpArgs sp;                 // special-token occurrences (sp.n == 0: none)
 };
 
 #ifdef SW_STAMPS
@@ -836,11 +848,13 @@ constexpr int kWinWords = kWin / 4 + 8;
 // (a last chunk that runs more than kShort bytes past its tile, end unknown to the tile: long,
 // its length found from the complete bitmap by k_lp_prep)
 constexpr int kRelEndLong = 1 << 30;
+template <bool kSp>  // kSp: the launch has special-token occurrences (a.sp)
 __device__ __forceinline__ void classify_chunks(const EncArgs& a, int64_t tile, const uint32_t* s_b32,
                                                 uint16_t* s_cstart, uint16_t* s_qbuf, uint32_t myhalf, int rel_end,
                                                 int64_t s_first);
 
 // one tile (the body of k_classify's tile loop): the chunk starts from the uploaded bitmap
+template <bool kSp>
 __device__ __forceinline__ void classify_tile(const EncArgs& a, int64_t tile, uint32_t* s_b32, uint16_t* s_cstart,
                                               uint16_t* s_qbuf) {
   const int lane = threadIdx.x & 63;
@@ -904,12 +918,13 @@ __device__ __forceinline__ void classify_tile(const EncArgs& a, int64_t tile, ui
       last_end = min(q, a.n_bytes);
     }
   }
-  classify_chunks(a, tile, s_b32, s_cstart, s_qbuf, myhalf, (int)(last_end - t0), s_first);
+  classify_chunks<kSp>(a, tile, s_b32, s_cstart, s_qbuf, myhalf, (int)(last_end - t0), s_first);
 }
 
 // The tile's chunks from its chunk-start bits on: lane l holds bits 32 l .. 32 l + 31 of the tile
 // (cut at the tile's end), rel_end is the end of the tile's last chunk relative to t0 (or
 // kRelEndLong), s_b32 the tile's bytes from t0 in LDS (with kWin - kTile bytes of halo).
+template <bool kSp>
 __device__ __forceinline__ void classify_chunks(const EncArgs& a, int64_t tile, const uint32_t* s_b32,
                                                 uint16_t* s_cstart, uint16_t* s_qbuf, uint32_t myhalf, int rel_end,
                                                 int64_t s_first) {
@@ -943,6 +958,9 @@ __device__ __forceinline__ void classify_chunks(const EncArgs& a, int64_t tile, 
   const uint32_t* gwords = (const uint32_t*)((uintptr_t)a.bytes - mis);
   const int64_t last_word = (mis + a.n_bytes - 1) >> 2;
   uint32_t bcount = 0;
+  // special-token occurrences starting in the tile (wave-uniform; none without specials)
+  const int64_t sp_lo = kSp ? a.sp.tile_sp[tile] : 0;
+  const int64_t sp_hi = kSp ? (tile + 1 < a.n_tiles ? a.sp.tile_sp[tile + 1] : a.sp.n) : 0;
   int nq = 0;    // wave-uniform: chunks waiting in s_qbuf
   int nown = 0;  // wave-uniform: chunks queued for the merge kernels
   int nref = 0;  // wave-uniform: slots that refer to a merge result (k_tile_count's list)
@@ -960,6 +978,15 @@ __device__ __forceinline__ void classify_chunks(const EncArgs& a, int64_t tile, 
           const int ls = valid ? s_cstart[k] : 0;
           const int end = (k + 1 < C) ? (int)s_cstart[k + 1] : rel_end;
           tok[u] = (valid && end - ls == 1) ? (s_b32[ls >> 2] >> (8 * (ls & 3))) & 0xFFu : kInf;
+        }
+      }
+      if (kSp && sp_lo < sp_hi) {  // special-token occurrences starting in the tile: their ids
+#pragma unroll
+        for (int u = 0; u < kLookRounds; ++u) {
+          const int k = ((r0 + u) << 6) + lane;
+          const int ls = k < C ? (int)s_cstart[k] : -1;
+          for (int64_t j = sp_lo; j < sp_hi; ++j)
+            if (ls == (int)(a.sp.pos[j] - t0)) tok[u] = (uint32_t)a.sp.id[j];
         }
       }
 #pragma unroll
@@ -1056,13 +1083,14 @@ __device__ __forceinline__ void classify_chunks(const EncArgs& a, int64_t tile, 
 }
 
 // one wave per tile
+template <bool kSp>
 __global__ void __launch_bounds__(kThreads) SW_CLS_ATTR k_classify(EncArgs a) {
   __shared__ __attribute__((aligned(16))) uint32_t s_b32_all[kWaves][kWinWords];  // window bytes (+ zero tail)
   __shared__ uint16_t s_cs_all[kWaves][kTile + 1];   // chunk starts (tile-relative)
   __shared__ uint16_t s_qb_all[kWaves][kQBuf];       // chunks not settled by a lookup, to dedupe
   const int wv = threadIdx.x >> 6;
   const int64_t tile = (int64_t)blockIdx.x * kWaves + wv;
-  if (tile < a.n_tiles) classify_tile(a, tile, s_b32_all[wv], s_cs_all[wv], s_qb_all[wv]);
+  if (tile < a.n_tiles) classify_tile<kSp>(a, tile, s_b32_all[wv], s_cs_all[wv], s_qb_all[wv]);
 }
 
 // ---------------------------------------------------------------------------------------

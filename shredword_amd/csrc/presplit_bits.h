@@ -125,25 +125,55 @@ SW_HD inline Masks classify(const Bytes& by, uint64_t ss, const Cls& cls, bool c
       const uint32_t x = by.word(i), h7 = (x ^ kLane7) & kLow7;  // (bytes >= 0x80, less 0x80)
       ct40 |= (uint64_t)mm4(in7(h7, 0x00, 0x3F) & x & kLane7) << (4 * i);
     }
-    for (uint64_t m = hi40 & ~ct40 & 0xFFFFFFFFFULL; m; m &= m - 1) {
-      const int k = __builtin_ctzll(m);
+    // one lead: its continuation bytes (0 if invalid), its code point (kInvalidCp if it needs
+    // no class: invalid, or before the chunk)
+    auto lead = [&](int k, uint64_t* tail_out) -> uint32_t {
       const uint32_t b4 = by.at4(k), c0 = b4 & 0xFFu, c1 = (b4 >> 8) & 0xFFu;
       const int n = c0 >= 0xF0 ? 4 : c0 >= 0xE0 ? 3 : 2;
       const uint64_t tail = ((1ULL << (n - 1)) - 1ULL) << (k + 1);
       bool ok = (ct40 & tail) == tail && (ss & tail) == 0 && c0 >= 0xC2 && c0 <= 0xF4;
       ok = ok && !(c0 == 0xE0 && c1 < 0xA0) && !(c0 == 0xED && c1 > 0x9F) && !(c0 == 0xF0 && c1 < 0x90) &&
            !(c0 == 0xF4 && c1 > 0x8F);
-      if (!ok) continue;
-      X |= tail;
-      if (k < 4) continue;
+      *tail_out = ok ? tail : 0ULL;
+      if (!ok || k < 4) return kInvalidCp;
       uint32_t v = c0 & (n == 2 ? 0x1Fu : n == 3 ? 0x0Fu : 0x07u);
       for (int q = 1; q < n; ++q) v = (v << 6) | ((b4 >> (8 * q)) & 0x3Fu);
-      const int c = cls(v);
+      return v;
+    };
+    auto apply = [&](int k, uint32_t v, int c) {
+      if (v == kInvalidCp) return;
       const uint32_t bit = 1u << (k - 4);
       if (c == kL) L |= bit;
       else if (c == kN) N |= bit;
       else if (c == kS) H |= bit;
+    };
+#ifndef SW_PSB_LEADS2
+#define SW_PSB_LEADS2 1
+#endif
+#if !SW_PSB_LEADS2
+    for (uint64_t m = hi40 & ~ct40 & 0xFFFFFFFFFULL; m; m &= m - 1) {
+      const int k = __builtin_ctzll(m);
+      uint64_t t;
+      const uint32_t v = lead(k, &t);
+      X |= t;
+      if (v != kInvalidCp) apply(k, v, cls(v));
     }
+#else
+    // two leads per step, both class lookups in flight together (each is two dependent table
+    // reads: one memory round trip per pair of leads instead of per lead)
+    for (uint64_t m = hi40 & ~ct40 & 0xFFFFFFFFFULL; m;) {
+      const int k1 = __builtin_ctzll(m);
+      m &= m - 1;
+      const int k2 = m ? __builtin_ctzll(m) : k1;
+      if (m) m &= m - 1;
+      uint64_t t1, t2;
+      const uint32_t v1 = lead(k1, &t1), v2 = lead(k2, &t2);
+      X |= t1 | t2;
+      const int cls1 = v1 != kInvalidCp ? cls(v1) : kOther, cls2 = v2 != kInvalidCp ? cls(v2) : kOther;
+      apply(k1, v1, cls1);
+      apply(k2, v2, cls2);
+    }
+#endif
   }
   // contractions after each apostrophe of the chunk (the next one or two code points, ASCII or
   // U+017F LONG S = C5 BF for cl100k's case-insensitive 's')

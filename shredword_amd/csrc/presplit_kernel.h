@@ -6,6 +6,7 @@
 
 #include <cstdint>
 
+#include "kernels.h"
 #include "presplit_bits.h"
 #include "presplit_match.h"
 #include "ucd_tables.h"
@@ -52,6 +53,7 @@ struct PbArgs {
   const int64_t* str_off;
   int64_t n_str;
   const int64_t* tile_slo;  // first string starting at or after each 2 KiB tile (k_tile_strings)
+  SpArgs sp;                // special-token occurrences: their ends are string boundaries (fused path only)
 };
 
 // string-start bits of bytes [p, p + 32) from str_off (batch end included): global fallback

@@ -49,6 +49,43 @@ __device__ __forceinline__ uint32_t ss32_hint(const int64_t* str_off, int64_t n_
   return v;
 }
 
+// Special-token occurrences (SpArgs) in the pre-split: both ends of an occurrence are string
+// boundaries, and the bits strictly inside it are cleared (it is one chunk).  The first
+// occurrence whose end (pos + len) is at or after p: ends ascend; the ones before tile_sp[t] - 1
+// end before tile t's first byte, and tile_sp[t + 1]'s starts past p.
+__device__ __forceinline__ int64_t sp_first_end(const SpArgs& sp, int64_t n_tiles, int64_t p) {
+  int64_t lo = 0, hi = sp.n;
+  if (p > 0) {
+    const int64_t t = p >> kTileBits;
+    if (t < n_tiles) {
+      lo = max(sp.tile_sp[t] - 1, (int64_t)0);
+      hi = t + 1 < n_tiles ? sp.tile_sp[t + 1] : sp.n;
+    } else {
+      lo = max(sp.n - 1, (int64_t)0);
+    }
+  }
+  while (lo < hi) {
+    const int64_t m = (lo + hi) >> 1;
+    if (sp.pos[m] + sp.len[m] < p) lo = m + 1; else hi = m;
+  }
+  return lo;
+}
+
+// bits of [p, p + 32): the occurrences' starts and ends (*ss) and their inner bytes (*inner)
+__device__ __forceinline__ void sp_bits32(const SpArgs& sp, int64_t n_tiles, int64_t p, uint32_t* ss, uint32_t* inner) {
+  uint32_t s = 0, in = 0;
+  for (int64_t j = sp_first_end(sp, n_tiles, p); j < sp.n; ++j) {
+    const int64_t a = sp.pos[j], e = a + sp.len[j];
+    if (a >= p + 32) break;
+    if (a >= p) s |= 1u << (a - p);
+    if (e >= p && e < p + 32) s |= 1u << (e - p);
+    const int64_t lo = max(a + 1, p) - p, hi = min(e, p + 32) - p;  // inner bytes, chunk-relative
+    if (lo < hi) in |= (hi - lo >= 32 ? ~0u : ((1u << (hi - lo)) - 1u)) << lo;
+  }
+  *ss = s;
+  *inner = in;
+}
+
 // psb::carries' view of the batch from global memory only (k_edges, and k_split_classify's walks
 // past its tile): every chunk classified from its 40 bytes
 struct GSrc {
@@ -56,7 +93,13 @@ struct GSrc {
   int64_t n_tiles, n_chunks;
   bool cl;
   __device__ __forceinline__ uint32_t ss_at(int64_t q) const {
-    return ss32_hint(g.str_off, g.n_str, g.n_bytes, g.tile_slo, n_tiles, q);
+    uint32_t v = ss32_hint(g.str_off, g.n_str, g.n_bytes, g.tile_slo, n_tiles, q);
+    if (g.sp.n > 0) {
+      uint32_t s, in;
+      sp_bits32(g.sp, n_tiles, q, &s, &in);
+      v |= s;
+    }
+    return v;
   }
   __device__ __forceinline__ uint32_t ss(int64_t c) const { return ss_at(32 * c); }
   __device__ __forceinline__ psb::Masks get(int64_t c) const {
@@ -93,6 +136,11 @@ __global__ void __launch_bounds__(256) k_edges(PbArgs g, int64_t n_tiles, int pa
         r = psb::rules(m0, m1, m2, ssw, pattern == 0, cy, &need);
       }
     }
+    if (g.sp.n > 0) {  // (an occurrence's inner bytes start no chunk)
+      uint32_t s, in;
+      sp_bits32(g.sp, n_tiles, 32 * c, &s, &in);
+      r &= ~in;
+    }
     if (32 * c + 32 > g.n_bytes) r &= (1u << (g.n_bytes - 32 * c)) - 1u;
   }
   edge[0 * stride + b] = m1.L; edge[1 * stride + b] = m1.N; edge[2 * stride + b] = m1.C;
@@ -100,6 +148,18 @@ __global__ void __launch_bounds__(256) k_edges(PbArgs g, int64_t n_tiles, int pa
   edge[6 * stride + b] = m1.X; edge[7 * stride + b] = m1.K1; edge[8 * stride + b] = m1.K2;
   edge[9 * stride + b] = r;
 }
+
+// a lane's 40 bytes [pos - 4, pos + 36) in the LDS window, for psb::classify: word(i) = bytes
+// [pos - 4 + 4 i, pos + 4 i); at4(k) = bytes k .. k + 3 of the 40 (k <= 36), two LDS reads
+// instead of RegBytes' select chain over ten registers
+struct LdsBytes {
+  const uint32_t* w;
+  __device__ __forceinline__ uint32_t word(int i) const { return w[i]; }
+  __device__ __forceinline__ uint32_t at4(int k) const {
+    const int q = k >> 2;
+    return __builtin_amdgcn_alignbyte(w[q + 1], w[q], (uint32_t)(k & 3));
+  }
+};
 
 // per-wave LDS of k_split_classify
 constexpr int kScPre = 32;                         // bytes staged before the tile
@@ -110,6 +170,7 @@ struct ScMasks {
   uint32_t m[9][66];       // class masks: chunk c0 + j at column j + 1; column 0 zeros (lane 0's left
                            // neighbour, unused: k_edges has its word), column 65 the next tile's first
   uint32_t ss[kScSsWords]; // string starts
+  uint32_t in[64];         // bytes inside special-token occurrences (lane l: bits 32 l ..), if any
 };
 union ScShared {           // the masks are dead once the tile's chunk starts are known
   ScMasks pre;
@@ -144,6 +205,7 @@ struct FSrc {
 };
 
 // one tile: pre-split, then classify_chunks
+template <bool kSp>
 __device__ __forceinline__ void split_classify_tile(const EncArgs& a, const PbArgs& g, int pattern, const uint32_t* edge,
                                                     uint32_t* bits32, int64_t tile, uint32_t* s_win, ScShared* sh,
                                                     uint16_t* s_qbuf) {
@@ -192,6 +254,31 @@ __device__ __forceinline__ void split_classify_tile(const EncArgs& a, const PbAr
       if (__ballot(r < (int64_t)kScSsWords * 32) != ~0ULL) break;  // (offsets ascend: past the window)
     }
   }
+  constexpr bool has_sp = kSp;
+  if (has_sp) {  // special-token occurrences: their ends as string starts, their inner bytes
+    sm.in[lane] = 0u;
+    wave_sync_mem();
+    const int64_t w0 = t0 - kScSsPre, w1 = w0 + (int64_t)kScSsWords * 32;
+    for (int64_t j0 = sp_first_end(a.sp, a.n_tiles, w0); j0 < a.sp.n; j0 += 64) {
+      const int64_t j = j0 + lane;
+      int64_t pa = w1, pe = w1;
+      if (j < a.sp.n) {
+        pa = a.sp.pos[j];
+        pe = pa + a.sp.len[j];
+      }
+      if (pa < w1) {
+        if (pa >= w0) atomicOr(&sm.ss[(pa - w0) >> 5], 1u << ((pa - w0) & 31));
+        if (pe >= w0 && pe < w1) atomicOr(&sm.ss[(pe - w0) >> 5], 1u << ((pe - w0) & 31));
+        for (int64_t q = max(pa + 1, t0); q < min(pe, t0 + (int64_t)kTile);) {  // (inner bytes, word by word)
+          const int64_t qe = min(min(pe, t0 + (int64_t)kTile), ((q - t0) | 31) + 1 + t0);
+          const int sh = (int)((q - t0) & 31), nb = (int)(qe - q);
+          atomicOr(&sm.in[(q - t0) >> 5], (nb >= 32 ? ~0u : ((1u << nb) - 1u)) << sh);
+          q = qe;
+        }
+      }
+      if (__ballot(pa < w1) != ~0ULL) break;  // (positions ascend: past the window)
+    }
+  }
   wave_sync_mem();
   const FSrc src{GSrc{g, a.n_tiles, n_chunks, cl}, &sm, c0, t0, n_chunks};
   // 3. this lane's chunk: class masks (to LDS, where the rules read them: nothing is held in
@@ -203,10 +290,15 @@ __device__ __forceinline__ void split_classify_tile(const EncArgs& a, const PbAr
     {
       psb::Masks m1{};
       if (c < n_chunks) {
+#ifndef SW_SC_LDSBYTES
+#define SW_SC_LDSBYTES 1
+#endif
+#if SW_SC_LDSBYTES
+        const LdsBytes by{s_win + (kScPre / 4 - 1) + 8 * lane};  // bytes [t0 + 32 lane - 4, +40)
+#else
         psb::RegBytes by;
-        const uint32_t* w = s_win + (kScPre / 4 - 1) + 8 * lane;  // bytes [t0 + 32 lane - 4, +40)
-#pragma unroll
-        for (int i = 0; i < 10; ++i) by.w[i] = w[i];
+        for (int i = 0; i < 10; ++i) by.w[i] = s_win[(kScPre / 4 - 1) + 8 * lane + i];
+#endif
         const int64_t p = 32 * c;
         const uint64_t s = (uint64_t)src.ss_at(p - 4) | ((uint64_t)(src.ss_at(p + 28) & 0xFFu) << 32);
         m1 = psb::classify(by, s, UcdClass{}, cl);
@@ -236,6 +328,7 @@ __device__ __forceinline__ void split_classify_tile(const EncArgs& a, const PbAr
     }
   }
   if (c < n_chunks) {
+    if (has_sp && lane > 0) r &= ~sm.in[lane];  // (lane 0: k_edges cleared them)
     if (32 * c + 32 > a.n_bytes) r &= (1u << (a.n_bytes - 32 * c)) - 1u;
     bits32[c] = r;
     if (c == n_chunks - 1 && (c & 1) == 0) bits32[c + 1] = 0;  // (the last word's upper half)
@@ -247,12 +340,13 @@ __device__ __forceinline__ void split_classify_tile(const EncArgs& a, const PbAr
   else if (a.n_bytes <= t1 + 32) rel_end = (int)(a.n_bytes - t0);
   else rel_end = kRelEndLong;
   wave_sync_mem();  // (the masks' LDS becomes the chunk-start list)
-  classify_chunks(a, tile, s_win + kScPre / 4, sh->cstart, s_qbuf, r, rel_end, s_first);
+  classify_chunks<kSp>(a, tile, s_win + kScPre / 4, sh->cstart, s_qbuf, r, rel_end, s_first);
 }
 
 #ifndef SW_SC_WAVES
 #define SW_SC_WAVES 6
 #endif
+template <bool kSp>
 __global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(SW_SC_WAVES, SW_SC_WAVES))) k_split_classify(EncArgs a, PbArgs g, int pattern,
                                                                          const uint32_t* edge, uint32_t* bits32) {
   __shared__ __attribute__((aligned(16))) uint32_t s_win_all[kWaves][kScWinWords];
@@ -261,7 +355,7 @@ __global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(S
   const int wv = threadIdx.x >> 6;
   const int64_t tile = (int64_t)blockIdx.x * kWaves + wv;
   if (tile < a.n_tiles)
-    split_classify_tile(a, g, pattern, edge, bits32, tile, s_win_all[wv], &s_sh_all[wv], s_qb_all[wv]);
+    split_classify_tile<kSp>(a, g, pattern, edge, bits32, tile, s_win_all[wv], &s_sh_all[wv], s_qb_all[wv]);
 }
 
 }  // namespace sw

@@ -926,8 +926,10 @@ struct TempBufs {
 };
 
 // bpe_load_corpus on the device (the kernels above); returns 1 when a 64-bit hash collision
-// between two distinct words makes it give way to the host path
+// between two distinct words makes it give way to the host path, and for corpora whose byte or
+// word counts pass the int item counts of the hipcub passes (the host path is int64 throughout)
 int32_t load_words_device(sw_trainer* t, const uint8_t* text, int64_t n) {
+  if (n > (int64_t)INT32_MAX) return 1;
   hipStream_t st = t->st;
   TempBufs b;  // (temporaries, freed on every return)
   uint8_t* d_text;
@@ -961,6 +963,7 @@ int32_t load_words_device(sw_trainer* t, const uint8_t* text, int64_t n) {
   // distinct words: the occurrences sorted by hash (stable: corpus order within a run), one
   // run per distinct word, every occurrence checked against its run's first
   const int64_t m = nwords;
+  if (m > (int64_t)INT32_MAX) return 1;  // (cannot happen below 2^31 bytes; kept with the sorts' int counts)
   uint64_t *d_hk, *d_hk2, *d_hv, *d_hv2;
   int64_t *d_head, *d_roff, *d_rcnt64;
   SW_HIP_TRY(b.get(&d_hk, sizeof(uint64_t) * (size_t)std::max<int64_t>(m, 1)));

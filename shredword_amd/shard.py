@@ -46,7 +46,7 @@ def reassemble(local_ids, local_off, group=None, device=None, concat=True, width
     """Collective reassembly of per-rank encodes (steps 1-4 above) on every rank.
 
     local_ids: torch int32 [>= local count] on `device` (or int16 holding each id's low 16 bits, e.g.
-    from an encode with SW_OPT_OUT_BITS 16, when id_bits=16); local_off: torch int64 [m+1] with
+    from an encode with out_bits 16 -- sw_encode_ex -- when id_bits=16); local_off: torch int64 [m+1] with
     local_off[0] == 0.  Returns (ids int32 [total], off int64 [n+1]) for the whole batch, on
     `device`, identical on every rank.
 
@@ -114,7 +114,7 @@ def reassemble(local_ids, local_off, group=None, device=None, concat=True, width
         raise ValueError("id_bits must be 16 or 32")
     wide = id_bits == 32
     # the send buffer: the caller's ids as they are when they already have the transport's width
-    # (16-bit: an encode with SW_OPT_OUT_BITS 16 -- no conversion pass), else converted
+    # (16-bit: an encode with out_bits 16 -- no conversion pass), else converted
     want = torch.int32 if wide else torch.int16
     if local_ids.numel() >= width and local_ids.dtype == want and local_ids.device == dev:
         send = local_ids[:width]  # (slots past the count are padding: never read)
@@ -225,7 +225,13 @@ class _BoundsCheck:
 def check_bounds():
     """Raise if a width bound given to reassemble (concat=False) since the last call was exceeded by
     an actual count; a too-small bound truncates the gathered ids, so call this once per batch (or
-    per group of batches) before using their results.  Synchronises with the devices."""
+    per group of batches) before using their results.  Synchronises with the devices: the flags
+    may have been written on any stream (an async reassembly folds them on the stream its works
+    were waited on), so the whole device is synchronised before they are read."""
+    import torch
+    for dev in _bound_flags:
+        if dev.type == "cuda":
+            torch.cuda.synchronize(dev)
     bad = [str(dev) for dev, flag in _bound_flags.items() if bool(flag.item())]
     _bound_flags.clear()
     if bad:

@@ -7,7 +7,6 @@ base.py:22-36).  Pre-split runs in native host code, the merge loop in HIP kerne
 device.  There is no CPU fallback: without the library or a device, encode raises.
 """
 import ctypes
-import re
 
 import numpy as np
 
@@ -88,8 +87,6 @@ class Tokenizer(BaseTokenizer):
         self._dec = None
         self._dec_key = None
         self._dec_len = None
-        self._sp_key = None
-        self._sp_re = None
         self.last_stats = None
 
     # merges is tracked so that edits (README-style `tok.merges[(a, b)] = id`) reach the device
@@ -203,104 +200,94 @@ class Tokenizer(BaseTokenizer):
         buf, off = _pack_strings(datas)
         return self.encode_packed(buf, off)
 
-    def encode_packed(self, buf, off, chunk_bits=None):
+    def encode_packed(self, buf, off, chunk_bits=None, specials=None, out=None, out_off=None):
         """Encode the strings buf[off[s]:off[s+1]] (uint8 buffer, int64 offsets) in one device
-        batch.  chunk_bits: optional host pre-split bitmap (sw_presplit_host layout).
-        Returns (ids int32[total], out_off int64[n+1])."""
+        batch.  chunk_bits: optional host pre-split bitmap (sw_presplit_host layout; with specials,
+        sw_presplit_host_specials').  specials: None (ordinary encode) or a dict str -> id of special
+        tokens to split on (sw_encode_batch_ex: found by the library's host threads, no Python loop).
+        out / out_off: optional caller arrays (int32 [>= total bytes], int64 [n+1], e.g. reused or
+        pinned across calls, so the ids are not written into a freshly page-faulted array).
+        Returns (ids int32[n_tokens] -- a view of out when given --, out_off int64[n+1])."""
         buf = np.ascontiguousarray(buf, dtype=np.uint8)
         off = np.ascontiguousarray(off, dtype=np.int64)
         if buf.size == 0:
             buf = np.zeros(1, np.uint8)
         n = len(off) - 1
         total = int(off[-1] - off[0]) if n > 0 else 0
-        out = np.empty(max(total, 1), dtype=np.int32)
-        out_off = np.empty(n + 1, dtype=np.int64)
+        if out is None:
+            out = np.empty(max(total, 1), dtype=np.int32)
+        elif out.dtype != np.int32 or not out.flags["C_CONTIGUOUS"] or out.size < total:
+            raise ValueError("out: a contiguous int32 array of at least the batch's byte count")
+        if out_off is None:
+            out_off = np.empty(n + 1, dtype=np.int64)
+        elif out_off.dtype != np.int64 or not out_off.flags["C_CONTIGUOUS"] or out_off.size < n + 1:
+            raise ValueError("out_off: a contiguous int64 array of at least n + 1 entries")
         stats = _lib.SwStats()
         L = _lib.lib()
         bits = None if chunk_bits is None else np.ascontiguousarray(chunk_bits, dtype=np.uint64)
-        _lib.check(L.sw_encode_batch(self._encoder(), _lib.ptr(buf, ctypes.c_uint8), _lib.ptr(off, ctypes.c_int64),
-                                     n, pattern_id(self.pattern), _lib.ptr(bits, ctypes.c_uint64),
-                                     _lib.ptr(out, ctypes.c_int32), total, _lib.ptr(out_off, ctypes.c_int64),
-                                     ctypes.byref(stats)))
+        args = (self._encoder(), _lib.ptr(buf, ctypes.c_uint8), _lib.ptr(off, ctypes.c_int64), n,
+                pattern_id(self.pattern), _lib.ptr(bits, ctypes.c_uint64))
+        tail = (_lib.ptr(out, ctypes.c_int32), max(out.size, total), _lib.ptr(out_off, ctypes.c_int64), ctypes.byref(stats))
+        if specials:
+            st, keep = _lib.specials_struct(specials)
+            _lib.check(L.sw_encode_batch_ex(*args, ctypes.byref(st), *tail))
+            del keep
+        else:
+            _lib.check(L.sw_encode_batch(*args, *tail))
         self.last_stats = stats
-        return out[:int(out_off[-1])], out_off
+        return out[:int(out_off[n])], out_off[:n + 1]
 
-    def encode_device(self, d_buf, d_off, d_bits=None, d_out=None, d_out_off=None, stream=None):
+    def encode_device(self, d_buf, d_off, d_bits=None, d_out=None, d_out_off=None, stream=None, out_bits=32,
+                      d_specials=None):
         """Encode strings already on this tokenizer's device (torch tensors: uint8 bytes, int64
         offsets from 0; optional pre-split bitmap as int64 words, else the device pre-splits with
-        `pattern`), on torch's current stream (or `stream`).  Returns (ids int32 [n_tokens],
-        offsets int64 [n+1]) as device tensors; the token count is read back (one
-        synchronisation).  d_out / d_out_off: optional output buffers (>= n_bytes / n+1)."""
+        `pattern`), on torch's current stream (or `stream`).  out_bits 16: the ids are written as
+        16 bits (int16 tensor holding each id's low 16 bits; tables whose every id fits, the
+        multi-GPU transport).  d_specials: optional special-token occurrences on the device,
+        (pos int64, len int32, id int32) as corpus.find_specials gives them (a caller bitmap must
+        then come from presplit_specials).  Returns (ids [n_tokens], offsets int64 [n+1]) as device
+        tensors; the token count is read back (one synchronisation).  d_out / d_out_off: optional
+        output buffers (>= n_bytes of the output dtype / n+1)."""
         import torch
+        if out_bits not in (16, 32):
+            raise ValueError("out_bits must be 16 or 32")
         dev = d_buf.device
         n = int(d_off.numel()) - 1
         n_bytes = int(d_off[-1].item()) if n >= 0 else 0
+        want = torch.int16 if out_bits == 16 else torch.int32
         if d_out is None:
-            d_out = torch.empty(max(n_bytes, 1), dtype=torch.int32, device=dev)
+            d_out = torch.empty(max(n_bytes, 1), dtype=want, device=dev)
+        elif d_out.dtype != want or d_out.numel() < n_bytes:
+            raise ValueError("d_out: %s with at least n_bytes elements" % want)
         if d_out_off is None:
             d_out_off = torch.empty(n + 1, dtype=torch.int64, device=dev)
         L = _lib.lib()
         h = self._encoder()
         _lib.check(L.sw_encoder_set_option(h, _lib.SW_OPT_PATTERN, pattern_id(self.pattern)))
         st = stream if stream is not None else torch.cuda.current_stream(dev).cuda_stream
+        ex = _lib.SwEncodeEx(d_bits.data_ptr() if d_bits is not None else None, out_bits, None, None, None, 0)
+        if d_specials is not None and d_specials[0].numel() > 0:
+            pos, ln, ids = d_specials
+            if pos.dtype != torch.int64 or ln.dtype != torch.int32 or ids.dtype != torch.int32:
+                raise ValueError("d_specials: (int64 positions, int32 lengths, int32 ids)")
+            ex.sp_pos, ex.sp_len, ex.sp_id, ex.n_sp = pos.data_ptr(), ln.data_ptr(), ids.data_ptr(), pos.numel()
         n_tok = ctypes.c_int64()
-        _lib.check(L.sw_encode_device(h, d_buf.data_ptr(), n_bytes, d_off.data_ptr(), n,
-                                      d_bits.data_ptr() if d_bits is not None else None,
-                                      d_out.data_ptr(), d_out_off.data_ptr(), st, ctypes.byref(n_tok)))
+        _lib.check(L.sw_encode_device_ex(h, d_buf.data_ptr(), n_bytes, d_off.data_ptr(), n, ctypes.byref(ex),
+                                         d_out.data_ptr(), d_out_off.data_ptr(), st, ctypes.byref(n_tok)))
         return d_out[:int(n_tok.value)], d_out_off
 
-    def _split_specials(self, text):
-        """Split on special tokens: leftmost occurrence first, dictionary order breaking ties
-        (the reference stores special_tokens at base.py:103 but defines no split).  One regex
-        alternation of the escaped specials in dict order: `re` takes the leftmost match and,
-        at one position, the first alternative that matches -- exactly that rule."""
-        key = tuple(self.special_tokens.items())
-        if key != self._sp_key:
-            specials = [s for s in self.special_tokens if s]
-            self._sp_re = re.compile("|".join(map(re.escape, specials))) if specials else None
-            self._sp_key = key
-        if self._sp_re is None:
-            return [text]
-        parts, seg = [], 0
-        for m in self._sp_re.finditer(text):
-            parts.append(text[seg:m.start()])
-            parts.append(self.special_tokens[m.group()])
-            seg = m.end()
-        parts.append(text[seg:])
-        return parts
-
     def encode_batch(self, texts, allowed_special="all"):
-        """Encode many strings in one device batch; returns a list of id lists."""
+        """Encode many strings in one device batch; returns a list of id lists.  allowed_special
+        "all": occurrences of self.special_tokens encode to their ids -- leftmost first, the first
+        special in dict order at one position (the reference stores special_tokens, base.py:103,
+        but defines no split) -- found by the library's host threads; "none": ordinary text."""
         if allowed_special not in ("all", "none"):
             raise ValueError("allowed_special must be 'all' or 'none'")
         texts = list(texts)
-        split = allowed_special == "all" and any(self.special_tokens)
-        if not split:  # one piece per text: one device batch, one list conversion
-            ids, off = self.encode_ordinary_batch_np([t.encode("utf-8") for t in texts])
-            flat, o = ids.tolist(), off.tolist()
-            return [flat[o[k]:o[k + 1]] for k in range(len(texts))]
-        pieces, layout = [], []
-        for t in texts:
-            lay = []
-            for p in self._split_specials(t):
-                if isinstance(p, int):
-                    lay.append(p)
-                else:
-                    lay.append(-1 - len(pieces))
-                    pieces.append(p.encode("utf-8"))
-            layout.append(lay)
-        ids, off = self.encode_ordinary_batch_np(pieces)
+        specials = self.special_tokens if allowed_special == "all" and any(self.special_tokens) else None
+        ids, off = self.encode_packed(*_pack_strings([t.encode("utf-8") for t in texts]), specials=specials)
         flat, o = ids.tolist(), off.tolist()
-        out = []
-        for lay in layout:
-            r = []
-            for x in lay:
-                if x >= 0:
-                    r.append(x)
-                else:
-                    r.extend(flat[o[-1 - x]:o[-x]])
-            out.append(r)
-        return out
+        return [flat[o[k]:o[k + 1]] for k in range(len(texts))]
 
     def encode(self, text, allowed_special="all"):
         return self.encode_batch([text], allowed_special)[0]

@@ -338,10 +338,12 @@ def test_dedupe_options_validated():
 
 
 @pytest.mark.parametrize("fixture,model", [("enc_bl50k_stress.npz", "bl50k.model"), ("enc_bl32k_mixed.npz", "bl32k.model")])
-def test_out_bits16_option(fixture, model):
-    """SW_OPT_OUT_BITS 16: sw_encode_device writes uint16 ids (the multi-GPU transport's width) --
-    the reference-generated ids' low 16 bits, ids >= 32768 included (bl50k); rejected for a table
-    with an id over 16 bits; sw_encode_batch still returns int32."""
+def test_out_bits16_per_call(fixture, model):
+    """sw_encode_device_ex out_bits 16 writes uint16 ids (the multi-GPU transport's width) -- the
+    reference-generated ids' low 16 bits, ids >= 32768 included (bl50k) -- for that call only: a
+    later sw_encode_device / Tokenizer.encode_device on the same handle writes int32 again (the
+    former persistent SW_OPT_OUT_BITS is rejected); 16 bits is refused for a table with an id over
+    16 bits; sw_encode_batch returns int32."""
     import ctypes
 
     import torch
@@ -349,25 +351,35 @@ def test_out_bits16_option(fixture, model):
     t = sa.Tokenizer(device=0)
     t.merges = load_model_merges(model)
     L, h = _lib.lib(), t._encoder()
-    _lib.check(L.sw_encoder_set_option(h, _lib.SW_OPT_OUT_BITS, 16))
+    assert L.sw_encoder_set_option(h, _lib.SW_OPT_OUT_BITS, 16) == _lib.SW_ERR_ARG
     dev = torch.device("cuda", 0)
     d_buf, d_off = torch.from_numpy(fx["bytes"]).to(dev), torch.from_numpy(fx["off"]).to(dev)
     d_out = torch.full((len(fx["bytes"]) + 8,), -1, dtype=torch.int16, device=dev)
     d_oo = torch.empty(len(fx["off"]), dtype=torch.int64, device=dev)
     n_tok = ctypes.c_int64()
-    _lib.check(L.sw_encode_device(h, d_buf.data_ptr(), len(fx["bytes"]), d_off.data_ptr(), len(fx["off"]) - 1, None,
-                                  d_out.data_ptr(), d_oo.data_ptr(), torch.cuda.current_stream(dev).cuda_stream,
-                                  ctypes.byref(n_tok)))
+    ex = _lib.SwEncodeEx(None, 16, None, None, None, 0)
+    _lib.check(L.sw_encode_device_ex(h, d_buf.data_ptr(), len(fx["bytes"]), d_off.data_ptr(), len(fx["off"]) - 1,
+                                     ctypes.byref(ex), d_out.data_ptr(), d_oo.data_ptr(),
+                                     torch.cuda.current_stream(dev).cuda_stream, ctypes.byref(n_tok)))
     n = n_tok.value
     assert n == len(fx["ids"])
     np.testing.assert_array_equal(d_out[:n].cpu().numpy().view(np.uint16).astype(np.int64), fx["ids"])
     assert int(d_out[n].item()) == -1  # (nothing written past the ids)
     np.testing.assert_array_equal(d_oo.cpu().numpy(), fx["ids_off"])
+    # the next calls on the same handle: int32 again
+    ids, off = t.encode_device(d_buf, d_off)
+    assert ids.dtype == torch.int32
+    np.testing.assert_array_equal(ids.cpu().numpy(), fx["ids"])
+    ids16, _ = t.encode_device(d_buf, d_off, out_bits=16)
+    np.testing.assert_array_equal(ids16.cpu().numpy().view(np.uint16).astype(np.int64), fx["ids"])
     assert_same(t.encode_packed(fx["bytes"], fx["off"]), (fx["ids"], fx["ids_off"]))  # (host path: int32)
-    _lib.check(L.sw_encoder_set_option(h, _lib.SW_OPT_OUT_BITS, 32))
-    assert L.sw_encoder_set_option(h, _lib.SW_OPT_OUT_BITS, 8) == _lib.SW_ERR_ARG
+    ex.out_bits = 8
+    assert L.sw_encode_device_ex(h, d_buf.data_ptr(), len(fx["bytes"]), d_off.data_ptr(), len(fx["off"]) - 1,
+                                 ctypes.byref(ex), d_out.data_ptr(), d_oo.data_ptr(), None, None) == _lib.SW_ERR_ARG
     t.close()
     w = sa.Tokenizer(device=0)
     w.merges = {(97, 98): 70000}
-    assert L.sw_encoder_set_option(w._encoder(), _lib.SW_OPT_OUT_BITS, 16) == _lib.SW_ERR_ARG
+    ex.out_bits = 16
+    assert L.sw_encode_device_ex(w._encoder(), d_buf.data_ptr(), len(fx["bytes"]), d_off.data_ptr(), len(fx["off"]) - 1,
+                                 ctypes.byref(ex), d_out.data_ptr(), d_oo.data_ptr(), None, None) == _lib.SW_ERR_ARG
     w.close()

@@ -1,0 +1,158 @@
+"""Special tokens (E1) through the native path: the occurrences found on the host threads, each one
+chunk encoding to its id on the GPU, the text between them pre-split on its own -- on the device
+(k_split_classify with the occurrences' ends as string boundaries) or on the host
+(sw_presplit_host_specials) -- against the oracle's orc_encode_with_specials (pinned: the pieces are
+ordinary encodes, pinned to the reference's primitives by the golden vectors).
+
+The reference stores special_tokens (shredword/base.py:103) but defines no split; the rule is the
+build's (leftmost first, dict order on ties), the one tests/test_specials.py pins on the host."""
+import ctypes
+import os
+import random
+
+import numpy as np
+import pytest
+
+import oracle
+import shredword_amd as sa
+from shredword_amd import _lib, corpus
+from conftest import GOLD, load_model_merges
+
+pytestmark = pytest.mark.gpu
+
+SPECIALS = {"<|endoftext|>": 100257, "<|fim_prefix|>": 100258, "<|fim|>": 100259, "<|": 100260}
+PAT = {"cl100k": oracle.PAT_CL100K, "gpt2": oracle.PAT_GPT2, "none": oracle.PAT_NONE}
+
+
+def tok_for(model, pattern="cl100k"):
+    t = sa.Tokenizer(device=0)
+    t.merges = load_model_merges(model)
+    t.pattern = {"cl100k": "", "gpt2": sa.GPT2_PATTERN, "none": "none"}[pattern]
+    return t
+
+
+def expected(t, buf, off, specials, pattern):
+    return oracle.OracleModel(t.merges).encode_batch_specials(buf, off, specials, PAT[pattern], n_threads=8)
+
+
+def fuzz_texts(seed, n, kmax=60):
+    rng = random.Random(seed)
+    alphabet = ["word", " the", " ", "  ", "\n", "\n\n", "123", "45678", "'s", "'LL", "!!", "...", " <", "|", ">",
+                "<|fim|>", "<|endoftext|>", "<|fim_prefix|>", "<|", "中文", "\U0001f642", "été", "\t", "\r\n",
+                " x", "aaaa", "Hello", " world"]
+    return ["".join(rng.choice(alphabet) for _ in range(rng.randint(0, kmax))) for _ in range(n)]
+
+
+def pack(datas):
+    off = np.zeros(len(datas) + 1, dtype=np.int64)
+    np.cumsum([len(d) for d in datas], out=off[1:])
+    return np.frombuffer(b"".join(datas) or b"\0", dtype=np.uint8)[:int(off[-1])].copy(), off
+
+
+@pytest.mark.parametrize("pattern", ["cl100k", "gpt2", "none"])
+@pytest.mark.parametrize("host_presplit", [0, 1])
+def test_encode_batch_specials_fuzz(pattern, host_presplit):
+    """Tokenizer.encode_batch with special tokens (the native path) == the oracle, device and host
+    pre-split, on fuzzed strings full of specials, partial specials, empty strings."""
+    t = tok_for("bl32k.model", pattern)
+    t.special_tokens = dict(SPECIALS)
+    texts = fuzz_texts(3 + host_presplit, 1500) + ["", "<|endoftext|>", "<|endoftext|><|endoftext|>", "<|fim", "x<|"]
+    L, h = _lib.lib(), t._encoder()
+    _lib.check(L.sw_encoder_set_option(h, _lib.SW_OPT_HOST_PRESPLIT, host_presplit))
+    try:
+        got = t.encode_batch(texts)
+    finally:
+        L.sw_encoder_set_option(h, _lib.SW_OPT_HOST_PRESPLIT, 0)
+    om = oracle.OracleModel(t.merges)
+    for i, s in enumerate(texts):
+        assert got[i] == om.encode_with_specials(s, SPECIALS, PAT[pattern]), (i, s)
+    # allowed_special="none": the specials' text is ordinary text
+    assert t.encode_batch(texts[:50], "none") == [om.encode_with_specials(s, {}, PAT[pattern]) for s in texts[:50]]
+    t.close()
+
+
+def test_golden_gpt2_fixture_with_specials():
+    """The enc_bl32k_gpt2 golden strings: as they are, the native path gives the reference-generated
+    ids; with specials spliced in, the oracle's."""
+    fx = np.load(os.path.join(GOLD, "enc_bl32k_gpt2.npz"))
+    t = tok_for("bl32k.model", "gpt2")
+    t.special_tokens = dict(SPECIALS)
+    ids, off = t.encode_packed(fx["bytes"], fx["off"], specials=SPECIALS)
+    np.testing.assert_array_equal(ids, fx["ids"])
+    np.testing.assert_array_equal(off, fx["ids_off"])
+    buf, soff = corpus.splice_specials(fx["bytes"], fx["off"], SPECIALS, per_kib=8.0, end_special=0)
+    ids, off = t.encode_packed(buf, soff, specials=SPECIALS)
+    e_ids, e_off = expected(t, buf, soff, SPECIALS, "gpt2")
+    np.testing.assert_array_equal(off, e_off)
+    np.testing.assert_array_equal(ids, e_ids)
+    t.close()
+
+
+def test_device_entry_specials_and_bitmap():
+    """sw_encode_device_ex with device occurrences: the fused device pre-split (no bitmap) and a host
+    bitmap from sw_presplit_host_specials give the oracle's ids; 16-bit output with specials is
+    refused."""
+    import torch
+    t = tok_for("bl50k.model")
+    texts = [s.encode() for s in fuzz_texts(9, 3000, 120)]
+    buf, off = pack(texts)
+    pos, ln, ids = corpus.find_specials(buf, off, SPECIALS)
+    assert len(pos) > 1000
+    e_ids, e_off = expected(t, buf, off, SPECIALS, "cl100k")
+    dev = torch.device("cuda", 0)
+    d_buf, d_off = torch.from_numpy(buf).to(dev), torch.from_numpy(off).to(dev)
+    d_sp = tuple(torch.from_numpy(x).to(dev) for x in (pos, ln, ids))
+    g_ids, g_off = t.encode_device(d_buf, d_off, d_specials=d_sp)
+    np.testing.assert_array_equal(g_off.cpu().numpy(), e_off)
+    np.testing.assert_array_equal(g_ids.cpu().numpy(), e_ids)
+    bits, _ = corpus.presplit_specials(buf, off, pos, ln, _lib.SW_PAT_CL100K)
+    d_bits = torch.from_numpy(bits.view(np.int64)).to(dev)
+    g_ids, g_off = t.encode_device(d_buf, d_off, d_bits=d_bits, d_specials=d_sp)
+    np.testing.assert_array_equal(g_ids.cpu().numpy(), e_ids)
+    with pytest.raises(_lib.ShredwordError):
+        t.encode_device(d_buf, d_off, d_specials=d_sp, out_bits=16)
+    t.close()
+
+
+def test_specials_tile_edges_and_long_occurrences():
+    """Occurrences across the 2 KiB tile and 32-byte lane edges, a special longer than a tile, runs of
+    adjacent occurrences, strings that are only specials."""
+    long_sp = "<|" + "x" * 3000 + "|>"
+    sp = {"<|endoftext|>": 100257, long_sp: 100261, "<|fim|>": 100259}
+    t = tok_for("bl32k.model")
+    t.special_tokens = sp
+    rng = random.Random(5)
+    texts = []
+    for k in range(200):
+        pre = "a" * rng.randint(0, 2100) + " word 12345"
+        texts.append(pre + rng.choice(list(sp)) * rng.randint(1, 4) + " tail" * rng.randint(0, 30))
+    texts += [long_sp, long_sp + long_sp, "<|fim|>" * 500, "<|endoftext|> " * 300]
+    got = t.encode_batch(texts)
+    om = oracle.OracleModel(t.merges)
+    for i, s in enumerate(texts):
+        assert got[i] == om.encode_with_specials(s, sp, oracle.PAT_CL100K), i
+    t.close()
+
+
+def test_pipelined_batch_with_specials():
+    """A host batch above the pipeline's run size (runs of whole strings, each run's occurrences
+    rebased) and above the launch limit (SW_OPT_MAX_LAUNCH_BYTES), with ids over 16 bits (32-bit
+    downloads) -- equal to the oracle."""
+    t = tok_for("bl32k.model", "gpt2")
+    t.special_tokens = dict(SPECIALS)
+    buf, off = corpus.synth(21, corpus.MIXED, 6000, 900, n_threads=8)
+    buf, off = corpus.splice_specials(buf, off, SPECIALS, per_kib=1.5, end_special=0)
+    e_ids, e_off = expected(t, buf, off, SPECIALS, "gpt2")
+    L, h = _lib.lib(), t._encoder()
+    try:
+        for opt, val in ((_lib.SW_OPT_PIPE_RUN_BYTES, 1 << 20), (_lib.SW_OPT_MAX_LAUNCH_BYTES, 1 << 20)):
+            _lib.check(L.sw_encoder_set_option(h, _lib.SW_OPT_PIPE_RUN_BYTES, val if opt == _lib.SW_OPT_PIPE_RUN_BYTES else 0))
+            _lib.check(L.sw_encoder_set_option(h, _lib.SW_OPT_MAX_LAUNCH_BYTES, val if opt == _lib.SW_OPT_MAX_LAUNCH_BYTES else 0))
+            out = np.zeros(len(buf), dtype=np.int32)
+            g_ids, g_off = t.encode_packed(buf, off, specials=SPECIALS, out=out)
+            np.testing.assert_array_equal(g_off, e_off)
+            np.testing.assert_array_equal(g_ids, e_ids)
+    finally:
+        L.sw_encoder_set_option(h, _lib.SW_OPT_PIPE_RUN_BYTES, 64 << 20)
+        L.sw_encoder_set_option(h, _lib.SW_OPT_MAX_LAUNCH_BYTES, 0)
+    t.close()

@@ -167,17 +167,6 @@ def test_tracked_merges_and_vocab():
     assert t._vocab_now()[5] == b"zz" and t.vocab.version == ver + 2
 
 
-def test_special_split_rule():
-    t = sa.Tokenizer(device=0)
-    t.special_tokens = {"<a>": 300, "<a><b>": 301, "<b>": 302}
-    # leftmost first; at one position the first special in dict order wins
-    assert t._split_specials("x<a><b>y<b>") == ["x", 300, "", 302, "y", 302, ""]
-    t.special_tokens = {"<a><b>": 301, "<a>": 300}
-    assert t._split_specials("x<a><b>y<a>") == ["x", 301, "y", 300, ""]
-    t.special_tokens = {}
-    assert t._split_specials("x<a>") == ["x<a>"]
-
-
 def test_corpus_deterministic_across_threads():
     a, ao = corpus.synth(5, corpus.MIXED, 300, 500, n_threads=1)
     b, bo = corpus.synth(5, corpus.MIXED, 300, 500, n_threads=5)

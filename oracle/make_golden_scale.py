@@ -37,6 +37,8 @@ CONFIGS = {
     "c2_mixed_bl32k_cl100k": (corpus.MIXED, 1074, "bl32k", "cl100k"),
     "c5_stress_bl50k_cl100k": (corpus.STRESS, 600, "bl50k", "cl100k"),
     "c2_mixed_bl32k_gpt2": (corpus.MIXED, 1074, "bl32k", "gpt2"),
+    # round 4: the low-repetition corpus (bench.py --corpus entropy)
+    "entropy_bl32k_cl100k": (corpus.ENTROPY, 1074, "bl32k", "cl100k"),
 }
 
 _MERGES = {}
@@ -70,10 +72,17 @@ def main():
     ap.add_argument("--mb", type=float, default=16.0)
     ap.add_argument("--gpt2-mb", type=float, default=4.0)
     ap.add_argument("--procs", type=int, default=8)
+    ap.add_argument("--only", default=None, help="regenerate this config only, keeping the others' digests")
     args = ap.parse_args()
     out = {"reference": mg.REF_BASE, "seed": BENCH_SEED, "block_strings": BLOCK, "configs": {}}
+    path = os.path.join(mg.GOLD, "scale_digests.json")
+    if args.only:
+        with open(path) as f:
+            out = json.load(f)
     with mp.get_context("fork").Pool(args.procs) as pool:
         for name, (kind, mean, model, pattern) in CONFIGS.items():
+            if args.only and name != args.only:
+                continue
             mb = args.gpt2_mb if pattern == "gpt2" else args.mb
             buf, off = prefix(kind, mean, int(mb * 1e6))
             data = bytes(buf)
@@ -90,7 +99,7 @@ def main():
             print("%s: %d strings, %.1f MB, %d tokens, %.0f s" % (name, n, off[-1] / 1e6,
                                                                     out["configs"][name]["n_tokens"], time.time() - t),
                   flush=True)
-    with open(os.path.join(mg.GOLD, "scale_digests.json"), "w") as f:
+    with open(path, "w") as f:
         json.dump(out, f, indent=0)
 
 

@@ -9,10 +9,10 @@
 //                          digit runs, whitespace runs, contractions
 //   SW_CORPUS_STRESS (C5)  Zipf string lengths 4..4096 B, >=1% strings that are a single
 //                          4096-B letter run, long whitespace runs, (a,a) runs
-//   SW_CORPUS_ENTROPY      low-repetition text: a flat Zipf over 1 M words in six scripts (Latin
-//                          with accents, Cyrillic, Greek, CJK, Hangul, Devanagari), random casing,
-//                          digits inside words -- most multi-token chunks are distinct, so the
-//                          merge loop itself, not the memoisation, carries the encode
+//   SW_CORPUS_ENTROPY      low-repetition text: a flat Zipf over 1 M words -- mixed-case Latin
+//                          pseudo-words with accents, and Cyrillic, Greek, CJK, Hangul, Devanagari
+//                          letter strings -- so that many multi-token chunks are distinct and the
+//                          merge loop itself, not the memoisation, carries much of the encode
 //
 // sw_synth_splice_specials inserts special tokens into such a corpus (the C3 workload: a
 // document separator at every string's end and others at random code-point boundaries).
@@ -136,29 +136,48 @@ struct Lexicon {
     for (size_t i = 0; i < n; ++i) zw[i] = 1.0 / std::pow((double)i + 2.7, 1.07);
     zipf.build(zw);
   }
-  // 1 M words, each in one script, 1..12 code points; letters cased at random (Latin, Cyrillic,
-  // Greek), a digit inside 8% of the words; a flat Zipf (exponent 0.75)
+  // 1 M words: 62% pseudo-words of 1..5 syllables (the MIXED syllables, accented vowels; prose()
+  // flips their case per occurrence), the rest random letters of Cyrillic / Greek (2..10,
+  // random case), CJK (1..4), Hangul (1..3), Devanagari (2..6); a digit inside 3% of the words; a
+  // flat Zipf (exponent 0.8) -- the word list is large and mixed-case enough that most chunks the
+  // merge loop gets are distinct in a 1 GiB batch
   void build_entropy(Rng& r) {
     const size_t n = 1000000;
     words.reserve(n);
-    static const uint32_t kBase[] = {0x61, 0x430, 0x3B1, 0x4E00, 0xAC00, 0x915};
-    static const uint32_t kSpan[] = {26, 32, 25, 0x51A6, 11172, 37};
     for (size_t i = 0; i < n; ++i) {
       std::string w;
-      double u = r.uni();
-      const int script = u < 0.45 ? 0 : u < 0.62 ? 1 : u < 0.74 ? 2 : u < 0.86 ? 3 : u < 0.94 ? 4 : 5;
-      const int len = script >= 3 ? 1 + (int)r.below(4) : 2 + (int)r.below(11);
-      for (int k = 0; k < len; ++k) {
-        if (r.uni() < 0.01) { w += (char)('0' + r.below(10)); continue; }
-        if (script == 0 && r.uni() < 0.12) { put_utf8(w, kLatin1[r.below(20)]); continue; }
-        uint32_t cp = kBase[script] + r.below(kSpan[script]);
-        if (script <= 2 && r.uni() < 0.3) cp -= script == 0 ? 0x20 : script == 1 ? 0x20 : 0x20;  // upper case
-        put_utf8(w, cp);
+      const double u = r.uni();
+      if (u < 0.62) {
+        const double v = r.uni();
+        const int syl = v < 0.25 ? 1 : v < 0.55 ? 2 : v < 0.80 ? 3 : v < 0.93 ? 4 : 5;
+        for (int k = 0; k < syl; ++k) {
+          w += pick(r, kOnset);
+          if (r.uni() < 0.10) put_utf8(w, kLatin1[r.below(20)]);
+          else w += pick(r, kVowel);
+          if (k + 1 == syl || r.uni() < 0.3) w += pick(r, kCoda);
+        }
+      } else {
+        const int script = u < 0.72 ? 1 : u < 0.80 ? 2 : u < 0.89 ? 3 : u < 0.95 ? 4 : 5;
+        static const uint32_t kBase[] = {0, 0x430, 0x3B1, 0x4E00, 0xAC00, 0x915};
+        static const uint32_t kSpan[] = {0, 32, 24, 0x51A6, 11172, 37};
+        const int len = script <= 2 ? 2 + (int)r.below(9) : script == 3 ? 1 + (int)r.below(4)
+                                                           : script == 4 ? 1 + (int)r.below(3) : 2 + (int)r.below(5);
+        for (int k = 0; k < len; ++k) {
+          uint32_t cp = kBase[script] + r.below(kSpan[script]);
+          if (script == 2 && cp >= 0x3C2) ++cp;              // (skip final sigma's slot: U+03A2 upper is unassigned)
+          if (script <= 2 && r.uni() < 0.3) cp -= 0x20;      // upper case
+          put_utf8(w, cp);
+        }
+      }
+      if (r.uni() < 0.03) {  // a digit at a code-point boundary
+        size_t at = r.below((uint32_t)w.size() + 1);
+        while (at < w.size() && ((unsigned char)w[at] & 0xC0) == 0x80) ++at;
+        w.insert(at, 1, (char)('0' + r.below(10)));
       }
       words.push_back(std::move(w));
     }
     std::vector<double> zw(n);
-    for (size_t i = 0; i < n; ++i) zw[i] = 1.0 / std::pow((double)i + 2.7, 0.75);
+    for (size_t i = 0; i < n; ++i) zw[i] = 1.0 / std::pow((double)i + 2.7, 0.8);
     zipf.build(zw);
   }
 };
@@ -167,7 +186,10 @@ const char* kContractions[] = {"'s", "'t", "'re", "'ve", "'ll", "'d", "'m", "'S"
 const char* kPunct[] = {",", ".", "!", "?", ";", ":", "\"", ")", "...", "-", "--", "%", "&"};
 
 // Emits prose until s.size() >= len, then trims to exactly len bytes at a code point edge.
+// (SW_CORPUS_ENTROPY: every ASCII letter of every occurrence upper-cased with probability 0.12,
+// so a word's occurrences are rarely byte-equal)
 void prose(const Lexicon& lx, Rng& r, std::string& s, size_t len, bool ascii_lines) {
+  const bool flip = lx.kind == SW_CORPUS_ENTROPY;
   bool sentence_start = true;
   int words_in_line = 0, line_len = 5 + r.below(16);
   while (s.size() < len) {
@@ -181,6 +203,9 @@ void prose(const Lexicon& lx, Rng& r, std::string& s, size_t len, bool ascii_lin
       size_t at = s.size();
       if (!ascii_lines && r.uni() < 0.03) s += (r.uni() < 0.5 ? '(' : '"');
       s += w;
+      if (flip)
+        for (size_t k = s.size() - w.size(); k < s.size(); ++k)
+          if (s[k] >= 'a' && s[k] <= 'z' && r.uni() < 0.12) s[k] = (char)(s[k] - 32);
       if ((sentence_start && r.uni() < 0.9) || r.uni() < 0.05) {
         char& c = s[at + (s[at] == '(' || s[at] == '"')];
         if (c >= 'a' && c <= 'z') c = (char)(c - 32);

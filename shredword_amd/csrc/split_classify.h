@@ -209,6 +209,7 @@ template <bool kSp>
 __device__ __forceinline__ void split_classify_tile(const EncArgs& a, const PbArgs& g, int pattern, const uint32_t* edge,
                                                     uint32_t* bits32, int64_t tile, uint32_t* s_win, ScShared* sh,
                                                     uint16_t* s_qbuf) {
+  SW_STAMP_INIT;
   const int lane = threadIdx.x & 63;
   const int64_t t0 = tile * kTile;
   const int64_t t1 = min(t0 + (int64_t)kTile, a.n_bytes);
@@ -280,6 +281,10 @@ __device__ __forceinline__ void split_classify_tile(const EncArgs& a, const PbAr
     }
   }
   wave_sync_mem();
+#ifdef SW_STAMPS
+  __builtin_amdgcn_s_waitcnt(0);
+  SW_STAMP(12);
+#endif
   const FSrc src{GSrc{g, a.n_tiles, n_chunks, cl}, &sm, c0, t0, n_chunks};
   // 3. this lane's chunk: class masks (to LDS, where the rules read them: nothing is held in
   //    registers across the rare walk of psb::carries, which would otherwise cost ~60 VGPRs)
@@ -308,6 +313,7 @@ __device__ __forceinline__ void split_classify_tile(const EncArgs& a, const PbAr
       sm.m[5][k] = m1.A; sm.m[6][k] = m1.X; sm.m[7][k] = m1.K1; sm.m[8][k] = m1.K2;
     }
     wave_sync_mem();
+    SW_STAMP(13);
     auto col = [&](int k) {
       return psb::Masks{sm.m[0][k], sm.m[1][k], sm.m[2][k], sm.m[3][k], sm.m[4][k], sm.m[5][k], sm.m[6][k], sm.m[7][k], sm.m[8][k]};
     };
@@ -333,6 +339,7 @@ __device__ __forceinline__ void split_classify_tile(const EncArgs& a, const PbAr
     bits32[c] = r;
     if (c == n_chunks - 1 && (c & 1) == 0) bits32[c + 1] = 0;  // (the last word's upper half)
   }
+  SW_STAMP(14);
   // 4. the end of the tile's last chunk: the first chunk start of the next tile (k_edges)
   int rel_end;
   if (t1 >= a.n_bytes) rel_end = (int)(a.n_bytes - t0);

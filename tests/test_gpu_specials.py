@@ -27,7 +27,7 @@ PAT = {"cl100k": oracle.PAT_CL100K, "gpt2": oracle.PAT_GPT2, "none": oracle.PAT_
 def tok_for(model, pattern="cl100k"):
     t = sa.Tokenizer(device=0)
     t.merges = load_model_merges(model)
-    t.pattern = {"cl100k": "", "gpt2": sa.GPT2_PATTERN, "none": "none"}[pattern]
+    t.pattern = {"cl100k": "", "gpt2": sa.GPT2_PATTERN, "none": _lib.SW_PAT_NONE}[pattern]
     return t
 
 

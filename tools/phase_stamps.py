@@ -18,6 +18,8 @@ kind = corpus.STRESS if (len(sys.argv) > 2 and sys.argv[2] == "stress") else cor
 model = "bl50k.model" if kind == corpus.STRESS else "bl32k.model"
 buf, off = corpus.synth(1_000_003, kind, n, 1074 if kind == corpus.MIXED else 600, n_threads=16)
 bits, nch = corpus.presplit(buf, off, 0, n_threads=16)
+if len(sys.argv) > 3 and sys.argv[3] == "fused":  # the device pre-split inside k_split_classify
+    bits = None
 tok = Tokenizer(0)
 tok.load(os.path.join(ROOT, "tests", "golden", model))
 tok.encode_packed(buf, off, bits)  # warm
@@ -32,6 +34,7 @@ tiles = (len(buf) + 2047) // 2048
 names = {0: "classify: stage+enum", 1: "classify: lookups", 7: "classify: dedupe", 2: "classify: counts",
          3: "classify: strings",
          4: "merge N<16 (blk)", 5: "merge N>=16 (blk)", 6: "merge long (blk)",
+         12: "fused: stage+strings", 13: "fused: class masks", 14: "fused: rules",
          8: "compact: prologue loads", 9: "compact: slots+gathers", 10: "compact: scan+stores", 11: "compact: strings"}
 tot = sum(out[i] for i in names)
 print("kind=%s bytes=%d chunks=%d tiles=%d kernel_ms=%.3f" % (model, len(buf), nch, tiles, tok.last_stats.ms_kernels))

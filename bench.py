@@ -212,9 +212,19 @@ def main():
         d_sp = tuple(torch.from_numpy(np.ascontiguousarray(x)).to(dev) for x in sp_host)
         ex.sp_pos, ex.sp_len, ex.sp_id, ex.n_sp = d_sp[0].data_ptr(), d_sp[1].data_ptr(), d_sp[2].data_ptr(), len(sp_host[0])
 
+    plain = not out16 and not specials  # (sw_encode_device: what an A/B build of an earlier revision has)
+
+    def encode_into(o_ids, o_off, n_tok_ptr=None):
+        if plain:
+            _lib.check(L.sw_encode_device(h, d_buf.data_ptr(), n_bytes, d_off.data_ptr(), n_str,
+                                          d_bits.data_ptr() if host_ps else None, o_ids.data_ptr(), o_off.data_ptr(),
+                                          stream, n_tok_ptr))
+        else:
+            _lib.check(L.sw_encode_device_ex(h, d_buf.data_ptr(), n_bytes, d_off.data_ptr(), n_str, ctypes.byref(ex),
+                                             o_ids.data_ptr(), o_off.data_ptr(), stream, n_tok_ptr))
+
     def encode(n_tok_ptr=None):
-        _lib.check(L.sw_encode_device_ex(h, d_buf.data_ptr(), n_bytes, d_off.data_ptr(), n_str, ctypes.byref(ex),
-                                         d_out.data_ptr(), d_oo.data_ptr(), stream, n_tok_ptr))
+        encode_into(d_out, d_oo, n_tok_ptr)
 
     if not host_ps and not specials:  # chunk count for the report (outside the timed region)
         tmp_bits = torch.empty((n_bytes + 63) // 64, dtype=torch.int64, device=dev)
@@ -263,8 +273,7 @@ def main():
             torch.cuda.current_stream(dev).wait_event(done_ev[slot])
             done_ev[slot] = None
         o_ids, o_off = outs[slot]
-        _lib.check(L.sw_encode_device_ex(h, d_buf.data_ptr(), n_bytes, d_off.data_ptr(), n_str, ctypes.byref(ex),
-                                         o_ids.data_ptr(), o_off.data_ptr(), stream, None))
+        encode_into(o_ids, o_off)
         h1 = time.perf_counter()
         host_t["encode"] += h1 - h0
         if not gather:

@@ -154,7 +154,10 @@ def lib():
         except Exception:
             pass
         cdll = ctypes.CDLL(_get_lib_path())
+        ab = bool(os.environ.get("SHREDWORD_HIP_LIB"))  # (an A/B build of an earlier revision may lack new entry points)
         for name, (res, args) in _SIGNATURES.items():
+            if ab and not hasattr(cdll, name):
+                continue
             fn = getattr(cdll, name)
             fn.restype = res
             fn.argtypes = args

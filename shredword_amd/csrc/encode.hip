@@ -144,6 +144,7 @@ struct sw_encoder {
   bool host_presplit = false;         // SW_OPT_HOST_PRESPLIT: sw_encode_batch pre-splits on the host
   uint64_t* d_pbits = nullptr;        // [n_bytes / 64] device pre-split bitmap
   uint32_t* d_edge = nullptr;         // [kEdgeWords][n_tiles + 1] k_edges: the tile boundaries' masks and words
+  unsigned int* d_redo = nullptr;     // k_split_classify's tiles for k_split_redo: count, then the list (int64)
   bool fused_presplit = true;         // SW_OPT_FUSED_PRESPLIT: the device pre-split inside k_split_classify
   unsigned long long* d_pcount = nullptr;
   uint32_t dedupe_fp_mask = (1u << 26) - 1;
@@ -182,7 +183,7 @@ struct DeviceGuard {
 };
 
 void free_workspace(sw_encoder* h) {
-  (void)hipFree(h->d_scratch); (void)hipFree(h->d_res); (void)hipFree(h->d_pbits); (void)hipFree(h->d_edge); (void)hipFree(h->d_pcount); (void)hipFree(h->d_part);
+  (void)hipFree(h->d_scratch); (void)hipFree(h->d_res); (void)hipFree(h->d_pbits); (void)hipFree(h->d_edge); (void)hipFree(h->d_redo); (void)hipFree(h->d_pcount); (void)hipFree(h->d_part);
   (void)hipFree(h->d_tile_slo); (void)hipFree(h->d_tile_sp); (void)hipFree(h->d_stamps);
   (void)hipFree(h->d_tile_slots); (void)hipFree(h->d_tile_nref); (void)hipFree(h->d_rlist); (void)hipFree(h->d_queue); (void)hipFree(h->d_bcnt); (void)hipFree(h->d_boff);
   (void)hipFree(h->d_qtotal);
@@ -194,7 +195,7 @@ void free_workspace(sw_encoder* h) {
   h->d_dres = nullptr; h->d_big = nullptr; h->d_dcnt = nullptr; h->d_lp = nullptr; h->d_lpart = nullptr;
   h->lp = LongArgs{};
   (void)hipFree(h->d_total);
-  h->d_scratch = nullptr; h->d_res = nullptr; h->d_pbits = nullptr; h->d_edge = nullptr; h->d_pcount = nullptr; h->d_part = nullptr;
+  h->d_scratch = nullptr; h->d_res = nullptr; h->d_pbits = nullptr; h->d_edge = nullptr; h->d_redo = nullptr; h->d_pcount = nullptr; h->d_part = nullptr;
   h->d_dtab = nullptr; h->d_tile_base = nullptr; h->d_tile_cnt = nullptr; h->d_total = nullptr;
   h->cap_bytes = -1; h->cap_str = -1;
 }
@@ -283,6 +284,7 @@ int32_t ensure_workspace(sw_encoder* h, int64_t n_bytes) {
   HIP_TRY(hipMalloc(&h->d_total, sizeof(int64_t)));
   HIP_TRY(hipMalloc(&h->d_pbits, sizeof(uint64_t) * ((nb + 63) / 64)));
   HIP_TRY(hipMalloc(&h->d_edge, sizeof(uint32_t) * kEdgeWords * (n_tiles + 1)));
+  HIP_TRY(hipMalloc(&h->d_redo, sizeof(int64_t) * (n_tiles + 1)));
   HIP_TRY(hipMalloc(&h->d_pcount, sizeof(unsigned long long)));
 #ifdef SW_STAMPS
   HIP_TRY(hipMalloc(&h->d_stamps, sizeof(unsigned long long) * 32 * 64));  // 64 copies per counter
@@ -748,12 +750,19 @@ int32_t encode_device(sw_encoder* h, const uint8_t* d_bytes, int64_t n_bytes, co
       hipLaunchKernelGGL(k_edges, dim3((unsigned)((n_tiles + 1 + 255) / 256)), dim3(256), 0, st, pg, n_tiles,
                          (int)h->pattern, h->d_edge);
       const dim3 gc((unsigned)((n_tiles + kWaves - 1) / kWaves));
-      if (sp.n > 0)
+      const RedoList redo{h->d_redo, (int64_t*)(h->d_redo + 2)};
+      HIP_TRY(hipMemsetAsync(h->d_redo, 0, sizeof(unsigned int), st));
+      if (sp.n > 0) {
         hipLaunchKernelGGL(k_split_classify<true>, gc, dim3(kThreads), 0, st, a, pg, (int)h->pattern,
-                           (const uint32_t*)h->d_edge, (uint32_t*)h->d_pbits);
-      else
+                           (const uint32_t*)h->d_edge, (uint32_t*)h->d_pbits, redo);
+        hipLaunchKernelGGL(k_split_redo<true>, dim3(kRedoGrid), dim3(kThreads), 0, st, a, pg, (int)h->pattern,
+                           (const uint32_t*)h->d_edge, (uint32_t*)h->d_pbits, redo);
+      } else {
         hipLaunchKernelGGL(k_split_classify<false>, gc, dim3(kThreads), 0, st, a, pg, (int)h->pattern,
-                           (const uint32_t*)h->d_edge, (uint32_t*)h->d_pbits);
+                           (const uint32_t*)h->d_edge, (uint32_t*)h->d_pbits, redo);
+        hipLaunchKernelGGL(k_split_redo<false>, dim3(kRedoGrid), dim3(kThreads), 0, st, a, pg, (int)h->pattern,
+                           (const uint32_t*)h->d_edge, (uint32_t*)h->d_pbits, redo);
+      }
     } else if (sp.n > 0) {
       hipLaunchKernelGGL(k_classify<true>, dim3((unsigned)((n_tiles + kWaves - 1) / kWaves)), dim3(kThreads), 0, st, a);
     } else {

@@ -65,6 +65,9 @@ __host__ __device__ inline uint32_t slot_did(int32_t v) { return (uint32_t)(-(in
 constexpr uint32_t kRlDense = 0x80000000u;
 constexpr uint32_t kNoDid = 0x7FFFFFFu;    // (27-bit dense result field of a queue entry: none)
 constexpr int kDdExactMax = 7;             // dedupe keys of <= this many bytes are exact (no verification)
+#ifndef SW_PAIR_MAX_N
+#define SW_PAIR_MAX_N 16                   // k_merge_bucket<N>: two chunks per lane up to this N (0: never)
+#endif
 
 // streaming accesses (read or written once per launch) carry the non-temporal hint, so the
 // caches keep the randomly gathered merge results instead
@@ -548,6 +551,107 @@ __device__ __forceinline__ uint32_t lane_merge_lds_wf(const DevTable& t, const u
     }
   }
   return alive;
+}
+
+// lane_merge_lds_wf for TWO chunks per lane, run side by side: every step of both loops issues
+// its lookups before either waits, so a lane keeps twice the lookups in flight (the merge loop
+// without memoisation is a chain of dependent L2-hit lookups per chunk, not work: 66-71% of its
+// wave cycles were issue stalls, profiles/r3n_none.md).  Chunk q's ids at s_id[64 (q N + k) + l].
+template <bool kWide, int N>
+__device__ __forceinline__ void lane_merge_lds_wf2(const DevTable& t, const uint32_t (&u)[2][N / 4], const int (&n)[2],
+                                                   uint32_t* s_id, int lane, uint32_t (&alive)[2]) {
+  static_assert(N <= 32, "alive masks are 32 bits");
+  constexpr uint32_t KINF = 0xFFFFu << 5;
+  uint32_t rk[2][N];
+#pragma unroll
+  for (int q = 0; q < 2; ++q)
+#pragma unroll
+    for (int k = 0; k < N; ++k) s_id[64 * (q * N + k) + lane] = (u[q][k >> 2] >> (8 * (k & 3))) & 0xFFu;
+  // initial ranks: four lookups of each chunk in flight at a time
+#pragma unroll
+  for (int g = 0; g < N; g += 4) {
+#pragma unroll
+    for (int q = 0; q < 2; ++q)
+#pragma unroll
+      for (int k = g; k < g + 4 && k < N; ++k) {
+        const uint32_t b0 = (u[q][k >> 2] >> (8 * (k & 3))) & 0xFFu;
+        const uint32_t b1 = (k + 1 < N) ? (u[q][(k + 1) >> 2] >> (8 * ((k + 1) & 3))) & 0xFFu : 0u;
+        rk[q][k] = lookup<kWide>(t, b0, b1);
+      }
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+#pragma unroll
+      for (int k = g; k < g + 4 && k < N; ++k)
+        rk[q][k] = ((k + 1 < n[q]) ? (min(rk[q][k], 0xFFFFu) << 5) : KINF) | (uint32_t)k;
+      rank_group_done<N>(rk[q], g);
+    }
+  }
+#pragma unroll
+  for (int q = 0; q < 2; ++q) alive[q] = (n[q] >= 32) ? 0xFFFFFFFFu : ((1u << n[q]) - 1u);
+  while (true) {
+    uint32_t need[2];
+    bool any = false;
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {  // one step of each chunk's loop (base.py:10-36), as lane_merge_lds_wf
+      uint32_t best = 0xFFFFFFFFu;
+#pragma unroll
+      for (int k = 0; k < N; ++k) best = min(best, rk[q][k]);
+      const uint32_t nv = best >> 5;
+      need[q] = 0;
+      if (nv >= 0xFFFFu) continue;
+      any = true;
+      const uint32_t bound = (nv + 1) << 5;
+      uint32_t m0 = 0;
+#pragma unroll
+      for (int k = 0; k < N; ++k) m0 |= (rk[q][k] < bound ? 1u : 0u) << k;
+      uint32_t match = m0, cons = next_alive(alive[q], m0);
+      if (cons & m0) {  // an (a, a) pair with adjacent occurrences: left to right
+        match = 0;
+        for (uint32_t av = m0; av;) {
+          const uint32_t s = av & (0u - av);
+          match |= s;
+          av &= ~(s | next_alive(alive[q], s));
+        }
+        cons = next_alive(alive[q], match);
+      }
+      alive[q] &= ~cons;
+      for (uint32_t m = match; m; m &= m - 1) s_id[64 * (q * N + __ffs(m) - 1) + lane] = nv;
+      const uint32_t last = 1u << (31 - __clz(alive[q]));
+      const uint32_t kill = cons | (match & last);
+      need[q] = (match | prev_alive(alive[q], match)) & alive[q] & ~last;
+#pragma unroll
+      for (int k = 0; k < N; ++k) rk[q][k] = ((kill >> k) & 1u) ? (KINF | (uint32_t)k) : rk[q][k];
+    }
+    if (!any) break;
+    while (need[0] | need[1]) {  // two lookups of each chunk in flight per round
+      int j1[2], j2[2];
+      uint32_t k1[2], k2[2];
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        j1[q] = need[q] ? __ffs(need[q]) - 1 : -1;
+        need[q] &= need[q] - 1;
+        j2[q] = need[q] ? __ffs(need[q]) - 1 : j1[q];
+        need[q] &= need[q] - 1;
+        k1[q] = k2[q] = 0;
+        if (j1[q] < 0) continue;
+        const int a1 = j1[q], a2 = j2[q];
+        const int x1 = __ffs(next_alive(alive[q], 1u << a1)) - 1, x2 = __ffs(next_alive(alive[q], 1u << a2)) - 1;
+        const uint32_t ia1 = s_id[64 * (q * N + a1) + lane], ib1 = s_id[64 * (q * N + x1) + lane];
+        const uint32_t ia2 = s_id[64 * (q * N + a2) + lane], ib2 = s_id[64 * (q * N + x2) + lane];
+        k1[q] = (min(lookup<kWide>(t, ia1, ib1), 0xFFFFu) << 5) | (uint32_t)a1;
+        k2[q] = (min(lookup<kWide>(t, ia2, ib2), 0xFFFFu) << 5) | (uint32_t)a2;
+      }
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        if (j1[q] < 0) continue;
+#pragma unroll
+        for (int k = 0; k < N; ++k) {
+          rk[q][k] = (k == j1[q]) ? k1[q] : rk[q][k];
+          rk[q][k] = (k == j2[q]) ? k2[q] : rk[q][k];
+        }
+      }
+    }
+  }
 }
 
 template <bool kWide, bool k16, int N, bool kWF = false>
@@ -1232,6 +1336,31 @@ __device__ __forceinline__ void merge_entry(const EncArgs& a, const uint32_t (&u
   }
 }
 
+// the result of a chunk merged by lane_merge_lds_wf2 (ids in LDS at s_q[64 k + lane], k in alive)
+// to res and, when it is shared, its dense head -- merge_entry's kLds branch
+__device__ __forceinline__ void put_lds_result(const EncArgs& a, uint64_t e, uint32_t alive, const uint32_t* s_q,
+                                               int lane) {
+  const int64_t start = (int64_t)(e >> 33);
+  const uint32_t did = (uint32_t)e & kNoDid;
+  uint32_t* dst = a.res + 2 * start;
+  int m = 0;
+  uint32_t h0 = 0, h1 = 0, h2 = 0, h3 = 0;
+  for (uint32_t al = alive; al; al &= al - 1) {
+    const uint32_t x = s_q[64 * (__ffs(al) - 1) + lane];
+    dst[1 + m] = x;
+    h0 |= m == 0 ? x << 16 : 0u;
+    h1 |= m == 1 ? x : m == 2 ? x << 16 : 0u;
+    h2 |= m == 3 ? x : m == 4 ? x << 16 : 0u;
+    h3 |= m == 5 ? x : m == 6 ? x << 16 : 0u;
+    ++m;
+  }
+  dst[0] = (uint32_t)m;
+  if (did != kNoDid) {
+    a.dres[did] = make_uint4((uint32_t)m | h0, m <= 7 ? h1 : (uint32_t)start, h2, h3);
+    a.dcnt[did] = (uint8_t)m;
+  }
+}
+
 // ---------------------------------------------------------------------------------------
 // k_merge_bucket<N>: queued chunks of buckets [b_lo, b_hi] (length <= N), one per lane;
 // persistent grid-stride over 64-entry batches of the bucket-major queue
@@ -1248,8 +1377,33 @@ __global__ void __launch_bounds__(kThreads) k_merge_bucket(EncArgs a, int b_lo, 
   const uint32_t* words = (const uint32_t*)((uintptr_t)a.bytes - mis);
   const int64_t last_word = (mis + a.n_bytes - 1) >> 2;  // last word holding input bytes
   constexpr bool kLds = kWF && k16 && !kWide;
-  __shared__ uint32_t s_ids[kLds ? kWaves * 64 * N : 1];  // (lane_merge_lds_wf: the waves' ids)
-  uint32_t* s_id = s_ids + (kLds ? (threadIdx.x >> 6) * 64 * N : 0);
+  // two chunks per lane (lane_merge_lds_wf2) for the short buckets of well-formed 16-bit tables
+  constexpr bool kPair = kLds && N <= SW_PAIR_MAX_N;
+  constexpr int kPer = kPair ? 2 : 1;
+  __shared__ uint32_t s_ids[kLds ? kWaves * 64 * N * kPer : 1];  // (lane_merge_lds_wf: the waves' ids)
+  uint32_t* s_id = s_ids + (kLds ? (threadIdx.x >> 6) * 64 * N * kPer : 0);
+  if constexpr (kPair) {  // batches of 128 entries per wave: entries base + lane and base + 64 + lane
+    int64_t i = lo + gw * 128 + lane;
+    uint64_t e0 = i < hi ? a.queue[i] : 0, e1 = i + 64 < hi ? a.queue[i + 64] : 0;
+    for (int64_t base = lo + gw * 128; base < hi; base += n_waves * 128) {
+      uint32_t u[2][N / 4];
+      int n[2];
+      n[0] = i < hi ? (int)((e0 >> 27) & 63u) : 0;
+      n[1] = i + 64 < hi ? (int)((e1 >> 27) & 63u) : 0;
+      chunk_words<N>(words, last_word, (int64_t)(e0 >> 33) + mis, n[0], u[0]);
+      chunk_words<N>(words, last_word, (int64_t)(e1 >> 33) + mis, n[1], u[1]);
+      const int64_t i2 = i + n_waves * 128;
+      const uint64_t f0 = i2 < hi ? a.queue[i2] : 0, f1 = i2 + 64 < hi ? a.queue[i2 + 64] : 0;
+      uint32_t alive[2];
+      lane_merge_lds_wf2<kWide, N>(a.table, u, n, s_id, lane, alive);
+      if (i < hi) put_lds_result(a, e0, alive[0], s_id, lane);
+      if (i + 64 < hi) put_lds_result(a, e1, alive[1], s_id + 64 * N, lane);
+      i = i2;
+      e0 = f0;
+      e1 = f1;
+    }
+    return;
+  }
   // software-pipelined: the next batch's queue entry and chunk bytes load before this batch's
   // merge loop runs (two dependent round trips per batch off the critical path)
   int64_t i = lo + gw * 64 + lane;

@@ -86,6 +86,17 @@ __device__ __forceinline__ void sp_bits32(const SpArgs& sp, int64_t n_tiles, int
   *inner = in;
 }
 
+#ifndef SW_SC_GSRC_NOINLINE
+#define SW_SC_GSRC_NOINLINE 0
+#endif
+#if SW_SC_GSRC_NOINLINE
+#define SW_SC_GSRC_ATTR __noinline__
+#else
+#define SW_SC_GSRC_ATTR __forceinline__
+#endif
+struct GSrc;
+__device__ SW_SC_GSRC_ATTR psb::Masks gsrc_masks(const GSrc& s, int64_t c);
+
 // psb::carries' view of the batch from global memory only (k_edges, and k_split_classify's walks
 // past its tile): every chunk classified from its 40 bytes
 struct GSrc {
@@ -104,12 +115,76 @@ struct GSrc {
   __device__ __forceinline__ uint32_t ss(int64_t c) const { return ss_at(32 * c); }
   __device__ __forceinline__ psb::Masks get(int64_t c) const {
     if (c < 0 || c >= n_chunks) return psb::Masks{};
-    psb::RegBytes by;
-    pb_load40(g, 32 * c, by.w);
-    const uint64_t s = (uint64_t)ss_at(32 * c - 4) | ((uint64_t)(ss_at(32 * c + 28) & 0xFFu) << 32);
-    return psb::classify(by, s, UcdClass{}, cl);
+    return gsrc_masks(*this, c);
   }
 };
+
+// (SW_SC_GSRC_NOINLINE: out of line -- a whole classify per call site is otherwise inlined into
+// every walk of psb::carries, ~100 KB of code for the fused kernel -- at the price of the call's
+// register saves)
+__device__ SW_SC_GSRC_ATTR psb::Masks gsrc_masks(const GSrc& s, int64_t c) {
+  psb::RegBytes by;
+  pb_load40(s.g, 32 * c, by.w);
+  const uint64_t ss = (uint64_t)s.ss_at(32 * c - 4) | ((uint64_t)(s.ss_at(32 * c + 28) & 0xFFu) << 32);
+  return psb::classify(by, ss, UcdClass{}, s.cl);
+}
+
+// string starts (special-token ends included) of [base, base + 160) as five words, from ONE
+// search of str_off (and of the occurrences) -- k_edges' three classifies and its rules window
+// otherwise searched eight times, each a chain of dependent loads
+struct SsWin5 {
+  uint32_t w[5];
+  int64_t base;
+  __device__ __forceinline__ uint32_t at(int64_t q) const {  // bits of [q, q + 32), q in [base, base + 128]
+    const int r = (int)(q - base), i = r >> 5, sh = r & 31;
+    uint32_t lo = w[0], hi = w[1];
+#pragma unroll
+    for (int k = 1; k < 4; ++k) {
+      lo = i == k ? w[k] : lo;
+      hi = i == k ? w[k + 1] : hi;
+    }
+    return sh ? (lo >> sh) | (hi << (32 - sh)) : lo;
+  }
+};
+
+__device__ __forceinline__ void ss_win5(const PbArgs& g, int64_t n_tiles, int64_t base, SsWin5* out) {
+  out->base = base;
+#pragma unroll
+  for (int k = 0; k < 5; ++k) out->w[k] = 0u;
+  const int64_t end = base + 160;
+  auto set = [&](int64_t q) {
+    if (q >= base && q < end) {
+      const int r = (int)(q - base);
+#pragma unroll
+      for (int k = 0; k < 5; ++k) out->w[k] |= (r >> 5) == k ? 1u << (r & 31) : 0u;
+    }
+  };
+  if (base <= g.n_bytes) {
+    int64_t lo = 0, hi = 0;
+    if (base > 0) {
+      const int64_t t = base >> kTileBits;
+      lo = t < n_tiles ? g.tile_slo[t] : g.n_str;
+      hi = t + 1 < n_tiles ? g.tile_slo[t + 1] : g.n_str;
+    }
+    while (lo < hi) {
+      const int64_t m = (lo + hi) >> 1;
+      if (g.str_off[m] < base) lo = m + 1; else hi = m;
+    }
+    for (int64_t i = lo; i <= g.n_str; ++i) {
+      const int64_t o = g.str_off[i];
+      if (o >= end) break;
+      set(o);
+    }
+  }
+  if (g.sp.n > 0) {
+    for (int64_t j = sp_first_end(g.sp, n_tiles, base); j < g.sp.n; ++j) {
+      const int64_t a = g.sp.pos[j];
+      if (a >= end) break;
+      set(a);
+      set(a + g.sp.len[j]);
+    }
+  }
+}
 
 // k_edges: per tile boundary b in [0, n_tiles] (byte 2048 b, chunk c = 64 b): the class masks of
 // chunk c and its final chunk-start word (zeros past the batch).  edge[k * (n_tiles + 1) + b].
@@ -123,12 +198,21 @@ __global__ void __launch_bounds__(256) k_edges(PbArgs g, int64_t n_tiles, int pa
   psb::Masks m1{};
   uint32_t r = 0;
   if (c < n_chunks) {
+    SsWin5 sw;
+    ss_win5(g, n_tiles, 32 * c - 64, &sw);  // (chunks c - 1 .. c + 1 with their 4-byte margins)
     if (pattern == 2) {  // (the chunks are the strings)
-      r = src.ss(c);
+      r = sw.at(32 * c);
     } else {
-      const psb::Masks m0 = src.get(c - 1), m2 = src.get(c + 1);
-      m1 = src.get(c);
-      const uint64_t ssw = (uint64_t)src.ss_at(32 * c - 16) | ((uint64_t)src.ss_at(32 * c + 16) << 32);
+      auto masks = [&](int64_t k) -> psb::Masks {
+        if (k < 0 || k >= n_chunks) return psb::Masks{};
+        psb::RegBytes by;
+        pb_load40(g, 32 * k, by.w);
+        const uint64_t s = (uint64_t)sw.at(32 * k - 4) | ((uint64_t)(sw.at(32 * k + 28) & 0xFFu) << 32);
+        return psb::classify(by, s, UcdClass{}, pattern == 0);
+      };
+      const psb::Masks m0 = masks(c - 1), m2 = masks(c + 1);
+      m1 = masks(c);
+      const uint64_t ssw = (uint64_t)sw.at(32 * c - 16) | ((uint64_t)sw.at(32 * c + 16) << 32);
       uint32_t need = 0;
       r = psb::rules(m0, m1, m2, ssw, pattern == 0, psb::Carry{}, &need);
       if (need) {
@@ -204,11 +288,50 @@ struct FSrc {
   }
 };
 
-// one tile: pre-split, then classify_chunks
-template <bool kSp>
+// psb::carries' view inside k_split_classify: the tile's masks (and the next tile's first chunk,
+// from k_edges) and string starts in LDS, nothing else.  A walk that leaves them sets *edge: the
+// tile is then redone by k_split_redo (FSrc, global memory), so that the common kernel carries no
+// inlined global classify (which made it ~100 KB of code and cost spills)
+struct LSrc {
+  const ScMasks* sm;
+  int64_t c0, t0, n_chunks;
+  bool* edge;
+  __device__ __forceinline__ uint32_t ss_at(int64_t q) const {
+    const int64_t r = q - (t0 - kScSsPre);
+    if (r >= 0 && r + 32 <= (int64_t)kScSsWords * 32) {
+      const int wi = (int)(r >> 5), sh = (int)(r & 31);
+      const uint64_t two = (uint64_t)sm->ss[wi] | ((wi + 1 < kScSsWords ? (uint64_t)sm->ss[wi + 1] : 0ULL) << 32);
+      return (uint32_t)(two >> sh);
+    }
+    *edge = true;
+    return 0u;
+  }
+  __device__ __forceinline__ uint32_t ss(int64_t c) const { return ss_at(32 * c); }
+  __device__ __forceinline__ psb::Masks get(int64_t c) const {
+    if (c < 0 || c >= n_chunks) return psb::Masks{};  // (past the batch: no code points)
+    const int64_t j = c - c0;
+    if (j >= 0 && j <= 64) {
+      const int k = (int)j + 1;
+      return psb::Masks{sm->m[0][k], sm->m[1][k], sm->m[2][k], sm->m[3][k], sm->m[4][k],
+                        sm->m[5][k], sm->m[6][k], sm->m[7][k], sm->m[8][k]};
+    }
+    *edge = true;
+    return psb::Masks{};
+  }
+};
+
+// k_split_classify's tiles whose pre-split needs a walk past the tile (k_split_redo redoes them)
+struct RedoList {
+  unsigned int* count;
+  int64_t* tiles;
+};
+
+// one tile: pre-split, then classify_chunks.  kRedo: the walks may read global memory (FSrc) --
+// k_split_redo; else they stay in LDS (LSrc) and a tile that needs more is listed in `redo`
+template <bool kSp, bool kRedo>
 __device__ __forceinline__ void split_classify_tile(const EncArgs& a, const PbArgs& g, int pattern, const uint32_t* edge,
                                                     uint32_t* bits32, int64_t tile, uint32_t* s_win, ScShared* sh,
-                                                    uint16_t* s_qbuf) {
+                                                    uint16_t* s_qbuf, const RedoList& redo) {
   SW_STAMP_INIT;
   const int lane = threadIdx.x & 63;
   const int64_t t0 = tile * kTile;
@@ -289,6 +412,7 @@ __device__ __forceinline__ void split_classify_tile(const EncArgs& a, const PbAr
   // 3. this lane's chunk: class masks (to LDS, where the rules read them: nothing is held in
   //    registers across the rare walk of psb::carries, which would otherwise cost ~60 VGPRs)
   uint32_t r = 0;
+  bool unresolved = false;  // (a walk left the tile: the tile goes to k_split_redo)
   if (pattern == 2) {  // the chunks are the strings
     if (c < n_chunks) r = src.ss(c);
   } else {
@@ -327,10 +451,25 @@ __device__ __forceinline__ void split_classify_tile(const EncArgs& a, const PbAr
         need = 0;
       }
       if (need) {
-        const psb::Carry cy = psb::carries(src, c, need);
-        asm volatile("" ::: "memory");  // (the masks re-read from LDS, not kept live across the walk)
-        r = psb::rules(col(lane), col(lane + 1), col(lane + 2), ssw, cl, cy, &need);
+        if constexpr (kRedo) {
+          const psb::Carry cy = psb::carries(src, c, need);
+          asm volatile("" ::: "memory");  // (the masks re-read from LDS, not kept live across the walk)
+          r = psb::rules(col(lane), col(lane + 1), col(lane + 2), ssw, cl, cy, &need);
+        } else {
+          bool hit = false;
+          const LSrc ls{&sm, c0, t0, n_chunks, &hit};
+          const psb::Carry cy = psb::carries(ls, c, need);
+          asm volatile("" ::: "memory");
+          if (hit) unresolved = true;
+          else r = psb::rules(col(lane), col(lane + 1), col(lane + 2), ssw, cl, cy, &need);
+        }
       }
+    }
+  }
+  if constexpr (!kRedo) {
+    if (__ballot(unresolved)) {  // (rare: nothing of the tile is written yet; k_split_redo does it all)
+      if (lane == 0) redo.tiles[atomicAdd(redo.count, 1u)] = tile;
+      return;
     }
   }
   if (c < n_chunks) {
@@ -354,15 +493,34 @@ __device__ __forceinline__ void split_classify_tile(const EncArgs& a, const PbAr
 #define SW_SC_WAVES 6
 #endif
 template <bool kSp>
-__global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(SW_SC_WAVES, SW_SC_WAVES))) k_split_classify(EncArgs a, PbArgs g, int pattern,
-                                                                         const uint32_t* edge, uint32_t* bits32) {
+__global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(SW_SC_WAVES, SW_SC_WAVES)))
+k_split_classify(EncArgs a, PbArgs g, int pattern, const uint32_t* edge, uint32_t* bits32, RedoList redo) {
   __shared__ __attribute__((aligned(16))) uint32_t s_win_all[kWaves][kScWinWords];
   __shared__ ScShared s_sh_all[kWaves];
   __shared__ uint16_t s_qb_all[kWaves][kQBuf];
   const int wv = threadIdx.x >> 6;
   const int64_t tile = (int64_t)blockIdx.x * kWaves + wv;
   if (tile < a.n_tiles)
-    split_classify_tile<kSp>(a, g, pattern, edge, bits32, tile, s_win_all[wv], &s_sh_all[wv], s_qb_all[wv]);
+    split_classify_tile<kSp, false>(a, g, pattern, edge, bits32, tile, s_win_all[wv], &s_sh_all[wv], s_qb_all[wv],
+                                    redo);
+}
+
+// the tiles k_split_classify listed (a run crossing the tile: walks over global memory), one wave
+// each, the waves of a fixed grid taking them in turn
+constexpr int kRedoGrid = 256;
+template <bool kSp>
+__global__ void __launch_bounds__(kThreads) k_split_redo(EncArgs a, PbArgs g, int pattern, const uint32_t* edge,
+                                                         uint32_t* bits32, RedoList redo) {
+  __shared__ __attribute__((aligned(16))) uint32_t s_win_all[kWaves][kScWinWords];
+  __shared__ ScShared s_sh_all[kWaves];
+  __shared__ uint16_t s_qb_all[kWaves][kQBuf];
+  const int wv = threadIdx.x >> 6;
+  const int64_t n = (int64_t)*redo.count;
+  for (int64_t i = (int64_t)blockIdx.x * kWaves + wv; i < n; i += (int64_t)gridDim.x * kWaves) {
+    split_classify_tile<kSp, true>(a, g, pattern, edge, bits32, redo.tiles[i], s_win_all[wv], &s_sh_all[wv],
+                                   s_qb_all[wv], redo);
+    wave_sync_mem();  // (the next tile reuses the wave's LDS)
+  }
 }
 
 }  // namespace sw

@@ -113,3 +113,48 @@ def test_encode_batch_device_vs_host_presplit():
             L.sw_encoder_set_option(h, _lib.SW_OPT_HOST_PRESPLIT, 0)
         np.testing.assert_array_equal(dev_ids[0], host_ids[0])
         np.testing.assert_array_equal(dev_ids[1], host_ids[1])
+
+
+@pytest.mark.parametrize("pattern", PATS)
+def test_fused_presplit_runs_across_tiles(pattern):
+    """The pre-split fused into the classification (k_split_classify, the default of a device encode
+    without a bitmap): runs that cross its 2 KiB tiles -- digit runs of thousands of digits (the
+    phase of every third digit), whitespace runs with a \\n far inside or at their end, \\r\\n runs
+    after punctuation, a whitespace run ending the batch -- walk past the tile and take
+    k_split_redo; the ids must equal those of the host bitmap's encode and of the oracle."""
+    import oracle
+    rng = random.Random(17 + pattern)
+    parts = []
+    for k in range(300):
+        kind = rng.randrange(6)
+        if kind == 0:
+            parts.append("".join(rng.choice("0123456789") for _ in range(rng.randint(1500, 6000))))
+        elif kind == 1:
+            ws = [" "] * rng.randint(100, 4000)
+            if rng.random() < 0.7:
+                ws[rng.randrange(len(ws))] = "\n"
+            parts.append("x" + "".join(ws) + rng.choice(["y", "", "\n", "7"]))
+        elif kind == 2:
+            parts.append("!!" + "\r\n" * rng.randint(50, 2000) + " z")
+        elif kind == 3:
+            parts.append("word " * rng.randint(1, 600) + "٣" * rng.randint(1, 3000))
+        elif kind == 4:
+            parts.append("\t" * rng.randint(1, 3000) + "'s" + "　" * rng.randint(0, 900))
+        else:
+            parts.append("hello world 123 . " * rng.randint(1, 200))
+    datas = [p.encode("utf-8") for p in parts] + [b" " * 5000, b"9" * 4097, b"\n" * 3000]
+    off = np.zeros(len(datas) + 1, dtype=np.int64)
+    np.cumsum([len(d) for d in datas], out=off[1:])
+    buf = np.frombuffer(b"".join(datas), dtype=np.uint8).copy()
+    t = sa.Tokenizer(device=0)
+    t.merges = {(48, 49): 256, (32, 32): 257, (257, 257): 258, (10, 10): 259, (119, 111): 260}
+    t.pattern = pattern
+    fused = t.encode_packed(buf, off)                                  # device pre-split, fused
+    host_bits, _ = corpus.presplit(buf, off, pattern)
+    hosted = t.encode_packed(buf, off, host_bits)                      # host bitmap, k_classify
+    np.testing.assert_array_equal(fused[1], hosted[1])
+    np.testing.assert_array_equal(fused[0], hosted[0])
+    exp = oracle.OracleModel(t.merges).encode_batch(buf, off, pattern, n_threads=8)
+    np.testing.assert_array_equal(fused[0], exp[0])
+    np.testing.assert_array_equal(fused[1], exp[1])
+    t.close()

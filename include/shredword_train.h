@@ -66,8 +66,9 @@ int64_t sw_trainer_token_freq(const sw_trainer* t, uint64_t* freq, int64_t cap);
 int32_t sw_trainer_save(const sw_trainer* t, const char* model_path, const char* vocab_path);
 
 /* Timing of the last load + train (ms): [0] corpus load (host), [1] upload, [2] pair histogram
- * (device) + heap seed, [3] merge rewrites on the device (sum), [4] change application on the
- * host (sum), [5] merges, [6] distinct words, [7] symbols. */
+ * (device) + heap seed, [3] host time spent waiting for the merge rewrites on the device (sum),
+ * [4] host work on the critical path: pops, launches, change application not hidden behind a
+ * merge launched ahead (sum), [5] merges, [6] distinct words, [7] symbols. */
 int32_t sw_trainer_stats(const sw_trainer* t, double* out8);
 
 #ifdef __cplusplus

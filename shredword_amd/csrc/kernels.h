@@ -459,6 +459,21 @@ __device__ __forceinline__ void rank_group_done(uint32_t (&rk)[N], int g) {
   }
 }
 
+// min / rank-match mask over a lane's N keys as balanced trees: a left-to-right chain is N
+// dependent instructions per step, and the loop's steps are short enough that those RAW stalls
+// were most of its issue time (k_lp_encode / k_merge_bucket: 52-71% of wave cycles in
+// SQ_WAIT_INST_ANY)
+template <int N, int L = 0, int R = N>
+__device__ __forceinline__ uint32_t tree_min(const uint32_t (&x)[N]) {
+  if constexpr (R - L == 1) return x[L];
+  else return min(tree_min<N, L, (L + R) / 2>(x), tree_min<N, (L + R) / 2, R>(x));
+}
+template <int N, int L = 0, int R = N>
+__device__ __forceinline__ uint32_t tree_below(const uint32_t (&x)[N], uint32_t bound) {  // bit k: x[k] < bound
+  if constexpr (R - L == 1) return (x[L] < bound ? 1u : 0u) << L;
+  else return tree_below<N, L, (L + R) / 2>(x, bound) | tree_below<N, (L + R) / 2, R>(x, bound);
+}
+
 // Alive-set arithmetic on a lane's position mask A (bit k: position k holds a token):
 // next_alive(A, S): for each position of S (a subset of A) the next alive position after it
 // (none past bit 31): the bits just above S, carried through the gaps of A by one addition.
@@ -506,15 +521,11 @@ __device__ __forceinline__ uint32_t lane_merge_lds_wf(const DevTable& t, const u
   }
   uint32_t alive = (n >= 32) ? 0xFFFFFFFFu : ((1u << n) - 1u);
   while (true) {
-    uint32_t best = 0xFFFFFFFFu;
-#pragma unroll
-    for (int k = 0; k < N; ++k) best = min(best, rk[k]);
+    const uint32_t best = tree_min<N>(rk);
     const uint32_t nv = best >> 5;
     if (nv >= 0xFFFFu) break;
     const uint32_t bound = (nv + 1) << 5;  // (every key is >= best: rank nv <=> key < bound)
-    uint32_t m0 = 0;
-#pragma unroll
-    for (int k = 0; k < N; ++k) m0 |= (rk[k] < bound ? 1u : 0u) << k;
+    const uint32_t m0 = tree_below<N>(rk, bound);
     uint32_t match = m0, cons = next_alive(alive, m0);
     if (cons & m0) {  // an (a, a) pair with adjacent occurrences: left to right
       match = 0;
@@ -593,17 +604,13 @@ __device__ __forceinline__ void lane_merge_lds_wf2(const DevTable& t, const uint
     bool any = false;
 #pragma unroll
     for (int q = 0; q < 2; ++q) {  // one step of each chunk's loop (base.py:10-36), as lane_merge_lds_wf
-      uint32_t best = 0xFFFFFFFFu;
-#pragma unroll
-      for (int k = 0; k < N; ++k) best = min(best, rk[q][k]);
+      const uint32_t best = tree_min<N>(rk[q]);
       const uint32_t nv = best >> 5;
       need[q] = 0;
       if (nv >= 0xFFFFu) continue;
       any = true;
       const uint32_t bound = (nv + 1) << 5;
-      uint32_t m0 = 0;
-#pragma unroll
-      for (int k = 0; k < N; ++k) m0 |= (rk[q][k] < bound ? 1u : 0u) << k;
+      const uint32_t m0 = tree_below<N>(rk[q], bound);
       uint32_t match = m0, cons = next_alive(alive[q], m0);
       if (cons & m0) {  // an (a, a) pair with adjacent occurrences: left to right
         match = 0;

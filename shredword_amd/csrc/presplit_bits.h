@@ -147,8 +147,8 @@ SW_HD inline Masks classify(const Bytes& by, uint64_t ss, const Cls& cls, bool c
       else if (c == kN) N |= bit;
       else if (c == kS) H |= bit;
     };
-#ifndef SW_PSB_LEADS2
-#define SW_PSB_LEADS2 1
+#ifndef SW_PSB_LEADS2  // (1: two leads per step; inside k_split_classify 1-2% slower, r4b A/B)
+#define SW_PSB_LEADS2 0
 #endif
 #if !SW_PSB_LEADS2
     for (uint64_t m = hi40 & ~ct40 & 0xFFFFFFFFFULL; m; m &= m - 1) {

@@ -24,7 +24,9 @@
 #include <chrono>
 #include <cstdint>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
+#include <new>
 #include <string>
 #include <string_view>
 #include <thread>
@@ -222,14 +224,26 @@ __device__ __forceinline__ void merge_cand(int32_t* ids, const int64_t* woff, in
   uint32_t w = 0;
   if (i < n0 + n1 + n2) {
     w = i < n0 ? c0[i] : i < n0 + n1 ? c1[i - n0] : c2[i - n0 - n1];
-    // the word's filter, start, length and count loaded beside the stamp claim (one round trip,
-    // not three: only the claimant uses them, and nothing else rewrites the word in this step)
+    // the word's filter, start, length and count in one round trip; a word whose filter lacks A
+    // or B is dropped before any atomic.  The others load their first kRegIds symbols beside the
+    // stamp claim (one more round trip: nothing else rewrites the word in this step, so reading
+    // before the claim is safe) and a word without the pair among them is read only once.
     const uint64_t bl = bloom[w];
     const int64_t base = woff[w];
     const int L = len[w];
     const uint64_t wcw = wcnt[w];
-    if (atomicExch(&stamp[w], seq) != seq)
-      done = merge_word_pre(ids, len, bloom, w, bl, base, L, wcw, A, B, X, tab, mask, used, n_used);
+    const uint64_t need = sym_bit(A) | sym_bit(B);
+    if ((bl & need) == need) {
+      constexpr int kRegIds = 16;
+      int32_t v[kRegIds];
+#pragma unroll
+      for (int k = 0; k < kRegIds; ++k) v[k] = k < L ? ids[base + k] : 0;
+      bool has = L > kRegIds;  // (longer words: the scan in merge_word_pre decides)
+#pragma unroll
+      for (int k = 0; k + 1 < kRegIds; ++k) has |= k + 1 < L && v[k] == A && v[k + 1] == B;
+      if (atomicExch(&stamp[w], seq) != seq && has)
+        done = merge_word_pre(ids, len, bloom, w, bl, base, L, wcw, A, B, X, tab, mask, used, n_used);
+    }
   }
   const uint64_t m = __ballot(done);  // (one pool append per wave)
   if (!m) return;
@@ -500,35 +514,84 @@ struct HeapEntry {
   uint32_t version;
 };
 
-// heap_push / heap_pop (heap.cpp:53-114): ties fall where these sift rules put them
+// heap_push / heap_pop (heap.cpp:53-114): ties fall where these sift rules put them.  The same
+// binary heap (parent >= child on push, the larger child taken only if strictly larger on pop),
+// laid out for the cache: 16-byte nodes {a, b, freq << 24 | version}, 1-based in a 64-byte
+// aligned array, so a node's two children share a half line and its four grandchildren one line,
+// prefetched two levels ahead of the sift-down (a pop walks ~20 levels of a 1 M-entry heap of
+// mostly stale entries; the stale pops outnumber the merges ~16:1).  freq < 2^40 and
+// version < 2^24 (checked: overflow() -> SW_ERR_CAP).
 struct MaxHeap {
-  std::vector<HeapEntry> d;
+  struct Node {
+    int32_t a, b;
+    uint64_t fv;
+  };
+  static_assert(sizeof(Node) == 16, "16-byte heap nodes");
+  static constexpr int kVerBits = 24;
+  Node* d = nullptr;
+  size_t n = 0, cap = 0;
+  bool over = false;
+  MaxHeap() = default;
+  MaxHeap(const MaxHeap&) = delete;
+  MaxHeap& operator=(const MaxHeap&) = delete;
+  ~MaxHeap() { std::free(d); }
+  static uint64_t freq_of(uint64_t fv) { return fv >> kVerBits; }
+  bool empty() const { return n == 0; }
+  size_t size() const { return n; }
+  bool overflow() const { return over; }
+  void reserve(size_t want) {
+    if (want + 1 <= cap) return;
+    size_t c = 1024;
+    while (c < want + 1) c <<= 1;
+    Node* nd = static_cast<Node*>(std::aligned_alloc(64, c * sizeof(Node)));
+    if (!nd) throw std::bad_alloc();
+    if (d) std::memcpy(nd, d, (n + 1) * sizeof(Node));
+    std::free(d);
+    d = nd;
+    cap = c;
+  }
+  HeapEntry top() const { return decode(d[1]); }
+  static HeapEntry decode(const Node& x) {
+    return HeapEntry{x.a, x.b, freq_of(x.fv), (uint32_t)(x.fv & ((1u << kVerBits) - 1u))};
+  }
   void push(int32_t a, int32_t b, uint64_t freq, uint32_t version) {
-    d.push_back(HeapEntry{a, b, freq, version});
-    size_t i = d.size() - 1;
-    while (i > 0) {
-      const size_t p = (i - 1) >> 1;
-      if (d[p].freq >= d[i].freq) break;
-      std::swap(d[p], d[i]);
+    if ((freq >> (64 - kVerBits)) != 0 || (version >> kVerBits) != 0) over = true;
+    if (n + 2 > cap) reserve(2 * n + 2);
+    const Node x{a, b, (freq << kVerBits) | (version & ((1u << kVerBits) - 1u))};
+    const uint64_t f = freq_of(x.fv);
+    size_t i = ++n;
+    while (i > 1) {
+      const size_t p = i >> 1;
+      if (freq_of(d[p].fv) >= f) break;
+      d[i] = d[p];
       i = p;
     }
+    d[i] = x;
   }
   HeapEntry pop() {
-    const HeapEntry top = d[0];
-    d[0] = d.back();
-    d.pop_back();
-    size_t i = 0;
-    const size_t n = d.size();
-    for (;;) {
-      const size_t l = 2 * i + 1, r = l + 1;
-      size_t best = i;
-      if (l < n && d[l].freq > d[best].freq) best = l;
-      if (r < n && d[r].freq > d[best].freq) best = r;
-      if (best == i) break;
-      std::swap(d[i], d[best]);
-      i = best;
+    const Node top = d[1];
+    const Node x = d[n];
+    --n;
+    if (n > 0) {
+      const uint64_t f = freq_of(x.fv);
+      size_t i = 1;
+      for (;;) {
+        if (8 * i + 4 < cap) {
+          __builtin_prefetch(&d[8 * i]);
+          __builtin_prefetch(&d[8 * i + 4]);
+        }
+        const size_t l = 2 * i, r = l + 1;
+        size_t best = i;
+        uint64_t bf = f;
+        if (l <= n && freq_of(d[l].fv) > bf) { best = l; bf = freq_of(d[l].fv); }
+        if (r <= n && freq_of(d[r].fv) > bf) best = r;
+        if (best == i) break;
+        d[i] = d[best];
+        i = best;
+      }
+      d[i] = x;
     }
-    return top;
+    return decode(top);
   }
 };
 
@@ -1181,7 +1244,7 @@ int64_t train(sw_trainer* t) {
   std::sort(seeds.begin(), seeds.end(),
             [](const Seed& x, const Seed& y) { return x.bucket != y.bucket ? x.bucket < y.bucket : x.first < y.first; });
   MaxHeap heap;
-  heap.d.reserve(seeds.size() * 2 + 16);
+  heap.reserve(seeds.size() * 2 + 16);
   for (const Seed& s : seeds) heap.push(s.a, s.b, s.freq, 0);
   // per-pair word lists (k_merge_cand): the loaded corpus's adjacent pairs sorted by pair, their
   // distinct keys and run lengths on the host; SW_TRAIN_FULL_SCAN=1 keeps every merge on the
@@ -1244,22 +1307,22 @@ int64_t train(sw_trainer* t) {
   // merges (bpe_train / bpe_merge_batch: batch boundaries do not change the result)
   const int64_t target = (int64_t)t->cfg.target_vocab_size - 256;
   t->merges.clear();
-  double dev_ms = 0, host_ms = 0;
-  struct Change { uint32_t bucket; uint64_t first; uint64_t h; int64_t delta; };
-  std::vector<Change> ch, ch2;
+  double dev_ms = 0, host_ms = 0, ahead_ms = 0;
+  struct Push { uint32_t bucket; uint64_t first; int32_t a, b; uint64_t freq; uint32_t version; };
+  std::vector<Push> pl, pl2;
   std::vector<uint32_t> bstart(1025), bfill(1024);
   int64_t nm = 0;
   unsigned long long seq = 0;
-  uint64_t n_pops = 0, n_changes = 0, n_pushes = 0;  // (SW_TRAIN_DEBUG)
+  uint64_t n_pops = 0, n_changes = 0, n_pushes = 0, n_ahead = 0;  // (SW_TRAIN_DEBUG)
   double launch_ms = 0;
-  while (nm < target && !heap.d.empty()) {
-    const HeapEntry top = heap.pop();
-    ++n_pops;
-    PairInfo& pi = info[pkey(top.a, top.b)];
-    if (top.version != pi.version) continue;  // stale
-    if (pi.freq < min_freq) continue;
-    const int32_t A = top.a, B = top.b, X = (int32_t)(256 + nm);
-    const auto t0 = clk::now();
+  const char* ov_env = std::getenv("SW_TRAIN_NO_AHEAD");
+  const bool ahead_ok = !(ov_env && ov_env[0] == '1');
+  const char* fb_env = std::getenv("SW_TRAIN_FUSE_BLOCKS");  // (A/B: the one-launch threshold)
+  const unsigned fuse_blocks = fb_env ? (unsigned)std::max(1, std::atoi(fb_env)) : kFuseBlocks;
+  // one merge's rewrite on the device (X - 256 merges done before it)
+  auto launch = [&](int32_t A, int32_t B, int32_t X) -> int32_t {
+    const auto tl = clk::now();
+    const int64_t before = (int64_t)X - 256;
     ++seq;
     if (lists) {  // the candidate words: the initial list of (A, B), the words A's and B's merges rewrote
       const uint64_t key = pkey(A, B);
@@ -1270,14 +1333,17 @@ int64_t train(sw_trainer* t) {
         o0 = uoff[k];
         n0 = uoff[k + 1] - uoff[k];
       }
-      if (A >= 256 && A - 256 < nm) { o1 = (int64_t)touched[(size_t)(A - 256)].first; n1 = (int64_t)touched[(size_t)(A - 256)].second; }
-      if (B >= 256 && B - 256 < nm && B != A) {
+      if (A >= 256 && A - 256 < before) {
+        o1 = (int64_t)touched[(size_t)(A - 256)].first;
+        n1 = (int64_t)touched[(size_t)(A - 256)].second;
+      }
+      if (B >= 256 && B - 256 < before && B != A) {
         o2 = (int64_t)touched[(size_t)(B - 256)].first;
         n2 = (int64_t)touched[(size_t)(B - 256)].second;
       }
       const int64_t nc = n0 + n1 + n2;
       const unsigned g = (unsigned)std::max<int64_t>((nc + kBlock - 1) / kBlock, 1);
-      if (g <= kFuseBlocks) {  // (one launch)
+      if (g <= fuse_blocks) {  // (one launch)
         hipLaunchKernelGGL(k_merge_cand_fused, dim3(g), dim3(kBlock), 0, t->st, t->d_ids, t->d_woff, t->d_len,
                            t->d_wcnt, t->d_bloom, t->d_pwords + o0, n0, t->d_pool + o1, n1, t->d_pool + o2, n2,
                            t->d_stamp, (uint32_t)seq, A, B, X, t->d_tab, t->tab_mask, t->d_used, t->d_step_used,
@@ -1300,56 +1366,67 @@ int64_t train(sw_trainer* t) {
                          (const unsigned int*)t->d_step_used);  // (full scan: no pool; these two fields unused)
     }
     SW_HIP_TRY(hipGetLastError());
-    {
-      const auto t_issued = clk::now();
-      launch_ms += std::chrono::duration<double, std::milli>(t_issued - t0).count();
-      if (int32_t rc = wait_step(t, seq, &rec)) return rc;
+    launch_ms += ms_since(tl);
+    return SW_OK;
+  };
+  // The reference loop (bpe.cpp:486-535) pops the heap top, merges it, pushes the changed pairs'
+  // new entries in FreqChangeMap order (hash % 1024 ascending, newest first within a bucket), and
+  // pops again.  The next pop is known before those pushes whenever it is provably the heap root
+  // after them: a push reaches the root iff its frequency is above the root's (the sift-up
+  // stops at a parent >= it), so the root after the pushes is the first pushed entry with the
+  // largest pushed frequency if that beats the current root, else the current root -- taken
+  // only if it is live (its version current, its frequency >= min).  Then the next merge is
+  // launched first and the pushes (and that pop, checked) run on the host while the device
+  // rewrites; every heap operation still happens in the reference's order.
+  bool ahead = false;  // the next merge was launched before the pushes (cur = its entry)
+  HeapEntry cur{};
+  while (true) {
+    if (!ahead) {
+      if (nm >= target || heap.empty()) break;
+      const auto tp = clk::now();
+      const HeapEntry top = heap.pop();
+      ++n_pops;
+      const PairInfo& pi = info[pkey(top.a, top.b)];
+      if (top.version != pi.version || pi.freq < min_freq) {  // stale / below the threshold
+        host_ms += ms_since(tp);
+        continue;
+      }
+      cur = top;
+      if (int32_t rc = launch(cur.a, cur.b, (int32_t)(256 + nm))) return rc;
+      host_ms += ms_since(tp);
     }
+    ahead = false;
+    const int32_t A = cur.a, B = cur.b, X = (int32_t)(256 + nm);
+    {
+      const auto tw = clk::now();
+      if (int32_t rc = wait_step(t, seq, &rec)) return rc;
+      dev_ms += ms_since(tw);
+    }
+    const auto t1 = clk::now();
     if (lists) {
       const uint64_t pn = ((volatile unsigned long long*)t->h_cnt)[2];
       const uint64_t before = touched.empty() ? 0 : touched.back().first + touched.back().second;
       if (((volatile unsigned long long*)t->h_cnt)[3]) lists = false;  // (cannot happen: <= ns rewrites)
       touched.emplace_back(before, pn - before);
     }
-    const auto t1 = clk::now();
-    dev_ms += std::chrono::duration<double, std::milli>(t1 - t0).count();
-    // FreqChangeMap order: hash % 1024 ascending, newest first within a bucket
-    ch.clear();
+    // the changes' new frequencies (each pair once per merge: the device table is keyed by it)
+    for (const Slot& s : rec) info.prefetch(s.key);
+    n_changes += rec.size();
+    pl.clear();
     for (const Slot& s : rec) {
-      ch.push_back(Change{(uint32_t)(s.key % 1024u), s.first, s.key, (int64_t)s.val});
-      info.prefetch(pkey((int32_t)(s.key >> 32), (int32_t)(s.key & 0xFFFFFFFFu)));
-    }
-    n_changes += ch.size();
-    if (ch.size() <= 256) {
-      std::sort(ch.begin(), ch.end(),
-                [](const Change& x, const Change& y) { return x.bucket != y.bucket ? x.bucket < y.bucket : x.first > y.first; });
-    } else {  // (many changes: a counting sort by bucket, then each bucket's few by first call)
-      std::fill(bstart.begin(), bstart.end(), 0u);
-      for (const Change& c : ch) bstart[c.bucket + 1]++;
-      for (int q = 0; q < 1024; ++q) bstart[q + 1] += bstart[q];
-      ch2.resize(ch.size());
-      std::copy(bstart.begin(), bstart.begin() + 1024, bfill.begin());
-      for (const Change& c : ch) ch2[bfill[c.bucket]++] = c;
-      for (int q = 0; q < 1024; ++q)
-        if (bstart[q + 1] - bstart[q] > 1)
-          std::sort(ch2.begin() + bstart[q], ch2.begin() + bstart[q + 1],
-                    [](const Change& x, const Change& y) { return x.first > y.first; });
-      ch.swap(ch2);
-    }
-    for (const Change& c : ch) {
-      const int32_t pa = (int32_t)(c.h >> 32), pb = (int32_t)(c.h & 0xFFFFFFFFu);
+      const int32_t pa = (int32_t)(s.key >> 32), pb = (int32_t)(s.key & 0xFFFFFFFFu);
       if (pa == A && pb == B) continue;
-      PairInfo& q = info[pkey(pa, pb)];
-      if (c.delta < 0) {
-        const uint64_t ad = (uint64_t)(-c.delta);
+      PairInfo& q = info[s.key];
+      const int64_t delta = (int64_t)s.val;
+      if (delta < 0) {
+        const uint64_t ad = (uint64_t)(-delta);
         q.freq = q.freq >= ad ? q.freq - ad : 0;
       } else {
-        q.freq += (uint64_t)c.delta;
+        q.freq += (uint64_t)delta;
       }
       if (q.freq >= min_freq) {
         q.version++;
-        heap.push(pa, pb, q.freq, q.version);
-        ++n_pushes;
+        pl.push_back(Push{(uint32_t)(s.key % 1024u), s.first, pa, pb, q.freq, q.version});
       }
     }
     PairInfo& done = info[pkey(A, B)];
@@ -1359,12 +1436,67 @@ int64_t train(sw_trainer* t) {
     t->merges.push_back(B);
     t->merges.push_back(X);
     ++nm;
-    host_ms += ms_since(t1);
+    // the next pop, if it is provable now
+    if (ahead_ok && nm < target && (!pl.empty() || !heap.empty())) {
+      const Push* best = nullptr;
+      for (const Push& p : pl)
+        if (!best || p.freq > best->freq ||
+            (p.freq == best->freq && (p.bucket < best->bucket || (p.bucket == best->bucket && p.first > best->first))))
+          best = &p;
+      if (best && (heap.empty() || best->freq > heap.top().freq)) {
+        cur = HeapEntry{best->a, best->b, best->freq, best->version};
+        ahead = true;
+      } else if (!heap.empty()) {
+        const HeapEntry r = heap.top();
+        const PairInfo& ri = info[pkey(r.a, r.b)];
+        if (r.version == ri.version && ri.freq >= min_freq) {
+          cur = r;
+          ahead = true;
+        }
+      }
+      if (ahead) {
+        if (int32_t rc = launch(cur.a, cur.b, (int32_t)(256 + nm))) return rc;
+        ++n_ahead;
+      }
+    }
+    const auto t2 = clk::now();
+    // the pushes in FreqChangeMap order
+    if (pl.size() <= 256) {
+      std::sort(pl.begin(), pl.end(),
+                [](const Push& x, const Push& y) { return x.bucket != y.bucket ? x.bucket < y.bucket : x.first > y.first; });
+    } else {  // (many changes: a counting sort by bucket, then each bucket's few by first call)
+      std::fill(bstart.begin(), bstart.end(), 0u);
+      for (const Push& c : pl) bstart[c.bucket + 1]++;
+      for (int q = 0; q < 1024; ++q) bstart[q + 1] += bstart[q];
+      pl2.resize(pl.size());
+      std::copy(bstart.begin(), bstart.begin() + 1024, bfill.begin());
+      for (const Push& c : pl) pl2[bfill[c.bucket]++] = c;
+      for (int q = 0; q < 1024; ++q)
+        if (bstart[q + 1] - bstart[q] > 1)
+          std::sort(pl2.begin() + bstart[q], pl2.begin() + bstart[q + 1],
+                    [](const Push& x, const Push& y) { return x.first > y.first; });
+      pl.swap(pl2);
+    }
+    for (const Push& p : pl) heap.push(p.a, p.b, p.freq, p.version);
+    n_pushes += pl.size();
+    if (ahead) {  // the pop the reference makes next: the entry already launched
+      const HeapEntry top = heap.pop();
+      ++n_pops;
+      if (top.a != cur.a || top.b != cur.b || top.version != cur.version)
+        return sw::set_error(SW_ERR_HIP, "sw_trainer_train: internal error: the merge launched ahead is not the heap's next pop");
+      ahead_ms += ms_since(t2);
+      host_ms += std::chrono::duration<double, std::milli>(t2 - t1).count();
+    } else {
+      host_ms += ms_since(t1);
+    }
   }
+  if (heap.overflow())
+    return sw::set_error(SW_ERR_CAP, "sw_trainer_train: a pair frequency >= 2^40 or more than 2^24 merges");
   if (const char* dbg = std::getenv("SW_TRAIN_DEBUG"); dbg && dbg[0] == '1')
-    std::fprintf(stderr, "sw_trainer: %lld merges, %llu heap pops, %llu change records, %llu heap pushes, heap %zu, "
-                 "launch calls %.1f ms\n", (long long)nm, (unsigned long long)n_pops, (unsigned long long)n_changes,
-                 (unsigned long long)n_pushes, heap.d.size(), launch_ms);
+    std::fprintf(stderr, "sw_trainer: %lld merges (%llu launched ahead), %llu heap pops, %llu change records, "
+                 "%llu heap pushes, heap %zu, launch calls %.1f ms, host work behind the device %.1f ms\n",
+                 (long long)nm, (unsigned long long)n_ahead, (unsigned long long)n_pops, (unsigned long long)n_changes,
+                 (unsigned long long)n_pushes, heap.size(), launch_ms, ahead_ms);
   t->stats[3] = dev_ms;
   t->stats[4] = host_ms;
   t->stats[5] = (double)nm;

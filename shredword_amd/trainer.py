@@ -68,8 +68,9 @@ class BPETrainer:
 
     @property
     def stats(self):
-        """ms: load, upload, histogram + heap seed, device rewrites, host change application;
-        then merges, distinct words, symbols."""
+        """ms: load, upload, histogram + heap seed, waiting on the device rewrites, host work on
+        the critical path (pops, launches, change application not hidden behind a merge launched
+        ahead); then merges, distinct words, symbols."""
         out = (ctypes.c_double * 8)()
         _lib.check(_lib.lib().sw_trainer_stats(self.trainer, out))
         keys = ("ms_load", "ms_upload", "ms_histogram", "ms_rewrites", "ms_host_apply", "merges", "words", "symbols")

@@ -10,6 +10,7 @@ Times cover corpus load + training (+ the reference's file read).
 usage: python tools/bench_train.py [--workloads toy500,mixed32m] [--no-cpu] [--reference-on toy500]
 """
 import argparse
+import hashlib
 import json
 import os
 import subprocess
@@ -95,7 +96,9 @@ def main():
         line = {"workload": name, "corpus_bytes": len(text), "config": list(cfg), "words": int(st["words"]),
                 "symbols": int(st["symbols"]), "merges": n, "gpu_s": round(gpu_s, 4),
                 "gpu_breakdown_ms": {k: round(v, 2) for k, v in st.items() if k.startswith("ms_")},
-                "ms_per_merge_device": round(st["ms_rewrites"] / max(n, 1), 4)}
+                "ms_per_merge_device": round(st["ms_rewrites"] / max(n, 1), 4),
+                "merges_sha1": hashlib.sha1(np.ascontiguousarray(rows, dtype=np.int64).tobytes()).hexdigest(),
+                "launch_ahead": os.environ.get("SW_TRAIN_NO_AHEAD", "0") != "1"}
         if not args.no_cpu and (name != "mixed128m" or args.cpu_big):
             import oracle
             c0 = time.perf_counter()

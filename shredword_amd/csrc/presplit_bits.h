@@ -140,12 +140,13 @@ SW_HD inline Masks classify(const Bytes& by, uint64_t ss, const Cls& cls, bool c
       for (int q = 1; q < n; ++q) v = (v << 6) | ((b4 >> (8 * q)) & 0x3Fu);
       return v;
     };
+    // (selects, not an if-chain: the compiler turned the chain into a scratch array of {L, N, H}
+    // indexed by the class -- a scratch load + store, i.e. a memory round trip, per lead)
     auto apply = [&](int k, uint32_t v, int c) {
-      if (v == kInvalidCp) return;
-      const uint32_t bit = 1u << (k - 4);
-      if (c == kL) L |= bit;
-      else if (c == kN) N |= bit;
-      else if (c == kS) H |= bit;
+      const uint32_t bit = v == kInvalidCp ? 0u : 1u << (k - 4);
+      L |= c == kL ? bit : 0u;
+      N |= c == kN ? bit : 0u;
+      H |= c == kS ? bit : 0u;
     };
 #ifndef SW_PSB_LEADS2  // (1: two leads per step; inside k_split_classify 1-2% slower, r4b A/B)
 #define SW_PSB_LEADS2 0

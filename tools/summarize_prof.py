@@ -41,7 +41,8 @@ def main():
     shutil.copy(stats_csv, os.path.join(out, tag + "_kernel_stats.csv"))
     rows = list(csv.DictReader(open(stats_csv)))
     calls = {r["Name"].split("(")[0].replace("void ", ""): int(r["Calls"]) for r in rows}
-    launches = max(1, calls.get("sw::k_classify", 1))
+    # one classification dispatch per launch: k_classify (host bitmap) or k_split_classify (fused)
+    launches = max([1] + [v for k, v in calls.items() if k.split("<")[0] in ("sw::k_classify", "sw::k_split_classify")])
 
     def per_launch(name):  # dispatches of a kernel per encode launch (bench.py's one extra
         # k_presplit + k_popcount outside the timed steps, for the chunk count, is not one)

@@ -35,6 +35,12 @@ namespace sw {
 constexpr int kTileBits = 11;
 constexpr int kTile = 1 << kTileBits;        // input bytes per classify workgroup
 constexpr int kThreads = 256;                // 4 waves
+constexpr int kWaves = kThreads / 64;
+// this thread's wave in its workgroup.  (As a scalar, __builtin_amdgcn_readfirstlane, the compiler
+// keeps the tile indices in SGPRs: k_split_classify 80 VGPRs + 40 B of scratch -> 75 VGPRs, no
+// scratch, but it ran 180x slower for a reason not found (r4i-r4k A/B: not kernarg placement, not
+// a missing wait), and k_compact got no faster: not used)
+__device__ __forceinline__ int wave_in_block() { return (int)(threadIdx.x >> 6); }
 constexpr int kShort = 32;                   // per-lane merge loop up to this many bytes
 constexpr int kWin = kTile + 64;             // LDS byte window (tile + halo for key reads)
 constexpr int kTileWords = kTile / 64 + 1;   // bitmap words staged (tile + 64-bit halo)
@@ -943,7 +949,6 @@ __device__ __forceinline__ DdOut dedupe_claim(const EncArgs& a, const uint32_t* 
 // and the per-bucket queue counts come from wave ballots (no atomics).
 static_assert(kTile <= 0x10000, "chunk starts are uint16");
 // ---------------------------------------------------------------------------------------
-constexpr int kWaves = kThreads / 64;
 // two rounds of table probes in flight per wave: 5.52 -> 5.46 ms per C2 launch (one round or
 // three: 5.55 / 5.75 ms; four cap the kernel at 5 waves per SIMD)
 constexpr int kLookRounds = 2;
@@ -1199,7 +1204,7 @@ __global__ void __launch_bounds__(kThreads) SW_CLS_ATTR k_classify(EncArgs a) {
   __shared__ __attribute__((aligned(16))) uint32_t s_b32_all[kWaves][kWinWords];  // window bytes (+ zero tail)
   __shared__ uint16_t s_cs_all[kWaves][kTile + 1];   // chunk starts (tile-relative)
   __shared__ uint16_t s_qb_all[kWaves][kQBuf];       // chunks not settled by a lookup, to dedupe
-  const int wv = threadIdx.x >> 6;
+  const int wv = wave_in_block();
   const int64_t tile = (int64_t)blockIdx.x * kWaves + wv;
   if (tile < a.n_tiles) classify_tile<kSp>(a, tile, s_b32_all[wv], s_cs_all[wv], s_qb_all[wv]);
 }
@@ -1210,7 +1215,7 @@ __global__ void __launch_bounds__(kThreads) SW_CLS_ATTR k_classify(EncArgs a) {
 __global__ void __launch_bounds__(kThreads) k_scatter(EncArgs a) {
   // one wave per tile: lane b < kNumBuckets holds (count, next destination) of bucket b; the
   // tile's entries (any order) are routed 64 at a time, one ballot per bucket present
-  const int64_t t = ((int64_t)blockIdx.x * kThreads + threadIdx.x) >> 6;
+  const int64_t t = ((int64_t)blockIdx.x * kWaves + wave_in_block());
   const int lane = threadIdx.x & 63;
   if (t >= a.n_tiles) return;
   const uint64_t lt_mask = (lane == 0) ? 0ULL : (~0ULL >> (64 - lane));
@@ -1375,7 +1380,7 @@ __device__ __forceinline__ void put_lds_result(const EncArgs& a, uint64_t e, uin
 template <bool kWide, bool k16, int N, bool kWF = false>  // kWF: a well-formed table (lane_merge_lds_wf)
 __global__ void __launch_bounds__(kThreads) k_merge_bucket(EncArgs a, int b_lo, int b_hi) {
   SW_STAMP_INIT;
-  const int64_t gw = ((int64_t)blockIdx.x * kThreads + threadIdx.x) >> 6;  // global wave id
+  const int64_t gw = ((int64_t)blockIdx.x * kWaves + wave_in_block());  // global wave id
   const int64_t n_waves = ((int64_t)gridDim.x * kThreads) >> 6;
   const int lane = threadIdx.x & 63;
   int64_t lo, hi;
@@ -1388,7 +1393,7 @@ __global__ void __launch_bounds__(kThreads) k_merge_bucket(EncArgs a, int b_lo, 
   constexpr bool kPair = kLds && N <= SW_PAIR_MAX_N;
   constexpr int kPer = kPair ? 2 : 1;
   __shared__ uint32_t s_ids[kLds ? kWaves * 64 * N * kPer : 1];  // (lane_merge_lds_wf: the waves' ids)
-  uint32_t* s_id = s_ids + (kLds ? (threadIdx.x >> 6) * 64 * N * kPer : 0);
+  uint32_t* s_id = s_ids + (kLds ? wave_in_block() * 64 * N * kPer : 0);
   if constexpr (kPair) {  // batches of 128 entries per wave: entries base + lane and base + 64 + lane
     int64_t i = lo + gw * 128 + lane;
     uint64_t e0 = i < hi ? a.queue[i] : 0, e1 = i + 64 < hi ? a.queue[i + 64] : 0;
@@ -1775,7 +1780,7 @@ __device__ uint64_t wave_merge64(const DevTable& t, uint32_t& id, uint32_t& rk, 
 template <bool kWide>
 __global__ void __launch_bounds__(kThreads) k_merge_long(EncArgs a) {
   SW_STAMP_INIT;
-  const int64_t gw = ((int64_t)blockIdx.x * kThreads + threadIdx.x) >> 6;
+  const int64_t gw = ((int64_t)blockIdx.x * kWaves + wave_in_block());
   const int64_t n_waves = ((int64_t)gridDim.x * kThreads) >> 6;
   const int lane = threadIdx.x & 63;
   const uint32_t n_big = *a.big_count;  // (listed by k_merge_long_lds)
@@ -2020,7 +2025,7 @@ __device__ __forceinline__ uint32_t ref_count(const EncArgs& a, uint32_t r) {
 // references on prose, so one wave per tile spent most of its life waiting)
 constexpr int kTcTiles = 2;
 __global__ void __launch_bounds__(kThreads) k_tile_count(EncArgs a) {
-  const int64_t tb = (((int64_t)blockIdx.x * kThreads + threadIdx.x) >> 6) * kTcTiles;
+  const int64_t tb = (((int64_t)blockIdx.x * kWaves + wave_in_block())) * kTcTiles;
   const int lane = threadIdx.x & 63;
   if (tb >= a.n_tiles) return;
   uint32_t p0[kTcTiles], c[kTcTiles];
@@ -2220,8 +2225,8 @@ __global__ void __launch_bounds__(kThreads) k_compact(EncArgs a, const int64_t* 
   __shared__ uint32_t s_rp_all[kWaves][kRefCap];
   __shared__ uint4 s_rq_all[kWaves][kRefCap];
   __shared__ int32_t s_out_all[kWaves][kOutCapW];  // a group's ids, staged for 256-B stores
-  const int wv = threadIdx.x >> 6;
-  const int64_t t = ((int64_t)blockIdx.x * kThreads + threadIdx.x) >> 6;
+  const int wv = wave_in_block();
+  const int64_t t = ((int64_t)blockIdx.x * kWaves + wave_in_block());
   if (t >= a.n_tiles) return;
   compact_tile(a, t, tile_base[t], out, s_rp_all[wv], s_rq_all[wv], s_out_all[wv]);
 }

@@ -158,7 +158,7 @@ __global__ void __launch_bounds__(kThreads) k_lp_fill(LongArgs L) {
   const int64_t n_long = lp_count(&L.ctl[kLcLong], L.lcap);
   const int lane = threadIdx.x & 63;
   const int64_t n_waves = (int64_t)gridDim.x * (kThreads / 64);
-  for (int64_t i = ((int64_t)blockIdx.x * kThreads + threadIdx.x) >> 6; i < n_long; i += n_waves) {
+  for (int64_t i = ((int64_t)blockIdx.x * kWaves + wave_in_block()); i < n_long; i += n_waves) {
     const int P = (int)L.lnp[i];
     const int64_t j0 = L.lpo[i];
     if (j0 + P > L.pcap) continue;  // (cannot happen: pcap >= n_bytes / 8)
@@ -215,13 +215,13 @@ __global__ void __launch_bounds__(kThreads) k_lp_encode(EncArgs a, LongArgs L) {
   __shared__ uint32_t s_ids[kLds ? kWaves * 64 * kPieceN : 1];  // (lane_merge_lds_wf: the waves' ids)
   const int64_t np = lp_count(&L.ctl[kLcPieces], L.pcap);
   const int lane = threadIdx.x & 63;
-  uint32_t* s_id = s_ids + (kLds ? (threadIdx.x >> 6) * 64 * kPieceN : 0);
+  uint32_t* s_id = s_ids + (kLds ? wave_in_block() * 64 * kPieceN : 0);
   const uint64_t lt_mask = (lane == 0) ? 0ULL : (~0ULL >> (64 - lane));
   const int64_t mis = (int64_t)((uintptr_t)a.bytes & 3);
   const uint32_t* words = (const uint32_t*)((uintptr_t)a.bytes - mis);
   const int64_t last_word = (mis + a.n_bytes - 1) >> 2;
   const int64_t n_waves = (int64_t)gridDim.x * (kThreads / 64);
-  for (int64_t g = ((int64_t)blockIdx.x * kThreads + threadIdx.x) >> 6; 63 * g < np; g += n_waves) {
+  for (int64_t g = ((int64_t)blockIdx.x * kWaves + wave_in_block()); 63 * g < np; g += n_waves) {
     const int64_t j = 63 * g - 1 + lane;
     const bool act = j >= 0 && j < np;
     const bool own = act && lane > 0;
@@ -366,7 +366,7 @@ __global__ void __launch_bounds__(kThreads) k_lp_windows(EncArgs a, LongArgs L, 
   constexpr bool kLds = k16 && !kWide;
   __shared__ uint32_t s_ids[kLds ? kWaves * 64 * kShort : 1];  // (lane_merge_lds_wf: the waves' ids)
   const int lane = threadIdx.x & 63;
-  uint32_t* s_id = s_ids + (kLds ? (threadIdx.x >> 6) * 64 * kShort : 0);
+  uint32_t* s_id = s_ids + (kLds ? wave_in_block() * 64 * kShort : 0);
   const int64_t nh = lp_count(&L.ctl[kLcHead + r], L.pcap), np = lp_count(&L.ctl[kLcPieces], L.pcap);
   const int64_t mis = (int64_t)((uintptr_t)a.bytes & 3);
   const uint32_t* words = (const uint32_t*)((uintptr_t)a.bytes - mis);
@@ -492,7 +492,7 @@ __global__ void __launch_bounds__(kThreads) k_lp_gather(EncArgs a, LongArgs L) {
   const int lane = threadIdx.x & 63;
   const uint64_t lt_mask = (lane == 0) ? 0ULL : (~0ULL >> (64 - lane));
   const int64_t n_waves = (int64_t)gridDim.x * (kThreads / 64);
-  for (int64_t i = ((int64_t)blockIdx.x * kThreads + threadIdx.x) >> 6; i < n_long; i += n_waves) {
+  for (int64_t i = ((int64_t)blockIdx.x * kWaves + wave_in_block()); i < n_long; i += n_waves) {
     if (L.lfall[i]) continue;
     const int64_t start = L.lstart[i], len = L.llen[i];
     uint32_t* dst = a.res + 2 * start + 1;

@@ -94,6 +94,21 @@ struct RegBytes {
   }
 };
 
+// The class of a code point in one of the big single-class ranges of the most common non-ASCII
+// scripts, from registers; -1 when cp is outside them (the caller then reads the UCD tables: two
+// dependent memory reads, which a wave waits for if any of its lanes needs them).  Latin-1
+// letters + Latin Extended-A/B + IPA, Greek, Cyrillic, Kana, CJK (+ extension A, B), Hangul
+// syllables: \p{L}; the emoji / pictograph planes 0x1F10D-0x1FBEF: other.  Every range is one
+// class in ucd_tables.h (tests/test_presplit_bits.py checks all of 0..0x10FFFF).
+SW_HD inline int fast_class(uint32_t cp) {
+  auto in = [](uint32_t x, uint32_t lo, uint32_t hi) -> uint32_t { return x - lo <= hi - lo ? 1u : 0u; };
+  const uint32_t L = (in(cp, 0xC0, 0x2C1) & (cp != 0xD7 ? 1u : 0u) & (cp != 0xF7 ? 1u : 0u)) | in(cp, 0x391, 0x3A1) |
+                     in(cp, 0x3A3, 0x3F5) | in(cp, 0x3F7, 0x481) | in(cp, 0x48A, 0x52F) | in(cp, 0x3041, 0x3096) |
+                     in(cp, 0x30A1, 0x30FA) | in(cp, 0x3400, 0x4DBF) | in(cp, 0x4E00, 0xA48C) | in(cp, 0xAC00, 0xD7A3) |
+                     in(cp, 0x20000, 0x2A6DF);
+  return L ? kL : in(cp, 0x1F10D, 0x1FBEF) ? kOther : -1;
+}
+
 // Bytes: word(i) = bytes [pos - 4 + 4i, pos + 4i) as a little-endian word (i < 10); at4(k) = the
 // bytes k .. k + 3 of those 40 (k <= 36).
 template <class Cls, class Bytes>
@@ -157,7 +172,11 @@ SW_HD inline Masks classify(const Bytes& by, uint64_t ss, const Cls& cls, bool c
       uint64_t t;
       const uint32_t v = lead(k, &t);
       X |= t;
-      if (v != kInvalidCp) apply(k, v, cls(v));
+      if (v != kInvalidCp) {
+        int c = fast_class(v);
+        if (c < 0) c = cls(v);
+        apply(k, v, c);
+      }
     }
 #else
     // two leads per step, both class lookups in flight together (each is two dependent table
@@ -170,7 +189,9 @@ SW_HD inline Masks classify(const Bytes& by, uint64_t ss, const Cls& cls, bool c
       uint64_t t1, t2;
       const uint32_t v1 = lead(k1, &t1), v2 = lead(k2, &t2);
       X |= t1 | t2;
-      const int cls1 = v1 != kInvalidCp ? cls(v1) : kOther, cls2 = v2 != kInvalidCp ? cls(v2) : kOther;
+      int cls1 = v1 != kInvalidCp ? fast_class(v1) : kOther, cls2 = v2 != kInvalidCp ? fast_class(v2) : kOther;
+      if (cls1 < 0) cls1 = cls(v1);
+      if (cls2 < 0) cls2 = cls(v2);
       apply(k1, v1, cls1);
       apply(k2, v2, cls2);
     }

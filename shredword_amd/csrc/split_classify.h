@@ -498,7 +498,7 @@ k_split_classify(EncArgs a, PbArgs g, int pattern, const uint32_t* edge, uint32_
   __shared__ __attribute__((aligned(16))) uint32_t s_win_all[kWaves][kScWinWords];
   __shared__ ScShared s_sh_all[kWaves];
   __shared__ uint16_t s_qb_all[kWaves][kQBuf];
-  const int wv = threadIdx.x >> 6;
+  const int wv = wave_in_block();
   const int64_t tile = (int64_t)blockIdx.x * kWaves + wv;
   if (tile < a.n_tiles)
     split_classify_tile<kSp, false>(a, g, pattern, edge, bits32, tile, s_win_all[wv], &s_sh_all[wv], s_qb_all[wv],
@@ -514,7 +514,7 @@ __global__ void __launch_bounds__(kThreads) k_split_redo(EncArgs a, PbArgs g, in
   __shared__ __attribute__((aligned(16))) uint32_t s_win_all[kWaves][kScWinWords];
   __shared__ ScShared s_sh_all[kWaves];
   __shared__ uint16_t s_qb_all[kWaves][kQBuf];
-  const int wv = threadIdx.x >> 6;
+  const int wv = wave_in_block();
   const int64_t n = (int64_t)*redo.count;
   for (int64_t i = (int64_t)blockIdx.x * kWaves + wv; i < n; i += (int64_t)gridDim.x * kWaves) {
     split_classify_tile<kSp, true>(a, g, pattern, edge, bits32, redo.tiles[i], s_win_all[wv], &s_sh_all[wv],

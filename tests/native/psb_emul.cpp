@@ -86,3 +86,18 @@ extern "C" int64_t psb_emul(const uint8_t* bytes, const int64_t* off, int64_t n_
   }
   return slow;
 }
+
+// fast_class (presplit_bits.h) against the UCD tables for every code point: the number of code
+// points it answers differently (it may decline any: -1); *covered: how many it answers
+extern "C" int64_t psb_fast_class_check(int64_t* covered) {
+  const Ucd ucd;
+  int64_t bad = 0, cov = 0;
+  for (uint32_t cp = 0; cp <= 0x10FFFF; ++cp) {
+    const int f = sw::psb::fast_class(cp);
+    if (f < 0) continue;
+    ++cov;
+    if (f != ucd(cp)) ++bad;
+  }
+  *covered = cov;
+  return bad;
+}

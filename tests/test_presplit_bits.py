@@ -53,6 +53,7 @@ def psb():
         slow = lib.psb_emul(buf.ctypes.data, off.ctypes.data, len(off) - 1, pattern, bits.ctypes.data)
         assert slow >= 0, "a second rules() pass still asked for carries"
         return bits, slow
+    run.lib = lib
     return run
 
 
@@ -115,3 +116,14 @@ def test_empty_and_single(psb):
     check(psb, *pack([b""]))
     check(psb, *pack([b"a"]))
     check(psb, *pack([b"", b"'", b"s", b"", b"'s", b" ", b"1"]))
+
+
+def test_fast_class_exhaustive(psb):
+    """The pre-split's register fast path for code-point classes (presplit_bits.h fast_class)
+    agrees with the UCD tables (exported from `regex`) on every code point it answers."""
+    lib = psb.lib
+    lib.psb_fast_class_check.argtypes = [ctypes.c_void_p]
+    lib.psb_fast_class_check.restype = ctypes.c_int64
+    cov = ctypes.c_int64(0)
+    assert lib.psb_fast_class_check(ctypes.byref(cov)) == 0
+    assert cov.value > 80000  # (CJK, Hangul, CJK extension B, the emoji planes, ...)

@@ -112,7 +112,10 @@ def main():
     for ln in open(os.path.join(src, "trace.log"), errors="replace"):
         if ln.startswith("{") and '"metric"' in ln:
             bench = json.loads(ln)
-    if bench and "traffic_bytes_per_launch" in derived and bench["config"].get("workload", "").startswith("C2:"):
+    cfg = bench["config"] if bench else {}
+    headline = (cfg.get("workload", "").startswith("C2:") and cfg.get("chunk_table") and cfg.get("dedupe")
+                and cfg.get("corpus", "mixed") == "mixed" and not bench.get("specials"))
+    if bench and "traffic_bytes_per_launch" in derived and headline:  # (the headline config only)
         with open(os.path.join(out, "traffic.json"), "w") as f:
             json.dump({"source": "profiles/%s.md" % tag, "n_bytes": bench["config"]["bytes_per_rank"],
                        "merges": bench["config"]["merges"], "pattern": bench["config"]["pattern"],

@@ -153,6 +153,7 @@ int32_t sw_encoder_set_option(sw_encoder* h, int32_t option, int64_t value);
 #define SW_INFO_WIDE_TABLE 3
 #define SW_INFO_IDS16 4
 #define SW_INFO_SPLIT 5     /* the table is well-formed: long chunks may take the split path */
+#define SW_INFO_DEDUPE_SLOTS 6  /* entries of the dedupe table now (it grows after a launch overflows it) */
 int64_t sw_encoder_get_info(const sw_encoder* h, int32_t what);
 
 /* ---- host pre-split (apply_regex, base.py:38-58) ---------------------------------------

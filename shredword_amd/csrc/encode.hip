@@ -130,6 +130,10 @@ struct sw_encoder {
   unsigned long long* d_stamps = nullptr;  // SW_STAMPS builds
   uint64_t* d_dtab = nullptr;         // chunk dedupe table
   uint32_t dmask = 0;
+  int64_t dd_slots = 0;               // entries of d_dtab (grown by grow_dedupe, kept across workspace reallocations)
+  unsigned long long* d_ddfull = nullptr;     // per launch: dedupable chunks that found every candidate taken
+  unsigned long long* h_ddfull = nullptr;     // ... published by k_string_offsets (host-mapped, coherent)
+  unsigned long long* hd_ddfull = nullptr;    // (its device address)
   uint4* d_dres = nullptr;            // dense result heads, one per table entry
   uint8_t* d_dcnt = nullptr;          // their id counts (<= 32), one byte per table entry
   uint32_t* d_big = nullptr;          // chunks over kLongLds bytes: count, then their long-list indices
@@ -184,6 +188,7 @@ struct DeviceGuard {
 
 void free_workspace(sw_encoder* h) {
   (void)hipFree(h->d_scratch); (void)hipFree(h->d_res); (void)hipFree(h->d_pbits); (void)hipFree(h->d_edge); (void)hipFree(h->d_redo); (void)hipFree(h->d_pcount); (void)hipFree(h->d_part);
+  (void)hipFree(h->d_ddfull); h->d_ddfull = nullptr;
   (void)hipFree(h->d_tile_slo); (void)hipFree(h->d_tile_sp); (void)hipFree(h->d_stamps);
   (void)hipFree(h->d_tile_slots); (void)hipFree(h->d_tile_nref); (void)hipFree(h->d_rlist); (void)hipFree(h->d_queue); (void)hipFree(h->d_bcnt); (void)hipFree(h->d_boff);
   (void)hipFree(h->d_qtotal);
@@ -242,10 +247,12 @@ int32_t ensure_workspace(sw_encoder* h, int64_t n_bytes) {
   HIP_TRY(hipMalloc(&h->d_boff, sizeof(int64_t) * kNumBuckets * n_tiles));
   HIP_TRY(hipMalloc(&h->d_qtotal, sizeof(int64_t)));
   HIP_TRY(hipMalloc(&h->d_part, sizeof(int64_t) * ((kNumBuckets * n_tiles + kScanBlock - 1) / kScanBlock + 1)));
-  {  // dedupe table: ~1 entry per 64 input bytes, 2^6 .. 2^22 entries (32 MiB), and a 16-byte
-     // result head per entry
+  {  // dedupe table: ~1 entry per 64 input bytes, 2^6 .. 2^22 entries (32 MiB) to start with, more
+     // when a launch overflows it (grow_dedupe), and a 16-byte result head + a count byte per entry
     int64_t slots = 64;
-    while (slots < nb / 64 && slots < (1LL << 22)) slots <<= 1;
+    while (slots < nb / 64 && slots < kDdSlotsDefault) slots <<= 1;
+    slots = std::max(slots, h->dd_slots);
+    h->dd_slots = slots;
     HIP_TRY(hipMalloc(&h->d_dtab, sizeof(uint64_t) * slots));
     HIP_TRY(hipMalloc(&h->d_dres, sizeof(uint4) * slots));
     HIP_TRY(hipMalloc(&h->d_dcnt, slots));
@@ -286,6 +293,8 @@ int32_t ensure_workspace(sw_encoder* h, int64_t n_bytes) {
   HIP_TRY(hipMalloc(&h->d_edge, sizeof(uint32_t) * kEdgeWords * (n_tiles + 1)));
   HIP_TRY(hipMalloc(&h->d_redo, sizeof(int64_t) * (n_tiles + 1)));
   HIP_TRY(hipMalloc(&h->d_pcount, sizeof(unsigned long long)));
+  HIP_TRY(hipMalloc(&h->d_ddfull, sizeof(unsigned long long)));
+  HIP_TRY(hipMemset(h->d_ddfull, 0, sizeof(unsigned long long)));
 #ifdef SW_STAMPS
   HIP_TRY(hipMalloc(&h->d_stamps, sizeof(unsigned long long) * 32 * 64));  // 64 copies per counter
   HIP_TRY(hipMemset(h->d_stamps, 0, sizeof(unsigned long long) * 32 * 64));
@@ -478,6 +487,12 @@ extern "C" int32_t sw_encoder_create(const int32_t* pairs, const int32_t* vals, 
     h->n_inv = (uint32_t)inv.size();
   }
   e = hipEventCreateWithFlags(&h->ws_done, hipEventDisableTiming);
+  if (e == hipSuccess)  // (the dedupe overflow count of the last launch, written by the device)
+    e = hipHostMalloc((void**)&h->h_ddfull, sizeof(unsigned long long), hipHostMallocMapped | hipHostMallocCoherent);
+  if (e == hipSuccess) {
+    *h->h_ddfull = 0;
+    e = hipHostGetDevicePointer((void**)&h->hd_ddfull, h->h_ddfull, 0);
+  }
   if (e != hipSuccess) {
     sw_encoder_destroy(h);
     return fail(SW_ERR_HIP, std::string("sw_encoder_create: ") + hipGetErrorString(e));
@@ -507,6 +522,7 @@ extern "C" void sw_encoder_destroy(sw_encoder* h) {
     (void)hipFree(h->d_chunks);
     (void)hipFree(h->d_inv);
     if (h->ws_done) (void)hipEventDestroy(h->ws_done);
+    if (h->h_ddfull) (void)hipHostFree(h->h_ddfull);
     for (hipEvent_t ev : h->ev_pool) (void)hipEventDestroy(ev);
     if (h->stream) (void)hipStreamDestroy(h->stream);
   }
@@ -567,6 +583,7 @@ extern "C" int64_t sw_encoder_get_info(const sw_encoder* h, int32_t what) {
     case SW_INFO_WIDE_TABLE: return h->table.wide;
     case SW_INFO_IDS16: return h->ids16 ? 1 : 0;
     case SW_INFO_SPLIT: return h->split_ok ? 1 : 0;
+    case SW_INFO_DEDUPE_SLOTS: return h->dd_slots;
     default: return SW_ERR_ARG;
   }
 }
@@ -682,6 +699,29 @@ struct DevSpecials {
 };
 
 // the device pipeline; d_out_ids is int32_t*, or uint16_t* when out16 (the table is ids16)
+// A launch whose dedupe table overflowed (chunks that found all 8 candidates of their line taken,
+// counted by the device and published to host memory by k_string_offsets) grows the table for
+// the launches after it: to the power of two >= 2 x (entries + overflow), at most kDdSlotsMax.
+// The count is read without waiting: a launch still running is seen by a later call.
+int32_t grow_dedupe(sw_encoder* h) {
+  const unsigned long long over = h->h_ddfull ? __atomic_load_n(h->h_ddfull, __ATOMIC_ACQUIRE) : 0ULL;
+  if (!h->d_dtab || h->dedupe_slots || over <= (unsigned long long)h->dd_slots / 32 || h->dd_slots >= kDdSlotsMax)
+    return SW_OK;  // (SW_OPT_DEDUPE_SLOTS caps the table on purpose: no growth)
+  int64_t slots = h->dd_slots;
+  while (slots < 2 * (h->dd_slots + (int64_t)over) && slots < kDdSlotsMax) slots <<= 1;
+  if (h->ws_pending) HIP_TRY(hipEventSynchronize(h->ws_done));
+  (void)hipFree(h->d_dtab); (void)hipFree(h->d_dres); (void)hipFree(h->d_dcnt);
+  h->d_dtab = nullptr; h->d_dres = nullptr; h->d_dcnt = nullptr;
+  HIP_TRY(hipMalloc(&h->d_dtab, sizeof(uint64_t) * slots));
+  HIP_TRY(hipMemset(h->d_dtab, 0, sizeof(uint64_t) * slots));
+  HIP_TRY(hipMalloc(&h->d_dres, sizeof(uint4) * slots));
+  HIP_TRY(hipMalloc(&h->d_dcnt, slots));
+  h->dd_slots = slots;
+  h->dmask = (uint32_t)(slots - 1);
+  __atomic_store_n(h->h_ddfull, 0ULL, __ATOMIC_RELEASE);
+  return SW_OK;
+}
+
 int32_t encode_device(sw_encoder* h, const uint8_t* d_bytes, int64_t n_bytes, const int64_t* d_str_off, int64_t n_str,
                       const uint64_t* d_chunk_bits, const DevSpecials& sp, void* d_out_ids, bool out16,
                       int64_t* d_out_off, void* stream, int64_t* n_tokens_host) {
@@ -697,6 +737,7 @@ int32_t encode_device(sw_encoder* h, const uint8_t* d_bytes, int64_t n_bytes, co
   // the workspace belongs to the handle: order this launch after the previous one on any stream
   if (h->ws_pending && h->ws_stream != st) HIP_TRY(hipStreamWaitEvent(st, h->ws_done, 0));
   int32_t rc = ensure_workspace(h, n_bytes);
+  if (rc == SW_OK && h->dedupe) rc = grow_dedupe(h);
   if (rc) return rc;
   const int64_t n_tiles = (n_bytes + kTile - 1) / kTile;
   h->last_tiles = n_tiles;
@@ -736,6 +777,7 @@ int32_t encode_device(sw_encoder* h, const uint8_t* d_bytes, int64_t n_bytes, co
     a.dexact = h->dedupe_exact ? (uint32_t)kDdExactMax : 0u;
     a.dres = h->d_dres;
     a.dcnt = h->d_dcnt;
+    a.dd_full = h->d_ddfull;
     a.big_count = h->d_big; a.big_list = h->d_big + 1;
     a.out_off = d_out_off; a.tile_slo = h->d_tile_slo;
     a.n_tiles = n_tiles; a.qtmp = h->d_res; a.bcnt = h->d_bcnt; a.boff = h->d_boff; a.q_total = h->d_qtotal;
@@ -744,14 +786,16 @@ int32_t encode_device(sw_encoder* h, const uint8_t* d_bytes, int64_t n_bytes, co
     a.lstart = h->lp.wstart; a.llen = h->lp.wlen; a.n_long = &h->lp.ctl[kLcWave]; a.lcap = h->lp.lcap;
     a.sp = spa;
     const bool split = h->split_ok && h->long_split;  // (split + verify needs a well-formed table)
+    // (cleared per launch rather than entry by entry by the merge kernels that empty the claims:
+    // the memset leaves the table's lines in the caches, and the probes then hit -- clearing only
+    // the claims made k_split_classify 2% slower on C2, r4n/r4o A/B)
     if (h->dedupe) HIP_TRY(hipMemsetAsync(h->d_dtab, 0, sizeof(uint64_t) * ((size_t)a.dmask + 1), st));
     if (fused) {
       const PbArgs pg{d_bytes, n_bytes, d_str_off, n_str, h->d_tile_slo, spa};
       hipLaunchKernelGGL(k_edges, dim3((unsigned)((n_tiles + 1 + 255) / 256)), dim3(256), 0, st, pg, n_tiles,
-                         (int)h->pattern, h->d_edge);
+                         (int)h->pattern, h->d_edge, h->d_redo);
       const dim3 gc((unsigned)((n_tiles + kWaves - 1) / kWaves));
-      const RedoList redo{h->d_redo, (int64_t*)(h->d_redo + 2)};
-      HIP_TRY(hipMemsetAsync(h->d_redo, 0, sizeof(unsigned int), st));
+      const RedoList redo{h->d_redo, (int64_t*)(h->d_redo + 2)};  // (its count zeroed by k_edges)
       if (sp.n > 0) {
         hipLaunchKernelGGL(k_split_classify<true>, gc, dim3(kThreads), 0, st, a, pg, (int)h->pattern,
                            (const uint32_t*)h->d_edge, (uint32_t*)h->d_pbits, redo);
@@ -832,7 +876,7 @@ int32_t encode_device(sw_encoder* h, const uint8_t* d_bytes, int64_t n_bytes, co
     HIP_TRY(hipMemsetAsync(h->d_total, 0, sizeof(int64_t), st));
   }
   hipLaunchKernelGGL(k_string_offsets, dim3((unsigned)((n_str + 1 + 255) / 256)), dim3(256), 0, st, d_str_off, n_str,
-                     n_bytes, h->d_total, d_out_off);
+                     n_bytes, h->d_total, d_out_off, h->d_ddfull, h->hd_ddfull);
   HIP_TRY(hipGetLastError());
   if (h->timing) {
     HIP_TRY(hipEventRecord(e1, st));

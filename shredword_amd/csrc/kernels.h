@@ -70,6 +70,8 @@ __host__ __device__ inline uint32_t slot_did(int32_t v) { return (uint32_t)(-(in
 // need no second read.  A reference list entry (rlist) is p or kRlDense | d.
 constexpr uint32_t kRlDense = 0x80000000u;
 constexpr uint32_t kNoDid = 0x7FFFFFFu;    // (27-bit dense result field of a queue entry: none)
+constexpr int64_t kDdSlotsDefault = 1LL << 22;  // dedupe table entries at most to start with (32 MiB)
+constexpr int64_t kDdSlotsMax = 1LL << 26;      // ... and after growing (a queue entry's dense field: 27 bits)
 constexpr int kDdExactMax = 7;             // dedupe keys of <= this many bytes are exact (no verification)
 #ifndef SW_PAIR_MAX_N
 #define SW_PAIR_MAX_N 16                   // k_merge_bucket<N>: two chunks per lane up to this N (0: never)
@@ -791,13 +793,14 @@ struct EncArgs {
   const int64_t* boff;       // [kNumBuckets * n_tiles] exclusive scan of bcnt (bucket-major)
   const int64_t* q_total;    // queued chunks in all
   uint64_t* queue;           // dense merge queue, bucket-major: start << 33 | len << 27 | dense result
-  uint64_t* dtab;            // chunk dedupe table (dedupe_claim), dmask + 1 entries
+  uint64_t* dtab;            // chunk dedupe table (dedupe_claim), dmask + 1 entries, cleared per launch
   uint32_t dmask;
   uint32_t dfp_mask;         // fingerprint bits in use (all 26 except in collision tests)
   uint32_t dedupe;           // 0: every queued chunk runs its own merge loop
   uint32_t dexact;           // longest exact dedupe key (kDdExactMax, or 0: every key verified)
   uint4* dres;               // [dmask + 1] dense result heads (slot_dref), by table entry
   uint8_t* dcnt;             // [dmask + 1] their id counts (<= 32): k_tile_count's reads stay in L2
+  unsigned long long* dd_full;  // dedupable chunks of the launch that found no free candidate (k_scatter)
   unsigned long long* stamps;  // SW_STAMPS builds: cycles per phase, summed
   const uint2* inv;          // [n_inv] merge value -> its pair (a, b); well-formed tables only
   uint32_t n_inv;
@@ -940,7 +943,7 @@ __device__ __forceinline__ DdOut dedupe_claim(const EncArgs& a, const uint32_t* 
     if (!same) continue;
     return DdOut{2, idx};
   }
-  return DdOut{0, 0};
+  return DdOut{0, 0};  // (the table's overflow: counted by k_scatter for grow_dedupe)
 }
 
 // ---------------------------------------------------------------------------------------
@@ -951,7 +954,10 @@ static_assert(kTile <= 0x10000, "chunk starts are uint16");
 // ---------------------------------------------------------------------------------------
 // two rounds of table probes in flight per wave: 5.52 -> 5.46 ms per C2 launch (one round or
 // three: 5.55 / 5.75 ms; four cap the kernel at 5 waves per SIMD)
-constexpr int kLookRounds = 2;
+#ifndef SW_LOOK_ROUNDS
+#define SW_LOOK_ROUNDS 2
+#endif
+constexpr int kLookRounds = SW_LOOK_ROUNDS;
 constexpr int kQBuf = 64 * (kLookRounds + 1);        // dedupe buffer: one batch + a group of rounds
 constexpr int kWinWords = kWin / 4 + 8;
 
@@ -1237,6 +1243,10 @@ __global__ void __launch_bounds__(kThreads) k_scatter(EncArgs a) {
     const uint32_t did = act ? SW_LDNT2(&a.qtmp[t0 + kTile / 2 + i]) : kNoDid;
     const uint32_t ns = e >> (2 * kTileBits);
     const int b = act ? (ns ? bucket_of(ns) : kLongBucket) : 15;
+    if (a.dedupe) {  // (a dedupable chunk queued without an entry: its table line was full, see grow_dedupe)
+      const uint64_t full = __ballot(act && ns != 0 && did == kNoDid);
+      if (full && lane == 0) atomicAdd(a.dd_full, (unsigned long long)__popcll(full));
+    }
     int64_t d = 0;
     uint64_t pend = __ballot(act);
     while (pend) {
@@ -2233,9 +2243,15 @@ __global__ void __launch_bounds__(kThreads) k_compact(EncArgs a, const int64_t* 
 
 // every string offset: a complemented value is one k_compact finished; strings starting at or
 // past n_bytes (trailing empty strings) and the end sentinel get the total
+// (and the launch's dedupe overflow count to host memory, zeroed for the next launch)
 __global__ void k_string_offsets(const int64_t* str_off, int64_t n_str, int64_t n_bytes, const int64_t* total,
-                                 int64_t* out_off) {
+                                 int64_t* out_off, unsigned long long* dd_full, unsigned long long* h_dd_full) {
   const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (s == 0 && dd_full) {
+    const unsigned long long v = *dd_full;
+    *dd_full = 0;
+    __hip_atomic_store(h_dd_full, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
   if (s > n_str) return;
   if (s == n_str || str_off[s] >= n_bytes) {
     out_off[s] = *total;

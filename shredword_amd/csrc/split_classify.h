@@ -188,8 +188,10 @@ __device__ __forceinline__ void ss_win5(const PbArgs& g, int64_t n_tiles, int64_
 
 // k_edges: per tile boundary b in [0, n_tiles] (byte 2048 b, chunk c = 64 b): the class masks of
 // chunk c and its final chunk-start word (zeros past the batch).  edge[k * (n_tiles + 1) + b].
-__global__ void __launch_bounds__(256) k_edges(PbArgs g, int64_t n_tiles, int pattern, uint32_t* edge) {
+__global__ void __launch_bounds__(256) k_edges(PbArgs g, int64_t n_tiles, int pattern, uint32_t* edge,
+                                               unsigned int* redo_count) {
   const int64_t b = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (b == 0) *redo_count = 0;  // (k_split_classify's redo list, empty)
   if (b > n_tiles) return;
   const int64_t n_chunks = (g.n_bytes + psb::kChunk - 1) / psb::kChunk;
   const int64_t c = b << (kTileBits - 5);

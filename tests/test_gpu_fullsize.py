@@ -28,8 +28,10 @@ THREADS = min(16, len(os.sched_getaffinity(0)))
 BENCH_SEED = 1_000_003  # bench.py: corpus.synth(1_000_003 + rank, ...)
 
 
-def device_encode(tok, buf, off):
-    """The bench's step: sw_encode_device on HBM-resident torch buffers, device pre-split."""
+def device_encode(tok, buf, off, reps=1):
+    """The bench's step: sw_encode_device on HBM-resident torch buffers, device pre-split; reps
+    launches on the same encoder (the dedupe table is cleared by the launches themselves, and grows
+    after one that overflowed it): every launch's (ids, offsets)."""
     import torch
     dev = torch.device("cuda", 0)
     d_buf = torch.from_numpy(buf).to(dev)
@@ -37,13 +39,16 @@ def device_encode(tok, buf, off):
     d_out = torch.empty(len(buf), dtype=torch.int32, device=dev)
     d_oo = torch.empty(len(off), dtype=torch.int64, device=dev)
     n_tok = ctypes.c_int64()
-    _lib.check(_lib.lib().sw_encode_device(tok._encoder(), d_buf.data_ptr(), len(buf), d_off.data_ptr(), len(off) - 1,
-                                           None, d_out.data_ptr(), d_oo.data_ptr(),
-                                           torch.cuda.current_stream(dev).cuda_stream, ctypes.byref(n_tok)))
-    ids, oo = d_out[:n_tok.value].cpu().numpy(), d_oo.cpu().numpy()
+    outs = []
+    for _ in range(reps):
+        d_out.fill_(-7)
+        _lib.check(_lib.lib().sw_encode_device(tok._encoder(), d_buf.data_ptr(), len(buf), d_off.data_ptr(),
+                                               len(off) - 1, None, d_out.data_ptr(), d_oo.data_ptr(),
+                                               torch.cuda.current_stream(dev).cuda_stream, ctypes.byref(n_tok)))
+        outs.append((d_out[:n_tok.value].cpu().numpy(), d_oo.cpu().numpy()))
     del d_buf, d_off, d_out, d_oo
     torch.cuda.empty_cache()
-    return ids, oo
+    return outs if reps > 1 else outs[0]
 
 
 def first_mismatch(got, exp):
@@ -61,12 +66,19 @@ def test_bench_batch_vs_oracle(cfg):
         assert len(buf) == 1_073_322_961  # (the bench's C2 batch, BENCH_r02)
     tok = sa.Tokenizer(device=0)
     tok.merges = load_model_merges(model)
-    got_ids, got_off = device_encode(tok, buf, off)
+    # ENTROPY overflows the first launch's dedupe table (~15 M distinct chunks): the second launch
+    # grows it, the third runs on the grown table -- every launch against the oracle
+    reps = 3 if cfg == "entropy" else 1
+    outs = device_encode(tok, buf, off, reps)
+    outs = outs if reps > 1 else [outs]
     exp_ids, exp_off = oracle.OracleModel(tok.merges).encode_batch(buf, off, oracle.PAT_CL100K, n_threads=THREADS)
-    assert len(got_ids) == len(exp_ids), (len(got_ids), len(exp_ids), first_mismatch(got_ids, exp_ids))
-    assert np.array_equal(got_off, exp_off)
-    i = first_mismatch(got_ids, exp_ids)
-    assert i == len(exp_ids), "first differing id at %d" % i
+    for got_ids, got_off in outs:
+        assert len(got_ids) == len(exp_ids), (len(got_ids), len(exp_ids), first_mismatch(got_ids, exp_ids))
+        assert np.array_equal(got_off, exp_off)
+        i = first_mismatch(got_ids, exp_ids)
+        assert i == len(exp_ids), "first differing id at %d" % i
+    if cfg == "entropy":
+        assert _lib.lib().sw_encoder_get_info(tok._encoder(), _lib.SW_INFO_DEDUPE_SLOTS) > (1 << 22)
     tok.close()
 
 

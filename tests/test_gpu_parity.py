@@ -329,6 +329,25 @@ def test_dedupe_exact_key_prefix_collisions():
         L.sw_encoder_set_option(h, _lib.SW_OPT_DEDUPE_SLOTS, 0)
 
 
+def test_dedupe_table_grows_and_clears_itself():
+    """A low-repetition batch overflows the dedupe table the encoder starts with (~1 entry per 64
+    input bytes): the launch after it grows the table, and no launch clears the table (the merge
+    kernels empty the entries their chunks claimed) -- three launches of the same batch, each
+    against the oracle, and another batch after them."""
+    buf, off = corpus.synth(31, corpus.ENTROPY, 60000, 1074)
+    buf2, off2 = corpus.synth(32, corpus.ENTROPY, 6000, 1074)
+    t = tok_for("bl32k.model")
+    exp = oracle_encode(t.merges, buf, off, "cl100k")
+    L, h = _lib.lib(), t._encoder()
+    slots0 = None
+    for rep in range(3):
+        assert_same(gpu_encode(t, buf, off), exp)
+        if rep == 0:
+            slots0 = L.sw_encoder_get_info(h, _lib.SW_INFO_DEDUPE_SLOTS)
+    assert L.sw_encoder_get_info(h, _lib.SW_INFO_DEDUPE_SLOTS) > slots0
+    assert_same(gpu_encode(t, buf2, off2), oracle_encode(t.merges, buf2, off2, "cl100k"))
+
+
 def test_dedupe_options_validated():
     t = tok_for("toy500.model")
     L, h = _lib.lib(), t._encoder()

@@ -112,6 +112,7 @@ struct sw_encoder {
   bool merge_fork = true;             // SW_OPT_MERGE_STREAMS
   hipStream_t s_fork[2] = {nullptr, nullptr};
   hipEvent_t ev_fork = nullptr, ev_join[2] = {nullptr, nullptr};
+  hipEvent_t ev_fork_long = nullptr;  // (the long chunks' fork, right after k_classify)
   sw::HostPool* pool = nullptr;
   // workspace
   int64_t cap_bytes = -1, cap_str = -1;
@@ -151,6 +152,8 @@ struct sw_encoder {
   unsigned int* d_redo = nullptr;     // k_split_classify's tiles for k_split_redo: count, then the list (int64)
   bool fused_presplit = true;         // SW_OPT_FUSED_PRESPLIT: the device pre-split inside k_split_classify
   unsigned long long* d_pcount = nullptr;
+  uint64_t* d_llist = nullptr;        // k_classify's long chunks (EncArgs::llist) and their count
+  unsigned long long* d_lcount = nullptr;
   uint32_t dedupe_fp_mask = (1u << 26) - 1;
   uint32_t* d_tile_cnt = nullptr;
   int64_t* d_tile_base = nullptr;
@@ -189,6 +192,8 @@ struct DeviceGuard {
 void free_workspace(sw_encoder* h) {
   (void)hipFree(h->d_scratch); (void)hipFree(h->d_res); (void)hipFree(h->d_pbits); (void)hipFree(h->d_edge); (void)hipFree(h->d_redo); (void)hipFree(h->d_pcount); (void)hipFree(h->d_part);
   (void)hipFree(h->d_ddfull); h->d_ddfull = nullptr;
+  (void)hipFree(h->d_llist); h->d_llist = nullptr;
+  (void)hipFree(h->d_lcount); h->d_lcount = nullptr;
   (void)hipFree(h->d_tile_slo); (void)hipFree(h->d_tile_sp); (void)hipFree(h->d_stamps);
   (void)hipFree(h->d_tile_slots); (void)hipFree(h->d_tile_nref); (void)hipFree(h->d_rlist); (void)hipFree(h->d_queue); (void)hipFree(h->d_bcnt); (void)hipFree(h->d_boff);
   (void)hipFree(h->d_qtotal);
@@ -294,6 +299,8 @@ int32_t ensure_workspace(sw_encoder* h, int64_t n_bytes) {
   HIP_TRY(hipMalloc(&h->d_redo, sizeof(int64_t) * (n_tiles + 1)));
   HIP_TRY(hipMalloc(&h->d_pcount, sizeof(unsigned long long)));
   HIP_TRY(hipMalloc(&h->d_ddfull, sizeof(unsigned long long)));
+  HIP_TRY(hipMalloc(&h->d_llist, sizeof(uint64_t) * (nb / (kShort + 1) + 64)));
+  HIP_TRY(hipMalloc(&h->d_lcount, sizeof(unsigned long long)));
   HIP_TRY(hipMemset(h->d_ddfull, 0, sizeof(unsigned long long)));
 #ifdef SW_STAMPS
   HIP_TRY(hipMalloc(&h->d_stamps, sizeof(unsigned long long) * 32 * 64));  // 64 copies per counter
@@ -518,6 +525,7 @@ extern "C" void sw_encoder_destroy(sw_encoder* h) {
       if (h->ev_join[k]) (void)hipEventDestroy(h->ev_join[k]);
     }
     if (h->ev_fork) (void)hipEventDestroy(h->ev_fork);
+    if (h->ev_fork_long) (void)hipEventDestroy(h->ev_fork_long);
     (void)hipFree(h->d_table);
     (void)hipFree(h->d_chunks);
     (void)hipFree(h->d_inv);
@@ -636,9 +644,14 @@ extern "C" int32_t sw_encoder_phase_cycles(sw_encoder* h, double* out32, int32_t
 namespace {
 // the long-chunk split + verify passes (long_split.h) on stream s: well-formed tables only
 template <bool kWide, bool k16>
-hipError_t launch_long_split(sw_encoder* h, hipStream_t s, const EncArgs& a) {
+hipError_t launch_long_split(sw_encoder* h, hipStream_t s, const EncArgs& a, int part) {
   LongArgs& L = h->lp;
   const dim3 g(kLpGrid), b(kThreads);
+  if (part == 2) {  // (the passes that write res, where k_classify's tile-local queue lives until k_scatter)
+    hipLaunchKernelGGL((k_lp_fallback<kWide, k16>), g, dim3(64), 0, s, a, L);
+    hipLaunchKernelGGL(k_lp_gather, g, b, 0, s, a, L);
+    return hipGetLastError();
+  }
   hipLaunchKernelGGL(k_dscan_reduce, dim3(kDscanGrid), b, 0, s, L.lnp, L.lcap, &L.ctl[kLcLong], h->d_lpart);
   hipLaunchKernelGGL(k_dscan_parts, dim3(1), dim3(kDscanGrid), 0, s, h->d_lpart, &L.ctl[kLcPieces]);
   hipLaunchKernelGGL(k_dscan_apply, dim3(kDscanGrid), b, 0, s, L.lnp, L.lcap, &L.ctl[kLcLong], h->d_lpart, L.lpo);
@@ -650,8 +663,6 @@ hipError_t launch_long_split(sw_encoder* h, hipStream_t s, const EncArgs& a) {
     hipLaunchKernelGGL((k_lp_bigwin<kWide, k16>), g, dim3(64), 0, s, a, L, r);
     hipLaunchKernelGGL((k_lp_junctions<kWide>), g, b, 0, s, a, L, r + 1);  // (r + 1 == kLpRounds: the final check)
   }
-  hipLaunchKernelGGL((k_lp_fallback<kWide, k16>), g, dim3(64), 0, s, a, L);
-  hipLaunchKernelGGL(k_lp_gather, g, b, 0, s, a, L);
   return hipGetLastError();
 }
 
@@ -660,20 +671,24 @@ hipError_t launch_long_split(sw_encoder* h, hipStream_t s, const EncArgs& a) {
 // (Started from the bitmap right after the pre-split, beside k_classify, they only slowed it
 // down by as much: both fill the chip.  They run beside the merge kernels, which leave it
 // mostly idle.)
+// part 1 right after k_classify (its long list and the complete bitmap); part 2, the passes that
+// write res, after k_scatter has consumed the tile-local queue aliased there (a.qtmp)
 template <bool kWide, bool k16>
-hipError_t launch_long(sw_encoder* h, hipStream_t s, const EncArgs& a, bool split) {
+hipError_t launch_long(sw_encoder* h, hipStream_t s, const EncArgs& a, bool split, int part) {
   constexpr unsigned kLongGrid = 32768;  // k_merge_long_lds: a workgroup per long chunk (grid-stride past that)
   LongArgs& L = h->lp;
-  hipError_t e = hipMemsetAsync(L.ctl, 0, sizeof(int64_t) * kLcAlloc, s);
-  if (e == hipSuccess) e = hipMemsetAsync(h->d_big, 0, sizeof(uint32_t), s);
-  if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(k_lp_prep, dim3(kLpPrepGrid), dim3(kThreads), 0, s, a, L, split ? (int64_t)kShort : INT64_MAX);
-  if (!split) {
+  if (part == 2) {
+    if (split) return launch_long_split<kWide, k16>(h, s, a, 2);
     hipLaunchKernelGGL((k_merge_long_lds<kWide, k16>), dim3(kLongGrid), dim3(64), 0, s, a);
     hipLaunchKernelGGL((k_merge_long<kWide>), dim3(512), dim3(kThreads), 0, s, a);  // (over kLongLds bytes)
     return hipGetLastError();
   }
-  e = launch_long_split<kWide, k16>(h, s, a);
+  hipError_t e = hipMemsetAsync(L.ctl, 0, sizeof(int64_t) * kLcAlloc, s);
+  if (e == hipSuccess) e = hipMemsetAsync(h->d_big, 0, sizeof(uint32_t), s);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(k_lp_prep, dim3(kLpPrepGrid), dim3(kThreads), 0, s, a, L, split ? (int64_t)kShort : INT64_MAX);
+  if (!split) return hipGetLastError();
+  e = launch_long_split<kWide, k16>(h, s, a, 1);
 #ifdef SW_LP_DEBUG
   if (e == hipSuccess && getenv("SW_LP_DEBUG")) {
     int64_t c[kLcAlloc];
@@ -753,11 +768,11 @@ int32_t encode_device(sw_encoder* h, const uint8_t* d_bytes, int64_t n_bytes, co
   }
   if (n_tiles > 0)  // (the pre-split and k_classify start from each tile's first string)
     hipLaunchKernelGGL(k_tile_strings, dim3((unsigned)((n_tiles + 255) / 256)), dim3(256), 0, st, d_str_off, n_str,
-                       n_tiles, h->d_tile_slo);
+                       n_tiles, h->d_tile_slo, h->d_lcount);  // (and the long list emptied)
   const SpArgs spa{sp.pos, sp.len, sp.id, sp.n, h->d_tile_sp};
   if (n_tiles > 0 && sp.n > 0)  // (... and their first special-token occurrence)
     hipLaunchKernelGGL(k_tile_strings, dim3((unsigned)((n_tiles + 255) / 256)), dim3(256), 0, st, sp.pos, sp.n,
-                       n_tiles, h->d_tile_sp);
+                       n_tiles, h->d_tile_sp, nullptr);
   // the full path (no caller bitmap): the device pre-split, fused into the classification
   // (k_edges + k_split_classify) or as its own kernel first (SW_OPT_FUSED_PRESPLIT 0; special
   // tokens always take the fused kernel)
@@ -778,6 +793,7 @@ int32_t encode_device(sw_encoder* h, const uint8_t* d_bytes, int64_t n_bytes, co
     a.dres = h->d_dres;
     a.dcnt = h->d_dcnt;
     a.dd_full = h->d_ddfull;
+    a.llist = h->d_llist; a.l_count = h->d_lcount;
     a.big_count = h->d_big; a.big_list = h->d_big + 1;
     a.out_off = d_out_off; a.tile_slo = h->d_tile_slo;
     a.n_tiles = n_tiles; a.qtmp = h->d_res; a.bcnt = h->d_bcnt; a.boff = h->d_boff; a.q_total = h->d_qtotal;
@@ -813,13 +829,12 @@ int32_t encode_device(sw_encoder* h, const uint8_t* d_bytes, int64_t n_bytes, co
       hipLaunchKernelGGL(k_classify<false>, dim3((unsigned)((n_tiles + kWaves - 1) / kWaves)), dim3(kThreads), 0, st, a);
     }
     HIP_TRY(hipGetLastError());
-    HIP_TRY(launch_scan(st, h->d_bcnt, kNumBuckets * n_tiles, h->d_part, h->d_boff, h->d_qtotal));
-    hipLaunchKernelGGL(k_scatter, dim3((unsigned)((n_tiles + 3) / 4)), dim3(kThreads), 0, st, a);
-    const dim3 pg(2048), pb(kThreads);  // persistent grid for the queue kernels
     // streams of the merge kernels: [0] buckets 17..32 B, then 5..8 B, [1] 9..16 B, then 2..4 B
-    // (balanced for the memo-off loads: 9.4 + 6.6 against 12.3 + 3.1 ms), [3] long.  (Two forks
-    // only: streams beyond the process's hardware queues (4) share one and run in launch order,
-    // which put the long chunks behind a bucket.)
+    // (balanced for the memo-off loads: 9.4 + 6.6 against 12.3 + 3.1 ms), [3] the long chunks,
+    // forked right here: they start from k_classify's long list and the complete bitmap, beside
+    // the scan and the scatter (C2: their ~20 small passes no longer outlast the merge kernels).
+    // (Two forks only: streams beyond the process's hardware queues (4) share one and run in
+    // launch order, which put the long chunks behind a bucket.)
     hipStream_t ms[4] = {st, st, st, st};
     if (h->merge_fork) {
       for (int k = 0; k < 2; ++k) {
@@ -827,14 +842,26 @@ int32_t encode_device(sw_encoder* h, const uint8_t* d_bytes, int64_t n_bytes, co
         if (!h->ev_join[k]) HIP_TRY(hipEventCreateWithFlags(&h->ev_join[k], hipEventDisableTiming));
       }
       if (!h->ev_fork) HIP_TRY(hipEventCreateWithFlags(&h->ev_fork, hipEventDisableTiming));
-      HIP_TRY(hipEventRecord(h->ev_fork, st));
-      for (int k = 0; k < 2; ++k) HIP_TRY(hipStreamWaitEvent(h->s_fork[k], h->ev_fork, 0));
+      if (!h->ev_fork_long) HIP_TRY(hipEventCreateWithFlags(&h->ev_fork_long, hipEventDisableTiming));
+      HIP_TRY(hipEventRecord(h->ev_fork_long, st));
+      HIP_TRY(hipStreamWaitEvent(h->s_fork[1], h->ev_fork_long, 0));
       ms[1] = h->s_fork[0];
       ms[3] = h->s_fork[1];
     }
-    if (h->table.wide) HIP_TRY((launch_long<true, false>(h, ms[3], a, split)));  // (the longest path: first)
-    else if (h->ids16) HIP_TRY((launch_long<false, true>(h, ms[3], a, split)));
-    else HIP_TRY((launch_long<false, false>(h, ms[3], a, split)));
+    auto long_part = [&](int part) -> hipError_t {
+      if (h->table.wide) return launch_long<true, false>(h, ms[3], a, split, part);
+      if (h->ids16) return launch_long<false, true>(h, ms[3], a, split, part);
+      return launch_long<false, false>(h, ms[3], a, split, part);
+    };
+    HIP_TRY(long_part(1));
+    HIP_TRY(launch_scan(st, h->d_bcnt, kNumBuckets * n_tiles, h->d_part, h->d_boff, h->d_qtotal));
+    hipLaunchKernelGGL(k_scatter, dim3((unsigned)((n_tiles + 15) / 16)), dim3(kThreads), 0, st, a);  // (4 tiles a wave)
+    const dim3 pg(2048), pb(kThreads);  // persistent grid for the queue kernels
+    if (h->merge_fork) {
+      HIP_TRY(hipEventRecord(h->ev_fork, st));
+      for (int k = 0; k < 2; ++k) HIP_TRY(hipStreamWaitEvent(h->s_fork[k], h->ev_fork, 0));
+    }
+    HIP_TRY(long_part(2));
     if (h->table.wide) {
       hipLaunchKernelGGL((k_merge_bucket<true, false, 32>), pg, pb, 0, ms[0], a, 8, 9);
       hipLaunchKernelGGL((k_merge_bucket<true, false, 16>), pg, pb, 0, ms[1], a, 5, 7);
@@ -1470,7 +1497,7 @@ extern "C" int32_t sw_presplit_device(sw_encoder* h, const uint8_t* d_bytes, int
   if (rc) return rc;
   if (n_bytes > 0)
     hipLaunchKernelGGL(k_tile_strings, dim3((unsigned)(((n_bytes + kTile - 1) / kTile + 255) / 256)), dim3(256), 0, st,
-                       d_str_off, n_str, (n_bytes + kTile - 1) / kTile, h->d_tile_slo);
+                       d_str_off, n_str, (n_bytes + kTile - 1) / kTile, h->d_tile_slo, nullptr);
   HIP_TRY(launch_presplit(st, d_bytes, n_bytes, d_str_off, n_str, pattern, d_chunk_bits, h->d_tile_slo));
   if (n_chunks_host) {
     *n_chunks_host = 0;

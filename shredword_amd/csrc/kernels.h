@@ -801,6 +801,10 @@ struct EncArgs {
   uint4* dres;               // [dmask + 1] dense result heads (slot_dref), by table entry
   uint8_t* dcnt;             // [dmask + 1] their id counts (<= 32): k_tile_count's reads stay in L2
   unsigned long long* dd_full;  // dedupable chunks of the launch that found no free candidate (k_scatter)
+  uint64_t* llist;           // chunks over kShort bytes, as k_classify finds them: start << 32 | length
+                             // (kNoDid: too long for the field, or running past its tile: k_lp_prep
+                             // finds the end in the bitmap); any order.  Count in *l_count
+  unsigned long long* l_count;  // (zeroed by k_tile_strings)
   unsigned long long* stamps;  // SW_STAMPS builds: cycles per phase, summed
   const uint2* inv;          // [n_inv] merge value -> its pair (a, b); well-formed tables only
   uint32_t n_inv;
@@ -1155,7 +1159,20 @@ __device__ __forceinline__ void classify_chunks(const EncArgs& a, int64_t tile, 
         SW_STNT2(&a.rlist[t0 + nref + lane], dd.kind ? (kRlDense | did) : (uint32_t)own);  // (act lanes are 0 .. n-1: coalesced)
       }
       nref += (int)__popcll(__ballot(act));
-      const bool queued = act && dd.kind != 2;
+      // chunks over kShort bytes go to the long list (the long-chunk passes start from it right
+      // after this kernel, beside the scan, the scatter and the merge kernels); the rest to the
+      // tile-local queue
+      const bool longc = act && len > kShort;
+      const uint64_t lm = __ballot(longc);
+      if (lm) {
+        unsigned long long lb = 0;
+        if (lane == 0) lb = atomicAdd(a.l_count, (unsigned long long)__popcll(lm));
+        lb = __shfl(lb, 0, 64);
+        if (longc)
+          a.llist[lb + __popcll(lm & lt_mask)] =
+              ((uint64_t)(t0 + ls) << 32) | (len < (int)kNoDid ? (uint32_t)len : kNoDid);
+      }
+      const bool queued = act && dd.kind != 2 && !longc;
       const int b = queued ? bucket_of(len) : 15;
       uint64_t pend = __ballot(queued);
       // tile-local queue entry (any order; k_scatter routes by length): chunk start in tile
@@ -1163,9 +1180,8 @@ __device__ __forceinline__ void classify_chunks(const EncArgs& a, int64_t tile, 
       // (or kNoDid) kTile / 2 entries on (a tile queues at most kTile / 2 chunks of >= 2 bytes)
       if (queued) {
         const int64_t qi = t0 + nown + __popcll(pend & lt_mask);
-        SW_STNT2(&a.qtmp[qi], (uint32_t)ls | ((uint32_t)k << kTileBits) | ((uint32_t)(len <= kShort ? len : 0) << (2 * kTileBits)));
-        // (a long chunk has no dense result: the field carries its length, kNoDid if too long)
-        SW_STNT2(&a.qtmp[qi + kTile / 2], len > kShort ? (len < (int)kNoDid ? (uint32_t)len : kNoDid) : did);
+        SW_STNT2(&a.qtmp[qi], (uint32_t)ls | ((uint32_t)k << kTileBits) | ((uint32_t)len << (2 * kTileBits)));
+        SW_STNT2(&a.qtmp[qi + kTile / 2], did);
       }
       nown += __popcll(pend);
       while (pend) {  // one ballot per bucket present
@@ -1219,26 +1235,32 @@ __global__ void __launch_bounds__(kThreads) SW_CLS_ATTR k_classify(EncArgs a) {
 // k_scatter: tile-local queue entries -> the dense bucket-major queue
 // ---------------------------------------------------------------------------------------
 __global__ void __launch_bounds__(kThreads) k_scatter(EncArgs a) {
-  // one wave per tile: lane b < kNumBuckets holds (count, next destination) of bucket b; the
-  // tile's entries (any order) are routed 64 at a time, one ballot per bucket present
-  const int64_t t = ((int64_t)blockIdx.x * kWaves + wave_in_block());
-  const int lane = threadIdx.x & 63;
-  if (t >= a.n_tiles) return;
+  // four tiles per wave, one 16-lane group each (a tile queues ~1.4 chunks on C2: a wave per tile
+  // spent its life on two dependent loads): lane b < kNumBuckets of a group holds (count, next
+  // destination) of bucket b; the tile's entries (any order) are routed 16 at a time, one ballot
+  // per bucket present in each group (the groups side by side)
+  constexpr int kG = 16;
+  const int lane = threadIdx.x & 63, g = lane >> 4, gl = lane & (kG - 1);
+  const int64_t t = ((int64_t)blockIdx.x * kWaves + wave_in_block()) * (64 / kG) + g;
+  const bool tile_ok = t < a.n_tiles;
   const uint64_t lt_mask = (lane == 0) ? 0ULL : (~0ULL >> (64 - lane));
+  const uint64_t gmask = 0xFFFFULL << (kG * g);
   const int64_t t0 = t * kTile;
   uint32_t c = 0;
   int64_t dst = 0;
-  if (lane < kNumBuckets) {
-    c = a.bcnt[(int64_t)lane * a.n_tiles + t];
-    dst = a.boff[(int64_t)lane * a.n_tiles + t];
+  if (tile_ok && gl < kNumBuckets) {
+    c = a.bcnt[(int64_t)gl * a.n_tiles + t];
+    dst = a.boff[(int64_t)gl * a.n_tiles + t];
   }
   uint32_t n = c;
 #pragma unroll
-  for (int off = 1; off < 16; off <<= 1) n += __shfl_xor(n, off, 64);  // lanes 0..15: total
-  n = (uint32_t)__shfl((int)n, 0, 64);
-  for (uint32_t i0 = 0; i0 < n; i0 += 64) {
-    const uint32_t i = i0 + lane;
-    const bool act = i < n;
+  for (int off = 1; off < kG; off <<= 1) n += __shfl_xor(n, off, 64);  // (the group's total, in every lane of it)
+  uint32_t n_max = n;
+#pragma unroll
+  for (int off = kG; off < 64; off <<= 1) n_max = max(n_max, (uint32_t)__shfl_xor((int)n_max, off, 64));
+  for (uint32_t i0 = 0; i0 < n_max; i0 += kG) {
+    const uint32_t i = i0 + gl;
+    const bool act = tile_ok && i < n;
     const uint32_t e = act ? SW_LDNT2(&a.qtmp[t0 + i]) : 0u;
     const uint32_t did = act ? SW_LDNT2(&a.qtmp[t0 + kTile / 2 + i]) : kNoDid;
     const uint32_t ns = e >> (2 * kTileBits);
@@ -1250,11 +1272,12 @@ __global__ void __launch_bounds__(kThreads) k_scatter(EncArgs a) {
     int64_t d = 0;
     uint64_t pend = __ballot(act);
     while (pend) {
-      const int bb = __shfl(b, __ffsll((long long)pend) - 1, 64);
-      const uint64_t m = __ballot(b == bb);
-      const int64_t db = __shfl(dst, bb, 64);
-      if (b == bb) d = db + __popcll(m & lt_mask);
-      if (lane == bb) dst += __popcll(m);
+      const uint64_t pg = pend & gmask;  // (this lane's group: its first pending lane's bucket)
+      const int bb = pg ? __shfl(b, __ffsll((long long)pg) - 1, 64) : -1;
+      const uint64_t m = __ballot(act && b == bb && ((pend >> lane) & 1));
+      const int64_t db = __shfl(dst, kG * g + (bb < 0 ? 0 : bb), 64);
+      if (act && b == bb && ((pend >> lane) & 1)) d = db + __popcll(m & gmask & lt_mask);
+      if (gl == bb) dst += __popcll(m & gmask);
       pend &= ~m;
     }
     if (act) {
@@ -1811,8 +1834,11 @@ __global__ void __launch_bounds__(kThreads) k_merge_long(EncArgs a) {
 }
 
 // first string starting at or after each tile's first byte (binary search per tile)
-__global__ void k_tile_strings(const int64_t* str_off, int64_t n_str, int64_t n_tiles, int64_t* tile_slo) {
+// (zero: a launch's counter to clear before its k_classify, or NULL)
+__global__ void k_tile_strings(const int64_t* str_off, int64_t n_str, int64_t n_tiles, int64_t* tile_slo,
+                               unsigned long long* zero) {
   const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t == 0 && zero) *zero = 0;
   if (t >= n_tiles) return;
   const int64_t t0 = t * kTile;
   int64_t lo = 0, hi = n_str;
@@ -2033,7 +2059,10 @@ __device__ __forceinline__ uint32_t ref_count(const EncArgs& a, uint32_t r) {
 // k_tile_count: kTcTiles tiles per wave, their first 64 list entries and sizes loaded together,
 // then their counts: one dependent round trip serves kTcTiles tiles (a tile holds ~58
 // references on prose, so one wave per tile spent most of its life waiting)
-constexpr int kTcTiles = 2;
+#ifndef SW_TC_TILES
+#define SW_TC_TILES 4
+#endif
+constexpr int kTcTiles = SW_TC_TILES;
 __global__ void __launch_bounds__(kThreads) k_tile_count(EncArgs a) {
   const int64_t tb = (((int64_t)blockIdx.x * kWaves + wave_in_block())) * kTcTiles;
   const int lane = threadIdx.x & 63;

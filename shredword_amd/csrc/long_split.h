@@ -6,7 +6,7 @@
 // ranks highest) and ALL pieces of ALL long chunks are then processed side by side, one lane
 // per piece, by a handful of grid-wide passes -- no chunk is walked by one wave, so a 1 MiB
 // letter run costs as many passes as a 40-byte one:
-//   k_lp_prep       the long chunks (the queue's long bucket): start, length, piece count
+//   k_lp_prep       the long chunks (k_classify's long list): start, length, piece count
 //   (scan)          piece offsets of the chunks
 //   k_lp_fill       every piece's chunk (one wave per chunk)
 //   k_lp_encode     every piece's cuts (where the byte pair ranks highest), the piece encoded
@@ -116,16 +116,14 @@ __device__ __forceinline__ void lp_fall(const LongArgs& L, uint32_t i) {
 __global__ void __launch_bounds__(kThreads) k_lp_prep(EncArgs a, LongArgs L, int64_t lp_min) {
   const int lane = threadIdx.x & 63;
   const uint64_t lt_mask = (lane == 0) ? 0ULL : (~0ULL >> (64 - lane));
-  int64_t lo, hi;
-  bucket_range(a, kLongBucket, kLongBucket, &lo, &hi);
-  const int64_t n = hi - lo, stride = (int64_t)gridDim.x * kThreads;
+  const int64_t n = (int64_t)*a.l_count, stride = (int64_t)gridDim.x * kThreads;
   for (int64_t t0 = (int64_t)blockIdx.x * kThreads + (threadIdx.x & ~63); t0 < n; t0 += stride) {  // (whole waves)
     const int64_t t = t0 + lane;
     int64_t start = 0, len = 0;
     if (t < n) {
-      const uint64_t e = a.queue[lo + t];
-      start = (int64_t)(e >> 33);
-      const uint32_t ql = (uint32_t)e & kNoDid;  // (the length, from k_classify)
+      const uint64_t e = a.llist[t];
+      start = (int64_t)(e >> 32);
+      const uint32_t ql = (uint32_t)e;  // (the length, from k_classify)
       len = ql != kNoDid ? (int64_t)ql : next_set_bit(a.bits, a.n_words, start + 1, a.n_bytes) - start;
     }
     const uint64_t mw = __ballot(t < n && len <= lp_min), ml = __ballot(t < n && len > lp_min);

@@ -1234,18 +1234,49 @@ __global__ void __launch_bounds__(kThreads) SW_CLS_ATTR k_classify(EncArgs a) {
 // ---------------------------------------------------------------------------------------
 // k_scatter: tile-local queue entries -> the dense bucket-major queue
 // ---------------------------------------------------------------------------------------
+// one round of k_scatter's routing: lanes with act hold a tile-local entry (e, did); lanes of a
+// group of kG lanes serve one tile, whose lane b < kNumBuckets holds bucket b's next destination
+// (dst); one ballot per bucket present in each group, the groups side by side
+template <int kG>
+__device__ __forceinline__ void scatter_round(const EncArgs& a, int64_t t0, bool act, uint32_t e, uint32_t did,
+                                              int64_t& dst) {
+  const int lane = threadIdx.x & 63, g = lane / kG;
+  const uint64_t lt_mask = (lane == 0) ? 0ULL : (~0ULL >> (64 - lane));
+  const uint64_t gmask = (kG == 64 ? ~0ULL : ((1ULL << kG) - 1ULL)) << (kG * g);
+  const uint32_t ns = e >> (2 * kTileBits);
+  const int b = act ? (ns ? bucket_of(ns) : kLongBucket) : 15;
+  if (a.dedupe) {  // (a dedupable chunk queued without an entry: its table line was full, see grow_dedupe)
+    const uint64_t full = __ballot(act && ns != 0 && did == kNoDid);
+    if (full && lane == 0) atomicAdd(a.dd_full, (unsigned long long)__popcll(full));
+  }
+  int64_t d = 0;
+  uint64_t pend = __ballot(act);
+  while (pend) {
+    const uint64_t pg = pend & gmask;  // (this lane's group: its first pending lane's bucket)
+    const int bb = pg ? __shfl(b, __ffsll((long long)pg) - 1, 64) : -1;
+    const bool mine = act && b == bb && ((pend >> lane) & 1);
+    const uint64_t m = __ballot(mine);
+    const int64_t db = __shfl(dst, kG * g + (bb < 0 ? 0 : bb), 64);
+    if (mine) d = db + __popcll(m & gmask & lt_mask);
+    if (lane - kG * g == bb) dst += __popcll(m & gmask);
+    pend &= ~m;
+  }
+  if (act) {
+    const uint64_t start = (uint64_t)(t0 + (e & (kTile - 1)));
+    a.queue[d] = (start << 33) | ((uint64_t)ns << 27) | did;
+  }
+}
+
 __global__ void __launch_bounds__(kThreads) k_scatter(EncArgs a) {
-  // four tiles per wave, one 16-lane group each (a tile queues ~1.4 chunks on C2: a wave per tile
-  // spent its life on two dependent loads): lane b < kNumBuckets of a group holds (count, next
-  // destination) of bucket b; the tile's entries (any order) are routed 16 at a time, one ballot
-  // per bucket present in each group (the groups side by side)
+  // four tiles per wave, their bucket counts in one load: a tile that queued <= 16 chunks (C2: ~1.4
+  // on average; a wave per tile spent its life on two dependent loads) is routed by its 16-lane
+  // group, the four side by side; a larger tile (every chunk queued: the memo-off runs) by the
+  // whole wave, 64 entries a round, after them
   constexpr int kG = 16;
   const int lane = threadIdx.x & 63, g = lane >> 4, gl = lane & (kG - 1);
-  const int64_t t = ((int64_t)blockIdx.x * kWaves + wave_in_block()) * (64 / kG) + g;
+  const int64_t tb = ((int64_t)blockIdx.x * kWaves + wave_in_block()) * (64 / kG);
+  const int64_t t = tb + g;
   const bool tile_ok = t < a.n_tiles;
-  const uint64_t lt_mask = (lane == 0) ? 0ULL : (~0ULL >> (64 - lane));
-  const uint64_t gmask = 0xFFFFULL << (kG * g);
-  const int64_t t0 = t * kTile;
   uint32_t c = 0;
   int64_t dst = 0;
   if (tile_ok && gl < kNumBuckets) {
@@ -1255,34 +1286,23 @@ __global__ void __launch_bounds__(kThreads) k_scatter(EncArgs a) {
   uint32_t n = c;
 #pragma unroll
   for (int off = 1; off < kG; off <<= 1) n += __shfl_xor(n, off, 64);  // (the group's total, in every lane of it)
-  uint32_t n_max = n;
-#pragma unroll
-  for (int off = kG; off < 64; off <<= 1) n_max = max(n_max, (uint32_t)__shfl_xor((int)n_max, off, 64));
-  for (uint32_t i0 = 0; i0 < n_max; i0 += kG) {
-    const uint32_t i = i0 + gl;
-    const bool act = tile_ok && i < n;
-    const uint32_t e = act ? SW_LDNT2(&a.qtmp[t0 + i]) : 0u;
-    const uint32_t did = act ? SW_LDNT2(&a.qtmp[t0 + kTile / 2 + i]) : kNoDid;
-    const uint32_t ns = e >> (2 * kTileBits);
-    const int b = act ? (ns ? bucket_of(ns) : kLongBucket) : 15;
-    if (a.dedupe) {  // (a dedupable chunk queued without an entry: its table line was full, see grow_dedupe)
-      const uint64_t full = __ballot(act && ns != 0 && did == kNoDid);
-      if (full && lane == 0) atomicAdd(a.dd_full, (unsigned long long)__popcll(full));
-    }
-    int64_t d = 0;
-    uint64_t pend = __ballot(act);
-    while (pend) {
-      const uint64_t pg = pend & gmask;  // (this lane's group: its first pending lane's bucket)
-      const int bb = pg ? __shfl(b, __ffsll((long long)pg) - 1, 64) : -1;
-      const uint64_t m = __ballot(act && b == bb && ((pend >> lane) & 1));
-      const int64_t db = __shfl(dst, kG * g + (bb < 0 ? 0 : bb), 64);
-      if (act && b == bb && ((pend >> lane) & 1)) d = db + __popcll(m & gmask & lt_mask);
-      if (gl == bb) dst += __popcll(m & gmask);
-      pend &= ~m;
-    }
-    if (act) {
-      const uint64_t start = (uint64_t)(t0 + (e & (kTile - 1)));
-      a.queue[d] = (start << 33) | ((uint64_t)ns << 27) | did;
+  {  // the small tiles, side by side
+    const bool act = tile_ok && n <= (uint32_t)kG && (uint32_t)gl < n;
+    const uint32_t e = act ? SW_LDNT2(&a.qtmp[t * kTile + gl]) : 0u;
+    const uint32_t did = act ? SW_LDNT2(&a.qtmp[t * kTile + kTile / 2 + gl]) : kNoDid;
+    scatter_round<kG>(a, t * kTile, act, e, did, dst);
+  }
+  for (int q = 0; q < 64 / kG; ++q) {  // the large ones, one by one (wave-uniform)
+    const uint32_t nq = (uint32_t)__shfl((int)n, kG * q, 64);
+    if (nq <= (uint32_t)kG) continue;
+    const int64_t tq = tb + q, tq0 = tq * kTile;
+    int64_t dq = __shfl(dst, kG * q + (lane < kNumBuckets ? lane : 0), 64);  // (lane b: bucket b)
+    for (uint32_t i0 = 0; i0 < nq; i0 += 64) {
+      const uint32_t i = i0 + lane;
+      const bool act = i < nq;
+      const uint32_t e = act ? SW_LDNT2(&a.qtmp[tq0 + i]) : 0u;
+      const uint32_t did = act ? SW_LDNT2(&a.qtmp[tq0 + kTile / 2 + i]) : kNoDid;
+      scatter_round<64>(a, tq0, act, e, did, dq);
     }
   }
 }
@@ -2059,10 +2079,7 @@ __device__ __forceinline__ uint32_t ref_count(const EncArgs& a, uint32_t r) {
 // k_tile_count: kTcTiles tiles per wave, their first 64 list entries and sizes loaded together,
 // then their counts: one dependent round trip serves kTcTiles tiles (a tile holds ~58
 // references on prose, so one wave per tile spent most of its life waiting)
-#ifndef SW_TC_TILES
-#define SW_TC_TILES 4
-#endif
-constexpr int kTcTiles = SW_TC_TILES;
+constexpr int kTcTiles = 2;  // (4: no faster, r4s)
 __global__ void __launch_bounds__(kThreads) k_tile_count(EncArgs a) {
   const int64_t tb = (((int64_t)blockIdx.x * kWaves + wave_in_block())) * kTcTiles;
   const int lane = threadIdx.x & 63;

@@ -109,34 +109,10 @@ SW_HD inline int fast_class(uint32_t cp) {
   return L ? kL : in(cp, 0x1F10D, 0x1FBEF) ? kOther : -1;
 }
 
-// One non-ASCII lead byte at byte k (< 36) of the 40 (strict UTF-8: no overlongs, surrogates or
-// code points past U+10FFFF, continuation bytes 0x80..0xBF, not crossing a string start): its
-// continuation bytes as bits of the 40 (*tail_out; 0 if the sequence is invalid), and its code
-// point (kInvalidCp: invalid, or a lead before the chunk, k < 4, which needs no class)
-template <class Bytes>
-SW_HD inline uint32_t utf8_lead(const Bytes& by, uint64_t ss, int k, uint64_t* tail_out) {
-  const uint32_t b4 = by.at4(k), c0 = b4 & 0xFFu, c1 = (b4 >> 8) & 0xFFu;
-  const int n = c0 >= 0xF0 ? 4 : c0 >= 0xE0 ? 3 : 2;
-  const uint64_t tail = ((1ULL << (n - 1)) - 1ULL) << (k + 1);
-  const uint32_t cm = n == 2 ? 0xC000u : n == 3 ? 0xC0C000u : 0xC0C0C000u;  // (bytes k + 1 .. k + n - 1
-  const uint32_t cv = n == 2 ? 0x8000u : n == 3 ? 0x808000u : 0x80808000u;  //  are 10xxxxxx)
-  bool ok = (b4 & cm) == cv && (ss & tail) == 0 && c0 >= 0xC2 && c0 <= 0xF4;
-  ok = ok && !(c0 == 0xE0 && c1 < 0xA0) && !(c0 == 0xED && c1 > 0x9F) && !(c0 == 0xF0 && c1 < 0x90) &&
-       !(c0 == 0xF4 && c1 > 0x8F);
-  *tail_out = ok ? tail : 0ULL;
-  if (!ok || k < 4) return kInvalidCp;
-  uint32_t v = c0 & (n == 2 ? 0x1Fu : n == 3 ? 0x0Fu : 0x07u);
-  for (int q = 1; q < n; ++q) v = (v << 6) | ((b4 >> (8 * q)) & 0x3Fu);
-  return v;
-}
-
 // Bytes: word(i) = bytes [pos - 4 + 4i, pos + 4i) as a little-endian word (i < 10); at4(k) = the
 // bytes k .. k + 3 of those 40 (k <= 36).
-// kDefer: the non-ASCII leads are left out (their X tails and class bits: utf8_lead + fast_class /
-// cls, which the caller applies, as k_split_classify does for the whole wave at once) and
-// returned as bits of the 40 in *leads_out
-template <class Cls, class Bytes, bool kDefer = false>
-SW_HD inline Masks classify(const Bytes& by, uint64_t ss, const Cls& cls, bool cl, uint64_t* leads_out = nullptr) {
+template <class Cls, class Bytes>
+SW_HD inline Masks classify(const Bytes& by, uint64_t ss, const Cls& cls, bool cl) {
   // ASCII classes of the chunk's bytes (words 1..8)
   uint32_t L = 0, N = 0, C = 0, P = 0, H = 0, A = 0;
 #pragma unroll
@@ -151,39 +127,53 @@ SW_HD inline Masks classify(const Bytes& by, uint64_t ss, const Cls& cls, bool c
     P |= mm4(in7(x7, ' ', ' ') & asc) << s;
     A |= mm4(in7(x7, '\'', '\'') & asc) << s;
   }
-  // UTF-8: every lead byte of [pos - 4, pos + 32) checked on its own (utf8_lead); the
-  // continuation bytes of the valid ones make X, and the chunk's non-ASCII code points get their
-  // class
+  // UTF-8: every lead byte of [pos - 4, pos + 32) checked on its own (strict: no overlongs,
+  // surrogates or code points past U+10FFFF, not crossing a string start); the continuation
+  // bytes of the valid ones make X, and the chunk's non-ASCII code points get their class
   uint64_t X = 0;
   uint64_t hi40 = 0, ct40 = 0;
 #pragma unroll
   for (int i = 0; i < 10; ++i) hi40 |= (uint64_t)mm4(by.word(i)) << (4 * i);
-  uint64_t leads = 0;
   if (hi40) {
 #pragma unroll
     for (int i = 0; i < 10; ++i) {
       const uint32_t x = by.word(i), h7 = (x ^ kLane7) & kLow7;  // (bytes >= 0x80, less 0x80)
       ct40 |= (uint64_t)mm4(in7(h7, 0x00, 0x3F) & x & kLane7) << (4 * i);
     }
-    leads = hi40 & ~ct40 & 0xFFFFFFFFFULL;
-  }
-  if constexpr (kDefer) {
-    *leads_out = leads;
-  } else {
-    for (uint64_t m = leads; m; m &= m - 1) {
+    // one lead: its continuation bytes (0 if invalid), its code point (kInvalidCp if it needs
+    // no class: invalid, or before the chunk)
+    auto lead = [&](int k, uint64_t* tail_out) -> uint32_t {
+      const uint32_t b4 = by.at4(k), c0 = b4 & 0xFFu, c1 = (b4 >> 8) & 0xFFu;
+      const int n = c0 >= 0xF0 ? 4 : c0 >= 0xE0 ? 3 : 2;
+      const uint64_t tail = ((1ULL << (n - 1)) - 1ULL) << (k + 1);
+      bool ok = (ct40 & tail) == tail && (ss & tail) == 0 && c0 >= 0xC2 && c0 <= 0xF4;
+      ok = ok && !(c0 == 0xE0 && c1 < 0xA0) && !(c0 == 0xED && c1 > 0x9F) && !(c0 == 0xF0 && c1 < 0x90) &&
+           !(c0 == 0xF4 && c1 > 0x8F);
+      *tail_out = ok ? tail : 0ULL;
+      if (!ok || k < 4) return kInvalidCp;
+      uint32_t v = c0 & (n == 2 ? 0x1Fu : n == 3 ? 0x0Fu : 0x07u);
+      for (int q = 1; q < n; ++q) v = (v << 6) | ((b4 >> (8 * q)) & 0x3Fu);
+      return v;
+    };
+    // (selects, not an if-chain: the compiler turned the chain into a scratch array of {L, N, H}
+    // indexed by the class -- a scratch load + store, i.e. a memory round trip, per lead)
+    auto apply = [&](int k, uint32_t v, int c) {
+      const uint32_t bit = v == kInvalidCp ? 0u : 1u << (k - 4);
+      L |= c == kL ? bit : 0u;
+      N |= c == kN ? bit : 0u;
+      H |= c == kS ? bit : 0u;
+    };
+    // (a lane loops over its own leads: spreading a tile's leads over the wave's lanes through LDS
+    // made k_split_classify slower, 3.01 -> 3.12 ms; two leads per step 1-2% slower, r4 A/B)
+    for (uint64_t m = hi40 & ~ct40 & 0xFFFFFFFFFULL; m; m &= m - 1) {
       const int k = __builtin_ctzll(m);
       uint64_t t;
-      const uint32_t v = utf8_lead(by, ss, k, &t);
+      const uint32_t v = lead(k, &t);
       X |= t;
       if (v != kInvalidCp) {
         int c = fast_class(v);
         if (c < 0) c = cls(v);
-        // (selects, not an if-chain: the compiler turned the chain into a scratch array of
-        // {L, N, H} indexed by the class -- a scratch load + store per lead)
-        const uint32_t bit = 1u << (k - 4);
-        L |= c == kL ? bit : 0u;
-        N |= c == kN ? bit : 0u;
-        H |= c == kS ? bit : 0u;
+        apply(k, v, c);
       }
     }
   }

@@ -252,19 +252,16 @@ constexpr int kScPre = 32;                         // bytes staged before the ti
 constexpr int kScWinWords = (kScPre + kWin) / 4 + 8;  // [t0 - 32, t0 + kWin) + a zero tail
 constexpr int kScSsPre = 64;                       // string-start bits staged from t0 - 64 ...
 constexpr int kScSsWords = (kScSsPre + kTile + 128) / 32;  // ... to t0 + kTile + 128
-constexpr int kLeadCap = 592;                      // the wave's non-ASCII leads, spread over its lanes
 struct ScMasks {
   uint32_t m[9][66];       // class masks: chunk c0 + j at column j + 1; column 0 zeros (lane 0's left
                            // neighbour, unused: k_edges has its word), column 65 the next tile's first
   uint32_t ss[kScSsWords]; // string starts
   uint32_t in[64];         // bytes inside special-token occurrences (lane l: bits 32 l ..), if any
-  uint16_t lq[kLeadCap];   // the tile's non-ASCII leads: lane << 6 | byte of the lane's 40
 };
 union ScShared {           // the masks are dead once the tile's chunk starts are known
   ScMasks pre;
   uint16_t cstart[kTile + 2];
 };
-static_assert(sizeof(ScMasks) <= sizeof(uint16_t) * (kTile + 2), "the lead list fits beside the masks");
 
 // psb::carries' view inside k_split_classify: the tile's masks from LDS, the rest from global memory
 struct FSrc {
@@ -366,10 +363,10 @@ __device__ __forceinline__ void split_classify_tile(const EncArgs& a, const PbAr
   }
   if (lane < 8) s_win[(kScPre + kWin) / 4 + lane] = 0;
   const uint32_t r0 = edge[9 * stride + tile], r_next = edge[9 * stride + tile + 1];
+  const int64_t s_first = a.tile_slo[tile];
   ScMasks& sm = sh->pre;
   if (lane < 9) sm.m[lane][65] = edge[lane * stride + tile + 1];  // (k_edges: the next tile's first chunk)
   else if (lane < 18) sm.m[lane - 9][0] = 0u;
-  const int64_t s_first = a.tile_slo[tile];
   // 2. string starts of [t0 - kScSsPre, t0 + kTile + 128) (the batch end, str_off[n_str], included)
   for (int i = lane; i < kScSsWords; i += 64) sm.ss[i] = 0;
   wave_sync_mem();
@@ -423,54 +420,15 @@ __device__ __forceinline__ void split_classify_tile(const EncArgs& a, const PbAr
   } else {
     {
       psb::Masks m1{};
-      uint64_t leads = 0;  // (bits of the lane's 40 bytes: its non-ASCII leads, applied below)
       if (c < n_chunks) {
         const LdsBytes by{s_win + (kScPre / 4 - 1) + 8 * lane};  // bytes [t0 + 32 lane - 4, +40)
         const int64_t p = 32 * c;
         const uint64_t s = (uint64_t)src.ss_at(p - 4) | ((uint64_t)(src.ss_at(p + 28) & 0xFFu) << 32);
-        m1 = psb::classify<UcdClass, LdsBytes, true>(by, s, UcdClass{}, cl, &leads);
+        m1 = psb::classify(by, s, UcdClass{}, cl);
       }
       const int k = lane + 1;
       sm.m[0][k] = m1.L; sm.m[1][k] = m1.N; sm.m[2][k] = m1.C; sm.m[3][k] = m1.P; sm.m[4][k] = m1.H;
       sm.m[5][k] = m1.A; sm.m[6][k] = m1.X; sm.m[7][k] = m1.K1; sm.m[8][k] = m1.K2;
-      // the non-ASCII leads (UTF-8 checks, code point, class): the whole wave's leads spread over
-      // its lanes -- a lane's own 32 bytes hold 0 to 16 of them, and a lane loop over its own
-      // would keep the wave for its busiest lane (a CJK word beside ASCII); a lead's bits go into
-      // its chunk's LDS masks (atomic OR: several lanes may serve one chunk).  A tile with more
-      // leads than the list holds (CJK-dense: every lane busy anyway) keeps the lane loop.
-      const uint32_t nl = (uint32_t)__popcll(leads);
-      const uint32_t incl = wave_incl_scan(nl, lane), total = (uint32_t)__shfl((int)incl, 63, 64);
-      const bool spread = total <= (uint32_t)kLeadCap;
-      if (spread) {
-        uint32_t q = incl - nl;
-        for (uint64_t m = leads; m; m &= m - 1) sm.lq[q++] = (uint16_t)((lane << 6) | __builtin_ctzll(m));
-      }
-      wave_sync_mem();
-      auto apply_lead = [&](int ow, int kk) {  // lead kk of lane ow's 40 bytes
-        const LdsBytes ob{s_win + (kScPre / 4 - 1) + 8 * ow};
-        const int64_t op = 32 * (c0 + ow);
-        const uint64_t os = (uint64_t)src.ss_at(op - 4) | ((uint64_t)(src.ss_at(op + 28) & 0xFFu) << 32);
-        uint64_t t;
-        const uint32_t v = psb::utf8_lead(ob, os, kk, &t);
-        const uint32_t xb = (uint32_t)(t >> 4);
-        if (xb) atomicOr(&sm.m[6][ow + 1], xb);
-        if (v != kInvalidCp) {
-          int cc = psb::fast_class(v);
-          if (cc < 0) cc = UcdClass{}(v);
-          const int row = cc == kL ? 0 : cc == kN ? 1 : cc == kS ? 4 : -1;
-          if (row >= 0) atomicOr(&sm.m[row][ow + 1], 1u << (kk - 4));
-        }
-      };
-      if (spread) {
-        for (uint32_t i0 = 0; i0 < total; i0 += 64) {
-          if (i0 + lane < total) {
-            const uint32_t e = sm.lq[i0 + lane];
-            apply_lead((int)(e >> 6), (int)(e & 63));
-          }
-        }
-      } else {
-        for (uint64_t m = leads; m; m &= m - 1) apply_lead(lane, __builtin_ctzll(m));
-      }
     }
     wave_sync_mem();
     SW_STAMP(13);

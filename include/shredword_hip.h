@@ -83,6 +83,17 @@ void sw_encoder_destroy(sw_encoder* h);
  * encode grows it on demand otherwise). */
 int32_t sw_encoder_reserve(sw_encoder* h, int64_t max_bytes, int64_t max_strings);
 
+/* Pin (page-lock and map for the device) a caller's host buffer that it passes to sw_encode_batch
+ * call after call (no reference counterpart: the reference has no device path).  A batch whose
+ * input bytes lie inside a pinned range is read straight over PCIe (no staging copy on the host);
+ * a batch whose out_ids [out_cap] and out_off [n_str + 1] both lie inside pinned ranges gets its
+ * ids (int32) and string offsets written there by the device (no copy or widening pass on the
+ * host).  Results are the same either way.  A range stays pinned until sw_encoder_unpin_host(ptr)
+ * or sw_encoder_destroy; the caller keeps it alive that long.  SW_ERR_HIP if the runtime refuses
+ * the range, SW_ERR_ARG for an unknown ptr. */
+int32_t sw_encoder_pin_host(sw_encoder* h, void* ptr, int64_t bytes);
+int32_t sw_encoder_unpin_host(sw_encoder* h, void* ptr);
+
 /* Encoder options (sw_encoder_set_option).
  *   SW_OPT_CHUNK_TABLE  1 (default): a chunk of 2..16 bytes that encodes to exactly one token is
  *                       answered from a table built at creation (the vocabulary's byte strings
@@ -118,7 +129,7 @@ int32_t sw_encoder_reserve(sw_encoder* h, int64_t max_bytes, int64_t max_strings
  *                          value >= 64) */
 #define SW_OPT_LONG_SPLIT 7
 #define SW_OPT_MAX_LAUNCH_BYTES 8
-/*   SW_OPT_PIPE_RUN_BYTES  sw_encode_batch of more than 2 runs of this many bytes (default 64 MiB; 0:
+/*   SW_OPT_PIPE_RUN_BYTES  sw_encode_batch of more than 2 runs of this many bytes (default 128 MiB; 0:
  *                          never) pipelines runs of whole strings: pinned staging copied by a pool of
  *                          host threads, uploads, encodes and downloads of consecutive runs
  *                          overlapping, ids downloaded as 16 bits when every id fits */

@@ -94,6 +94,8 @@ _SIGNATURES = {
     "sw_encoder_create": (c_int32, [POINTER(c_int32), POINTER(c_int32), c_int64, c_int32, POINTER(c_void_p)]),
     "sw_encoder_destroy": (None, [c_void_p]),
     "sw_encoder_reserve": (c_int32, [c_void_p, c_int64, c_int64]),
+    "sw_encoder_pin_host": (c_int32, [c_void_p, c_void_p, c_int64]),
+    "sw_encoder_unpin_host": (c_int32, [c_void_p, c_void_p]),
     "sw_presplit_host": (c_int64, [POINTER(c_uint8), POINTER(c_int64), c_int64, c_int32, POINTER(c_uint64), c_int32]),
     "sw_encode_batch": (c_int32, [c_void_p, POINTER(c_uint8), POINTER(c_int64), c_int64, c_int32,
                                   POINTER(c_uint64), POINTER(c_int32), c_int64, POINTER(c_int64),

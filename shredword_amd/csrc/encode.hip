@@ -20,6 +20,7 @@
 //   k_compact        slots -> contiguous ids; string chunk index -> id offset
 //   k_string_offsets final per-string offsets
 #include <hip/hip_runtime.h>
+#include <immintrin.h>
 
 #include <algorithm>
 #include <chrono>
@@ -92,6 +93,19 @@ struct sw_encoder {
   // sw_encode_batch's pipeline for large host batches (SW_OPT_PIPE_RUN_BYTES): runs of whole
   // strings go host -> pinned -> device -> encode -> (16-bit ids when they fit) -> pinned -> host,
   // run k's copies overlapping run k-1's encode; two slots of buffers
+  struct Pinned {                     // sw_encoder_pin_host: a caller's range and its device address
+    char* h = nullptr;
+    int64_t n = 0;
+    char* d = nullptr;
+  };
+  std::vector<Pinned> pins;
+  int64_t* d_done = nullptr;          // the direct push (pinned caller arrays): ids written so far, overflow flag
+  // (device address of [p, p + n) when it lies in a pinned range, else nullptr)
+  void* pinned_dev(const void* p, int64_t n) const {
+    for (const Pinned& r : pins)
+      if ((const char*)p >= r.h && (const char*)p + n <= r.h + r.n) return r.d + ((const char*)p - r.h);
+    return nullptr;
+  }
   struct PipeSlot {
     uint8_t* h_in = nullptr; int64_t* h_off = nullptr; uint64_t* h_bits = nullptr;  // pinned
     void* h_out = nullptr; int64_t* h_oo = nullptr; int64_t* h_ntok = nullptr;        // pinned
@@ -104,7 +118,8 @@ struct sw_encoder {
     int64_t cap_bytes = 0, cap_str = 0;
   } pipe[4];
   int pipe_depth = 3;                 // SW_OPT_PIPE_DEPTH: runs in flight (slots)
-  int64_t pipe_run = 64LL << 20;      // run size; batches over 2 runs take the pipeline (0: never)
+  int64_t pipe_run = 128LL << 20;     // run size; batches over 2 runs take the pipeline (0: never; 128 MiB: e2e
+                                      // 28.2 -> 30.1 GB/s pageable, 29.9 -> 31.8 pinned input against 64 MiB, r4z)
   bool pipe_kcopy = true;             // SW_OPT_PIPE_COPY_KERNELS
   hipStream_t s_h2d = nullptr, s_d2h = nullptr;
   // the merge kernels of different length buckets are independent: forked onto these streams
@@ -517,6 +532,9 @@ extern "C" void sw_encoder_destroy(sw_encoder* h) {
     free_io(h);
     if (h->ws_done) (void)hipEventSynchronize(h->ws_done);
     free_pipe(h);
+    for (const auto& r : h->pins) (void)hipHostUnregister((void*)((uintptr_t)r.h & ~(uintptr_t)4095));
+    h->pins.clear();
+    (void)hipFree(h->d_done);
     delete h->pool;
     if (h->s_h2d) (void)hipStreamDestroy(h->s_h2d);
     if (h->s_d2h) (void)hipStreamDestroy(h->s_d2h);
@@ -535,6 +553,41 @@ extern "C" void sw_encoder_destroy(sw_encoder* h) {
     if (h->stream) (void)hipStreamDestroy(h->stream);
   }
   delete h;
+}
+
+extern "C" int32_t sw_encoder_pin_host(sw_encoder* h, void* ptr, int64_t bytes) {
+  if (!h || !ptr || bytes <= 0) return fail(SW_ERR_ARG, "sw_encoder_pin_host: bad arguments");
+  DeviceGuard g(h->device);
+  for (const auto& r : h->pins)  // (whole pages: two ranges may not share one)
+    if (((uintptr_t)ptr >> 12) <= (((uintptr_t)r.h + r.n - 1) >> 12) && (((uintptr_t)ptr + bytes - 1) >> 12) >= ((uintptr_t)r.h >> 12))
+      return fail(SW_ERR_ARG, "sw_encoder_pin_host: shares a page with a pinned range");
+  // (whole pages registered: a large numpy / malloc block starts 16 bytes into its first page)
+  const uintptr_t pg = 4096, a0 = (uintptr_t)ptr & ~(pg - 1), a1 = ((uintptr_t)ptr + (uintptr_t)bytes + pg - 1) & ~(pg - 1);
+  HIP_TRY(hipHostRegister((void*)a0, (size_t)(a1 - a0), hipHostRegisterMapped));
+  void* d = nullptr;
+  const hipError_t e = hipHostGetDevicePointer(&d, (void*)a0, 0);
+  if (e != hipSuccess) {
+    (void)hipHostUnregister((void*)a0);
+    return fail(SW_ERR_HIP, std::string("sw_encoder_pin_host: ") + hipGetErrorString(e));
+  }
+  h->pins.push_back(sw_encoder::Pinned{(char*)ptr, bytes, (char*)d + ((uintptr_t)ptr - a0)});
+  return SW_OK;
+}
+
+extern "C" int32_t sw_encoder_unpin_host(sw_encoder* h, void* ptr) {
+  if (!h || !ptr) return fail(SW_ERR_ARG, "sw_encoder_unpin_host: bad arguments");
+  DeviceGuard g(h->device);
+  for (size_t i = 0; i < h->pins.size(); ++i) {
+    if (h->pins[i].h != (char*)ptr) continue;
+    // (nothing of this encoder may still read or write it)
+    if (h->stream) HIP_TRY(hipStreamSynchronize(h->stream));
+    if (h->s_h2d) HIP_TRY(hipStreamSynchronize(h->s_h2d));
+    if (h->s_d2h) HIP_TRY(hipStreamSynchronize(h->s_d2h));
+    HIP_TRY(hipHostUnregister((void*)((uintptr_t)ptr & ~(uintptr_t)4095)));
+    h->pins.erase(h->pins.begin() + (long)i);
+    return SW_OK;
+  }
+  return fail(SW_ERR_ARG, "sw_encoder_unpin_host: not a pinned range");
 }
 
 extern "C" int32_t sw_encoder_reserve(sw_encoder* h, int64_t max_bytes, int64_t max_strings) {
@@ -975,6 +1028,25 @@ __global__ void __launch_bounds__(256) k_copy_segs(CopySegs c) {
     if (c.n[k] > 0) copy_seg(c.src[k], c.dst[k], c.n[k], t, nt);
 }
 
+// one run's results straight into the caller's pinned arrays (sw_encoder_pin_host): its ids as
+// int32 at the batch's running count done[0] and its string offsets rebased by it; done[1] set
+// (nothing written) if the ids would pass out_cap.  k_push_advance then adds the run's count.
+__global__ void __launch_bounds__(256) k_push_direct(const int32_t* __restrict__ ids, const int64_t* ntok,
+                                                     const int64_t* d_oo, int64_t n_oo, int32_t* out, int64_t* out_off,
+                                                     int64_t out_cap, const int64_t* done) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x, nt = (int64_t)gridDim.x * blockDim.x;
+  const int64_t n = *ntok, base = done[0];
+  if (done[1] || base + n > out_cap) return;
+  copy_seg((const uint8_t*)ids, (uint8_t*)(out + base), n * 4, t, nt);
+  for (int64_t j = t; j < n_oo; j += nt) out_off[j] = d_oo[j] + base;
+}
+__global__ void k_push_advance(const int64_t* ntok, int64_t out_cap, int64_t* done) {
+  if (threadIdx.x != 0) return;
+  const int64_t n = *ntok;
+  if (done[1] || done[0] + n > out_cap) done[1] = 1;
+  else done[0] += n;
+}
+
 // one run's results to pinned host memory: ids (16-bit when every id fits, 8 per 16-byte store;
 // else 32-bit) and the run's string offsets
 __global__ void __launch_bounds__(256) k_push_run(const int32_t* __restrict__ ids, const int64_t* ntok, int wide,
@@ -1017,6 +1089,22 @@ struct HostSpecials {
 void sp_range(const HostSpecials& sp, int64_t a, int64_t b, int64_t* j0, int64_t* j1) {
   *j0 = std::lower_bound(sp.pos, sp.pos + sp.n, a) - sp.pos;
   *j1 = std::lower_bound(sp.pos, sp.pos + sp.n, b) - sp.pos;
+}
+
+// 16-bit ids -> the caller's int32 array, 8 at a time with non-temporal stores (the array is written
+// once and not read back here: no read-for-ownership of its lines, about a third less host
+// memory traffic than plain stores)
+static void widen16_stream(const uint16_t* src, int32_t* dst, int64_t n) {
+  int64_t i = 0;
+  for (; i < n && ((uintptr_t)(dst + i) & 15); ++i) dst[i] = (int32_t)src[i];
+  const __m128i z = _mm_setzero_si128();
+  for (; i + 8 <= n; i += 8) {
+    const __m128i x = _mm_loadu_si128((const __m128i*)(src + i));
+    _mm_stream_si128((__m128i*)(dst + i), _mm_unpacklo_epi16(x, z));
+    _mm_stream_si128((__m128i*)(dst + i + 4), _mm_unpackhi_epi16(x, z));
+  }
+  for (; i < n; ++i) dst[i] = (int32_t)src[i];
+  _mm_sfence();
 }
 
 // sw_encode_batch for a large host batch: runs of whole strings (<= pipe_run bytes, or one longer
@@ -1091,6 +1179,18 @@ int32_t encode_batch_pipelined(sw_encoder* h, const uint8_t* bytes, const int64_
   (void)max_w;
   int32_t rc = ensure_workspace(h, max_b);
   if (rc) return rc;
+  // caller ranges pinned by sw_encoder_pin_host: the input read over PCIe by the copy kernel (no
+  // staging memcpy), the ids and offsets written by the device into the caller's arrays (no copy
+  // or widening on the host)
+  const uint8_t* in_dev =
+      h->pipe_kcopy ? (const uint8_t*)h->pinned_dev(bytes + b0, std::max<int64_t>(str_off[n_str] - b0, 1)) : nullptr;
+  int32_t* out_dev = h->pipe_kcopy ? (int32_t*)h->pinned_dev(out_ids, (int64_t)sizeof(int32_t) * out_cap) : nullptr;
+  int64_t* oo_dev = h->pipe_kcopy ? (int64_t*)h->pinned_dev(out_off, (int64_t)sizeof(int64_t) * (n_str + 1)) : nullptr;
+  const bool direct_out = out_dev && oo_dev;
+  if (direct_out) {
+    if (!h->d_done) HIP_TRY(hipMalloc(&h->d_done, 2 * sizeof(int64_t)));
+    HIP_TRY(hipMemsetAsync(h->d_done, 0, 2 * sizeof(int64_t), h->s_d2h));
+  }
   const bool count = stats && !chunk_bits;
   if (count) HIP_TRY(hipMemsetAsync(h->d_pcount, 0, sizeof(unsigned long long), h->stream));
   const bool was_timing = h->timing;
@@ -1119,7 +1219,8 @@ int32_t encode_batch_pipelined(sw_encoder* h, const uint8_t* bytes, const int64_
     const int64_t s_lo = runs[k].first, s_hi = runs[k].second, a0 = str_off[s_lo], nb = str_off[s_hi] - a0;
     auto t = std::chrono::steady_clock::now();
     const uint8_t* src = bytes + a0;
-    pool.parallel_for(nb, [&](int64_t lo, int64_t hi) { std::memcpy(p.h_in + lo, src + lo, (size_t)(hi - lo)); });
+    if (!in_dev)
+      pool.parallel_for(nb, [&](int64_t lo, int64_t hi) { std::memcpy(p.h_in + lo, src + lo, (size_t)(hi - lo)); });
     for (int64_t j = 0; j <= s_hi - s_lo; ++j) p.h_off[j] = str_off[s_lo + j] - a0;
     if (sp.n > 0) {  // the run's special-token occurrences, rebased: positions, then lengths and ids (int32)
       int64_t j0, j1;
@@ -1154,7 +1255,8 @@ int32_t encode_batch_pipelined(sw_encoder* h, const uint8_t* bytes, const int64_
     const int64_t n_bits = chunk_bits ? (int64_t)sizeof(uint64_t) * ((nb + 63) / 64) : 0;
     const int64_t m_sp = sp.n > 0 ? p_nsp[k % h->pipe_depth] : 0, n_sp_bytes = 16 * m_sp;  // (8 + 4 + 4 B each)
     if (h->pipe_kcopy) {
-      const CopySegs c{{p.h_in, (const uint8_t*)p.h_off, (const uint8_t*)p.h_bits, (const uint8_t*)p.h_sp, nullptr, nullptr},
+      const uint8_t* in_src = in_dev ? in_dev + (str_off[s_lo] - b0) : p.h_in;
+      const CopySegs c{{in_src, (const uint8_t*)p.h_off, (const uint8_t*)p.h_bits, (const uint8_t*)p.h_sp, nullptr, nullptr},
                        {p.d_in, (uint8_t*)p.d_off, (uint8_t*)p.d_bits, (uint8_t*)p.d_sp, nullptr, nullptr},
                        {nb, (int64_t)sizeof(int64_t) * (ns + 1), n_bits, n_sp_bytes, 0, 0}};
       hipLaunchKernelGGL(k_copy_segs, dim3(128), dim3(256), 0, h->s_h2d, c);
@@ -1187,8 +1289,14 @@ int32_t encode_batch_pipelined(sw_encoder* h, const uint8_t* bytes, const int64_
     HIP_TRY(hipEventRecord(p.e_comp, h->stream));
     if (h->pipe_kcopy) {
       HIP_TRY(hipStreamWaitEvent(h->s_d2h, p.e_comp, 0));
-      hipLaunchKernelGGL(k_push_run, dim3(128), dim3(256), 0, h->s_d2h, p.d_out, p.d_ntok, narrow ? 0 : 1,
-                         p.h_out, p.d_oo, ns + 1, p.h_oo);
+      if (direct_out) {
+        hipLaunchKernelGGL(k_push_direct, dim3(128), dim3(256), 0, h->s_d2h, p.d_out, p.d_ntok, p.d_oo, ns + 1, out_dev,
+                           oo_dev + s_lo, out_cap, h->d_done);
+        hipLaunchKernelGGL(k_push_advance, dim3(1), dim3(64), 0, h->s_d2h, p.d_ntok, out_cap, h->d_done);
+      } else {
+        hipLaunchKernelGGL(k_push_run, dim3(128), dim3(256), 0, h->s_d2h, p.d_out, p.d_ntok, narrow ? 0 : 1,
+                           p.h_out, p.d_oo, ns + 1, p.h_oo);
+      }
       HIP_TRY(hipGetLastError());
       HIP_TRY(hipEventRecord(p.e_out, h->s_d2h));
     }
@@ -1212,12 +1320,15 @@ int32_t encode_batch_pipelined(sw_encoder* h, const uint8_t* bytes, const int64_
     }
     HIP_TRY(hipEventSynchronize(p.e_out));
     stamp("pushed", k);
+    if (direct_out) {  // (the device wrote them into the caller's arrays)
+      done += nt;
+      ms_drain += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t).count();
+      return SW_OK;
+    }
     int32_t* dst = out_ids + done;
     if (narrow) {
       const uint16_t* s16 = (const uint16_t*)p.h_out;
-      pool.parallel_for(nt, [&](int64_t lo, int64_t hi) {
-        for (int64_t i = lo; i < hi; ++i) dst[i] = (int32_t)s16[i];
-      });
+      pool.parallel_for(nt, [&](int64_t lo, int64_t hi) { widen16_stream(s16 + lo, dst + lo, hi - lo); });
     } else {
       const int32_t* s32 = (const int32_t*)p.h_out;
       pool.parallel_for(nt, [&](int64_t lo, int64_t hi) { std::memcpy(dst + lo, s32 + lo, sizeof(int32_t) * (hi - lo)); });

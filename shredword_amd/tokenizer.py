@@ -124,7 +124,8 @@ class Tokenizer(BaseTokenizer):
     def close(self):
         h, self._handle = getattr(self, "_handle", None), None
         if h:
-            _lib.lib().sw_encoder_destroy(h)
+            _lib.lib().sw_encoder_destroy(h)  # (unpins whatever pin_host pinned)
+        self._pinned = []
         d, self._dec = getattr(self, "_dec", None), None
         if d:
             _lib.lib().sw_decoder_destroy(d)
@@ -236,6 +237,22 @@ class Tokenizer(BaseTokenizer):
             _lib.check(L.sw_encode_batch(*args, *tail))
         self.last_stats = stats
         return out[:int(out_off[n])], out_off[:n + 1]
+
+    def pin_host(self, arr):
+        """Pin a host numpy array this tokenizer's encode_packed will read (the bytes) or write
+        (out= / out_off=) call after call: its pages are locked and mapped for the device, so the
+        input is read over PCIe without a staging copy and the ids / offsets are written by the
+        device into the caller's arrays (sw_encoder_pin_host).  Keep the array alive until
+        unpin_host(arr) or close()."""
+        if not arr.flags["C_CONTIGUOUS"] or arr.nbytes == 0:
+            raise ValueError("pin_host: a non-empty contiguous array")
+        _lib.check(_lib.lib().sw_encoder_pin_host(self._encoder(), arr.ctypes.data, arr.nbytes))
+        self._pinned = getattr(self, "_pinned", [])
+        self._pinned.append(arr)  # (kept alive while pinned)
+
+    def unpin_host(self, arr):
+        _lib.check(_lib.lib().sw_encoder_unpin_host(self._encoder(), arr.ctypes.data))
+        self._pinned = [a for a in getattr(self, "_pinned", []) if a.ctypes.data != arr.ctypes.data]
 
     def encode_device(self, d_buf, d_off, d_bits=None, d_out=None, d_out_off=None, stream=None, out_bits=32,
                       d_specials=None):

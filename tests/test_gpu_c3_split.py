@@ -165,7 +165,7 @@ def test_pipeline_runs_cut_at_launch_limit():
             t.encode_packed(big, boff)
     finally:
         L.sw_encoder_set_option(h, _lib.SW_OPT_MAX_LAUNCH_BYTES, 0)
-        L.sw_encoder_set_option(h, _lib.SW_OPT_PIPE_RUN_BYTES, 64 << 20)
+        L.sw_encoder_set_option(h, _lib.SW_OPT_PIPE_RUN_BYTES, 128 << 20)
 
 
 def test_batch_split_string_over_limit_rejected():
@@ -368,3 +368,48 @@ def test_pipelined_depth(depth):
     assert L.sw_encoder_set_option(h, _lib.SW_OPT_PIPE_DEPTH, 5) == _lib.SW_ERR_ARG
     t.close()
 
+
+
+@pytest.mark.parametrize("pin", ["all", "input", "outputs", "out_only"])
+@pytest.mark.parametrize("wide", [False, True])
+def test_pipelined_pinned_caller_buffers(pin, wide):
+    """Caller arrays pinned with Tokenizer.pin_host (sw_encoder_pin_host): the input read over PCIe
+    without staging, the ids and offsets written by the device into the caller's arrays (only when
+    both output arrays are pinned) -- == the oracle, for a 16- and a 32-bit table, every
+    combination, calls repeated; a too-small pinned output is refused, not overrun; unpinned
+    arrays work as before."""
+    buf, off = corpus.synth(10, corpus.MIXED, 700, 700)
+    full, offs = pack([b"#" * 13] + [bytes(buf[off[i]:off[i + 1]]) for i in range(700)])
+    sub = offs[1:]
+    base = load_model_merges("bl32k.model")
+    merges = {(a if a < 256 else a + 70000, b if b < 256 else b + 70000): v + 70000
+              for (a, b), v in base.items()} if wide else base
+    t = sa.Tokenizer(device=0)
+    t.merges = merges
+    exp = oracle_encode(merges, full, sub, "cl100k")
+    L, h = _lib.lib(), t._encoder()
+    _lib.check(L.sw_encoder_set_option(h, _lib.SW_OPT_PIPE_RUN_BYTES, 5000))
+    out = np.full(len(full) + 100, -5, dtype=np.int32)
+    out_off = np.full(len(sub) + 3, -5, dtype=np.int64)
+    pins = {"all": (full, out, out_off), "input": (full,), "outputs": (out, out_off), "out_only": (out,)}[pin]
+    for arr in pins:
+        t.pin_host(arr)
+    for _ in range(2):
+        got = t.encode_packed(full, sub, out=out, out_off=out_off)
+        assert_same(got, exp)
+    if pin in ("all", "outputs"):  # (a pinned output too small for the batch, through the C-ABI: refused)
+        small = np.full(len(exp[0]) // 2 + 4096, -5, dtype=np.int32)
+        t.pin_host(small)
+        stats = _lib.SwStats()
+        rc = L.sw_encode_batch(h, _lib.ptr(full, ctypes.c_uint8), _lib.ptr(sub, ctypes.c_int64), len(sub) - 1, 0,
+                               None, _lib.ptr(small, ctypes.c_int32), len(exp[0]) // 2, _lib.ptr(out_off, ctypes.c_int64),
+                               ctypes.byref(stats))
+        assert rc == _lib.SW_ERR_CAP
+        assert (small[len(exp[0]) // 2:] == -5).all()  # (nothing written past out_cap)
+        t.unpin_host(small)
+    for arr in pins:
+        t.unpin_host(arr)
+    assert_same(t.encode_packed(full, sub, out=out, out_off=out_off), exp)
+    with pytest.raises(RuntimeError):
+        t.unpin_host(out)
+    t.close()

@@ -153,6 +153,6 @@ def test_pipelined_batch_with_specials():
             np.testing.assert_array_equal(g_off, e_off)
             np.testing.assert_array_equal(g_ids, e_ids)
     finally:
-        L.sw_encoder_set_option(h, _lib.SW_OPT_PIPE_RUN_BYTES, 64 << 20)
+        L.sw_encoder_set_option(h, _lib.SW_OPT_PIPE_RUN_BYTES, 128 << 20)
         L.sw_encoder_set_option(h, _lib.SW_OPT_MAX_LAUNCH_BYTES, 0)
     t.close()

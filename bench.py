@@ -55,6 +55,10 @@ def parse():
                          "others per KiB at random code-point boundaries; found (and, with --presplit host, "
                          "pre-split) on the host threads, timed apart from the GPU step; the batch is cut to "
                          "the 2^30 - 64-byte launch limit")
+    ap.add_argument("--specials-device", action="store_true",
+                    help="with --specials: the occurrences are found on the device inside the timed step "
+                         "(sw_find_specials_device, the count left on the device for sw_encode_device_ex) "
+                         "instead of on the host threads before it")
     ap.add_argument("--strings", type=int, default=None)
     ap.add_argument("--mean-len", type=int, default=None)
     ap.add_argument("--pattern", default="cl100k", choices=["cl100k", "gpt2"])
@@ -154,6 +158,9 @@ def main():
         buf, off = buf[:int(off[k])], off[:k + 1]
         n_str = k
     host_ps = args.presplit == "host"
+    sp_device = bool(specials) and args.specials_device
+    if sp_device and host_ps:
+        raise SystemExit("--specials-device needs the device pre-split (the host pre-split needs host occurrences)")
     t_data = time.time() - t
     t = time.time()
     if specials:
@@ -208,13 +215,25 @@ def main():
     # width, the special-token occurrences found on the host (uploaded once, like the bitmap)
     ex = _lib.SwEncodeEx(d_bits.data_ptr() if host_ps else None, 16 if out16 else 32, None, None, None, 0)
     d_sp = None
-    if specials:
+    if sp_device:  # found on the device inside the step: arrays for the worst case, the count on the device
+        st_sp, keep_sp = _lib.specials_struct(specials)
+        _lib.check(L.sw_encoder_set_specials(h, ctypes.byref(st_sp)))
+        cap_sp = n_bytes // min(len(k.encode()) for k in specials if k) + 1
+        d_sp = (torch.empty(cap_sp, dtype=torch.int64, device=dev), torch.empty(cap_sp, dtype=torch.int32, device=dev),
+                torch.empty(cap_sp, dtype=torch.int32, device=dev), torch.zeros(1, dtype=torch.int64, device=dev))
+        ex.sp_pos, ex.sp_len, ex.sp_id, ex.n_sp = d_sp[0].data_ptr(), d_sp[1].data_ptr(), d_sp[2].data_ptr(), cap_sp
+        ex.d_n_sp = d_sp[3].data_ptr()
+    elif specials:
         d_sp = tuple(torch.from_numpy(np.ascontiguousarray(x)).to(dev) for x in sp_host)
         ex.sp_pos, ex.sp_len, ex.sp_id, ex.n_sp = d_sp[0].data_ptr(), d_sp[1].data_ptr(), d_sp[2].data_ptr(), len(sp_host[0])
 
     plain = not out16 and not specials  # (sw_encode_device: what an A/B build of an earlier revision has)
 
     def encode_into(o_ids, o_off, n_tok_ptr=None):
+        if sp_device:
+            _lib.check(L.sw_find_specials_device(h, d_buf.data_ptr(), n_bytes, d_off.data_ptr(), n_str,
+                                                 d_sp[0].data_ptr(), d_sp[1].data_ptr(), d_sp[2].data_ptr(), cap_sp,
+                                                 d_sp[3].data_ptr(), stream, None))
         if plain:
             _lib.check(L.sw_encode_device(h, d_buf.data_ptr(), n_bytes, d_off.data_ptr(), n_str,
                                           d_bits.data_ptr() if host_ps else None, o_ids.data_ptr(), o_off.data_ptr(),
@@ -237,6 +256,11 @@ def main():
     n_tok_c = ctypes.c_int64()
     encode(ctypes.byref(n_tok_c))
     n_tok = int(n_tok_c.value)
+    sp_dev_ok = None
+    if sp_device:  # (the device finder's occurrences == the host threads', outside the timed region)
+        nd = int(d_sp[3].item())
+        sp_dev_ok = bool(nd == len(sp_host[0]) and np.array_equal(d_sp[0][:nd].cpu().numpy(), sp_host[0])
+                         and np.array_equal(d_sp[2][:nd].cpu().numpy(), sp_host[2]))
 
     # the gathers' widths: every rank's counts are the same every step (same corpus), so the
     # maxima are taken once here and the timed step has no host synchronisation
@@ -370,19 +394,23 @@ def main():
     # bytes in + ids out + offsets in/out (+ the bitmap when it comes from the host, C3)
     # (ids written as 16 bits by the N>1 step, out16: 2 bytes each)
     b_algo = n_bytes + (2 if out16 else 4) * n_tok + 16 * (n_str + 1) + ((n_bytes + 7) // 8 if host_ps else 0)
+    if sp_device:  # (the finder's kernels precede the encode's timing events: the whole step instead)
+        k_ms = ms_step
     achieved = b_algo / (k_ms * 1e-3) / 1e9 if k_ms > 0 else None
     # traffic: HBM bytes per launch from the committed PMC profile of this same workload, if any
     traffic, traffic_x2, traffic_src, counters = None, None, None, None
-    try:
+    try:  # (one entry per workload, written by tools/summarize_prof.py from that workload's PMC run)
         with open(os.path.join(ROOT, "profiles", "traffic.json")) as f:
             tj = json.load(f)
-        if (tj.get("n_bytes") == n_bytes and tj.get("merges") == len(tok.merges) and tj.get("pattern") == args.pattern
-                and tj.get("chunk_table") == (not args.no_chunk_table) and tj.get("dedupe") == (not args.no_dedupe)
-                and tj.get("presplit", "host") == args.presplit
-                and tj.get("corpus", "mixed") == corpus_name and tj.get("specials", 0.0) == args.specials):
-            traffic, traffic_src = int(tj["traffic_bytes_per_launch"]), tj["source"]
-            traffic_x2 = int(tj.get("traffic_bytes_per_launch_x2", 0)) or None
-            counters = tj.get("counters")
+        want = {"n_bytes": n_bytes, "merges": len(tok.merges), "pattern": args.pattern,
+                "chunk_table": not args.no_chunk_table, "dedupe": not args.no_dedupe, "presplit": args.presplit,
+                "corpus": corpus_name, "specials": args.specials,
+                "specials_found": "device" if sp_device else "host"}
+        for ent in tj.get("entries", []):
+            if all(ent.get(k) == v for k, v in want.items()):
+                traffic, traffic_src = int(ent["traffic_bytes_per_launch"]), ent["source"]
+                traffic_x2 = int(ent.get("traffic_bytes_per_launch_x2", 0)) or None
+                counters = ent.get("counters")
     except (OSError, ValueError, KeyError):
         pass
     roofline = {"bound": "hbm", "achieved": round(achieved, 2) if achieved else None, "peak": HBM_PEAK_GBS,
@@ -561,7 +589,11 @@ def main():
             "host_split_note": ("host threads, outside the timed GPU step: special-token occurrences%s (%d threads)" % (
                 " + %s pre-split bitmap" % args.pattern if host_ps else "", args.threads)) if (host_ps or specials) else None,
             "specials": ({"per_kib": args.specials, "occurrences": int(len(sp_host[0])), "tokens": SPECIALS,
-                          "end_of_string": "<|endoftext|>"} if specials else None),
+                          "end_of_string": "<|endoftext|>", "found": "device" if sp_device else "host",
+                          "found_note": ("sw_find_specials_device inside the timed step (its kernels before the "
+                                         "encode's; roofline.kernel_ms = the whole step)" if sp_device else
+                                         "host threads, before the timed step (host_split_s)"),
+                          "device_count_equals_host": sp_dev_ok} if specials else None),
         }
         print(json.dumps(line), flush=True)
     tok.close()

@@ -152,6 +152,14 @@ int32_t sw_encoder_unpin_host(sw_encoder* h, void* ptr);
  *                          inside the classification kernel (k_split_classify: the input is read once,
  *                          the bitmap is not read back); 0: as its own kernel first.  Results identical. */
 #define SW_OPT_FUSED_PRESPLIT 14
+/*   SW_OPT_TEST_FAIL_GROWTH  tests only: 1 makes the dedupe table's next growth allocation fail (the
+ *                          encoder must keep the table it has and go on encoding) */
+#define SW_OPT_TEST_FAIL_GROWTH 17
+/*   SW_OPT_DEVICE_SPECIALS 1 (default): sw_encode_batch_ex finds the special-token occurrences on the
+ *                          device (sw_find_specials_device, launch by launch) when every special is
+ *                          <= 64 bytes and the pre-split is the device's; 0: on the host threads.
+ *                          Results identical. */
+#define SW_OPT_DEVICE_SPECIALS 18
 /* (option 15 was an A/B knob of round 2, removed: set_option rejects it) */
 /* (option 16, a persistent 16-bit output of sw_encode_device, was replaced by the per-call
  * sw_encode_ex.out_bits: set_option rejects it; sw_encode_device always writes int32) */
@@ -197,6 +205,21 @@ typedef struct sw_specials {
  * SW_ERR_CAP if more than cap, or another negative status. */
 int64_t sw_find_specials_host(const uint8_t* bytes, const int64_t* str_off, int64_t n_str, const sw_specials* sp,
                               int64_t* sp_pos, int32_t* sp_len, int32_t* sp_id, int64_t cap, int32_t n_threads);
+
+/* The same occurrences found on the device.  sw_encoder_set_specials uploads the specials to the
+ * handle (once; calls with the same specials are free; NULL or n == 0 clears them).  Then
+ * sw_find_specials_device scans d_bytes[d_str_off[s] .. d_str_off[s+1]) (device arrays, as
+ * sw_encode_device takes them) and writes the occurrences to d_pos / d_len / d_id (positions
+ * relative to d_bytes, ascending) and their number to d_count (device int64), asynchronously on
+ * `stream`; n_host (optional) synchronises and receives the count.  cap >= n_bytes / (length of the
+ * shortest non-empty special) is required (SW_ERR_CAP: that many occurrences fit at most).  Every
+ * special must be <= 64 bytes (SW_ERR_ARG otherwise: the host finder takes any length).  The
+ * outputs feed sw_encode_device_ex (sp_pos, sp_len, sp_id, n_sp = cap, d_n_sp = d_count) with no
+ * synchronisation in between. */
+int32_t sw_encoder_set_specials(sw_encoder* h, const sw_specials* sp);
+int32_t sw_find_specials_device(sw_encoder* h, const uint8_t* d_bytes, int64_t n_bytes, const int64_t* d_str_off,
+                                int64_t n_str, int64_t* d_pos, int32_t* d_len, int32_t* d_id, int64_t cap,
+                                int64_t* d_count, void* stream, int64_t* n_host);
 
 /* sw_presplit_host with special-token occurrences (as sw_find_specials_host gives them): the
  * text between occurrences is pre-split on its own and each occurrence is one chunk.  Returns the
@@ -244,14 +267,21 @@ int32_t sw_encode_device(sw_encoder* h, const uint8_t* d_bytes, int64_t n_bytes,
 
 /* ---- the same with per-call choices ---------------------------------------------------------
  * sw_encode_device with (ex == NULL: exactly sw_encode_device):
- *   chunk_bits   as d_chunk_bits above (NULL: the device pre-splits with SW_OPT_PATTERN)
+ *   chunk_bits   as d_chunk_bits above (NULL: the device pre-splits with `pattern`)
  *   out_bits     32: d_out_ids is int32_t*; 16: uint16_t* -- the multi-GPU driver's 16-bit transport
- *                (SW_INFO_IDS16 tables with every special id below 65536; SW_ERR_ARG otherwise)
+ *                (SW_INFO_IDS16 tables only, and never together with special-token occurrences:
+ *                SW_ERR_ARG otherwise)
  *   sp_pos / sp_len / sp_id / n_sp   special-token occurrences (device arrays; sp_pos relative to
  *                d_bytes, ascending, non-overlapping, each inside one string; n_sp == 0: none), as
  *                sw_find_specials_host finds them: each is one chunk encoding to its id, and the
  *                device pre-split treats its ends as string boundaries (a caller bitmap must already:
- *                sw_presplit_host_specials) */
+ *                sw_presplit_host_specials)
+ *   pattern      the device pre-split's pattern for this call (SW_PAT_*), or -1: the handle's
+ *                SW_OPT_PATTERN.  Per call, so that callers sharing one handle with different
+ *                patterns do not race on the option.
+ *   d_n_sp       NULL, or the occurrence count in device memory (sw_find_specials_device's d_count,
+ *                not read back by the host): n_sp is then the arrays' capacity, and the encode reads
+ *                the count on the device -- the find + encode sequence needs no synchronisation */
 typedef struct sw_encode_ex {
   const uint64_t* chunk_bits;
   int32_t out_bits;
@@ -259,6 +289,8 @@ typedef struct sw_encode_ex {
   const int32_t* sp_len;
   const int32_t* sp_id;
   int64_t n_sp;
+  int32_t pattern;
+  const int64_t* d_n_sp;
 } sw_encode_ex;
 int32_t sw_encode_device_ex(sw_encoder* h, const uint8_t* d_bytes, int64_t n_bytes, const int64_t* d_str_off,
                             int64_t n_str, const sw_encode_ex* ex, void* d_out_ids, int64_t* d_out_off, void* stream,

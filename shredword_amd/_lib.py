@@ -30,6 +30,8 @@ SW_OPT_PIPE_COPY_KERNELS = 11
 SW_OPT_PIPE_DEPTH = 12
 SW_OPT_MERGE_STREAMS = 13
 SW_OPT_FUSED_PRESPLIT = 14
+SW_OPT_TEST_FAIL_GROWTH = 17
+SW_OPT_DEVICE_SPECIALS = 18
 SW_OPT_OUT_BITS = 16  # (removed: set_option rejects it; 16-bit output is sw_encode_ex.out_bits, per call)
 SW_INFO_MERGES, SW_INFO_CHUNK_ENTRIES, SW_INFO_WIDE_TABLE, SW_INFO_IDS16, SW_INFO_SPLIT, SW_INFO_DEDUPE_SLOTS = 1, 2, 3, 4, 5, 6
 
@@ -46,9 +48,14 @@ class SwSpecials(Structure):
 
 
 class SwEncodeEx(Structure):
-    """sw_encode_ex: per-call choices of sw_encode_device_ex (device pointers as integers)."""
+    """sw_encode_ex: per-call choices of sw_encode_device_ex (device pointers as integers).
+    pattern: SW_PAT_* for this call, or -1 (the default here): the handle's SW_OPT_PATTERN."""
     _fields_ = [("chunk_bits", c_void_p), ("out_bits", c_int32), ("sp_pos", c_void_p), ("sp_len", c_void_p),
-                ("sp_id", c_void_p), ("n_sp", c_int64)]
+                ("sp_id", c_void_p), ("n_sp", c_int64), ("pattern", c_int32), ("d_n_sp", c_void_p)]
+
+    def __init__(self, chunk_bits=None, out_bits=32, sp_pos=None, sp_len=None, sp_id=None, n_sp=0, pattern=-1,
+                 d_n_sp=None):
+        super().__init__(chunk_bits, out_bits, sp_pos, sp_len, sp_id, n_sp, pattern, d_n_sp)
 
 
 class TrainConfig(Structure):
@@ -111,6 +118,9 @@ _SIGNATURES = {
                                      POINTER(c_int64), POINTER(SwStats)]),
     "sw_find_specials_host": (c_int64, [POINTER(c_uint8), POINTER(c_int64), c_int64, POINTER(SwSpecials),
                                         POINTER(c_int64), POINTER(c_int32), POINTER(c_int32), c_int64, c_int32]),
+    "sw_encoder_set_specials": (c_int32, [c_void_p, POINTER(SwSpecials)]),
+    "sw_find_specials_device": (c_int32, [c_void_p, c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_void_p, c_void_p,
+                                          c_int64, c_void_p, c_void_p, POINTER(c_int64)]),
     "sw_presplit_host_specials": (c_int64, [POINTER(c_uint8), POINTER(c_int64), c_int64, c_int32, POINTER(c_int64),
                                             POINTER(c_int32), c_int64, POINTER(c_uint64), c_int32]),
     "sw_encoder_set_option": (c_int32, [c_void_p, c_int32, c_int64]),

@@ -37,6 +37,7 @@
 #include "long_split.h"
 #include "presplit_kernel.h"
 #include "split_classify.h"
+#include "specials_find.h"
 #include "shredword_hip.h"
 #include "table.h"
 
@@ -160,12 +161,15 @@ struct sw_encoder {
   bool dedupe = true;
   bool dedupe_exact = true;           // SW_OPT_DEDUPE_EXACT
   int64_t dedupe_slots = 0;           // SW_OPT_DEDUPE_SLOTS (0: automatic)
+  bool dd_grow_stop = false;          // a growth allocation failed: keep the table that works
+  int32_t test_fail_grow = 0;         // SW_OPT_TEST_FAIL_GROWTH: the next growth's allocations fail (tests)
   int32_t pattern = SW_PAT_CL100K;    // SW_OPT_PATTERN: device pre-split of sw_encode_device(bits = NULL)
   bool host_presplit = false;         // SW_OPT_HOST_PRESPLIT: sw_encode_batch pre-splits on the host
   uint64_t* d_pbits = nullptr;        // [n_bytes / 64] device pre-split bitmap
   uint32_t* d_edge = nullptr;         // [kEdgeWords][n_tiles + 1] k_edges: the tile boundaries' masks and words
   unsigned int* d_redo = nullptr;     // k_split_classify's tiles for k_split_redo: count, then the list (int64)
   bool fused_presplit = true;         // SW_OPT_FUSED_PRESPLIT: the device pre-split inside k_split_classify
+  bool device_specials = true;        // SW_OPT_DEVICE_SPECIALS: sw_encode_batch_ex finds specials on the device
   unsigned long long* d_pcount = nullptr;
   uint64_t* d_llist = nullptr;        // k_classify's long chunks (EncArgs::llist) and their count
   unsigned long long* d_lcount = nullptr;
@@ -180,6 +184,17 @@ struct sw_encoder {
   uint64_t* d_bits = nullptr;
   int32_t* d_out = nullptr;
   int64_t* d_out_off = nullptr;
+  // the device special-token finder (specials_find.h): the specials' table, keyed by content, and
+  // its per-tile work arrays
+  void* d_spt = nullptr;
+  SpTab spt{};
+  std::string spt_key;                // the specials the table holds (bytes, offsets, ids)
+  bool spt_dev = false;               // every special fits the device finder (<= kSpMaxLen bytes)
+  int32_t spt_min_len = 1;            // the shortest non-empty special
+  int64_t spf_tiles = 0;              // capacity of the finder's arrays, in tiles
+  uint32_t* d_spf = nullptr;          // candidate bits, occurrence bits, per-tile counts
+  int64_t* d_spf_off = nullptr;       // per-tile occurrence offsets (+ scan partials)
+  int64_t* d_nsp = nullptr;           // sw_encode_batch_ex: the finder's count
   int64_t sp_cap = 0;                 // special-token occurrences staged for sw_encode_batch_ex
   int64_t* d_sp_pos = nullptr;
   int32_t* d_sp_len = nullptr;
@@ -257,7 +272,7 @@ int32_t ensure_workspace(sw_encoder* h, int64_t n_bytes) {
   // (+ slack for k_compact's head reads; k_classify's tile-local queue, aliased here, takes whole tiles)
   HIP_TRY(hipMalloc(&h->d_res, sizeof(uint32_t) * std::max<int64_t>(2 * nb + 16, n_tiles * kTile)));
   HIP_TRY(hipMalloc(&h->d_tile_slo, sizeof(int64_t) * n_tiles));
-  HIP_TRY(hipMalloc(&h->d_tile_sp, sizeof(int64_t) * n_tiles));
+  HIP_TRY(hipMalloc(&h->d_tile_sp, sizeof(int64_t) * (n_tiles + 1)));
   HIP_TRY(hipMalloc(&h->d_tile_slots, sizeof(uint32_t) * n_tiles));
   HIP_TRY(hipMalloc(&h->d_tile_nref, sizeof(uint32_t) * n_tiles));
   HIP_TRY(hipMalloc(&h->d_rlist, sizeof(uint32_t) * n_tiles * kTile));
@@ -544,6 +559,10 @@ extern "C" void sw_encoder_destroy(sw_encoder* h) {
     }
     if (h->ev_fork) (void)hipEventDestroy(h->ev_fork);
     if (h->ev_fork_long) (void)hipEventDestroy(h->ev_fork_long);
+    (void)hipFree(h->d_spt);
+    (void)hipFree(h->d_spf);
+    (void)hipFree(h->d_spf_off);
+    (void)hipFree(h->d_nsp);
     (void)hipFree(h->d_table);
     (void)hipFree(h->d_chunks);
     (void)hipFree(h->d_inv);
@@ -619,6 +638,8 @@ extern "C" int32_t sw_encoder_set_option(sw_encoder* h, int32_t option, int64_t 
     case SW_OPT_PIPE_COPY_KERNELS: h->pipe_kcopy = value != 0; return SW_OK;
     case SW_OPT_MERGE_STREAMS: h->merge_fork = value != 0; return SW_OK;
     case SW_OPT_FUSED_PRESPLIT: h->fused_presplit = value != 0; return SW_OK;
+    case SW_OPT_TEST_FAIL_GROWTH: h->test_fail_grow = value ? 1 : 0; h->dd_grow_stop = false; return SW_OK;
+    case SW_OPT_DEVICE_SPECIALS: h->device_specials = value != 0; return SW_OK;
     case SW_OPT_PIPE_DEPTH:
       if (value < 2 || value > 4) return fail(SW_ERR_ARG, "pipeline depth: 2 .. 4");
       h->pipe_depth = (int)value;
@@ -763,7 +784,8 @@ struct DevSpecials {
   const int64_t* pos = nullptr;
   const int32_t* len = nullptr;
   const int32_t* id = nullptr;
-  int64_t n = 0;
+  int64_t n = 0;                    // the count, or (n_dev given) the arrays' capacity
+  const int64_t* n_dev = nullptr;   // the count in device memory (sw_find_specials_device)
 };
 
 // the device pipeline; d_out_ids is int32_t*, or uint16_t* when out16 (the table is ids16)
@@ -771,28 +793,169 @@ struct DevSpecials {
 // counted by the device and published to host memory by k_string_offsets) grows the table for
 // the launches after it: to the power of two >= 2 x (entries + overflow), at most kDdSlotsMax.
 // The count is read without waiting: a launch still running is seen by a later call.
+// The new table is allocated beside the old one and swapped in only when all three buffers exist:
+// growth is an optimisation, so an allocation failure keeps the table that works (and stops
+// further attempts on this handle) instead of leaving the handle half-built.
 int32_t grow_dedupe(sw_encoder* h) {
   const unsigned long long over = h->h_ddfull ? __atomic_load_n(h->h_ddfull, __ATOMIC_ACQUIRE) : 0ULL;
-  if (!h->d_dtab || h->dedupe_slots || over <= (unsigned long long)h->dd_slots / 32 || h->dd_slots >= kDdSlotsMax)
+  if (!h->d_dtab || h->dedupe_slots || h->dd_grow_stop || over <= (unsigned long long)h->dd_slots / 32 ||
+      h->dd_slots >= kDdSlotsMax)
     return SW_OK;  // (SW_OPT_DEDUPE_SLOTS caps the table on purpose: no growth)
   int64_t slots = h->dd_slots;
   while (slots < 2 * (h->dd_slots + (int64_t)over) && slots < kDdSlotsMax) slots <<= 1;
+  uint64_t* dtab = nullptr;
+  uint4* dres = nullptr;
+  uint8_t* dcnt = nullptr;
+  bool ok = !h->test_fail_grow;
+  ok = ok && hipMalloc(&dtab, sizeof(uint64_t) * slots) == hipSuccess;
+  ok = ok && hipMalloc(&dres, sizeof(uint4) * slots) == hipSuccess;
+  ok = ok && hipMalloc(&dcnt, slots) == hipSuccess;
+  __atomic_store_n(h->h_ddfull, 0ULL, __ATOMIC_RELEASE);
+  if (!ok) {
+    if (dtab) (void)hipFree(dtab);
+    if (dres) (void)hipFree(dres);
+    if (dcnt) (void)hipFree(dcnt);
+    (void)hipGetLastError();  // (the failed allocation's status: not this launch's error)
+    h->dd_grow_stop = true;
+    return SW_OK;
+  }
+  // the old table may still be in use by the previous launch
   if (h->ws_pending) HIP_TRY(hipEventSynchronize(h->ws_done));
   (void)hipFree(h->d_dtab); (void)hipFree(h->d_dres); (void)hipFree(h->d_dcnt);
-  h->d_dtab = nullptr; h->d_dres = nullptr; h->d_dcnt = nullptr;
-  HIP_TRY(hipMalloc(&h->d_dtab, sizeof(uint64_t) * slots));
-  HIP_TRY(hipMemset(h->d_dtab, 0, sizeof(uint64_t) * slots));
-  HIP_TRY(hipMalloc(&h->d_dres, sizeof(uint4) * slots));
-  HIP_TRY(hipMalloc(&h->d_dcnt, slots));
+  h->d_dtab = dtab; h->d_dres = dres; h->d_dcnt = dcnt;
   h->dd_slots = slots;
   h->dmask = (uint32_t)(slots - 1);
-  __atomic_store_n(h->h_ddfull, 0ULL, __ATOMIC_RELEASE);
+  return SW_OK;
+}
+
+// the specials' table on the device (rebuilt only when the specials change)
+int32_t set_specials(sw_encoder* h, const sw_specials* sp) {
+  if (sp && sp->n > 0 && (!sp->bytes || !sp->off || !sp->ids)) return fail(SW_ERR_ARG, "specials: null arrays");
+  const int64_t n = sp ? sp->n : 0;
+  std::string key;
+  if (n > 0) {
+    if (sp->off[0] < 0) return fail(SW_ERR_ARG, "specials: bad offsets");
+    for (int64_t k = 0; k < n; ++k)
+      if (sp->off[k + 1] < sp->off[k]) return fail(SW_ERR_ARG, "specials: bad offsets");
+    const int64_t nb = sp->off[n];
+    if (nb > INT32_MAX / 2 || n > INT32_MAX / 8) return fail(SW_ERR_ARG, "specials: too large");
+    key.assign((const char*)&n, sizeof(n));
+    key.append((const char*)sp->off, sizeof(int64_t) * (size_t)(n + 1));
+    key.append((const char*)sp->ids, sizeof(int32_t) * (size_t)n);
+    key.append((const char*)sp->bytes, (size_t)nb);
+  }
+  if (h->d_spt && key == h->spt_key) return SW_OK;
+  DeviceGuard g(h->device);
+  if (h->ws_pending) HIP_TRY(hipEventSynchronize(h->ws_done));  // (a finder still reading the old table)
+  (void)hipFree(h->d_spt);
+  h->d_spt = nullptr;
+  h->spt = SpTab{};
+  h->spt_key.clear();
+  h->spt_dev = false;
+  if (n == 0) return SW_OK;
+  const int64_t b0 = sp->off[0], nb = sp->off[n] - b0;
+  std::vector<int32_t> off((size_t)n + 1), ids((size_t)n), list, first(257, 0);
+  for (int64_t k = 0; k <= n; ++k) off[(size_t)k] = (int32_t)(sp->off[k] - b0);
+  for (int64_t k = 0; k < n; ++k) ids[(size_t)k] = sp->ids[k];
+  std::vector<std::vector<int32_t>> by_first(256);
+  int32_t max_len = 0, min_len = INT32_MAX;
+  for (int64_t k = 0; k < n; ++k) {
+    const int32_t L = off[(size_t)k + 1] - off[(size_t)k];
+    if (L == 0) continue;  // (an empty special never matches)
+    by_first[sp->bytes[sp->off[k]]].push_back((int32_t)k);
+    max_len = std::max(max_len, L);
+    min_len = std::min(min_len, L);
+  }
+  SpTab t{};
+  uint32_t fb = 0;
+  for (int b = 0; b < 256; ++b) {
+    first[(size_t)b] = (int32_t)list.size();
+    if (by_first[(size_t)b].empty()) continue;
+    t.filt[b >> 5] |= 1u << (b & 31);
+    if (t.n_first < kSpMaxFirstSwar) fb |= (uint32_t)b << (8 * t.n_first);
+    ++t.n_first;
+    list.insert(list.end(), by_first[(size_t)b].begin(), by_first[(size_t)b].end());
+  }
+  first[256] = (int32_t)list.size();
+  if (list.empty()) list.push_back(0);
+  t.fb = fb;
+  t.max_len = max_len;
+  t.n = (int32_t)n;
+  // one buffer: bytes | off | ids | list | first
+  const size_t o_off = ((size_t)nb + 15) & ~(size_t)15, o_ids = o_off + 4 * off.size(), o_list = o_ids + 4 * ids.size(),
+               o_first = o_list + 4 * list.size(), total = o_first + 4 * first.size();
+  std::vector<char> host(total, 0);
+  std::memcpy(host.data(), sp->bytes + b0, (size_t)nb);
+  std::memcpy(host.data() + o_off, off.data(), 4 * off.size());
+  std::memcpy(host.data() + o_ids, ids.data(), 4 * ids.size());
+  std::memcpy(host.data() + o_list, list.data(), 4 * list.size());
+  std::memcpy(host.data() + o_first, first.data(), 4 * first.size());
+  HIP_TRY(hipMalloc(&h->d_spt, total));
+  HIP_TRY(hipMemcpy(h->d_spt, host.data(), total, hipMemcpyHostToDevice));
+  char* d = (char*)h->d_spt;
+  t.bytes = (const uint8_t*)d;
+  t.off = (const int32_t*)(d + o_off);
+  t.ids = (const int32_t*)(d + o_ids);
+  t.list = (const int32_t*)(d + o_list);
+  t.first = (const int32_t*)(d + o_first);
+  h->spt = t;
+  h->spt_key = key;
+  h->spt_dev = t.n_first > 0 && max_len <= kSpMaxLen;
+  h->spt_min_len = t.n_first > 0 ? min_len : 1;
+  return SW_OK;
+}
+
+// the occurrences of the handle's specials in d_bytes (sw_find_specials_device), on stream st
+int32_t find_specials_device(sw_encoder* h, const uint8_t* d_bytes, int64_t n_bytes, const int64_t* d_str_off,
+                             int64_t n_str, int64_t* d_pos, int32_t* d_len, int32_t* d_id, int64_t cap, int64_t* d_count,
+                             hipStream_t st) {
+  if (!h || n_bytes < 0 || n_str < 0 || !d_str_off || !d_count || (n_bytes > 0 && !d_bytes))
+    return fail(SW_ERR_ARG, "sw_find_specials_device: bad arguments");
+  if (n_bytes > kMaxLaunchBytes) return fail(SW_ERR_ARG, "sw_find_specials_device: n_bytes > 2^30 - 64");
+  if (h->d_spt && h->spt.n_first > 0 && !h->spt_dev)
+    return fail(SW_ERR_ARG, "sw_find_specials_device: a special is longer than 64 bytes (use the host finder)");
+  if (h->spt.n_first > 0 && n_bytes > 0 && (cap < n_bytes / h->spt_min_len || !d_pos || !d_len || !d_id))
+    return fail(SW_ERR_CAP, "sw_find_specials_device: cap < n_bytes / (shortest special's length)");
+  if (h->ws_pending && h->ws_stream != st) HIP_TRY(hipStreamWaitEvent(st, h->ws_done, 0));
+  const int64_t n_tiles = (n_bytes + kTile - 1) / kTile;
+  if (h->spt.n_first == 0 || n_tiles == 0) {
+    HIP_TRY(hipMemsetAsync(d_count, 0, sizeof(int64_t), st));
+  } else {
+    int32_t rc = ensure_workspace(h, n_bytes);
+    if (rc) return rc;
+    if (n_tiles > h->spf_tiles) {
+      (void)hipFree(h->d_spf); (void)hipFree(h->d_spf_off);
+      h->d_spf = nullptr; h->d_spf_off = nullptr; h->spf_tiles = 0;
+      HIP_TRY(hipMalloc(&h->d_spf, sizeof(uint32_t) * (size_t)n_tiles * (2 * 64 + 2)));
+      HIP_TRY(hipMalloc(&h->d_spf_off, sizeof(int64_t) * (size_t)(n_tiles + (n_tiles + kScanBlock - 1) / kScanBlock + 1)));
+      h->spf_tiles = n_tiles;
+    }
+    SpFind f;
+    f.bytes = d_bytes; f.n_bytes = n_bytes; f.str_off = d_str_off; f.n_str = n_str;
+    f.tile_slo = h->d_tile_slo; f.n_tiles = n_tiles;
+    f.cbits = h->d_spf; f.chosen = h->d_spf + 64 * n_tiles;
+    f.tcand = h->d_spf + 128 * n_tiles; f.tcnt = f.tcand + n_tiles;
+    const dim3 gw((unsigned)((n_tiles + kWaves - 1) / kWaves)), bw(kThreads);
+    hipLaunchKernelGGL(k_tile_strings, dim3((unsigned)((n_tiles + 255) / 256)), dim3(256), 0, st, d_str_off, n_str,
+                       n_tiles, h->d_tile_slo, nullptr);
+    if (h->spt.n_first <= kSpMaxFirstSwar) hipLaunchKernelGGL(k_sp_detect<true>, gw, bw, 0, st, h->spt, f);
+    else hipLaunchKernelGGL(k_sp_detect<false>, gw, bw, 0, st, h->spt, f);
+    hipLaunchKernelGGL(k_sp_resolve, gw, bw, 0, st, h->spt, f);
+    hipLaunchKernelGGL(k_sp_count, gw, bw, 0, st, f);
+    HIP_TRY(launch_scan(st, f.tcnt, n_tiles, h->d_spf_off + n_tiles, h->d_spf_off, d_count));
+    hipLaunchKernelGGL(k_sp_write, gw, bw, 0, st, h->spt, f, (const int64_t*)h->d_spf_off, d_pos, d_len, d_id);
+    HIP_TRY(hipGetLastError());
+  }
+  HIP_TRY(hipEventRecord(h->ws_done, st));
+  h->ws_stream = st;
+  h->ws_pending = true;
   return SW_OK;
 }
 
 int32_t encode_device(sw_encoder* h, const uint8_t* d_bytes, int64_t n_bytes, const int64_t* d_str_off, int64_t n_str,
                       const uint64_t* d_chunk_bits, const DevSpecials& sp, void* d_out_ids, bool out16,
-                      int64_t* d_out_off, void* stream, int64_t* n_tokens_host) {
+                      int64_t* d_out_off, void* stream, int64_t* n_tokens_host, int32_t pattern_call = -1) {
+  if (pattern_call < -1 || pattern_call > SW_PAT_NONE) return fail(SW_ERR_ARG, "sw_encode_device: unknown pattern");
   if (!h || n_bytes < 0 || n_str < 0 || !d_str_off || !d_out_off || (n_bytes > 0 && (!d_bytes || !d_out_ids)))
     return fail(SW_ERR_ARG, "sw_encode_device: bad arguments");
   if (sp.n < 0 || (sp.n > 0 && (!sp.pos || !sp.len || !sp.id)))
@@ -801,6 +964,7 @@ int32_t encode_device(sw_encoder* h, const uint8_t* d_bytes, int64_t n_bytes, co
   if (out16 && sp.n > 0) return fail(SW_ERR_ARG, "sw_encode_device: 16-bit output with special tokens is not supported");
   if (n_bytes > kMaxLaunchBytes) return fail(SW_ERR_ARG, "sw_encode_device: n_bytes > 2^30 - 64 (split the batch)");
   DeviceGuard g(h->device);
+  const int32_t pattern = pattern_call >= 0 ? pattern_call : h->pattern;  // (per call, or the handle's option)
   hipStream_t st = (hipStream_t)stream;  // (NULL: the null stream, as torch's default stream)
   // the workspace belongs to the handle: order this launch after the previous one on any stream
   if (h->ws_pending && h->ws_stream != st) HIP_TRY(hipStreamWaitEvent(st, h->ws_done, 0));
@@ -823,15 +987,15 @@ int32_t encode_device(sw_encoder* h, const uint8_t* d_bytes, int64_t n_bytes, co
     hipLaunchKernelGGL(k_tile_strings, dim3((unsigned)((n_tiles + 255) / 256)), dim3(256), 0, st, d_str_off, n_str,
                        n_tiles, h->d_tile_slo, h->d_lcount);  // (and the long list emptied)
   const SpArgs spa{sp.pos, sp.len, sp.id, sp.n, h->d_tile_sp};
-  if (n_tiles > 0 && sp.n > 0)  // (... and their first special-token occurrence)
-    hipLaunchKernelGGL(k_tile_strings, dim3((unsigned)((n_tiles + 255) / 256)), dim3(256), 0, st, sp.pos, sp.n,
-                       n_tiles, h->d_tile_sp, nullptr);
+  if (n_tiles > 0 && sp.n > 0)  // (... and their first special-token occurrence; the count last)
+    hipLaunchKernelGGL(k_tile_specials, dim3((unsigned)((n_tiles + 1 + 255) / 256)), dim3(256), 0, st, sp.pos, sp.n,
+                       sp.n_dev, n_tiles, h->d_tile_sp);
   // the full path (no caller bitmap): the device pre-split, fused into the classification
   // (k_edges + k_split_classify) or as its own kernel first (SW_OPT_FUSED_PRESPLIT 0; special
   // tokens always take the fused kernel)
   const bool fused = n_tiles > 0 && !d_chunk_bits && (h->fused_presplit || sp.n > 0);
   if (n_tiles > 0 && !d_chunk_bits) {
-    if (!fused) HIP_TRY(launch_presplit(st, d_bytes, n_bytes, d_str_off, n_str, h->pattern, h->d_pbits, h->d_tile_slo));
+    if (!fused) HIP_TRY(launch_presplit(st, d_bytes, n_bytes, d_str_off, n_str, pattern, h->d_pbits, h->d_tile_slo));
     d_chunk_bits = h->d_pbits;
   }
   if (n_tiles > 0) {
@@ -862,18 +1026,18 @@ int32_t encode_device(sw_encoder* h, const uint8_t* d_bytes, int64_t n_bytes, co
     if (fused) {
       const PbArgs pg{d_bytes, n_bytes, d_str_off, n_str, h->d_tile_slo, spa};
       hipLaunchKernelGGL(k_edges, dim3((unsigned)((n_tiles + 1 + 255) / 256)), dim3(256), 0, st, pg, n_tiles,
-                         (int)h->pattern, h->d_edge, h->d_redo);
+                         (int)pattern, h->d_edge, h->d_redo);
       const dim3 gc((unsigned)((n_tiles + kWaves - 1) / kWaves));
       const RedoList redo{h->d_redo, (int64_t*)(h->d_redo + 2)};  // (its count zeroed by k_edges)
       if (sp.n > 0) {
-        hipLaunchKernelGGL(k_split_classify<true>, gc, dim3(kThreads), 0, st, a, pg, (int)h->pattern,
+        hipLaunchKernelGGL(k_split_classify<true>, gc, dim3(kThreads), 0, st, a, pg, (int)pattern,
                            (const uint32_t*)h->d_edge, (uint32_t*)h->d_pbits, redo);
-        hipLaunchKernelGGL(k_split_redo<true>, dim3(kRedoGrid), dim3(kThreads), 0, st, a, pg, (int)h->pattern,
+        hipLaunchKernelGGL(k_split_redo<true>, dim3(kRedoGrid), dim3(kThreads), 0, st, a, pg, (int)pattern,
                            (const uint32_t*)h->d_edge, (uint32_t*)h->d_pbits, redo);
       } else {
-        hipLaunchKernelGGL(k_split_classify<false>, gc, dim3(kThreads), 0, st, a, pg, (int)h->pattern,
+        hipLaunchKernelGGL(k_split_classify<false>, gc, dim3(kThreads), 0, st, a, pg, (int)pattern,
                            (const uint32_t*)h->d_edge, (uint32_t*)h->d_pbits, redo);
-        hipLaunchKernelGGL(k_split_redo<false>, dim3(kRedoGrid), dim3(kThreads), 0, st, a, pg, (int)h->pattern,
+        hipLaunchKernelGGL(k_split_redo<false>, dim3(kRedoGrid), dim3(kThreads), 0, st, a, pg, (int)pattern,
                            (const uint32_t*)h->d_edge, (uint32_t*)h->d_pbits, redo);
       }
     } else if (sp.n > 0) {
@@ -989,9 +1153,30 @@ extern "C" int32_t sw_encode_device_ex(sw_encoder* h, const uint8_t* d_bytes, in
                          stream, n_tokens_host);
   if (ex->out_bits != 16 && ex->out_bits != 32) return fail(SW_ERR_ARG, "sw_encode_device_ex: out_bits 16 or 32");
   DevSpecials sp;
-  sp.pos = ex->sp_pos; sp.len = ex->sp_len; sp.id = ex->sp_id; sp.n = ex->n_sp;
+  sp.pos = ex->sp_pos; sp.len = ex->sp_len; sp.id = ex->sp_id; sp.n = ex->n_sp; sp.n_dev = ex->d_n_sp;
+  if (sp.n_dev && sp.n <= 0) return fail(SW_ERR_ARG, "sw_encode_device_ex: d_n_sp needs n_sp = the arrays' capacity");
   return encode_device(h, d_bytes, n_bytes, d_str_off, n_str, ex->chunk_bits, sp, d_out_ids, ex->out_bits == 16,
-                       d_out_off, stream, n_tokens_host);
+                       d_out_off, stream, n_tokens_host, ex->pattern);
+}
+
+extern "C" int32_t sw_encoder_set_specials(sw_encoder* h, const sw_specials* sp) {
+  if (!h) return fail(SW_ERR_ARG, "sw_encoder_set_specials: null handle");
+  return set_specials(h, sp);
+}
+
+extern "C" int32_t sw_find_specials_device(sw_encoder* h, const uint8_t* d_bytes, int64_t n_bytes,
+                                           const int64_t* d_str_off, int64_t n_str, int64_t* d_pos, int32_t* d_len,
+                                           int32_t* d_id, int64_t cap, int64_t* d_count, void* stream, int64_t* n_host) {
+  if (!h) return fail(SW_ERR_ARG, "sw_find_specials_device: null handle");
+  DeviceGuard g(h->device);
+  const hipStream_t st = (hipStream_t)stream;
+  const int32_t rc = find_specials_device(h, d_bytes, n_bytes, d_str_off, n_str, d_pos, d_len, d_id, cap, d_count, st);
+  if (rc) return rc;
+  if (n_host) {
+    HIP_TRY(hipMemcpyAsync(n_host, d_count, sizeof(int64_t), hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+  }
+  return SW_OK;
 }
 
 // ids to 16 bits for the device -> host copy (every id of an ids16 table fits)
@@ -1003,8 +1188,11 @@ __global__ void k_pack16(const int32_t* in, const int64_t* total, uint16_t* out)
 
 // Pipeline copies as kernels over PCIe: a few hundred waves of 16-byte loads keep enough requests
 // in flight to run a copy at the link rate (about 57 GB/s each way measured, tools/h2d_probe.hip)
-// while the encode kernels run beside them.  Host buffers are hipHostMalloc'd (page aligned), device
-// buffers hipMalloc'd, so every segment starts 16-byte aligned.
+// while the encode kernels run beside them.  Staging buffers are hipHostMalloc'd (page aligned) and
+// device buffers hipMalloc'd, but two paths hand over arbitrary offsets: the caller's pinned input
+// (a run starts at any byte) and the caller's pinned output (a run's ids start at any id), so
+// copy_seg aligns the destination with a head of single bytes and then reads the source as
+// aligned 16-byte blocks, each lane taking its neighbour's block (a shuffle) to realign.
 typedef unsigned int v4u32 __attribute__((ext_vector_type(4)));
 
 constexpr int kCopySegs = 6;
@@ -1014,11 +1202,52 @@ struct CopySegs {
   int64_t n[kCopySegs];
 };
 
+// bytes [r, r + 16) of the 32 bytes lo | hi (0 < r < 16; r wave-uniform)
+__device__ __forceinline__ v4u32 realign16(const v4u32& lo, const v4u32& hi, uint32_t r) {
+  const uint32_t w[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+  const uint32_t sh = r & 3;
+  v4u32 o;
+  switch (r >> 2) {  // (uniform: no dynamically indexed registers)
+    case 0: o = v4u32{__builtin_amdgcn_alignbyte(w[1], w[0], sh), __builtin_amdgcn_alignbyte(w[2], w[1], sh),
+                      __builtin_amdgcn_alignbyte(w[3], w[2], sh), __builtin_amdgcn_alignbyte(w[4], w[3], sh)}; break;
+    case 1: o = v4u32{__builtin_amdgcn_alignbyte(w[2], w[1], sh), __builtin_amdgcn_alignbyte(w[3], w[2], sh),
+                      __builtin_amdgcn_alignbyte(w[4], w[3], sh), __builtin_amdgcn_alignbyte(w[5], w[4], sh)}; break;
+    case 2: o = v4u32{__builtin_amdgcn_alignbyte(w[3], w[2], sh), __builtin_amdgcn_alignbyte(w[4], w[3], sh),
+                      __builtin_amdgcn_alignbyte(w[5], w[4], sh), __builtin_amdgcn_alignbyte(w[6], w[5], sh)}; break;
+    default: o = v4u32{__builtin_amdgcn_alignbyte(w[4], w[3], sh), __builtin_amdgcn_alignbyte(w[5], w[4], sh),
+                       __builtin_amdgcn_alignbyte(w[6], w[5], sh), __builtin_amdgcn_alignbyte(w[7], w[6], sh)}; break;
+  }
+  return o;
+}
+
+// dst[0, n) = src[0, n); t / nt: this thread's index in the grid and the grid's size (whole waves)
 __device__ inline void copy_seg(const uint8_t* src, uint8_t* dst, int64_t n, int64_t t, int64_t nt) {
+  const int64_t head = min<int64_t>(n, (int64_t)((16 - ((uintptr_t)dst & 15)) & 15));
+  for (int64_t i = t; i < head; i += nt) dst[i] = src[i];
+  src += head;
+  dst += head;
+  n -= head;
   const int64_t n16 = n >> 4;
-  const v4u32* s = (const v4u32*)src;
   v4u32* d = (v4u32*)dst;
-  for (int64_t i = t; i < n16; i += nt) d[i] = __builtin_nontemporal_load(s + i);
+  const uint32_t mis = (uint32_t)((uintptr_t)src & 15);
+  if (mis == 0) {
+    const v4u32* s = (const v4u32*)src;
+    for (int64_t i = t; i < n16; i += nt) d[i] = __builtin_nontemporal_load(s + i);
+  } else {
+    // block i of dst = bytes [mis, mis + 16) of the aligned source blocks i, i + 1 (block n16 holds
+    // the last bytes block n16 - 1 needs; it lies in the same 16 bytes, hence the same page, as them)
+    const v4u32* s = (const v4u32*)(src - mis);
+    const int lane = (int)(threadIdx.x & 63);
+    for (int64_t i0 = t - lane; i0 < n16; i0 += nt) {  // (wave-uniform)
+      const int64_t i = i0 + lane;
+      const v4u32 x = i <= n16 ? __builtin_nontemporal_load(s + i) : v4u32{0, 0, 0, 0};
+      v4u32 y;
+      y.x = (uint32_t)__shfl_down((int)x.x, 1, 64); y.y = (uint32_t)__shfl_down((int)x.y, 1, 64);
+      y.z = (uint32_t)__shfl_down((int)x.z, 1, 64); y.w = (uint32_t)__shfl_down((int)x.w, 1, 64);
+      if (lane == 63 && i + 1 <= n16) y = __builtin_nontemporal_load(s + i + 1);
+      if (i < n16) d[i] = realign16(x, y, mis);
+    }
+  }
   for (int64_t i = (n16 << 4) + t; i < n; i += nt) dst[i] = src[i];
 }
 
@@ -1083,6 +1312,8 @@ struct HostSpecials {
   const int32_t* id = nullptr;
   int64_t n = 0;
   bool narrow = true;  // every id fits the 16-bit download (<= 0xFFFD)
+  bool dev = false;    // found on the device, launch by launch (the handle's specials table): pos /
+                       // len / id unused, n = 1
 };
 
 // the occurrences inside bytes [a, b) of the batch: [*j0, *j1)
@@ -1129,7 +1360,9 @@ int32_t encode_batch_pipelined(sw_encoder* h, const uint8_t* bytes, const int64_
     runs.emplace_back(s_lo, s_hi);
     max_b = std::max(max_b, nb);
     max_s = std::max(max_s, s_hi - s_lo);
-    if (sp.n > 0) {
+    if (sp.dev) {
+      max_sp = std::max(max_sp, nb / h->spt_min_len + 1);  // (the finder's capacity for the run)
+    } else if (sp.n > 0) {
       int64_t j0, j1;
       sp_range(sp, str_off[s_lo] - str_off[0], str_off[s_hi] - str_off[0], &j0, &j1);
       max_sp = std::max(max_sp, j1 - j0);
@@ -1195,14 +1428,11 @@ int32_t encode_batch_pipelined(sw_encoder* h, const uint8_t* bytes, const int64_
   if (count) HIP_TRY(hipMemsetAsync(h->d_pcount, 0, sizeof(unsigned long long), h->stream));
   const bool was_timing = h->timing;
   const size_t was_used = h->ev_used;
-  const int32_t was_pattern = h->pattern;
   h->timing = true;
   h->ev_used = 0;
-  if (!chunk_bits) h->pattern = pattern;
   auto restore = [&]() {
     h->timing = was_timing;
     h->ev_used = was_timing ? was_used : 0;
-    h->pattern = was_pattern;
   };
   sw::HostPool& pool = *h->pool;
   double ms_stage = 0, ms_drain = 0;
@@ -1222,7 +1452,9 @@ int32_t encode_batch_pipelined(sw_encoder* h, const uint8_t* bytes, const int64_
     if (!in_dev)
       pool.parallel_for(nb, [&](int64_t lo, int64_t hi) { std::memcpy(p.h_in + lo, src + lo, (size_t)(hi - lo)); });
     for (int64_t j = 0; j <= s_hi - s_lo; ++j) p.h_off[j] = str_off[s_lo + j] - a0;
-    if (sp.n > 0) {  // the run's special-token occurrences, rebased: positions, then lengths and ids (int32)
+    if (sp.dev) {
+      p_nsp[k % h->pipe_depth] = nb / h->spt_min_len + 1;  // (found on the device after the upload)
+    } else if (sp.n > 0) {  // the run's special-token occurrences, rebased: positions, then lengths and ids (int32)
       int64_t j0, j1;
       sp_range(sp, a0 - b0, a0 - b0 + nb, &j0, &j1);
       const int64_t m = j1 - j0;
@@ -1253,7 +1485,7 @@ int32_t encode_batch_pipelined(sw_encoder* h, const uint8_t* bytes, const int64_
     auto& p = h->pipe[k % h->pipe_depth];
     const int64_t s_lo = runs[k].first, s_hi = runs[k].second, nb = str_off[s_hi] - str_off[s_lo], ns = s_hi - s_lo;
     const int64_t n_bits = chunk_bits ? (int64_t)sizeof(uint64_t) * ((nb + 63) / 64) : 0;
-    const int64_t m_sp = sp.n > 0 ? p_nsp[k % h->pipe_depth] : 0, n_sp_bytes = 16 * m_sp;  // (8 + 4 + 4 B each)
+    const int64_t m_sp = sp.n > 0 ? p_nsp[k % h->pipe_depth] : 0, n_sp_bytes = sp.dev ? 0 : 16 * m_sp;  // (8 + 4 + 4 B each)
     if (h->pipe_kcopy) {
       const uint8_t* in_src = in_dev ? in_dev + (str_off[s_lo] - b0) : p.h_in;
       const CopySegs c{{in_src, (const uint8_t*)p.h_off, (const uint8_t*)p.h_bits, (const uint8_t*)p.h_sp, nullptr, nullptr},
@@ -1273,8 +1505,15 @@ int32_t encode_batch_pipelined(sw_encoder* h, const uint8_t* bytes, const int64_
     if (m_sp > 0) {
       dsp.pos = p.d_sp; dsp.len = (const int32_t*)(p.d_sp + m_sp); dsp.id = dsp.len + m_sp; dsp.n = m_sp;
     }
+    if (sp.dev) {  // the occurrences found on the device, the count left there (p.d_sp's tail)
+      int64_t* d_cnt = p.d_sp + 2 * m_sp;
+      const int32_t r = find_specials_device(h, p.d_in, nb, p.d_off, ns, p.d_sp, (int32_t*)dsp.len, (int32_t*)dsp.id,
+                                             m_sp, d_cnt, h->stream);
+      if (r) return r;
+      dsp.n_dev = d_cnt;
+    }
     const int32_t r = encode_device(h, p.d_in, nb, p.d_off, ns, chunk_bits ? p.d_bits : nullptr, dsp, p.d_out, false,
-                                    p.d_oo, h->stream, nullptr);
+                                    p.d_oo, h->stream, nullptr, pattern);
     if (r) return r;
     if (count && nb > 0)
       hipLaunchKernelGGL(k_popcount, dim3(1024), dim3(256), 0, h->stream, h->d_pbits, (nb + 63) / 64, h->d_pcount);
@@ -1425,7 +1664,7 @@ int32_t encode_batch_impl(sw_encoder* h, const uint8_t* bytes, const int64_t* st
       HostSpecials ssp = sp;  // (the run's occurrences, rebased to its first byte)
       int64_t j0 = 0, j1 = 0;
       std::vector<int64_t> spos;
-      if (sp.n > 0) {
+      if (sp.n > 0 && !sp.dev) {
         const int64_t g0 = str_off[s_lo] - b0;
         sp_range(sp, g0, str_off[s_hi] - b0, &j0, &j1);
         spos.resize((size_t)(j1 - j0));
@@ -1476,14 +1715,16 @@ int32_t encode_batch_impl(sw_encoder* h, const uint8_t* bytes, const int64_t* st
     HIP_TRY(hipMalloc(&h->d_out_off, sizeof(int64_t) * (ns + 1)));
     h->io_bytes = nb; h->io_str = ns;
   }
-  if (sp.n > h->sp_cap) {
+  const int64_t sp_need = sp.dev ? n_bytes / h->spt_min_len + 1 : sp.n;  // (the device finder's capacity)
+  if (sp_need > h->sp_cap) {
     (void)hipFree(h->d_sp_pos); (void)hipFree(h->d_sp_len); (void)hipFree(h->d_sp_id);
     h->d_sp_pos = nullptr; h->d_sp_len = nullptr; h->d_sp_id = nullptr; h->sp_cap = 0;
-    HIP_TRY(hipMalloc(&h->d_sp_pos, sizeof(int64_t) * sp.n));
-    HIP_TRY(hipMalloc(&h->d_sp_len, sizeof(int32_t) * sp.n));
-    HIP_TRY(hipMalloc(&h->d_sp_id, sizeof(int32_t) * sp.n));
-    h->sp_cap = sp.n;
+    HIP_TRY(hipMalloc(&h->d_sp_pos, sizeof(int64_t) * sp_need));
+    HIP_TRY(hipMalloc(&h->d_sp_len, sizeof(int32_t) * sp_need));
+    HIP_TRY(hipMalloc(&h->d_sp_id, sizeof(int32_t) * sp_need));
+    h->sp_cap = sp_need;
   }
+  if (sp.dev && !h->d_nsp) HIP_TRY(hipMalloc(&h->d_nsp, sizeof(int64_t)));
   std::vector<int64_t> rel((size_t)n_str + 1);
   for (int64_t s = 0; s <= n_str; ++s) rel[s] = n_str > 0 ? str_off[s] - b0 : 0;
   auto a = std::chrono::steady_clock::now();
@@ -1495,7 +1736,12 @@ int32_t encode_batch_impl(sw_encoder* h, const uint8_t* bytes, const int64_t* st
   }
   HIP_TRY(hipMemcpyAsync(h->d_str_off, rel.data(), sizeof(int64_t) * (n_str + 1), hipMemcpyHostToDevice, st));
   DevSpecials dsp;
-  if (sp.n > 0) {
+  if (sp.dev) {
+    const int32_t r = find_specials_device(h, h->d_bytes, n_bytes, h->d_str_off, n_str, h->d_sp_pos, h->d_sp_len,
+                                           h->d_sp_id, h->sp_cap, h->d_nsp, st);
+    if (r) return r;
+    dsp.pos = h->d_sp_pos; dsp.len = h->d_sp_len; dsp.id = h->d_sp_id; dsp.n = h->sp_cap; dsp.n_dev = h->d_nsp;
+  } else if (sp.n > 0) {
     HIP_TRY(hipMemcpyAsync(h->d_sp_pos, sp.pos, sizeof(int64_t) * sp.n, hipMemcpyHostToDevice, st));
     HIP_TRY(hipMemcpyAsync(h->d_sp_len, sp.len, sizeof(int32_t) * sp.n, hipMemcpyHostToDevice, st));
     HIP_TRY(hipMemcpyAsync(h->d_sp_id, sp.id, sizeof(int32_t) * sp.n, hipMemcpyHostToDevice, st));
@@ -1508,11 +1754,8 @@ int32_t encode_batch_impl(sw_encoder* h, const uint8_t* bytes, const int64_t* st
   const size_t was_used = h->ev_used;
   h->timing = true;
   h->ev_used = 0;
-  const int32_t was_pattern = h->pattern;
-  if (device_presplit) h->pattern = pattern;
   int32_t rc = encode_device(h, h->d_bytes, n_bytes, h->d_str_off, n_str, device_presplit ? nullptr : h->d_bits, dsp,
-                             h->d_out, false, h->d_out_off, st, &n_tok);
-  h->pattern = was_pattern;
+                             h->d_out, false, h->d_out_off, st, &n_tok, pattern);
   if (rc == SW_OK && device_presplit && stats && n_bytes > 0) {  // chunk count for the stats
     HIP_TRY(hipMemsetAsync(h->d_pcount, 0, sizeof(unsigned long long), st));
     hipLaunchKernelGGL(k_popcount, dim3(1024), dim3(256), 0, st, h->d_pbits, n_words, h->d_pcount);
@@ -1563,6 +1806,23 @@ extern "C" int32_t sw_encode_batch_ex(sw_encoder* h, const uint8_t* bytes, const
   for (int64_t k = 0; k < specials->n; ++k)
     if (specials->ids && (specials->ids[k] < 0 || specials->ids[k] == INT32_MAX))
       return fail(SW_ERR_ARG, "sw_encode_batch_ex: special token ids must be in [0, 2^31 - 2]");
+  // the device finder: every special <= 64 bytes, the device pre-split (the host pre-split needs the
+  // occurrences on the host), and room for its worst case (n / shortest special occurrences)
+  if (h->device_specials && !chunk_bits && !h->host_presplit) {
+    int32_t rc = set_specials(h, specials);
+    if (rc) return rc;
+    const int64_t nb = n_str > 0 ? str_off[n_str] - str_off[0] : 0;
+    const int64_t run = h->pipe_run > 0 && nb > 2 * h->pipe_run ? std::min(h->pipe_run, h->max_launch)
+                                                                   : std::min(nb, h->max_launch);
+    if (h->spt_dev && 16 * (run / h->spt_min_len + 1) <= (int64_t)1 << 31) {
+      HostSpecials sp;
+      sp.dev = true;
+      sp.n = 1;
+      for (int64_t k = 0; k < specials->n; ++k)
+        if (specials->ids[k] > 0xFFFD) sp.narrow = false;
+      return encode_batch_impl(h, bytes, str_off, n_str, pattern, chunk_bits, sp, out_ids, out_cap, out_off, stats);
+    }
+  }
   const int64_t cnt = sw_find_specials_host(bytes, str_off, n_str, specials, nullptr, nullptr, nullptr, 0, 0);
   if (cnt < 0) return fail((int32_t)cnt, "sw_encode_batch_ex: bad special tokens or string offsets");
   std::vector<int64_t> pos((size_t)std::max<int64_t>(cnt, 1));

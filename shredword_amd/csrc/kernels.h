@@ -36,11 +36,22 @@ constexpr int kTileBits = 11;
 constexpr int kTile = 1 << kTileBits;        // input bytes per classify workgroup
 constexpr int kThreads = 256;                // 4 waves
 constexpr int kWaves = kThreads / 64;
-// this thread's wave in its workgroup.  (As a scalar, __builtin_amdgcn_readfirstlane, the compiler
-// keeps the tile indices in SGPRs: k_split_classify 80 VGPRs + 40 B of scratch -> 75 VGPRs, no
-// scratch, but it ran 180x slower for a reason not found (r4i-r4k A/B: not kernarg placement, not
-// a missing wait), and k_compact got no faster: not used)
+// this thread's wave in its workgroup
 __device__ __forceinline__ int wave_in_block() { return (int)(threadIdx.x >> 6); }
+// ... as a scalar (readfirstlane): the compiler then keeps the tile indices in SGPRs.
+// k_split_classify: 80 VGPRs + 40 B of scratch -> 75-80 VGPRs, no scratch, 3.12 -> 3.03 ms
+// (r6b A/B).  Only where it is tested exact: with it in every kernel a batch cut into 2-tile
+// launches got wrong string offsets (r6d; not yet explained).
+#ifndef SW_WAVE_SCALAR
+#define SW_WAVE_SCALAR 0
+#endif
+__device__ __forceinline__ int wave_in_block_s() {
+#if SW_WAVE_SCALAR
+  return __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+#else
+  return (int)(threadIdx.x >> 6);
+#endif
+}
 constexpr int kShort = 32;                   // per-lane merge loop up to this many bytes
 constexpr int kWin = kTile + 64;             // LDS byte window (tile + halo for key reads)
 constexpr int kTileWords = kTile / 64 + 1;   // bitmap words staged (tile + 64-bit halo)
@@ -69,12 +80,19 @@ __host__ __device__ inline uint32_t slot_did(int32_t v) { return (uint32_t)(-(in
 // so 99.9% of the shared results (2-3 ids typical, 7 at most for a 32k vocabulary on prose)
 // need no second read.  A reference list entry (rlist) is p or kRlDense | d.
 constexpr uint32_t kRlDense = 0x80000000u;
+// a tile's chunk-start list (uint16, tile-relative positions < kTile): bit 15 marks a chunk that is a
+// special-token occurrence (its slot already holds the special's id), and lookups skip it
+constexpr uint32_t kCsPos = 0x7FFFu, kCsSpecial = 0x8000u;
+constexpr uint32_t kSpDone = 0xFFFFFFFEu;  // (table_lookups: the chunk's slot is written already)
 constexpr uint32_t kNoDid = 0x7FFFFFFu;    // (27-bit dense result field of a queue entry: none)
 constexpr int64_t kDdSlotsDefault = 1LL << 22;  // dedupe table entries at most to start with (32 MiB)
 constexpr int64_t kDdSlotsMax = 1LL << 26;      // ... and after growing (a queue entry's dense field: 27 bits)
 constexpr int kDdExactMax = 7;             // dedupe keys of <= this many bytes are exact (no verification)
 #ifndef SW_PAIR_MAX_N
 #define SW_PAIR_MAX_N 16                   // k_merge_bucket<N>: two chunks per lane up to this N (0: never)
+#endif
+#ifndef SW_QUAD_MAX_N
+#define SW_QUAD_MAX_N 4                    // ... and four up to this N (0: never)
 #endif
 
 // streaming accesses (read or written once per launch) carry the non-temporal hint, so the
@@ -165,7 +183,7 @@ __device__ __forceinline__ void regs_barrier(u32x4 (&x)[R], u32x4 (&y)[R]) {
 // and round is loaded (16 bytes for 2..8-byte chunks, 32 for 9..16), one wait, the compares,
 // then the (rare) second candidates the same way.  The chunk's bytes are read from the LDS
 // window again after the wait rather than held in registers across it.
-template <int R>
+template <int R, bool kSp>
 __device__ __forceinline__ void table_lookups(const DevChunkTable& c, const uint32_t* s_b32, const uint16_t* s_cstart,
                                               int C, int rel_end, int r0, int lane, uint32_t (&tok)[R]) {
   u32x4 qa[R], qb[R];
@@ -176,11 +194,13 @@ __device__ __forceinline__ void table_lookups(const DevChunkTable& c, const uint
   for (int u = 0; u < R; ++u) {  // first candidates: issue (the 32-byte entries' second half only
     const int k = ((r0 + u) << 6) + lane;  // for 9..16-byte chunks: no extra request for the rest)
     const bool valid = k < C;
-    const int ls = valid ? s_cstart[k] : 0;
-    const int end = (k + 1 < C) ? (int)s_cstart[k + 1] : rel_end;
-    len[u] = valid ? end - ls : 0;
+    const uint32_t cs = valid ? s_cstart[k] : 0u;
+    const int ls = (int)(cs & kCsPos);
+    const int end = (k + 1 < C) ? (int)(s_cstart[k + 1] & kCsPos) : rel_end;
+    const bool sp = kSp && (cs & kCsSpecial);  // (a special-token occurrence: its slot is written)
+    len[u] = valid && !sp ? end - ls : 0;
     window_words(s_b32, ls, min(max(len[u], 1), 16), w[u]);
-    tok[u] = len[u] == 1 ? (w[u][0] & 0xFFu) : kInf;
+    tok[u] = sp ? kSpDone : len[u] == 1 ? (w[u][0] & 0xFFu) : kInf;
     const uint4* pa = c.sb;  // (a lane without a probe loads the first bucket, unused)
     if (len[u] >= 2 && len[u] <= 8) pa = &c.sb[chunk_b1(chunk_hash(w[u][0], w[u][1], 0, 0, len[u], c.s_m1), c.s_shift)];
     if (len[u] > 8 && len[u] <= 16)
@@ -572,25 +592,26 @@ __device__ __forceinline__ uint32_t lane_merge_lds_wf(const DevTable& t, const u
   return alive;
 }
 
-// lane_merge_lds_wf for TWO chunks per lane, run side by side: every step of both loops issues
-// its lookups before either waits, so a lane keeps twice the lookups in flight (the merge loop
+// lane_merge_lds_wf for Q chunks per lane (2 or 4), run side by side: every step of every loop
+// issues its lookups before any waits, so a lane keeps Q times the lookups in flight (the merge loop
 // without memoisation is a chain of dependent L2-hit lookups per chunk, not work: 66-71% of its
-// wave cycles were issue stalls, profiles/r3n_none.md).  Chunk q's ids at s_id[64 (q N + k) + l].
-template <bool kWide, int N>
-__device__ __forceinline__ void lane_merge_lds_wf2(const DevTable& t, const uint32_t (&u)[2][N / 4], const int (&n)[2],
-                                                   uint32_t* s_id, int lane, uint32_t (&alive)[2]) {
+// wave cycles were issue stalls, profiles/r3n_none.md; the short buckets take 4 per lane: their
+// loops are a few steps each, almost all waiting).  Chunk q's ids at s_id[64 (q N + k) + l].
+template <bool kWide, int N, int Q>
+__device__ __forceinline__ void lane_merge_lds_wfq(const DevTable& t, const uint32_t (&u)[Q][N / 4], const int (&n)[Q],
+                                                   uint32_t* s_id, int lane, uint32_t (&alive)[Q]) {
   static_assert(N <= 32, "alive masks are 32 bits");
   constexpr uint32_t KINF = 0xFFFFu << 5;
-  uint32_t rk[2][N];
+  uint32_t rk[Q][N];
 #pragma unroll
-  for (int q = 0; q < 2; ++q)
+  for (int q = 0; q < Q; ++q)
 #pragma unroll
     for (int k = 0; k < N; ++k) s_id[64 * (q * N + k) + lane] = (u[q][k >> 2] >> (8 * (k & 3))) & 0xFFu;
   // initial ranks: four lookups of each chunk in flight at a time
 #pragma unroll
   for (int g = 0; g < N; g += 4) {
 #pragma unroll
-    for (int q = 0; q < 2; ++q)
+    for (int q = 0; q < Q; ++q)
 #pragma unroll
       for (int k = g; k < g + 4 && k < N; ++k) {
         const uint32_t b0 = (u[q][k >> 2] >> (8 * (k & 3))) & 0xFFu;
@@ -598,7 +619,7 @@ __device__ __forceinline__ void lane_merge_lds_wf2(const DevTable& t, const uint
         rk[q][k] = lookup<kWide>(t, b0, b1);
       }
 #pragma unroll
-    for (int q = 0; q < 2; ++q) {
+    for (int q = 0; q < Q; ++q) {
 #pragma unroll
       for (int k = g; k < g + 4 && k < N; ++k)
         rk[q][k] = ((k + 1 < n[q]) ? (min(rk[q][k], 0xFFFFu) << 5) : KINF) | (uint32_t)k;
@@ -606,12 +627,12 @@ __device__ __forceinline__ void lane_merge_lds_wf2(const DevTable& t, const uint
     }
   }
 #pragma unroll
-  for (int q = 0; q < 2; ++q) alive[q] = (n[q] >= 32) ? 0xFFFFFFFFu : ((1u << n[q]) - 1u);
+  for (int q = 0; q < Q; ++q) alive[q] = (n[q] >= 32) ? 0xFFFFFFFFu : ((1u << n[q]) - 1u);
   while (true) {
-    uint32_t need[2];
+    uint32_t need[Q];
     bool any = false;
 #pragma unroll
-    for (int q = 0; q < 2; ++q) {  // one step of each chunk's loop (base.py:10-36), as lane_merge_lds_wf
+    for (int q = 0; q < Q; ++q) {  // one step of each chunk's loop (base.py:10-36), as lane_merge_lds_wf
       const uint32_t best = tree_min<N>(rk[q]);
       const uint32_t nv = best >> 5;
       need[q] = 0;
@@ -638,11 +659,15 @@ __device__ __forceinline__ void lane_merge_lds_wf2(const DevTable& t, const uint
       for (int k = 0; k < N; ++k) rk[q][k] = ((kill >> k) & 1u) ? (KINF | (uint32_t)k) : rk[q][k];
     }
     if (!any) break;
-    while (need[0] | need[1]) {  // two lookups of each chunk in flight per round
-      int j1[2], j2[2];
-      uint32_t k1[2], k2[2];
+    while (true) {  // two lookups of each chunk in flight per round
+      uint32_t pend = 0;
 #pragma unroll
-      for (int q = 0; q < 2; ++q) {
+      for (int q = 0; q < Q; ++q) pend |= need[q];
+      if (!pend) break;
+      int j1[Q], j2[Q];
+      uint32_t k1[Q], k2[Q];
+#pragma unroll
+      for (int q = 0; q < Q; ++q) {
         j1[q] = need[q] ? __ffs(need[q]) - 1 : -1;
         need[q] &= need[q] - 1;
         j2[q] = need[q] ? __ffs(need[q]) - 1 : j1[q];
@@ -657,7 +682,7 @@ __device__ __forceinline__ void lane_merge_lds_wf2(const DevTable& t, const uint
         k2[q] = (min(lookup<kWide>(t, ia2, ib2), 0xFFFFu) << 5) | (uint32_t)a2;
       }
 #pragma unroll
-      for (int q = 0; q < 2; ++q) {
+      for (int q = 0; q < Q; ++q) {
         if (j1[q] < 0) continue;
 #pragma unroll
         for (int k = 0; k < N; ++k) {
@@ -760,14 +785,15 @@ __device__ __forceinline__ int64_t coop_merge(const DevTable& t, uint32_t* id, u
 // arguments shared by the pipeline's kernels
 // ---------------------------------------------------------------------------------------
 // special-token occurrences of a launch (E1; sw_encode_ex): ascending, non-overlapping, each
-// inside one string and one chunk of its own; tile_sp[t]: the first one starting at or after
-// tile t's first byte (k_tile_strings)
+// inside one string and one chunk of its own; tile_sp[t] (t <= n_tiles): the first one starting at
+// or after tile t's first byte (k_tile_specials), so tile_sp[n_tiles] is the live count -- the
+// host's, or the one the device finder left in device memory (n is then only the capacity)
 struct SpArgs {
   const int64_t* pos;
   const int32_t* len;
   const int32_t* id;
-  int64_t n;
-  const int64_t* tile_sp;
+  int64_t n;                 // > 0: the launch has occurrences (at most n)
+  const int64_t* tile_sp;    // [n_tiles + 1]
 };
 
 struct EncArgs {
@@ -1071,6 +1097,24 @@ __device__ __forceinline__ void classify_chunks(const EncArgs& a, int64_t tile, 
     }
   }
   wave_sync_mem();
+  if (kSp) {  // the special-token occurrences starting in the tile (each one whole chunk): their
+              // slots get the specials' ids, their chunks the flag the lookups skip -- once per tile
+    const int64_t sp_lo = a.sp.tile_sp[tile];
+    const int64_t sp_hi = a.sp.tile_sp[tile + 1];
+    for (int64_t j = sp_lo + lane; j < sp_hi; j += 64) {
+      const int p = (int)(a.sp.pos[j] - t0);
+      int lo = 0, hi = C;  // (its chunk: the first whose start is >= p, and it starts at p)
+      while (lo < hi) {
+        const int m = (lo + hi) >> 1;
+        if ((int)(s_cstart[m] & kCsPos) < p) lo = m + 1; else hi = m;
+      }
+      if (lo < C && (int)s_cstart[lo] == p) {
+        s_cstart[lo] = (uint16_t)(p | kCsSpecial);
+        SW_STNT(&a.scratch[t0 + lo], (int32_t)a.sp.id[j]);
+      }
+    }
+    wave_sync_mem();
+  }
   SW_STAMP(0);
 
   // 3. settle single bytes and whole-chunk-table hits (their slots written here).  The rest
@@ -1084,9 +1128,6 @@ __device__ __forceinline__ void classify_chunks(const EncArgs& a, int64_t tile, 
   const uint32_t* gwords = (const uint32_t*)((uintptr_t)a.bytes - mis);
   const int64_t last_word = (mis + a.n_bytes - 1) >> 2;
   uint32_t bcount = 0;
-  // special-token occurrences starting in the tile (wave-uniform; none without specials)
-  const int64_t sp_lo = kSp ? a.sp.tile_sp[tile] : 0;
-  const int64_t sp_hi = kSp ? (tile + 1 < a.n_tiles ? a.sp.tile_sp[tile + 1] : a.sp.n) : 0;
   int nq = 0;    // wave-uniform: chunks waiting in s_qbuf
   int nown = 0;  // wave-uniform: chunks queued for the merge kernels
   int nref = 0;  // wave-uniform: slots that refer to a merge result (k_tile_count's list)
@@ -1095,24 +1136,17 @@ __device__ __forceinline__ void classify_chunks(const EncArgs& a, int64_t tile, 
     if (r0 < rounds) {
       uint32_t tok[kLookRounds];
       if (use_table) {
-        table_lookups<kLookRounds>(a.chunks, s_b32, s_cstart, C, rel_end, r0, lane, tok);
+        table_lookups<kLookRounds, kSp>(a.chunks, s_b32, s_cstart, C, rel_end, r0, lane, tok);
       } else {
 #pragma unroll
         for (int u = 0; u < kLookRounds; ++u) {  // (no table: single bytes only)
           const int k = ((r0 + u) << 6) + lane;
           const bool valid = k < C;
-          const int ls = valid ? s_cstart[k] : 0;
-          const int end = (k + 1 < C) ? (int)s_cstart[k + 1] : rel_end;
-          tok[u] = (valid && end - ls == 1) ? (s_b32[ls >> 2] >> (8 * (ls & 3))) & 0xFFu : kInf;
-        }
-      }
-      if (kSp && sp_lo < sp_hi) {  // special-token occurrences starting in the tile: their ids
-#pragma unroll
-        for (int u = 0; u < kLookRounds; ++u) {
-          const int k = ((r0 + u) << 6) + lane;
-          const int ls = k < C ? (int)s_cstart[k] : -1;
-          for (int64_t j = sp_lo; j < sp_hi; ++j)
-            if (ls == (int)(a.sp.pos[j] - t0)) tok[u] = (uint32_t)a.sp.id[j];
+          const uint32_t cs = valid ? s_cstart[k] : 0u;
+          const int ls = (int)(cs & kCsPos);
+          const int end = (k + 1 < C) ? (int)(s_cstart[k + 1] & kCsPos) : rel_end;
+          tok[u] = (kSp && (cs & kCsSpecial)) ? kSpDone
+                   : (valid && end - ls == 1) ? (s_b32[ls >> 2] >> (8 * (ls & 3))) & 0xFFu : kInf;
         }
       }
 #pragma unroll
@@ -1120,7 +1154,7 @@ __device__ __forceinline__ void classify_chunks(const EncArgs& a, int64_t tile, 
         const int k = ((r0 + u) << 6) + lane;
         const bool valid = k < C;
         const bool queued = valid && tok[u] == kInf;
-        if (valid && !queued) SW_STNT(&dst[k], (int32_t)tok[u]);
+        if (valid && !queued && (!kSp || tok[u] != kSpDone)) SW_STNT(&dst[k], (int32_t)tok[u]);
         const uint64_t mq = __ballot(queued);
         if (queued) s_qbuf[nq + __popcll(mq & lt_mask)] = (uint16_t)k;
         nq += __popcll(mq);
@@ -1139,8 +1173,8 @@ __device__ __forceinline__ void classify_chunks(const EncArgs& a, int64_t tile, 
       for (int q = 1; q < kQBuf / 64; ++q)
         if (64 * q + lane < nq) s_qbuf[64 * (q - 1) + lane] = rest[q - 1];
       nq = nq > 64 ? nq - 64 : 0;
-      const int ls = act ? s_cstart[k] : 0;
-      const int end = (k + 1 < C) ? (int)s_cstart[k + 1] : rel_end;
+      const int ls = act ? (int)(s_cstart[k] & kCsPos) : 0;
+      const int end = (k + 1 < C) ? (int)(s_cstart[k + 1] & kCsPos) : rel_end;
       const int len = act ? end - ls : 0;
       DdOut dd{0, 0};
       if (act && a.dedupe && len <= kShort) {
@@ -1205,14 +1239,25 @@ __device__ __forceinline__ void classify_chunks(const EncArgs& a, int64_t tile, 
   SW_STAMP(2);
 
   // 6. strings starting in this tile: chunk (= slot) index within the tile (k_compact converts)
-  for (int64_t s = s_first + lane; s < a.n_str; s += 64) {
+  //    (the first one read here, not held in a register through the tile: with a scalar tile index
+  //    this is a scalar load)
+#ifndef SW_LATE_SFIRST
+#define SW_LATE_SFIRST 1
+#endif
+#if SW_LATE_SFIRST
+  (void)s_first;
+  const int64_t s_first_now = a.tile_slo[tile];
+#else
+  const int64_t s_first_now = s_first;
+#endif
+  for (int64_t s = s_first_now + lane; s < a.n_str; s += 64) {
     const int64_t p = a.str_off[s];
     if (p >= t1) break;
     int lo = 0, hi = C;  // first chunk with start >= p
     const int lp = (int)(p - t0);
     while (lo < hi) {
       const int m = (lo + hi) >> 1;
-      if (s_cstart[m] < lp) lo = m + 1; else hi = m;
+      if ((int)(s_cstart[m] & kCsPos) < lp) lo = m + 1; else hi = m;
     }
     a.out_off[s] = (int64_t)lo;
   }
@@ -1442,30 +1487,36 @@ __global__ void __launch_bounds__(kThreads) k_merge_bucket(EncArgs a, int b_lo, 
   const uint32_t* words = (const uint32_t*)((uintptr_t)a.bytes - mis);
   const int64_t last_word = (mis + a.n_bytes - 1) >> 2;  // last word holding input bytes
   constexpr bool kLds = kWF && k16 && !kWide;
-  // two chunks per lane (lane_merge_lds_wf2) for the short buckets of well-formed 16-bit tables
-  constexpr bool kPair = kLds && N <= SW_PAIR_MAX_N;
-  constexpr int kPer = kPair ? 2 : 1;
+  // two or four chunks per lane (lane_merge_lds_wfq) for the short buckets of well-formed 16-bit tables
+  constexpr int kPer = !kLds ? 1 : N <= SW_QUAD_MAX_N ? 4 : N <= SW_PAIR_MAX_N ? 2 : 1;
   __shared__ uint32_t s_ids[kLds ? kWaves * 64 * N * kPer : 1];  // (lane_merge_lds_wf: the waves' ids)
   uint32_t* s_id = s_ids + (kLds ? wave_in_block() * 64 * N * kPer : 0);
-  if constexpr (kPair) {  // batches of 128 entries per wave: entries base + lane and base + 64 + lane
-    int64_t i = lo + gw * 128 + lane;
-    uint64_t e0 = i < hi ? a.queue[i] : 0, e1 = i + 64 < hi ? a.queue[i + 64] : 0;
-    for (int64_t base = lo + gw * 128; base < hi; base += n_waves * 128) {
-      uint32_t u[2][N / 4];
-      int n[2];
-      n[0] = i < hi ? (int)((e0 >> 27) & 63u) : 0;
-      n[1] = i + 64 < hi ? (int)((e1 >> 27) & 63u) : 0;
-      chunk_words<N>(words, last_word, (int64_t)(e0 >> 33) + mis, n[0], u[0]);
-      chunk_words<N>(words, last_word, (int64_t)(e1 >> 33) + mis, n[1], u[1]);
-      const int64_t i2 = i + n_waves * 128;
-      const uint64_t f0 = i2 < hi ? a.queue[i2] : 0, f1 = i2 + 64 < hi ? a.queue[i2 + 64] : 0;
-      uint32_t alive[2];
-      lane_merge_lds_wf2<kWide, N>(a.table, u, n, s_id, lane, alive);
-      if (i < hi) put_lds_result(a, e0, alive[0], s_id, lane);
-      if (i + 64 < hi) put_lds_result(a, e1, alive[1], s_id + 64 * N, lane);
+  if constexpr (kPer > 1) {  // batches of 64 kPer entries per wave: entries base + 64 q + lane
+    constexpr int kB = 64 * kPer;
+    int64_t i = lo + gw * kB + lane;
+    uint64_t e[kPer];
+#pragma unroll
+    for (int q = 0; q < kPer; ++q) e[q] = i + 64 * q < hi ? a.queue[i + 64 * q] : 0;
+    for (int64_t base = lo + gw * kB; base < hi; base += n_waves * kB) {
+      uint32_t u[kPer][N / 4];
+      int n[kPer];
+#pragma unroll
+      for (int q = 0; q < kPer; ++q) {
+        n[q] = i + 64 * q < hi ? (int)((e[q] >> 27) & 63u) : 0;
+        chunk_words<N>(words, last_word, (int64_t)(e[q] >> 33) + mis, n[q], u[q]);
+      }
+      const int64_t i2 = i + n_waves * kB;
+      uint64_t f[kPer];
+#pragma unroll
+      for (int q = 0; q < kPer; ++q) f[q] = i2 + 64 * q < hi ? a.queue[i2 + 64 * q] : 0;
+      uint32_t alive[kPer];
+      lane_merge_lds_wfq<kWide, N, kPer>(a.table, u, n, s_id, lane, alive);
+#pragma unroll
+      for (int q = 0; q < kPer; ++q)
+        if (i + 64 * q < hi) put_lds_result(a, e[q], alive[q], s_id + 64 * N * q, lane);
       i = i2;
-      e0 = f0;
-      e1 = f1;
+#pragma unroll
+      for (int q = 0; q < kPer; ++q) e[q] = f[q];
     }
     return;
   }
@@ -1867,6 +1918,21 @@ __global__ void k_tile_strings(const int64_t* str_off, int64_t n_str, int64_t n_
     if (str_off[m] < t0) lo = m + 1; else hi = m;
   }
   tile_slo[t] = lo;
+}
+
+// tile_sp[t], t in [0, n_tiles]: the first special-token occurrence starting at or after byte
+// t * kTile; the count is n, or *n_dev (the device finder's) when n_dev is given
+__global__ void k_tile_specials(const int64_t* pos, int64_t n, const int64_t* n_dev, int64_t n_tiles, int64_t* tile_sp) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t > n_tiles) return;
+  const int64_t cnt = n_dev ? min(max(*n_dev, (int64_t)0), n) : n;
+  const int64_t t0 = t * kTile;
+  int64_t lo = 0, hi = cnt;
+  while (lo < hi) {
+    const int64_t m = (lo + hi) >> 1;
+    if (pos[m] < t0) lo = m + 1; else hi = m;
+  }
+  tile_sp[t] = lo;
 }
 
 // ---------------------------------------------------------------------------------------

@@ -94,6 +94,42 @@ struct RegBytes {
   }
 };
 
+// v_perm_b32: byte k of the result = byte sel_k of the 8 bytes hi:lo (selectors 0..7 here; 12
+// gives 0x00)
+SW_HD inline uint32_t perm_b32(uint32_t hi, uint32_t lo, uint32_t sel) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __builtin_amdgcn_perm(hi, lo, sel);
+#else
+  const uint64_t v = ((uint64_t)hi << 32) | lo;
+  uint32_t r = 0;
+  for (int k = 0; k < 4; ++k) {
+    const uint32_t q = (sel >> (8 * k)) & 0xFFu;
+    const uint32_t byte = q < 8 ? (uint32_t)(v >> (8 * q)) & 0xFFu : q == 12 ? 0u : q >= 13 ? 0xFFu : 0u;
+    r |= byte << (8 * k);
+  }
+  return r;
+#endif
+}
+
+// ASCII classes of 4 bytes at once, one class byte per byte: T = Thi[high nibble] & Tlo[low nibble]
+// (three v_perm_b32 table lookups: 8 entries each, the low nibble's 16 in two halves), with
+//   bit 7 L (0x41..0x4F, 0x61..0x6F)  bit 3 L (0x50..0x5A, 0x70..0x7A)  bit 6 N (0-9)
+//   bit 2 C (\n \r)                  bit 5 P (space)                     bit 1 H (\t \v \f)
+//   bit 4 A (apostrophe)
+// so that one multiply gathers two classes (bits 7 and 3 of each byte).  Bytes >= 0x80 get
+// garbage here; the caller clears them with the non-ASCII bits at mask level.
+SW_HD inline uint32_t ascii_class4(uint32_t x) {
+  const uint32_t lo = x & 0x07070707u;
+  const uint32_t pa = perm_b32(0xD8C8C8C8u, 0xC8C8C868u, lo);   // low nibble 0..7
+  const uint32_t pb = perm_b32(0x80808482u, 0x828CCAC8u, lo);   // low nibble 8..15
+  const uint32_t nm8 = perm_b32(0xFFFFFFFFu, 0u, (x & 0x08080808u) | 0x04040404u);  // 0xFF where nibble < 8
+  const uint32_t tlo = (nm8 & pa) | (~nm8 & pb);
+  const uint32_t thi = perm_b32(0x08800880u, 0x40300006u, (x >> 4) & 0x07070707u);
+  return tlo & thi;
+}
+// bits 7 and 3 of each byte lane of x -> 8 bits: bits 4..7 (bit 7s), bits 0..3 (bit 3s)
+SW_HD inline uint32_t mm8(uint32_t x) { return ((x & 0x88888888u) * 0x00204081u) >> 24; }
+
 // The class of a code point in one of the big single-class ranges of the most common non-ASCII
 // scripts, from registers; -1 when cp is outside them (the caller then reads the UCD tables: two
 // dependent memory reads, which a wave waits for if any of its lanes needs them).  Latin-1
@@ -113,8 +149,13 @@ SW_HD inline int fast_class(uint32_t cp) {
 // bytes k .. k + 3 of those 40 (k <= 36).
 template <class Cls, class Bytes>
 SW_HD inline Masks classify(const Bytes& by, uint64_t ss, const Cls& cls, bool cl) {
-  // ASCII classes of the chunk's bytes (words 1..8)
+  // ASCII classes of the chunk's bytes (words 1..8): a class byte per byte (ascii_class4), two
+  // classes gathered per multiply
   uint32_t L = 0, N = 0, C = 0, P = 0, H = 0, A = 0;
+#ifndef SW_PSB_LUT
+#define SW_PSB_LUT 1
+#endif
+#if !SW_PSB_LUT
 #pragma unroll
   for (int i = 1; i < 9; ++i) {
     const uint32_t x = by.word(i), asc = ~x & kLane7, x7 = x & kLow7;
@@ -127,6 +168,20 @@ SW_HD inline Masks classify(const Bytes& by, uint64_t ss, const Cls& cls, bool c
     P |= mm4(in7(x7, ' ', ' ') & asc) << s;
     A |= mm4(in7(x7, '\'', '\'') & asc) << s;
   }
+  if (false)
+#endif
+#pragma unroll
+  for (int i = 1; i < 9; ++i) {
+    const uint32_t t = ascii_class4(by.word(i));
+    const int s = 4 * (i - 1);
+    const uint32_t l = mm8(t), nc = mm8(t << 1), ph = mm8(t << 2);
+    L |= ((l >> 4) | (l & 15u)) << s;
+    N |= (nc >> 4) << s;
+    C |= (nc & 15u) << s;
+    P |= (ph >> 4) << s;
+    H |= (ph & 15u) << s;
+    A |= mm4(t << 3) << s;
+  }
   // UTF-8: every lead byte of [pos - 4, pos + 32) checked on its own (strict: no overlongs,
   // surrogates or code points past U+10FFFF, not crossing a string start); the continuation
   // bytes of the valid ones make X, and the chunk's non-ASCII code points get their class
@@ -134,6 +189,10 @@ SW_HD inline Masks classify(const Bytes& by, uint64_t ss, const Cls& cls, bool c
   uint64_t hi40 = 0, ct40 = 0;
 #pragma unroll
   for (int i = 0; i < 10; ++i) hi40 |= (uint64_t)mm4(by.word(i)) << (4 * i);
+  {  // (the ASCII classes of bytes >= 0x80 were garbage)
+    const uint32_t asc = ~(uint32_t)(hi40 >> 4);
+    L &= asc; N &= asc; C &= asc; P &= asc; H &= asc; A &= asc;
+  }
   if (hi40) {
 #pragma unroll
     for (int i = 0; i < 10; ++i) {

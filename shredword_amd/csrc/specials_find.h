@@ -1,0 +1,226 @@
+// The special-token finder on the device (sw_find_specials_device): the occurrences that
+// sw_find_specials_host finds on host threads (specials.cpp), bit for bit.  The rule (build-defined:
+// the reference stores special_tokens, shredword/base.py:103, but defines no split): scanning each
+// string left to right, the first position where some special matches starts an occurrence; at one
+// position the first special in dict order wins; the scan resumes after it.
+//
+// Leftmost-first with resumption is a sequential rule, but its chain is short: an occurrence only
+// hides the candidates that start inside it.  So, over 2 KiB tiles (one wave each):
+//   k_sp_detect   candidates: positions where some special matches inside its string (the first
+//                 byte against the specials' first bytes by SWAR compares, the rest only there), one
+//                 bit per byte; a count per tile
+//   k_sp_resolve  a candidate no earlier candidate covers is an occurrence ("clean"); from each clean
+//                 candidate that covers the next one, one lane walks the cluster of overlapping
+//                 candidates left to right exactly as the scan would (rare: only specials that can
+//                 overlap themselves or each other produce clusters)
+//   k_sp_count + scan + k_sp_write   the occurrences, ascending, with their lengths and ids
+// Only tiles with candidates do more than read a count after k_sp_detect.  Included by encode.hip.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "kernels.h"
+
+namespace sw {
+
+constexpr int kSpMaxLen = 64;     // the longest special the device finder takes (longer: host finder)
+constexpr int kSpMaxFirstSwar = 4;  // distinct first bytes compared by SWAR (more: a bit set in LDS)
+
+// the tokenizer's specials on the device (sw_encoder_set_specials)
+struct SpTab {
+  const uint8_t* bytes;  // every special's bytes, concatenated
+  const int32_t* off;    // [n + 1]
+  const int32_t* ids;    // [n]
+  const int32_t* list;   // the non-empty specials grouped by first byte, dict order within a group
+  const int32_t* first;  // [257]: first byte b's group is list[first[b] .. first[b + 1])
+  uint32_t filt[8];      // the first-byte set
+  uint32_t fb;           // the distinct first bytes, one per byte (n_first <= kSpMaxFirstSwar)
+  int32_t n_first;
+  int32_t max_len;
+  int32_t n;
+};
+
+struct SpFind {
+  const uint8_t* bytes;
+  int64_t n_bytes;
+  const int64_t* str_off;
+  int64_t n_str;
+  const int64_t* tile_slo;  // k_tile_strings
+  int64_t n_tiles;
+  uint32_t* cbits;   // [n_tiles * 64] candidate starts, one bit per byte
+  uint32_t* chosen;  // [n_tiles * 64] occurrence starts
+  uint32_t* tcand;   // [n_tiles] candidates per tile
+  uint32_t* tcnt;    // [n_tiles] occurrences per tile
+};
+
+// the end of the string holding byte p: the first string start past p
+__device__ __forceinline__ int64_t sp_str_end(const SpFind& f, int64_t p) {
+  const int64_t t = p >> kTileBits;
+  int64_t lo = f.tile_slo[t], hi = t + 1 < f.n_tiles ? f.tile_slo[t + 1] : f.n_str;
+  while (lo < hi) {  // (str_off[hi] > p: the next tile's first string, or the batch end)
+    const int64_t m = (lo + hi) >> 1;
+    if (f.str_off[m] <= p) lo = m + 1; else hi = m;
+  }
+  return f.str_off[lo];
+}
+
+// the special matching at p inside [p, end): the first of its first byte's group, in dict order,
+// or -1
+__device__ __forceinline__ int32_t sp_match(const SpTab& T, const SpFind& f, int64_t p, int64_t end) {
+  const uint32_t b = f.bytes[p];
+  for (int32_t g = T.first[b]; g < T.first[b + 1]; ++g) {
+    const int32_t k = T.list[g];
+    const int32_t o = T.off[k], L = T.off[k + 1] - o;
+    if (p + L > end) continue;
+    bool same = true;
+    for (int32_t q = 1; q < L && same; ++q) same = f.bytes[p + q] == T.bytes[o + q];
+    if (same) return k;
+  }
+  return -1;
+}
+__device__ __forceinline__ int32_t sp_len_at(const SpTab& T, const SpFind& f, int64_t p) {
+  const int32_t k = sp_match(T, f, p, sp_str_end(f, p));
+  return k < 0 ? 0 : T.off[k + 1] - T.off[k];
+}
+
+// exact zero bytes of x: bit 7 of each zero byte lane
+__device__ __forceinline__ uint32_t zero_bytes(uint32_t x) {
+  return ~(((x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | x) & 0x80808080u;
+}
+__device__ __forceinline__ uint32_t mm4_hi(uint32_t x) { return ((x & 0x80808080u) * 0x00204081u) >> 28; }
+
+// k_sp_detect: lane l of tile t's wave owns bytes [t0 + 32 l, + 32)
+template <bool kSwar>
+__global__ void __launch_bounds__(kThreads) k_sp_detect(SpTab T, SpFind f) {
+  __shared__ uint32_t s_filt[8];
+  if (!kSwar) {
+    if (threadIdx.x < 8) s_filt[threadIdx.x] = T.filt[threadIdx.x];
+    __syncthreads();
+  }
+  const int lane = threadIdx.x & 63;
+  const int64_t t = (int64_t)blockIdx.x * kWaves + wave_in_block();
+  if (t >= f.n_tiles) return;
+  const int64_t p0 = (t << kTileBits) + 32 * lane;
+  uint32_t w[8];
+  if (((uintptr_t)f.bytes & 15) == 0 && p0 + 32 <= f.n_bytes) {
+    const u32x4 x0 = SW_LDNT((const u32x4*)(f.bytes + p0)), x1 = SW_LDNT((const u32x4*)(f.bytes + p0 + 16));
+    w[0] = x0[0]; w[1] = x0[1]; w[2] = x0[2]; w[3] = x0[3];
+    w[4] = x1[0]; w[5] = x1[1]; w[6] = x1[2]; w[7] = x1[3];
+  } else {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      uint32_t v = 0;
+      for (int k = 0; k < 4; ++k) {
+        const int64_t p = p0 + 4 * i + k;
+        v |= (p < f.n_bytes ? (uint32_t)f.bytes[p] : 0u) << (8 * k);
+      }
+      w[i] = v;
+    }
+  }
+  uint32_t m = 0;  // bytes whose value starts some special
+  if (kSwar) {
+    for (int j = 0; j < T.n_first; ++j) {
+      const uint32_t fb = ((T.fb >> (8 * j)) & 0xFFu) * 0x01010101u;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) m |= mm4_hi(zero_bytes(w[i] ^ fb)) << (4 * i);
+    }
+  } else {
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+      for (int k = 0; k < 4; ++k) {
+        const uint32_t b = (w[i] >> (8 * k)) & 0xFFu;
+        m |= ((s_filt[b >> 5] >> (b & 31)) & 1u) << (4 * i + k);
+      }
+  }
+  if (p0 + 32 > f.n_bytes) m &= p0 >= f.n_bytes ? 0u : (1u << (f.n_bytes - p0)) - 1u;
+  // full matches only (inside the string)
+  uint32_t c = 0;
+  int64_t end = -1;
+  for (uint32_t x = m; x; x &= x - 1) {
+    const int64_t p = p0 + __builtin_ctz(x);
+    if (p >= end) end = sp_str_end(f, p);
+    if (sp_match(T, f, p, end) >= 0) c |= 1u << __builtin_ctz(x);
+  }
+  f.cbits[t * 64 + lane] = c;
+  f.chosen[t * 64 + lane] = 0u;
+  uint32_t n = (uint32_t)__popc(c);
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) n += (uint32_t)__shfl_xor((int)n, off, 64);
+  if (lane == 0) f.tcand[t] = n;
+}
+
+// the next candidate at or after q, below lim (-1: none); one word of the candidate bits at a time
+__device__ __forceinline__ int64_t sp_next_cand(const SpFind& f, int64_t q, int64_t lim) {
+  lim = min(lim, f.n_bytes);
+  while (q < lim) {
+    const uint32_t word = f.cbits[q >> 5] >> (q & 31);
+    if (word) {
+      const int64_t r = q + __builtin_ctz(word);
+      return r < lim ? r : -1;
+    }
+    q = (q | 31) + 1;
+  }
+  return -1;
+}
+
+__global__ void __launch_bounds__(kThreads) k_sp_resolve(SpTab T, SpFind f) {
+  const int lane = threadIdx.x & 63;
+  const int64_t t = (int64_t)blockIdx.x * kWaves + wave_in_block();
+  if (t >= f.n_tiles || f.tcand[t] == 0) return;
+  const int64_t p0 = (t << kTileBits) + 32 * lane;
+  for (uint32_t x = f.cbits[t * 64 + lane]; x; x &= x - 1) {
+    const int64_t p = p0 + __builtin_ctz(x);
+    // clean: no earlier candidate covers p (candidates never cross a string; one inside an earlier
+    // tile is read from its bits too)
+    bool clean = true;
+    for (int64_t q = sp_next_cand(f, max(p - (T.max_len - 1), (int64_t)0), p); q >= 0 && clean;
+         q = sp_next_cand(f, q + 1, p))
+      clean = q + sp_len_at(T, f, q) <= p;
+    if (!clean) continue;  // (decided by the walk from its cluster's clean head)
+    const int32_t L = sp_len_at(T, f, p);
+    atomicOr(&f.chosen[p >> 5], 1u << (p & 31));
+    // the cluster of candidates overlapping p's, left to right as the sequential scan goes
+    int64_t span = p + L, taken = p + L;
+    for (int64_t r = sp_next_cand(f, p + 1, span); r >= 0; r = sp_next_cand(f, r + 1, span)) {
+      const int32_t Lr = sp_len_at(T, f, r);
+      if (r >= taken) {
+        atomicOr(&f.chosen[r >> 5], 1u << (r & 31));
+        taken = r + Lr;
+      }
+      span = max(span, r + (int64_t)Lr);
+    }
+  }
+}
+
+__global__ void __launch_bounds__(kThreads) k_sp_count(SpFind f) {
+  const int lane = threadIdx.x & 63;
+  const int64_t t = (int64_t)blockIdx.x * kWaves + wave_in_block();
+  if (t >= f.n_tiles) return;
+  uint32_t n = f.tcand[t] ? (uint32_t)__popc(f.chosen[t * 64 + lane]) : 0u;
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) n += (uint32_t)__shfl_xor((int)n, off, 64);
+  if (lane == 0) f.tcnt[t] = n;
+}
+
+__global__ void __launch_bounds__(kThreads) k_sp_write(SpTab T, SpFind f, const int64_t* toff, int64_t* pos,
+                                                       int32_t* len, int32_t* id) {
+  const int lane = threadIdx.x & 63;
+  const int64_t t = (int64_t)blockIdx.x * kWaves + wave_in_block();
+  if (t >= f.n_tiles || f.tcnt[t] == 0) return;
+  const uint32_t c = f.chosen[t * 64 + lane];
+  const uint32_t cnt = (uint32_t)__popc(c);
+  const uint32_t incl = wave_incl_scan(cnt, lane);
+  int64_t o = toff[t] + (incl - cnt);
+  const int64_t p0 = (t << kTileBits) + 32 * lane;
+  for (uint32_t x = c; x; x &= x - 1) {
+    const int64_t p = p0 + __builtin_ctz(x);
+    const int32_t k = sp_match(T, f, p, sp_str_end(f, p));
+    pos[o] = p;
+    len[o] = T.off[k + 1] - T.off[k];
+    id[o] = T.ids[k];
+    ++o;
+  }
+}
+
+}  // namespace sw

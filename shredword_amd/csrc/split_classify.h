@@ -54,14 +54,15 @@ __device__ __forceinline__ uint32_t ss32_hint(const int64_t* str_off, int64_t n_
 // occurrence whose end (pos + len) is at or after p: ends ascend; the ones before tile_sp[t] - 1
 // end before tile t's first byte, and tile_sp[t + 1]'s starts past p.
 __device__ __forceinline__ int64_t sp_first_end(const SpArgs& sp, int64_t n_tiles, int64_t p) {
-  int64_t lo = 0, hi = sp.n;
+  const int64_t n = sp.tile_sp[n_tiles];  // (the live count: the host's, or the device finder's)
+  int64_t lo = 0, hi = n;
   if (p > 0) {
     const int64_t t = p >> kTileBits;
     if (t < n_tiles) {
       lo = max(sp.tile_sp[t] - 1, (int64_t)0);
-      hi = t + 1 < n_tiles ? sp.tile_sp[t + 1] : sp.n;
+      hi = sp.tile_sp[t + 1];
     } else {
-      lo = max(sp.n - 1, (int64_t)0);
+      lo = max(n - 1, (int64_t)0);
     }
   }
   while (lo < hi) {
@@ -74,7 +75,8 @@ __device__ __forceinline__ int64_t sp_first_end(const SpArgs& sp, int64_t n_tile
 // bits of [p, p + 32): the occurrences' starts and ends (*ss) and their inner bytes (*inner)
 __device__ __forceinline__ void sp_bits32(const SpArgs& sp, int64_t n_tiles, int64_t p, uint32_t* ss, uint32_t* inner) {
   uint32_t s = 0, in = 0;
-  for (int64_t j = sp_first_end(sp, n_tiles, p); j < sp.n; ++j) {
+  const int64_t n = sp.tile_sp[n_tiles];
+  for (int64_t j = sp_first_end(sp, n_tiles, p); j < n; ++j) {
     const int64_t a = sp.pos[j], e = a + sp.len[j];
     if (a >= p + 32) break;
     if (a >= p) s |= 1u << (a - p);
@@ -177,7 +179,8 @@ __device__ __forceinline__ void ss_win5(const PbArgs& g, int64_t n_tiles, int64_
     }
   }
   if (g.sp.n > 0) {
-    for (int64_t j = sp_first_end(g.sp, n_tiles, base); j < g.sp.n; ++j) {
+    const int64_t n = g.sp.tile_sp[n_tiles];
+    for (int64_t j = sp_first_end(g.sp, n_tiles, base); j < n; ++j) {
       const int64_t a = g.sp.pos[j];
       if (a >= end) break;
       set(a);
@@ -235,12 +238,15 @@ __global__ void __launch_bounds__(256) k_edges(PbArgs g, int64_t n_tiles, int pa
   edge[9 * stride + b] = r;
 }
 
-// a lane's 40 bytes [pos - 4, pos + 36) in the LDS window, for psb::classify: word(i) = bytes
-// [pos - 4 + 4 i, pos + 4 i); at4(k) = bytes k .. k + 3 of the 40 (k <= 36), two LDS reads
-// instead of RegBytes' select chain over ten registers
-struct LdsBytes {
+// a lane's 40 bytes [pos - 4, pos + 36) for psb::classify: word(i) = bytes [pos - 4 + 4 i, pos + 4 i)
+// from registers (the lane staged its own 32 bytes and took the words on either side from its
+// neighbours: no LDS reads, whose stride of 8 dwords per lane made every one an 8-way bank
+// conflict); at4(k) = bytes k .. k + 3 of the 40 (k <= 36, dynamic: the rare UTF-8 leads and
+// apostrophes) from the LDS window, two reads instead of a select chain over ten registers
+struct MixBytes {
+  const uint32_t (&r)[10];
   const uint32_t* w;
-  __device__ __forceinline__ uint32_t word(int i) const { return w[i]; }
+  __device__ __forceinline__ uint32_t word(int i) const { return r[i]; }
   __device__ __forceinline__ uint32_t at4(int k) const {
     const int q = k >> 2;
     return __builtin_amdgcn_alignbyte(w[q + 1], w[q], (uint32_t)(k & 3));
@@ -342,9 +348,17 @@ __device__ __forceinline__ void split_classify_tile(const EncArgs& a, const PbAr
   const int64_t c0 = tile << (kTileBits - 5), c = c0 + lane;
   const int64_t stride = a.n_tiles + 1;
   const bool cl = pattern == 0;
-  // 1. loads: the bytes [t0 - 32, t0 + kWin) into LDS, the edge words, the first strings
+  // 1. loads: the bytes [t0 - 32, t0 + kWin) into LDS (16-byte blocks: 2 before the tile, 128 of
+  //    it, 4 after), each lane its own chunk's two blocks, which it also keeps in registers for the
+  //    class masks (rw), the edge words, the first strings
   const int64_t wb = t0 - kScPre;
-  if (((uintptr_t)a.bytes & 15) == 0 && wb >= 0 && wb + kScPre + kWin <= a.n_bytes) {
+  uint32_t rw[10];
+  static_assert(kScPre == 32 && kWin == kTile + 64, "block layout of the window");
+#ifndef SW_SC_REGBYTES
+#define SW_SC_REGBYTES 1
+#endif
+  const bool fast = SW_SC_REGBYTES && ((uintptr_t)a.bytes & 15) == 0 && wb >= 0 && wb + kScPre + kWin <= a.n_bytes;
+  if (!SW_SC_REGBYTES && ((uintptr_t)a.bytes & 15) == 0 && wb >= 0 && wb + kScPre + kWin <= a.n_bytes) {
 #pragma unroll
     for (int q = 0; q < ((kScPre + kWin) / 16 + 63) / 64; ++q) {
       const int i = lane + 64 * q;
@@ -353,6 +367,25 @@ __device__ __forceinline__ void split_classify_tile(const EncArgs& a, const PbAr
         *(uint4*)(s_win + 4 * i) = make_uint4(x[0], x[1], x[2], x[3]);
       }
     }
+  } else if (fast) {
+    const u32x4* src = (const u32x4*)(a.bytes + wb);
+    const u32x4 x0 = SW_LDNT(src + 2 + 2 * lane), x1 = SW_LDNT(src + 3 + 2 * lane);
+    // the other six blocks: lane 0 block 1 (its word before the chunk), lane 63 block 130 (its word
+    // after it), lanes 1..4 blocks 0, 131..133
+    const bool ex = lane < 5 || lane == 63;
+    const int eb = lane == 0 ? 1 : lane == 1 ? 0 : lane == 63 ? 130 : 129 + lane;
+    u32x4 xe = u32x4{0, 0, 0, 0};
+    if (ex) xe = SW_LDNT(src + eb);
+    *(uint4*)(s_win + 4 * (2 + 2 * lane)) = make_uint4(x0[0], x0[1], x0[2], x0[3]);
+    *(uint4*)(s_win + 4 * (3 + 2 * lane)) = make_uint4(x1[0], x1[1], x1[2], x1[3]);
+    if (ex) *(uint4*)(s_win + 4 * eb) = make_uint4(xe[0], xe[1], xe[2], xe[3]);
+    rw[1] = x0[0]; rw[2] = x0[1]; rw[3] = x0[2]; rw[4] = x0[3];
+    rw[5] = x1[0]; rw[6] = x1[1]; rw[7] = x1[2]; rw[8] = x1[3];
+    // the word before the chunk: lane - 1's last; the word after it: lane + 1's first
+    const uint32_t up = (uint32_t)__shfl((int)rw[8], (lane + 63) & 63, 64);
+    const uint32_t dn = (uint32_t)__shfl((int)rw[1], (lane + 1) & 63, 64);
+    rw[0] = lane == 0 ? xe[3] : up;
+    rw[9] = lane == 63 ? xe[0] : dn;
   } else {
     for (int i = lane; i < (kScPre + kWin) / 4; i += 64) {
       const int64_t p = wb + 4 * (int64_t)i;
@@ -362,6 +395,12 @@ __device__ __forceinline__ void split_classify_tile(const EncArgs& a, const PbAr
     }
   }
   if (lane < 8) s_win[(kScPre + kWin) / 4 + lane] = 0;
+  if (!fast) {  // (the batch's first and last tiles, an unaligned input: the words from LDS; and
+                //  the A/B build without register bytes)
+    wave_sync_mem();
+#pragma unroll
+    for (int i = 0; i < 10; ++i) rw[i] = s_win[kScPre / 4 - 1 + 8 * lane + i];
+  }
   const uint32_t r0 = edge[9 * stride + tile], r_next = edge[9 * stride + tile + 1];
   const int64_t s_first = a.tile_slo[tile];
   ScMasks& sm = sh->pre;
@@ -385,10 +424,11 @@ __device__ __forceinline__ void split_classify_tile(const EncArgs& a, const PbAr
     sm.in[lane] = 0u;
     wave_sync_mem();
     const int64_t w0 = t0 - kScSsPre, w1 = w0 + (int64_t)kScSsWords * 32;
-    for (int64_t j0 = sp_first_end(a.sp, a.n_tiles, w0); j0 < a.sp.n; j0 += 64) {
+    const int64_t nsp = a.sp.tile_sp[a.n_tiles];
+    for (int64_t j0 = sp_first_end(a.sp, a.n_tiles, w0); j0 < nsp; j0 += 64) {
       const int64_t j = j0 + lane;
       int64_t pa = w1, pe = w1;
-      if (j < a.sp.n) {
+      if (j < nsp) {
         pa = a.sp.pos[j];
         pe = pa + a.sp.len[j];
       }
@@ -421,7 +461,7 @@ __device__ __forceinline__ void split_classify_tile(const EncArgs& a, const PbAr
     {
       psb::Masks m1{};
       if (c < n_chunks) {
-        const LdsBytes by{s_win + (kScPre / 4 - 1) + 8 * lane};  // bytes [t0 + 32 lane - 4, +40)
+        const MixBytes by{rw, s_win + (kScPre / 4 - 1) + 8 * lane};  // bytes [t0 + 32 lane - 4, +40)
         const int64_t p = 32 * c;
         const uint64_t s = (uint64_t)src.ss_at(p - 4) | ((uint64_t)(src.ss_at(p + 28) & 0xFFu) << 32);
         m1 = psb::classify(by, s, UcdClass{}, cl);
@@ -492,7 +532,7 @@ k_split_classify(EncArgs a, PbArgs g, int pattern, const uint32_t* edge, uint32_
   __shared__ __attribute__((aligned(16))) uint32_t s_win_all[kWaves][kScWinWords];
   __shared__ ScShared s_sh_all[kWaves];
   __shared__ uint16_t s_qb_all[kWaves][kQBuf];
-  const int wv = wave_in_block();
+  const int wv = wave_in_block_s();
   const int64_t tile = (int64_t)blockIdx.x * kWaves + wv;
   if (tile < a.n_tiles)
     split_classify_tile<kSp, false>(a, g, pattern, edge, bits32, tile, s_win_all[wv], &s_sh_all[wv], s_qb_all[wv],
@@ -508,11 +548,14 @@ __global__ void __launch_bounds__(kThreads) k_split_redo(EncArgs a, PbArgs g, in
   __shared__ __attribute__((aligned(16))) uint32_t s_win_all[kWaves][kScWinWords];
   __shared__ ScShared s_sh_all[kWaves];
   __shared__ uint16_t s_qb_all[kWaves][kQBuf];
-  const int wv = wave_in_block();
-  const int64_t n = (int64_t)*redo.count;
+  const int wv = wave_in_block_s();
+  // (the count and the list are this launch's, written by k_split_classify: read them coherently,
+  // never through the scalar cache, which can hold an earlier launch's values)
+  const int64_t n = (int64_t)__hip_atomic_load(redo.count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   for (int64_t i = (int64_t)blockIdx.x * kWaves + wv; i < n; i += (int64_t)gridDim.x * kWaves) {
-    split_classify_tile<kSp, true>(a, g, pattern, edge, bits32, redo.tiles[i], s_win_all[wv], &s_sh_all[wv],
-                                   s_qb_all[wv], redo);
+    const int64_t tile = __hip_atomic_load(&redo.tiles[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    split_classify_tile<kSp, true>(a, g, pattern, edge, bits32, tile, s_win_all[wv], &s_sh_all[wv], s_qb_all[wv],
+                                   redo);
     wave_sync_mem();  // (the next tile reuses the wave's LDS)
   }
 }

@@ -88,6 +88,19 @@ class Tokenizer(BaseTokenizer):
         self._dec_key = None
         self._dec_len = None
         self.last_stats = None
+        self._parent = None  # (a view made by shared(): encodes through the parent's device table)
+
+    def shared(self, pattern=None):
+        """A tokenizer that uses this one's merges and its device handle (one copy of the tables on
+        the device) with its own `pattern` and special tokens: several such views may encode
+        concurrently, on different streams, each with its own pattern (the pattern is passed per
+        call, never set on the shared handle).  The view does not own the handle."""
+        v = Tokenizer(self.device)
+        v._parent = self
+        v._merges = self._merges
+        v.special_tokens = dict(self.special_tokens)
+        v.pattern = self.pattern if pattern is None else pattern
+        return v
 
     # merges is tracked so that edits (README-style `tok.merges[(a, b)] = id`) reach the device
     @property
@@ -123,7 +136,7 @@ class Tokenizer(BaseTokenizer):
 
     def close(self):
         h, self._handle = getattr(self, "_handle", None), None
-        if h:
+        if h and getattr(self, "_parent", None) is None:
             _lib.lib().sw_encoder_destroy(h)  # (unpins whatever pin_host pinned)
         self._pinned = []
         d, self._dec = getattr(self, "_dec", None), None
@@ -165,6 +178,10 @@ class Tokenizer(BaseTokenizer):
 
     # ---------------------------------------------------------------- device table
     def _encoder(self):
+        if self._parent is not None:
+            if self._merges is not self._parent._merges:
+                raise RuntimeError("a shared() view's merges must stay its parent's")
+            return self._parent._encoder()
         key = (id(self._merges), self._merges.version, self.device)
         if self._handle is not None and self._handle_key == key:
             return self._handle
@@ -255,22 +272,32 @@ class Tokenizer(BaseTokenizer):
         self._pinned = [a for a in getattr(self, "_pinned", []) if a.ctypes.data != arr.ctypes.data]
 
     def encode_device(self, d_buf, d_off, d_bits=None, d_out=None, d_out_off=None, stream=None, out_bits=32,
-                      d_specials=None):
+                      d_specials=None, n_bytes=None, sync=True):
         """Encode strings already on this tokenizer's device (torch tensors: uint8 bytes, int64
         offsets from 0; optional pre-split bitmap as int64 words, else the device pre-splits with
         `pattern`), on torch's current stream (or `stream`).  out_bits 16: the ids are written as
         16 bits (int16 tensor holding each id's low 16 bits; tables whose every id fits, the
         multi-GPU transport).  d_specials: optional special-token occurrences on the device,
         (pos int64, len int32, id int32) as corpus.find_specials gives them (a caller bitmap must
-        then come from presplit_specials).  Returns (ids [n_tokens], offsets int64 [n+1]) as device
-        tensors; the token count is read back (one synchronisation).  d_out / d_out_off: optional
-        output buffers (>= n_bytes of the output dtype / n+1)."""
+        then come from presplit_specials).  d_out / d_out_off: optional output buffers (>= n_bytes
+        of the output dtype / n+1).
+
+        The pattern goes with the call (sw_encode_ex.pattern), so tokenizers with different patterns
+        may share one handle and call from several streams.  n_bytes: the batch's byte count
+        (d_off[-1]); None reads it back from the device (one synchronisation).  sync=True returns
+        (ids [n_tokens], offsets int64 [n+1]), the token count read back (one synchronisation);
+        sync=False enqueues the work and returns (d_out, d_out_off) whole, without waiting: the
+        count is d_out_off[-1] on the device."""
         import torch
         if out_bits not in (16, 32):
             raise ValueError("out_bits must be 16 or 32")
         dev = d_buf.device
         n = int(d_off.numel()) - 1
-        n_bytes = int(d_off[-1].item()) if n >= 0 else 0
+        if n_bytes is None:
+            n_bytes = int(d_off[-1].item()) if n >= 0 else 0
+        n_bytes = int(n_bytes)
+        if n_bytes > d_buf.numel():
+            raise ValueError("n_bytes exceeds d_buf")
         want = torch.int16 if out_bits == 16 else torch.int32
         if d_out is None:
             d_out = torch.empty(max(n_bytes, 1), dtype=want, device=dev)
@@ -280,18 +307,59 @@ class Tokenizer(BaseTokenizer):
             d_out_off = torch.empty(n + 1, dtype=torch.int64, device=dev)
         L = _lib.lib()
         h = self._encoder()
-        _lib.check(L.sw_encoder_set_option(h, _lib.SW_OPT_PATTERN, pattern_id(self.pattern)))
         st = stream if stream is not None else torch.cuda.current_stream(dev).cuda_stream
-        ex = _lib.SwEncodeEx(d_bits.data_ptr() if d_bits is not None else None, out_bits, None, None, None, 0)
+        ex = _lib.SwEncodeEx(d_bits.data_ptr() if d_bits is not None else None, out_bits,
+                             pattern=pattern_id(self.pattern))
         if d_specials is not None and d_specials[0].numel() > 0:
-            pos, ln, ids = d_specials
+            pos, ln, ids = d_specials[:3]
             if pos.dtype != torch.int64 or ln.dtype != torch.int32 or ids.dtype != torch.int32:
-                raise ValueError("d_specials: (int64 positions, int32 lengths, int32 ids)")
+                raise ValueError("d_specials: (int64 positions, int32 lengths, int32 ids[, int64 device count])")
             ex.sp_pos, ex.sp_len, ex.sp_id, ex.n_sp = pos.data_ptr(), ln.data_ptr(), ids.data_ptr(), pos.numel()
+            if len(d_specials) > 3:  # (find_specials_device's: the count stays on the device)
+                ex.d_n_sp = d_specials[3].data_ptr()
         n_tok = ctypes.c_int64()
         _lib.check(L.sw_encode_device_ex(h, d_buf.data_ptr(), n_bytes, d_off.data_ptr(), n, ctypes.byref(ex),
-                                         d_out.data_ptr(), d_out_off.data_ptr(), st, ctypes.byref(n_tok)))
+                                         d_out.data_ptr(), d_out_off.data_ptr(), st,
+                                         ctypes.byref(n_tok) if sync else None))
+        if not sync:
+            return d_out, d_out_off
         return d_out[:int(n_tok.value)], d_out_off
+
+    def find_specials_device(self, d_buf, d_off, n_bytes=None, stream=None, sync=False):
+        """The occurrences of self.special_tokens in strings already on the device (as encode_device
+        takes them), found on the device (sw_find_specials_device: leftmost first, dict order at one
+        position -- sw_find_specials_host's rule, bit for bit).  Returns (pos int64, len int32, id int32,
+        count int64[1]) device tensors sized for the worst case; the first `count` entries are the
+        occurrences.  Pass the tuple as encode_device(d_specials=...): the count is read on the
+        device, nothing synchronises.  sync=True also returns the count as an int (one
+        synchronisation).  Specials longer than 64 bytes need the host finder (ValueError)."""
+        import torch
+        L = _lib.lib()
+        h = self._encoder()
+        specials = {k: v for k, v in self.special_tokens.items()}
+        st, keep = _lib.specials_struct(specials)
+        _lib.check(L.sw_encoder_set_specials(h, ctypes.byref(st)))
+        del keep
+        dev = d_buf.device
+        n = int(d_off.numel()) - 1
+        if n_bytes is None:
+            n_bytes = int(d_off[-1].item()) if n >= 0 else 0
+        lens = [len(k.encode("utf-8")) for k in specials if k]
+        if lens and max(lens) > 64:
+            raise ValueError("a special token over 64 bytes: use the host finder (corpus.find_specials)")
+        cap = int(n_bytes) // max(min(lens), 1) + 1 if lens else 1
+        pos = torch.empty(cap, dtype=torch.int64, device=dev)
+        ln = torch.empty(cap, dtype=torch.int32, device=dev)
+        ids = torch.empty(cap, dtype=torch.int32, device=dev)
+        cnt = torch.zeros(1, dtype=torch.int64, device=dev)
+        stream_h = stream if stream is not None else torch.cuda.current_stream(dev).cuda_stream
+        n_host = ctypes.c_int64()
+        _lib.check(L.sw_find_specials_device(h, d_buf.data_ptr(), int(n_bytes), d_off.data_ptr(), n, pos.data_ptr(),
+                                             ln.data_ptr(), ids.data_ptr(), cap, cnt.data_ptr(), stream_h,
+                                             ctypes.byref(n_host) if sync else None))
+        if sync:
+            return pos, ln, ids, cnt, int(n_host.value)
+        return pos, ln, ids, cnt
 
     def encode_batch(self, texts, allowed_special="all"):
         """Encode many strings in one device batch; returns a list of id lists.  allowed_special

@@ -53,3 +53,16 @@ def index():
 @pytest.fixture(scope="session")
 def primitives():
     return json.load(open(os.path.join(GOLD, "primitives.json"), encoding="utf-8"))
+
+
+def page_array(n, dtype, fill=0):
+    """A numpy array of n elements on pages of its own (page-aligned start, nothing else on its last
+    page), for tests that pin several arrays with Tokenizer.pin_host: two arrays sharing a page
+    cannot both be pinned (sw_encoder_pin_host refuses overlapping pages)."""
+    import numpy as np
+    nbytes = n * np.dtype(dtype).itemsize
+    raw = np.empty(nbytes + 2 * 4096, dtype=np.uint8)
+    a0 = (-raw.ctypes.data) % 4096
+    a = raw[a0:a0 + nbytes].view(dtype)
+    a[:] = fill
+    return a  # (a view: keeps raw alive)

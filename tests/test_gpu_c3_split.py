@@ -11,7 +11,7 @@ import pytest
 import oracle
 import shredword_amd as sa
 from shredword_amd import _lib, corpus
-from conftest import PATTERNS, golden_index, load_fixture, load_model_merges
+from conftest import PATTERNS, golden_index, load_fixture, load_model_merges, page_array
 
 pytestmark = pytest.mark.gpu
 
@@ -389,8 +389,10 @@ def test_pipelined_pinned_caller_buffers(pin, wide):
     exp = oracle_encode(merges, full, sub, "cl100k")
     L, h = _lib.lib(), t._encoder()
     _lib.check(L.sw_encoder_set_option(h, _lib.SW_OPT_PIPE_RUN_BYTES, 5000))
-    out = np.full(len(full) + 100, -5, dtype=np.int32)
-    out_off = np.full(len(sub) + 3, -5, dtype=np.int64)
+    # (each pinned array on pages of its own: arrays sharing a page cannot both be pinned)
+    full = page_array(len(full), np.uint8, full)
+    out = page_array(len(full) + 100, np.int32, -5)
+    out_off = page_array(len(sub) + 3, np.int64, -5)
     pins = {"all": (full, out, out_off), "input": (full,), "outputs": (out, out_off), "out_only": (out,)}[pin]
     for arr in pins:
         t.pin_host(arr)
@@ -398,7 +400,7 @@ def test_pipelined_pinned_caller_buffers(pin, wide):
         got = t.encode_packed(full, sub, out=out, out_off=out_off)
         assert_same(got, exp)
     if pin in ("all", "outputs"):  # (a pinned output too small for the batch, through the C-ABI: refused)
-        small = np.full(len(exp[0]) // 2 + 4096, -5, dtype=np.int32)
+        small = page_array(len(exp[0]) // 2 + 4096, np.int32, -5)
         t.pin_host(small)
         stats = _lib.SwStats()
         rc = L.sw_encode_batch(h, _lib.ptr(full, ctypes.c_uint8), _lib.ptr(sub, ctypes.c_int64), len(sub) - 1, 0,

@@ -402,3 +402,65 @@ def test_out_bits16_per_call(fixture, model):
     assert L.sw_encode_device_ex(w._encoder(), d_buf.data_ptr(), len(fx["bytes"]), d_off.data_ptr(), len(fx["off"]) - 1,
                                  ctypes.byref(ex), d_out.data_ptr(), d_oo.data_ptr(), None, None) == _lib.SW_ERR_ARG
     w.close()
+
+
+def test_dedupe_growth_allocation_failure_keeps_table():
+    """An allocation failure while growing the dedupe table (forced by SW_OPT_TEST_FAIL_GROWTH) must
+    leave the encoder with the table it had: every later launch still equals the oracle, the
+    table size is unchanged, and once the failure is lifted growth works again."""
+    buf, off = corpus.synth(31, corpus.ENTROPY, 60000, 1074)
+    t = sa.Tokenizer(device=0)
+    t.merges = load_model_merges("bl32k.model")
+    exp = oracle_encode(t.merges, buf, off, "cl100k")
+    L, h = _lib.lib(), t._encoder()
+    try:
+        _lib.check(L.sw_encoder_set_option(h, _lib.SW_OPT_TEST_FAIL_GROWTH, 1))
+        slots0 = None
+        for rep in range(3):
+            assert_same(gpu_encode(t, buf, off), exp)
+            if rep == 0:
+                slots0 = L.sw_encoder_get_info(h, _lib.SW_INFO_DEDUPE_SLOTS)
+        assert L.sw_encoder_get_info(h, _lib.SW_INFO_DEDUPE_SLOTS) == slots0
+        _lib.check(L.sw_encoder_set_option(h, _lib.SW_OPT_TEST_FAIL_GROWTH, 0))
+        for rep in range(2):
+            assert_same(gpu_encode(t, buf, off), exp)
+        assert L.sw_encoder_get_info(h, _lib.SW_INFO_DEDUPE_SLOTS) > slots0
+    finally:
+        L.sw_encoder_set_option(h, _lib.SW_OPT_TEST_FAIL_GROWTH, 0)
+        t.close()
+
+
+def test_shared_handle_patterns_per_call_two_streams():
+    """Two tokenizer views with different patterns (cl100k, GPT-2) over ONE device handle
+    (Tokenizer.shared), calls interleaved on two streams without host synchronisation between them
+    (n_bytes given, sync=False): each result equals the oracle for its own pattern.  The pattern
+    travels with the call (sw_encode_ex.pattern), so nothing on the shared handle is raced."""
+    import torch
+    base = sa.Tokenizer(device=0)
+    base.merges = load_model_merges("bl32k.model")
+    va, vb = base.shared(""), base.shared(sa.GPT2_PATTERN)
+    assert va._encoder().value == vb._encoder().value == base._encoder().value
+    dev = torch.device("cuda", 0)
+    s1, s2 = torch.cuda.Stream(dev), torch.cuda.Stream(dev)
+    batches = []
+    for seed in range(4):
+        buf, off = corpus.synth(100 + seed, corpus.MIXED, 2000, 1074)
+        batches.append((buf, off, torch.from_numpy(buf).to(dev), torch.from_numpy(off).to(dev)))
+    torch.cuda.synchronize()
+    outs = []
+    for k, (buf, off, d_buf, d_off) in enumerate(batches):
+        for view, st in ((va, s1), (vb, s2)):
+            with torch.cuda.stream(st):
+                d_out, d_oo = view.encode_device(d_buf, d_off, n_bytes=len(buf), sync=False)
+            outs.append((k, view, d_out, d_oo))
+    torch.cuda.synchronize()
+    for k, view, d_out, d_oo in outs:
+        buf, off = batches[k][0], batches[k][1]
+        pat = "gpt2" if view is vb else "cl100k"
+        exp = oracle_encode(base.merges, buf, off, pat)
+        oo = d_oo.cpu().numpy()
+        np.testing.assert_array_equal(oo, exp[1])
+        np.testing.assert_array_equal(d_out[:int(oo[-1])].cpu().numpy(), exp[0])
+    va.close()
+    assert base._handle is not None  # (a view never destroys its parent's handle)
+    base.close()

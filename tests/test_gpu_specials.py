@@ -156,3 +156,88 @@ def test_pipelined_batch_with_specials():
         L.sw_encoder_set_option(h, _lib.SW_OPT_PIPE_RUN_BYTES, 128 << 20)
         L.sw_encoder_set_option(h, _lib.SW_OPT_MAX_LAUNCH_BYTES, 0)
     t.close()
+
+
+def _device_find(t, buf, off):
+    import torch
+    dev = torch.device("cuda", 0)
+    d_buf = torch.from_numpy(buf if len(buf) else np.zeros(1, np.uint8)).to(dev)
+    d_off = torch.from_numpy(off - off[0]).to(dev)
+    pos, ln, ids, cnt, n = t.find_specials_device(d_buf, d_off, n_bytes=int(off[-1] - off[0]), sync=True)
+    assert int(cnt.item()) == n
+    return pos[:n].cpu().numpy(), ln[:n].cpu().numpy(), ids[:n].cpu().numpy()
+
+
+@pytest.mark.parametrize("case", range(8))
+def test_device_finder_equals_host_finder(case):
+    """sw_find_specials_device == sw_find_specials_host (itself == the plain restatement split_ref,
+    tests/test_specials.py) on adversarial sets: specials that overlap themselves and each other
+    ("aa", "aaa", "ab"/"ba" chains, "<|a" inside "<|a|>"), more than four distinct first bytes (the
+    LDS bit-set path), an empty special, occurrences across 32-byte lanes and 2 KiB tiles, strings
+    cut inside a special, long runs of one letter (clusters of overlapping candidates)."""
+    rng = random.Random(100 + case)
+    sets = [
+        {"aa": 300, "aaa": 301},
+        {"aaa": 301, "aa": 300, "a": 299},
+        {"ab": 310, "ba": 311, "aba": 312},
+        {"<|a|>": 320, "<|a": 321, "|>": 322, "": 323},
+        {"x": 330, "yz": 331, "<|endoftext|>": 332, "\n\n": 333, "é": 334, "\U0001f642": 335, "q" * 64: 336},
+        dict(SPECIALS),
+        {"the": 340, " the": 341, "he": 342, "e ": 343},
+        {"\n": 350, "\n\n": 351, " ": 352},
+    ]
+    sp = sets[case]
+    t = tok_for("bl32k.model")
+    t.special_tokens = sp
+    names = [k for k in sp if k] + ["a", "b", "|", "<", ">", " ", "\n", "word", "é", "th", "e"]
+    datas = []
+    for k in range(400):
+        n_parts = rng.choice([0, 1, 5, 40, 300, 1200])
+        datas.append("".join(rng.choice(names) for _ in range(n_parts)).encode("utf-8"))
+    datas += [b"a" * 5000, b"ab" * 3000, b"<|a|>" * 900, b"", b"aa", b"a"]
+    buf, off = pack(datas)
+    h_pos, h_len, h_id = corpus.find_specials(buf, off, sp)
+    d_pos, d_len, d_id = _device_find(t, buf, off)
+    np.testing.assert_array_equal(d_pos, h_pos)
+    np.testing.assert_array_equal(d_len, h_len)
+    np.testing.assert_array_equal(d_id, h_id)
+    # a sub-batch starting at an odd byte: positions relative to its first byte
+    sub = off[3:200]
+    h2 = corpus.find_specials(buf, sub, sp)
+    d2 = _device_find(t, buf[int(sub[0]):int(sub[-1])].copy(), sub)
+    for a, b in zip(d2, h2):
+        np.testing.assert_array_equal(a, b)
+    t.close()
+
+
+@pytest.mark.parametrize("pattern", ["cl100k", "gpt2"])
+def test_encode_with_device_found_specials(pattern):
+    """The whole specials path on the device: find (sw_find_specials_device) -> encode
+    (sw_encode_device_ex with the count left on the device) with no synchronisation between them;
+    and sw_encode_batch_ex with the device finder (SW_OPT_DEVICE_SPECIALS 1, the default) and the
+    host threads' finder (0), pipelined and not -- all equal to the oracle."""
+    import torch
+    t = tok_for("bl32k.model", pattern)
+    t.special_tokens = dict(SPECIALS)
+    texts = [s.encode() for s in fuzz_texts(31, 4000, 150)]
+    buf, off = pack(texts)
+    e_ids, e_off = expected(t, buf, off, SPECIALS, pattern)
+    dev = torch.device("cuda", 0)
+    d_buf, d_off = torch.from_numpy(buf).to(dev), torch.from_numpy(off).to(dev)
+    found = t.find_specials_device(d_buf, d_off, n_bytes=len(buf))
+    g_ids, g_off = t.encode_device(d_buf, d_off, d_specials=found, n_bytes=len(buf))
+    np.testing.assert_array_equal(g_off.cpu().numpy(), e_off)
+    np.testing.assert_array_equal(g_ids.cpu().numpy(), e_ids)
+    L, h = _lib.lib(), t._encoder()
+    try:
+        for dev_sp in (1, 0):
+            _lib.check(L.sw_encoder_set_option(h, _lib.SW_OPT_DEVICE_SPECIALS, dev_sp))
+            for run in (0, 1 << 16):  # (one launch; the pipeline's runs)
+                _lib.check(L.sw_encoder_set_option(h, _lib.SW_OPT_PIPE_RUN_BYTES, run))
+                ids, o = t.encode_packed(buf, off, specials=SPECIALS)
+                np.testing.assert_array_equal(o, e_off)
+                np.testing.assert_array_equal(ids, e_ids)
+    finally:
+        L.sw_encoder_set_option(h, _lib.SW_OPT_DEVICE_SPECIALS, 1)
+        L.sw_encoder_set_option(h, _lib.SW_OPT_PIPE_RUN_BYTES, 128 << 20)
+    t.close()

@@ -17,6 +17,10 @@ import shutil
 import sys
 
 
+TRAFFIC_KEY = ("n_bytes", "merges", "pattern", "chunk_table", "dedupe", "presplit", "corpus", "specials",
+               "specials_found")
+
+
 def pmc(dirpath):
     """{kernel: {counter: mean per dispatch}}, {kernel: dispatches}"""
     vals = collections.defaultdict(lambda: collections.defaultdict(list))
@@ -112,34 +116,41 @@ def main():
     for ln in open(os.path.join(src, "trace.log"), errors="replace"):
         if ln.startswith("{") and '"metric"' in ln:
             bench = json.loads(ln)
-    cfg = bench["config"] if bench else {}
-    headline = (cfg.get("workload", "").startswith("C2:") and cfg.get("chunk_table") and cfg.get("dedupe")
-                and cfg.get("corpus", "mixed") == "mixed" and not bench.get("specials"))
-    if bench and "traffic_bytes_per_launch" in derived and headline:  # (the headline config only)
-        with open(os.path.join(out, "traffic.json"), "w") as f:
-            json.dump({"source": "profiles/%s.md" % tag, "n_bytes": bench["config"]["bytes_per_rank"],
-                       "merges": bench["config"]["merges"], "pattern": bench["config"]["pattern"],
-                       "chunk_table": bench["config"].get("chunk_table"), "dedupe": bench["config"].get("dedupe"),
-                       "presplit": bench["config"].get("presplit", "host"),
-                       "traffic_bytes_per_launch": derived["traffic_bytes_per_launch"],
-                       "traffic_bytes_per_launch_x2": derived["traffic_bytes_per_launch_x2"],
-                       # the LDS bank-conflict and VALU counters beside the bytes
-                       "counters": {"valu_wave_insts": tot.get("SQ_INSTS_VALU"),
-                                    "valu_issue_floor_ms": (tot["SQ_INSTS_VALU"] * 2 / 1024 / 2.4e6
-                                                            if "SQ_INSTS_VALU" in tot else None),
-                                    "lds_insts": tot.get("SQ_INSTS_LDS"),
-                                    "lds_bank_conflict_cycles": tot.get("SQ_LDS_BANK_CONFLICT"),
-                                    "lds_conflict_cycles_per_lds_inst": (
-                                        tot["SQ_LDS_BANK_CONFLICT"] / tot["SQ_INSTS_LDS"]
-                                        if tot.get("SQ_INSTS_LDS") else None),
-                                    "wait_fraction_of_wave_cycles": (
-                                        tot["SQ_WAIT_ANY"] / tot["SQ_WAVE_CYCLES"]
-                                        if tot.get("SQ_WAVE_CYCLES") else None),
-                                    "l2_hit_rate": derived.get("l2_hit_rate"),
-                                    "note": "pipeline totals per launch; VALU floor = wave instructions x 2 "
-                                            "cycles / 1024 SIMDs / 2.4 GHz"},
-                       "note": "FETCH_SIZE+WRITE_SIZE summed over the pipeline's kernels per launch (raw FETCH; "
-                               "_x2 doubles FETCH per the gfx950 wide-read correction)"}, f, indent=1)
+    if bench and "traffic_bytes_per_launch" in derived:  # one entry per workload, keyed as bench.py matches it
+        cfg = bench["config"]
+        entry = {"source": "profiles/%s.md" % tag, "n_bytes": cfg["bytes_per_rank"], "merges": cfg["merges"],
+                 "pattern": cfg["pattern"], "chunk_table": cfg.get("chunk_table"), "dedupe": cfg.get("dedupe"),
+                 "presplit": cfg.get("presplit", "host"), "corpus": cfg.get("corpus", "mixed"),
+                 "specials": (bench.get("specials") or {}).get("per_kib", 0.0),
+                 "specials_found": (bench.get("specials") or {}).get("found", "host"),
+                 "traffic_bytes_per_launch": derived["traffic_bytes_per_launch"],
+                 "traffic_bytes_per_launch_x2": derived["traffic_bytes_per_launch_x2"],
+                 # the LDS bank-conflict and VALU counters beside the bytes
+                 "counters": {"valu_wave_insts": tot.get("SQ_INSTS_VALU"),
+                              "valu_issue_floor_ms": (tot["SQ_INSTS_VALU"] * 2 / 1024 / 2.4e6
+                                                      if "SQ_INSTS_VALU" in tot else None),
+                              "lds_insts": tot.get("SQ_INSTS_LDS"),
+                              "lds_bank_conflict_cycles": tot.get("SQ_LDS_BANK_CONFLICT"),
+                              "lds_conflict_cycles_per_lds_inst": (
+                                  tot["SQ_LDS_BANK_CONFLICT"] / tot["SQ_INSTS_LDS"] if tot.get("SQ_INSTS_LDS") else None),
+                              "wait_fraction_of_wave_cycles": (
+                                  tot["SQ_WAIT_ANY"] / tot["SQ_WAVE_CYCLES"] if tot.get("SQ_WAVE_CYCLES") else None),
+                              "l2_hit_rate": derived.get("l2_hit_rate"),
+                              "note": "pipeline totals per launch; VALU floor = wave instructions x 2 cycles / "
+                                      "1024 SIMDs / 2.4 GHz"}}
+        path = os.path.join(out, "traffic.json")
+        try:
+            tj = json.load(open(path))
+        except (OSError, ValueError):
+            tj = {}
+        entries = tj.get("entries", [])
+        key = lambda e: tuple(e.get(k) for k in TRAFFIC_KEY)  # noqa: E731
+        entries = [e for e in entries if key(e) != key(entry)] + [entry]
+        with open(path, "w") as f:
+            json.dump({"note": "per workload: FETCH_SIZE+WRITE_SIZE summed over the pipeline's kernels per launch "
+                               "(raw FETCH; _x2 doubles FETCH per the gfx950 wide-read correction); bench.py quotes "
+                               "the entry whose key fields match its workload", "key": list(TRAFFIC_KEY),
+                       "entries": entries}, f, indent=1)
     print("\n".join(lines))
 
 

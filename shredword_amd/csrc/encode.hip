@@ -192,8 +192,10 @@ struct sw_encoder {
   bool spt_dev = false;               // every special fits the device finder (<= kSpMaxLen bytes)
   int32_t spt_min_len = 1;            // the shortest non-empty special
   int64_t spf_tiles = 0;              // capacity of the finder's arrays, in tiles
-  uint32_t* d_spf = nullptr;          // candidate bits, occurrence bits, per-tile counts
-  int64_t* d_spf_off = nullptr;       // per-tile occurrence offsets (+ scan partials)
+  int64_t spf_tcap = 0;               // ... and occurrences per tile
+  uint32_t* d_spf = nullptr;          // candidate bits, occurrence bits, per-tile counts, flag
+  uint32_t* d_spf_list = nullptr;     // per tile, its occurrences (k_sp_find)
+  int64_t* d_spf_off = nullptr;       // per-tile occurrence offsets, twice (+ scan partials, totals)
   int64_t* d_nsp = nullptr;           // sw_encode_batch_ex: the finder's count
   int64_t sp_cap = 0;                 // special-token occurrences staged for sw_encode_batch_ex
   int64_t* d_sp_pos = nullptr;
@@ -288,9 +290,9 @@ int32_t ensure_workspace(sw_encoder* h, int64_t n_bytes) {
     while (slots < nb / 64 && slots < kDdSlotsDefault) slots <<= 1;
     slots = std::max(slots, h->dd_slots);
     h->dd_slots = slots;
-    HIP_TRY(hipMalloc(&h->d_dtab, sizeof(uint64_t) * slots));
-    HIP_TRY(hipMalloc(&h->d_dres, sizeof(uint4) * slots));
-    HIP_TRY(hipMalloc(&h->d_dcnt, slots));
+    HIP_TRY(hipMalloc(&h->d_dtab, sizeof(uint64_t) * (slots + SW_DD_HOT)));
+    HIP_TRY(hipMalloc(&h->d_dres, sizeof(uint4) * (slots + SW_DD_HOT)));
+    HIP_TRY(hipMalloc(&h->d_dcnt, slots + SW_DD_HOT));
     h->dmask = (uint32_t)(slots - 1);
   }
   HIP_TRY(hipMalloc(&h->d_big, sizeof(uint32_t) * (nb / (kLongLds + 1) + 2)));  // (count + list)
@@ -561,6 +563,7 @@ extern "C" void sw_encoder_destroy(sw_encoder* h) {
     if (h->ev_fork_long) (void)hipEventDestroy(h->ev_fork_long);
     (void)hipFree(h->d_spt);
     (void)hipFree(h->d_spf);
+    (void)hipFree(h->d_spf_list);
     (void)hipFree(h->d_spf_off);
     (void)hipFree(h->d_nsp);
     (void)hipFree(h->d_table);
@@ -807,9 +810,9 @@ int32_t grow_dedupe(sw_encoder* h) {
   uint4* dres = nullptr;
   uint8_t* dcnt = nullptr;
   bool ok = !h->test_fail_grow;
-  ok = ok && hipMalloc(&dtab, sizeof(uint64_t) * slots) == hipSuccess;
-  ok = ok && hipMalloc(&dres, sizeof(uint4) * slots) == hipSuccess;
-  ok = ok && hipMalloc(&dcnt, slots) == hipSuccess;
+  ok = ok && hipMalloc(&dtab, sizeof(uint64_t) * (slots + SW_DD_HOT)) == hipSuccess;
+  ok = ok && hipMalloc(&dres, sizeof(uint4) * (slots + SW_DD_HOT)) == hipSuccess;
+  ok = ok && hipMalloc(&dcnt, slots + SW_DD_HOT) == hipSuccess;
   __atomic_store_n(h->h_ddfull, 0ULL, __ATOMIC_RELEASE);
   if (!ok) {
     if (dtab) (void)hipFree(dtab);
@@ -859,6 +862,7 @@ int32_t set_specials(sw_encoder* h, const sw_specials* sp) {
   for (int64_t k = 0; k < n; ++k) ids[(size_t)k] = sp->ids[k];
   std::vector<std::vector<int32_t>> by_first(256);
   int32_t max_len = 0, min_len = INT32_MAX;
+  const bool few = n <= 255;  // (the one-pass finder records a special's index in a byte)
   for (int64_t k = 0; k < n; ++k) {
     const int32_t L = off[(size_t)k + 1] - off[(size_t)k];
     if (L == 0) continue;  // (an empty special never matches)
@@ -900,7 +904,7 @@ int32_t set_specials(sw_encoder* h, const sw_specials* sp) {
   t.first = (const int32_t*)(d + o_first);
   h->spt = t;
   h->spt_key = key;
-  h->spt_dev = t.n_first > 0 && max_len <= kSpMaxLen;
+  h->spt_dev = t.n_first > 0 && max_len <= kSpMaxLen && few;
   h->spt_min_len = t.n_first > 0 ? min_len : 1;
   return SW_OK;
 }
@@ -913,7 +917,7 @@ int32_t find_specials_device(sw_encoder* h, const uint8_t* d_bytes, int64_t n_by
     return fail(SW_ERR_ARG, "sw_find_specials_device: bad arguments");
   if (n_bytes > kMaxLaunchBytes) return fail(SW_ERR_ARG, "sw_find_specials_device: n_bytes > 2^30 - 64");
   if (h->d_spt && h->spt.n_first > 0 && !h->spt_dev)
-    return fail(SW_ERR_ARG, "sw_find_specials_device: a special is longer than 64 bytes (use the host finder)");
+    return fail(SW_ERR_ARG, "sw_find_specials_device: a special over 64 bytes, or over 255 specials (use the host finder)");
   if (h->spt.n_first > 0 && n_bytes > 0 && (cap < n_bytes / h->spt_min_len || !d_pos || !d_len || !d_id))
     return fail(SW_ERR_CAP, "sw_find_specials_device: cap < n_bytes / (shortest special's length)");
   if (h->ws_pending && h->ws_stream != st) HIP_TRY(hipStreamWaitEvent(st, h->ws_done, 0));
@@ -923,27 +927,46 @@ int32_t find_specials_device(sw_encoder* h, const uint8_t* d_bytes, int64_t n_by
   } else {
     int32_t rc = ensure_workspace(h, n_bytes);
     if (rc) return rc;
-    if (n_tiles > h->spf_tiles) {
-      (void)hipFree(h->d_spf); (void)hipFree(h->d_spf_off);
-      h->d_spf = nullptr; h->d_spf_off = nullptr; h->spf_tiles = 0;
-      HIP_TRY(hipMalloc(&h->d_spf, sizeof(uint32_t) * (size_t)n_tiles * (2 * 64 + 2)));
-      HIP_TRY(hipMalloc(&h->d_spf_off, sizeof(int64_t) * (size_t)(n_tiles + (n_tiles + kScanBlock - 1) / kScanBlock + 1)));
+    const int64_t tcap = kTile / h->spt_min_len + 1;  // (a tile's occurrences: at most this many)
+    const int64_t n_parts = (n_tiles + kScanBlock - 1) / kScanBlock + 1;
+    if (n_tiles > h->spf_tiles || tcap > h->spf_tcap) {
+      (void)hipFree(h->d_spf); (void)hipFree(h->d_spf_list); (void)hipFree(h->d_spf_off);
+      h->d_spf = nullptr; h->d_spf_list = nullptr; h->d_spf_off = nullptr; h->spf_tiles = 0; h->spf_tcap = 0;
+      HIP_TRY(hipMalloc(&h->d_spf, sizeof(uint32_t) * ((size_t)n_tiles * (2 * 64 + 2) + 1)));
+      HIP_TRY(hipMalloc(&h->d_spf_list, sizeof(uint32_t) * (size_t)n_tiles * (size_t)tcap));
+      HIP_TRY(hipMalloc(&h->d_spf_off, sizeof(int64_t) * (size_t)(2 * (n_tiles + n_parts) + 1)));
       h->spf_tiles = n_tiles;
+      h->spf_tcap = tcap;
     }
     SpFind f;
     f.bytes = d_bytes; f.n_bytes = n_bytes; f.str_off = d_str_off; f.n_str = n_str;
     f.tile_slo = h->d_tile_slo; f.n_tiles = n_tiles;
     f.cbits = h->d_spf; f.chosen = h->d_spf + 64 * n_tiles;
     f.tcand = h->d_spf + 128 * n_tiles; f.tcnt = f.tcand + n_tiles;
+    f.flag = (unsigned int*)(f.tcnt + n_tiles);
+    f.list = h->d_spf_list; f.tcap = tcap;
+    int64_t* toff = h->d_spf_off;                     // [n_tiles] + partials
+    int64_t* toff2 = h->d_spf_off + n_tiles + n_parts;  // the global path's
+    int64_t* total2 = toff2 + n_tiles + n_parts;
     const dim3 gw((unsigned)((n_tiles + kWaves - 1) / kWaves)), bw(kThreads);
+    HIP_TRY(hipMemsetAsync(f.flag, 0, sizeof(unsigned int), st));
     hipLaunchKernelGGL(k_tile_strings, dim3((unsigned)((n_tiles + 255) / 256)), dim3(256), 0, st, d_str_off, n_str,
                        n_tiles, h->d_tile_slo, nullptr);
-    if (h->spt.n_first <= kSpMaxFirstSwar) hipLaunchKernelGGL(k_sp_detect<true>, gw, bw, 0, st, h->spt, f);
+    const bool swar = h->spt.n_first <= kSpMaxFirstSwar;
+    // the one-pass path
+    if (swar) hipLaunchKernelGGL(k_sp_find<true>, gw, bw, 0, st, h->spt, f);
+    else hipLaunchKernelGGL(k_sp_find<false>, gw, bw, 0, st, h->spt, f);
+    HIP_TRY(launch_scan(st, f.tcnt, n_tiles, toff + n_tiles, toff, d_count));
+    hipLaunchKernelGGL(k_sp_emit, gw, bw, 0, st, h->spt, f, (const int64_t*)toff, d_pos, d_len, d_id);
+    // the global-memory path: its kernels return at once unless k_sp_find raised the flag
+    if (swar) hipLaunchKernelGGL(k_sp_detect<true>, gw, bw, 0, st, h->spt, f);
     else hipLaunchKernelGGL(k_sp_detect<false>, gw, bw, 0, st, h->spt, f);
     hipLaunchKernelGGL(k_sp_resolve, gw, bw, 0, st, h->spt, f);
     hipLaunchKernelGGL(k_sp_count, gw, bw, 0, st, f);
-    HIP_TRY(launch_scan(st, f.tcnt, n_tiles, h->d_spf_off + n_tiles, h->d_spf_off, d_count));
-    hipLaunchKernelGGL(k_sp_write, gw, bw, 0, st, h->spt, f, (const int64_t*)h->d_spf_off, d_pos, d_len, d_id);
+    HIP_TRY(launch_scan(st, f.tcnt, n_tiles, toff2 + n_tiles, toff2, total2));
+    hipLaunchKernelGGL(k_sp_write, gw, bw, 0, st, h->spt, f, (const int64_t*)toff2, d_pos, d_len, d_id);
+    hipLaunchKernelGGL(k_sp_fix_count, dim3(1), dim3(64), 0, st, (const unsigned int*)f.flag, (const int64_t*)total2,
+                       d_count);
     HIP_TRY(hipGetLastError());
   }
   HIP_TRY(hipEventRecord(h->ws_done, st));
@@ -1022,7 +1045,7 @@ int32_t encode_device(sw_encoder* h, const uint8_t* d_bytes, int64_t n_bytes, co
     // (cleared per launch rather than entry by entry by the merge kernels that empty the claims:
     // the memset leaves the table's lines in the caches, and the probes then hit -- clearing only
     // the claims made k_split_classify 2% slower on C2, r4n/r4o A/B)
-    if (h->dedupe) HIP_TRY(hipMemsetAsync(h->d_dtab, 0, sizeof(uint64_t) * ((size_t)a.dmask + 1), st));
+    if (h->dedupe) HIP_TRY(hipMemsetAsync(h->d_dtab, 0, sizeof(uint64_t) * ((size_t)a.dmask + 1 + SW_DD_HOT), st));
     if (fused) {
       const PbArgs pg{d_bytes, n_bytes, d_str_off, n_str, h->d_tile_slo, spa};
       hipLaunchKernelGGL(k_edges, dim3((unsigned)((n_tiles + 1 + 255) / 256)), dim3(256), 0, st, pg, n_tiles,

@@ -88,6 +88,9 @@ constexpr uint32_t kNoDid = 0x7FFFFFFu;    // (27-bit dense result field of a qu
 constexpr int64_t kDdSlotsDefault = 1LL << 22;  // dedupe table entries at most to start with (32 MiB)
 constexpr int64_t kDdSlotsMax = 1LL << 26;      // ... and after growing (a queue entry's dense field: 27 bits)
 constexpr int kDdExactMax = 7;             // dedupe keys of <= this many bytes are exact (no verification)
+#ifndef SW_DD_HOT
+#define SW_DD_HOT 0                        // dedupe: entries of a small table probed first (0: none)
+#endif
 #ifndef SW_PAIR_MAX_N
 #define SW_PAIR_MAX_N 16                   // k_merge_bucket<N>: two chunks per lane up to this N (0: never)
 #endif
@@ -912,8 +915,17 @@ __device__ __forceinline__ DdOut dedupe_claim(const EncArgs& a, const uint32_t* 
                              : ((uint64_t)((h2 >> 6) & a.dfp_mask & 0x3FFFFFFu) << 37 | (uint64_t)n << 31);
   const uint64_t mine = exact ? tag : (tag | (uint64_t)start);
   const uint32_t grp = h & a.dmask & ~7u;
+#if SW_DD_HOT
+  // a small table first (SW_DD_HOT entries after the main table's, L2-resident): the first
+  // chunks to claim its lines are, on Zipf text, mostly the frequent ones, and their later
+  // occurrences then find them there instead of in a line of the large table (a miss to HBM)
+  const uint32_t hgrp = (a.dmask + 1) + ((h2 >> 9) & (uint32_t)(SW_DD_HOT - 1) & ~7u);
+  for (int j = 0; j < 16; ++j) {
+    const uint32_t idx = j < 8 ? (hgrp | ((h2 + j) & 7u)) : (grp | ((h2 + j) & 7u));
+#else
   for (int j = 0; j < 8; ++j) {
     const uint32_t idx = grp | ((h2 + j) & 7u);
+#endif
     unsigned long long* p = (unsigned long long*)a.dtab + idx;
     // an entry changes once (0 -> final), so a cached plain load is safe: a stale 0 only sends
     // this lane to the CAS, which returns the live value

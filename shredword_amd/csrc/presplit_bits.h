@@ -231,6 +231,9 @@ SW_HD inline Masks classify(const Bytes& by, uint64_t ss, const Cls& cls, bool c
       X |= t;
       if (v != kInvalidCp) {
         int c = fast_class(v);
+#if defined(SW_DIAG_NO_UCD)  // (diagnostic builds only: timing without the table reads, wrong classes)
+        if (c < 0) c = kOther;
+#endif
         if (c < 0) c = cls(v);
         apply(k, v, c);
       }

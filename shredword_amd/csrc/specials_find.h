@@ -5,16 +5,22 @@
 // position the first special in dict order wins; the scan resumes after it.
 //
 // Leftmost-first with resumption is a sequential rule, but its chain is short: an occurrence only
-// hides the candidates that start inside it.  So, over 2 KiB tiles (one wave each):
-//   k_sp_detect   candidates: positions where some special matches inside its string (the first
-//                 byte against the specials' first bytes by SWAR compares, the rest only there), one
-//                 bit per byte; a count per tile
-//   k_sp_resolve  a candidate no earlier candidate covers is an occurrence ("clean"); from each clean
-//                 candidate that covers the next one, one lane walks the cluster of overlapping
-//                 candidates left to right exactly as the scan would (rare: only specials that can
-//                 overlap themselves or each other produce clusters)
-//   k_sp_count + scan + k_sp_write   the occurrences, ascending, with their lengths and ids
-// Only tiles with candidates do more than read a count after k_sp_detect.  Included by encode.hip.
+// hides the candidates that start inside it.  A candidate (a position where some special matches
+// inside its string) that no earlier candidate covers is an occurrence ("clean"); the candidates a
+// clean one covers form its cluster, which the sequential scan walks left to right, and so does one
+// lane here (rare: only specials that overlap themselves or each other make clusters).
+//
+// The common path is one pass over the input, one wave per 2 KiB tile (k_sp_find): the tile and 128
+// bytes before it staged in LDS with their string starts, every candidate of that window found
+// (the first byte against the specials' first bytes by SWAR compares, the rest only there) and
+// recorded in LDS as its special's index, the clusters walked from every clean candidate of the
+// last 64 bytes before the tile on, and the tile's occurrences listed per tile; then a scan of the
+// per-tile counts and k_sp_emit writes them out, ascending.  A cluster that began more than 64
+// bytes before its tile (a long run of overlapping candidates, e.g. "aaaa..." with "aa" and "aaa")
+// cannot be walked inside one window: the tile raises a flag, and the launch is redone by the
+// global-memory path (k_sp_detect / k_sp_resolve / k_sp_count / k_sp_write: one bit per byte,
+// clusters walked across tiles), whose kernels return at once when the flag is clear.
+// Included by encode.hip.
 #pragma once
 #include <hip/hip_runtime.h>
 
@@ -52,6 +58,9 @@ struct SpFind {
   uint32_t* chosen;  // [n_tiles * 64] occurrence starts
   uint32_t* tcand;   // [n_tiles] candidates per tile
   uint32_t* tcnt;    // [n_tiles] occurrences per tile
+  uint32_t* list;    // [n_tiles * tcap] k_sp_find: per tile, its occurrences (offset | special << 11)
+  int64_t tcap;
+  unsigned int* flag;  // set by k_sp_find: the global-memory path redoes the launch
 };
 
 // the end of the string holding byte p: the first string start past p
@@ -93,6 +102,7 @@ __device__ __forceinline__ uint32_t mm4_hi(uint32_t x) { return ((x & 0x80808080
 // k_sp_detect: lane l of tile t's wave owns bytes [t0 + 32 l, + 32)
 template <bool kSwar>
 __global__ void __launch_bounds__(kThreads) k_sp_detect(SpTab T, SpFind f) {
+  if (__hip_atomic_load(f.flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) return;  // (the common path did it)
   __shared__ uint32_t s_filt[8];
   if (!kSwar) {
     if (threadIdx.x < 8) s_filt[threadIdx.x] = T.filt[threadIdx.x];
@@ -165,6 +175,7 @@ __device__ __forceinline__ int64_t sp_next_cand(const SpFind& f, int64_t q, int6
 }
 
 __global__ void __launch_bounds__(kThreads) k_sp_resolve(SpTab T, SpFind f) {
+  if (__hip_atomic_load(f.flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) return;
   const int lane = threadIdx.x & 63;
   const int64_t t = (int64_t)blockIdx.x * kWaves + wave_in_block();
   if (t >= f.n_tiles || f.tcand[t] == 0) return;
@@ -197,7 +208,8 @@ __global__ void __launch_bounds__(kThreads) k_sp_count(SpFind f) {
   const int lane = threadIdx.x & 63;
   const int64_t t = (int64_t)blockIdx.x * kWaves + wave_in_block();
   if (t >= f.n_tiles) return;
-  uint32_t n = f.tcand[t] ? (uint32_t)__popc(f.chosen[t * 64 + lane]) : 0u;
+  const bool on = __hip_atomic_load(f.flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
+  uint32_t n = on && f.tcand[t] ? (uint32_t)__popc(f.chosen[t * 64 + lane]) : 0u;
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) n += (uint32_t)__shfl_xor((int)n, off, 64);
   if (lane == 0) f.tcnt[t] = n;
@@ -205,6 +217,7 @@ __global__ void __launch_bounds__(kThreads) k_sp_count(SpFind f) {
 
 __global__ void __launch_bounds__(kThreads) k_sp_write(SpTab T, SpFind f, const int64_t* toff, int64_t* pos,
                                                        int32_t* len, int32_t* id) {
+  if (__hip_atomic_load(f.flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) return;
   const int lane = threadIdx.x & 63;
   const int64_t t = (int64_t)blockIdx.x * kWaves + wave_in_block();
   if (t >= f.n_tiles || f.tcnt[t] == 0) return;
@@ -221,6 +234,194 @@ __global__ void __launch_bounds__(kThreads) k_sp_write(SpTab T, SpFind f, const 
     id[o] = T.ids[k];
     ++o;
   }
+}
+
+// ---- the one-pass path ---------------------------------------------------------------------
+constexpr int kSfPre = 128;                          // bytes staged before the tile
+constexpr int kSfBytes = kSfPre + kTile + kSpMaxLen;  // the byte window [t0 - 128, t0 + 2048 + 64)
+constexpr int kSfCand = kSfPre + kTile;              // candidate positions [t0 - 128, t0 + 2048)
+constexpr int kSfSsWords = (kSfBytes + 32) / 32 + 1; // string-start bits of the window (+ its end)
+constexpr uint8_t kSfNone = 0xFF;                    // (no candidate: at most 255 specials here)
+
+struct SfShared {
+  uint32_t b[kSfBytes / 4 + 4];  // the window's bytes (zeros outside the batch)
+  uint32_t ss[kSfSsWords];       // string starts (the batch end included)
+  uint32_t chosen[kTile / 32];   // occurrences starting in the tile
+  uint32_t seen[kTile / 32];     // tile candidates some cluster walk decided
+  uint8_t ci[kSfCand];           // the candidate's special, or kSfNone
+};
+
+__device__ __forceinline__ uint32_t sf_byte(const SfShared& m, int r) { return (m.b[r >> 2] >> (8 * (r & 3))) & 0xFFu; }
+
+// the first string start after window position r (the window's end when none is staged)
+__device__ __forceinline__ int sf_next_start(const SfShared& m, int r) {
+  for (int q = r + 1; q < kSfSsWords * 32;) {
+    const uint32_t w = m.ss[q >> 5] >> (q & 31);
+    if (w) return q + __builtin_ctz(w);
+    q = (q | 31) + 1;
+  }
+  return kSfSsWords * 32;
+}
+
+template <bool kSwar>
+__global__ void __launch_bounds__(kThreads) k_sp_find(SpTab T, SpFind f) {
+  __shared__ SfShared s_all[kWaves];
+  __shared__ uint32_t s_filt[8];
+  if (!kSwar) {
+    if (threadIdx.x < 8) s_filt[threadIdx.x] = T.filt[threadIdx.x];
+    __syncthreads();
+  }
+  const int lane = threadIdx.x & 63;
+  const int64_t t = (int64_t)blockIdx.x * kWaves + wave_in_block();
+  if (t >= f.n_tiles) return;
+  SfShared& m = s_all[wave_in_block()];
+  const int64_t t0 = t << kTileBits, wb = t0 - kSfPre;
+  // 1. the window's bytes, its string starts; no candidates yet
+  if (((uintptr_t)f.bytes & 15) == 0 && wb >= 0 && wb + kSfBytes <= f.n_bytes) {
+    for (int i = lane; i < kSfBytes / 16; i += 64) {
+      const u32x4 x = SW_LDNT((const u32x4*)(f.bytes + wb) + i);
+      *(uint4*)(m.b + 4 * i) = make_uint4(x[0], x[1], x[2], x[3]);
+    }
+  } else {
+    for (int i = lane; i < kSfBytes / 4; i += 64) {
+      uint32_t v = 0;
+      for (int k = 0; k < 4; ++k) {
+        const int64_t p = wb + 4 * i + k;
+        v |= (p >= 0 && p < f.n_bytes ? (uint32_t)f.bytes[p] : 0u) << (8 * k);
+      }
+      m.b[i] = v;
+    }
+  }
+  if (lane < 4) m.b[kSfBytes / 4 + lane] = 0;
+  for (int i = lane; i < kSfSsWords; i += 64) m.ss[i] = 0;
+  m.chosen[lane] = 0;
+  m.seen[lane] = 0;
+  for (int i = lane; i < kSfCand / 4; i += 64) ((uint32_t*)m.ci)[i] = 0xFFFFFFFFu;
+  wave_sync_mem();
+  {
+    const int64_t first = t > 0 ? f.tile_slo[t - 1] : 0;  // (<= the first string starting in the window)
+    const int64_t span = (int64_t)kSfSsWords * 32;
+    for (int64_t i0 = first; i0 <= f.n_str; i0 += 64) {
+      const int64_t i = i0 + lane;
+      int64_t r = span;
+      if (i <= f.n_str) r = f.str_off[i] - wb;
+      if (r >= 0 && r < span) atomicOr(&m.ss[r >> 5], 1u << (r & 31));
+      if (__ballot(r < span) != ~0ULL) break;  // (offsets ascend: past the window)
+    }
+  }
+  wave_sync_mem();
+  // 2. candidates of [t0 - 128, t0 + 2048): 68 groups of 32 positions
+  for (int g = lane; g < kSfCand / 32; g += 64) {
+    uint32_t mk = 0;
+    if (kSwar) {
+      for (int j = 0; j < T.n_first; ++j) {
+        const uint32_t fb = ((T.fb >> (8 * j)) & 0xFFu) * 0x01010101u;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) mk |= mm4_hi(zero_bytes(m.b[8 * g + i] ^ fb)) << (4 * i);
+      }
+    } else {
+      for (int k = 0; k < 32; ++k) {
+        const uint32_t b = sf_byte(m, 32 * g + k);
+        mk |= ((s_filt[b >> 5] >> (b & 31)) & 1u) << k;
+      }
+    }
+    const int64_t p0 = wb + 32 * g;  // (positions outside the batch match nothing)
+    if (p0 < 0) mk &= p0 + 32 <= 0 ? 0u : ~0u << (-p0);
+    if (p0 + 32 > f.n_bytes) mk &= p0 >= f.n_bytes ? 0u : (1u << (f.n_bytes - p0)) - 1u;
+    int end = -1;
+    for (; mk; mk &= mk - 1) {
+      const int r = 32 * g + __builtin_ctz(mk);
+      if (r >= end) end = sf_next_start(m, r);
+      const uint32_t b = sf_byte(m, r);
+      for (int32_t gi = T.first[b]; gi < T.first[b + 1]; ++gi) {
+        const int32_t k = T.list[gi];
+        const int32_t o = T.off[k], L = T.off[k + 1] - o;
+        if (r + L > end) continue;
+        bool same = true;
+        for (int32_t q = 1; q < L && same; ++q) same = sf_byte(m, r + q) == T.bytes[o + q];
+        if (same) {
+          m.ci[r] = (uint8_t)k;
+          break;
+        }
+      }
+    }
+  }
+  wave_sync_mem();
+  auto len_of = [&](int r) -> int { const int32_t k = m.ci[r]; return T.off[k + 1] - T.off[k]; };
+  // 3. clean candidates of [t0 - 64, t0 + 2048) and their clusters' walks (decisions inside the tile)
+  for (int g = lane + 2; g < kSfCand / 32; g += 64) {
+    for (int k = 0; k < 32; ++k) {
+      const int r = 32 * g + k;
+      if (m.ci[r] == kSfNone) continue;
+      bool clean = true;
+      for (int q = max(r - (T.max_len - 1), 0); q < r && clean; ++q)
+        clean = m.ci[q] == kSfNone || q + len_of(q) <= r;
+      if (!clean) continue;
+      const int L = len_of(r);
+      if (r >= kSfPre) atomicOr(&m.chosen[(r - kSfPre) >> 5], 1u << ((r - kSfPre) & 31));
+      int span = r + L, taken = r + L;
+      for (int q = r + 1; q < span && q < kSfCand; ++q) {
+        if (m.ci[q] == kSfNone) continue;
+        const int Lq = len_of(q);
+        if (q >= kSfPre) atomicOr(&m.seen[(q - kSfPre) >> 5], 1u << ((q - kSfPre) & 31));
+        if (q >= taken) {
+          if (q >= kSfPre) atomicOr(&m.chosen[(q - kSfPre) >> 5], 1u << ((q - kSfPre) & 31));
+          taken = q + Lq;
+        }
+        span = max(span, q + Lq);
+      }
+    }
+  }
+  wave_sync_mem();
+  // 4. a tile candidate no walk decided (neither clean nor reached: its cluster began before the
+  //    window's decidable part) sends the launch to the global-memory path
+  {
+    uint32_t undecided = 0;
+    for (int k = 0; k < 32; ++k) {
+      const int r = kSfPre + 32 * lane + k;
+      if (m.ci[r] == kSfNone) continue;
+      const uint32_t bit = 1u << k;
+      if (!(m.chosen[lane] & bit) && !(m.seen[lane] & bit)) {
+        bool clean = true;  // (a clean candidate is always chosen: only dirty unreached ones count)
+        for (int q = max(r - (T.max_len - 1), 0); q < r && clean; ++q)
+          clean = m.ci[q] == kSfNone || q + len_of(q) <= r;
+        if (!clean) undecided |= bit;
+      }
+    }
+    if (__ballot(undecided != 0) && lane == 0) __hip_atomic_store(f.flag, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  // 5. the tile's occurrences, ascending: offset | special << 11
+  const uint32_t c = m.chosen[lane];
+  const uint32_t cnt = (uint32_t)__popc(c);
+  const uint32_t incl = wave_incl_scan(cnt, lane);
+  uint32_t o = incl - cnt;
+  for (uint32_t x = c; x; x &= x - 1) {
+    const int k = __builtin_ctz(x), r = kSfPre + 32 * lane + k;
+    f.list[t * f.tcap + o++] = (uint32_t)(32 * lane + k) | ((uint32_t)m.ci[r] << 11);
+  }
+  if (lane == 63) f.tcnt[t] = incl;
+}
+
+__global__ void __launch_bounds__(kThreads) k_sp_emit(SpTab T, SpFind f, const int64_t* toff, int64_t* pos,
+                                                      int32_t* len, int32_t* id) {
+  if (__hip_atomic_load(f.flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) return;  // (the global path writes)
+  const int lane = threadIdx.x & 63;
+  const int64_t t = (int64_t)blockIdx.x * kWaves + wave_in_block();
+  if (t >= f.n_tiles) return;
+  const uint32_t n = f.tcnt[t];
+  const int64_t o = toff[t];
+  for (uint32_t i = lane; i < n; i += 64) {
+    const uint32_t e = f.list[t * f.tcap + i];
+    const int32_t k = (int32_t)(e >> 11);
+    pos[o + i] = (t << kTileBits) + (int64_t)(e & 2047u);
+    len[o + i] = T.off[k + 1] - T.off[k];
+    id[o + i] = T.ids[k];
+  }
+}
+
+// the global path's count replaces the one-pass count when it ran
+__global__ void k_sp_fix_count(const unsigned int* flag, const int64_t* total2, int64_t* count) {
+  if (threadIdx.x == 0 && __hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) *count = *total2;
 }
 
 }  // namespace sw

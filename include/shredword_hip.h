@@ -134,7 +134,7 @@ int32_t sw_encoder_unpin_host(sw_encoder* h, void* ptr);
  *                          host threads, uploads, encodes and downloads of consecutive runs
  *                          overlapping, ids downloaded as 16 bits when every id fits */
 #define SW_OPT_PIPE_RUN_BYTES 9
-/*   SW_OPT_DEDUPE_EXACT    1 (default): dedupe keys of chunks up to 7 bytes are the bytes
+/*   SW_OPT_DEDUPE_EXACT    1 (default): dedupe keys of chunks up to 14 bytes are the bytes
  *                          themselves (no verification read); 0: every key is a fingerprint
  *                          verified against the first occurrence's bytes (testing) */
 #define SW_OPT_DEDUPE_EXACT 10
@@ -297,7 +297,9 @@ int32_t sw_encode_device_ex(sw_encoder* h, const uint8_t* d_bytes, int64_t n_byt
                             int64_t* n_tokens_host);
 
 /* sw_encode_batch with special tokens (specials NULL or empty: exactly sw_encode_batch): the
- * occurrences are found on the host threads (sw_find_specials_host); the pre-split is the
+ * occurrences are found on the device launch by launch (sw_find_specials_device; SW_OPT_DEVICE_SPECIALS)
+ * or on the host threads (sw_find_specials_host: a special over 64 bytes, a caller's bitmap, or the
+ * host pre-split) -- the same occurrences either way; the pre-split is the
  * device's, or the host threads' with SW_OPT_HOST_PRESPLIT (chunk_bits from the caller must come
  * from sw_presplit_host_specials on the same specials).  Host buffers; synchronous. */
 int32_t sw_encode_batch_ex(sw_encoder* h, const uint8_t* bytes, const int64_t* str_off, int64_t n_str, int32_t pattern,

@@ -284,15 +284,15 @@ int32_t ensure_workspace(sw_encoder* h, int64_t n_bytes) {
   HIP_TRY(hipMalloc(&h->d_boff, sizeof(int64_t) * kNumBuckets * n_tiles));
   HIP_TRY(hipMalloc(&h->d_qtotal, sizeof(int64_t)));
   HIP_TRY(hipMalloc(&h->d_part, sizeof(int64_t) * ((kNumBuckets * n_tiles + kScanBlock - 1) / kScanBlock + 1)));
-  {  // dedupe table: ~1 entry per 64 input bytes, 2^6 .. 2^22 entries (32 MiB) to start with, more
+  {  // dedupe table: ~1 entry per 64 input bytes, 2^6 .. 2^22 entries (64 MiB) to start with, more
      // when a launch overflows it (grow_dedupe), and a 16-byte result head + a count byte per entry
     int64_t slots = 64;
     while (slots < nb / 64 && slots < kDdSlotsDefault) slots <<= 1;
     slots = std::max(slots, h->dd_slots);
     h->dd_slots = slots;
-    HIP_TRY(hipMalloc(&h->d_dtab, sizeof(uint64_t) * (slots + SW_DD_HOT)));
-    HIP_TRY(hipMalloc(&h->d_dres, sizeof(uint4) * (slots + SW_DD_HOT)));
-    HIP_TRY(hipMalloc(&h->d_dcnt, slots + SW_DD_HOT));
+    HIP_TRY(hipMalloc(&h->d_dtab, sizeof(uint64_t) * kDdWords * (slots)));
+    HIP_TRY(hipMalloc(&h->d_dres, sizeof(uint4) * (slots)));
+    HIP_TRY(hipMalloc(&h->d_dcnt, slots));
     h->dmask = (uint32_t)(slots - 1);
   }
   HIP_TRY(hipMalloc(&h->d_big, sizeof(uint32_t) * (nb / (kLongLds + 1) + 2)));  // (count + list)
@@ -810,9 +810,9 @@ int32_t grow_dedupe(sw_encoder* h) {
   uint4* dres = nullptr;
   uint8_t* dcnt = nullptr;
   bool ok = !h->test_fail_grow;
-  ok = ok && hipMalloc(&dtab, sizeof(uint64_t) * (slots + SW_DD_HOT)) == hipSuccess;
-  ok = ok && hipMalloc(&dres, sizeof(uint4) * (slots + SW_DD_HOT)) == hipSuccess;
-  ok = ok && hipMalloc(&dcnt, slots + SW_DD_HOT) == hipSuccess;
+  ok = ok && hipMalloc(&dtab, sizeof(uint64_t) * kDdWords * (slots)) == hipSuccess;
+  ok = ok && hipMalloc(&dres, sizeof(uint4) * (slots)) == hipSuccess;
+  ok = ok && hipMalloc(&dcnt, slots) == hipSuccess;
   __atomic_store_n(h->h_ddfull, 0ULL, __ATOMIC_RELEASE);
   if (!ok) {
     if (dtab) (void)hipFree(dtab);
@@ -885,15 +885,35 @@ int32_t set_specials(sw_encoder* h, const sw_specials* sp) {
   t.fb = fb;
   t.max_len = max_len;
   t.n = (int32_t)n;
-  // one buffer: bytes | off | ids | list | first
+  // the LDS image of k_sp_find (specials_find.h, above sft_len), when the finder takes the table
+  std::vector<uint32_t> img;
+  if (few && max_len <= kSpMaxLen) {
+    t.o_first = (int32_t)n;
+    t.o_list = t.o_first + 129;
+    t.o_words = t.o_list + (int32_t)((n + 3) / 4);
+    img.assign((size_t)t.o_words, 0u);
+    for (int b = 0; b <= 256; ++b) img[(size_t)t.o_first + b / 2] |= (uint32_t)first[(size_t)b] << (16 * (b & 1));
+    for (size_t g = 0; g < (size_t)first[256]; ++g)
+      img[(size_t)t.o_list + g / 4] |= (uint32_t)list[g] << (8 * (g & 3));
+    for (int64_t k = 0; k < n; ++k) {
+      const int32_t L = off[(size_t)k + 1] - off[(size_t)k];
+      const size_t wo = img.size() - (size_t)t.o_words;
+      img[(size_t)k] = (uint32_t)wo | (uint32_t)L << 16;
+      img.resize(img.size() + (size_t)(L + 3) / 4, 0u);
+      std::memcpy(img.data() + t.o_words + wo, sp->bytes + sp->off[k], (size_t)L);
+    }
+    t.img_words = (int32_t)img.size();
+  }
+  // one buffer: bytes | off | ids | list | first | LDS image
   const size_t o_off = ((size_t)nb + 15) & ~(size_t)15, o_ids = o_off + 4 * off.size(), o_list = o_ids + 4 * ids.size(),
-               o_first = o_list + 4 * list.size(), total = o_first + 4 * first.size();
+               o_first = o_list + 4 * list.size(), o_img = o_first + 4 * first.size(), total = o_img + 4 * img.size();
   std::vector<char> host(total, 0);
   std::memcpy(host.data(), sp->bytes + b0, (size_t)nb);
   std::memcpy(host.data() + o_off, off.data(), 4 * off.size());
   std::memcpy(host.data() + o_ids, ids.data(), 4 * ids.size());
   std::memcpy(host.data() + o_list, list.data(), 4 * list.size());
   std::memcpy(host.data() + o_first, first.data(), 4 * first.size());
+  if (!img.empty()) std::memcpy(host.data() + o_img, img.data(), 4 * img.size());
   HIP_TRY(hipMalloc(&h->d_spt, total));
   HIP_TRY(hipMemcpy(h->d_spt, host.data(), total, hipMemcpyHostToDevice));
   char* d = (char*)h->d_spt;
@@ -902,6 +922,7 @@ int32_t set_specials(sw_encoder* h, const sw_specials* sp) {
   t.ids = (const int32_t*)(d + o_ids);
   t.list = (const int32_t*)(d + o_list);
   t.first = (const int32_t*)(d + o_first);
+  t.img = img.empty() ? nullptr : (const uint32_t*)(d + o_img);
   h->spt = t;
   h->spt_key = key;
   h->spt_dev = t.n_first > 0 && max_len <= kSpMaxLen && few;
@@ -954,17 +975,21 @@ int32_t find_specials_device(sw_encoder* h, const uint8_t* d_bytes, int64_t n_by
                        n_tiles, h->d_tile_slo, nullptr);
     const bool swar = h->spt.n_first <= kSpMaxFirstSwar;
     // the one-pass path
-    if (swar) hipLaunchKernelGGL(k_sp_find<true>, gw, bw, 0, st, h->spt, f);
-    else hipLaunchKernelGGL(k_sp_find<false>, gw, bw, 0, st, h->spt, f);
+    const size_t lds_tab = sizeof(uint32_t) * (size_t)h->spt.img_words;
+    if (swar) hipLaunchKernelGGL(k_sp_find<true>, gw, bw, lds_tab, st, h->spt, f);
+    else hipLaunchKernelGGL(k_sp_find<false>, gw, bw, lds_tab, st, h->spt, f);
     HIP_TRY(launch_scan(st, f.tcnt, n_tiles, toff + n_tiles, toff, d_count));
-    hipLaunchKernelGGL(k_sp_emit, gw, bw, 0, st, h->spt, f, (const int64_t*)toff, d_pos, d_len, d_id);
-    // the global-memory path: its kernels return at once unless k_sp_find raised the flag
-    if (swar) hipLaunchKernelGGL(k_sp_detect<true>, gw, bw, 0, st, h->spt, f);
-    else hipLaunchKernelGGL(k_sp_detect<false>, gw, bw, 0, st, h->spt, f);
-    hipLaunchKernelGGL(k_sp_resolve, gw, bw, 0, st, h->spt, f);
-    hipLaunchKernelGGL(k_sp_count, gw, bw, 0, st, f);
+    const dim3 ge((unsigned)((n_tiles + kWaves * kSfEmitTiles - 1) / (kWaves * kSfEmitTiles)));
+    hipLaunchKernelGGL(k_sp_emit, ge, bw, 0, st, h->spt, f, (const int64_t*)toff, d_pos, d_len, d_id);
+    // the global-memory path: its kernels return at once unless k_sp_find raised the flag (small
+    // grids that loop over the tiles)
+    const dim3 gg(std::min<unsigned>(gw.x, kSfGlobalBlocks));
+    if (swar) hipLaunchKernelGGL(k_sp_detect<true>, gg, bw, 0, st, h->spt, f);
+    else hipLaunchKernelGGL(k_sp_detect<false>, gg, bw, 0, st, h->spt, f);
+    hipLaunchKernelGGL(k_sp_resolve, gg, bw, 0, st, h->spt, f);
+    hipLaunchKernelGGL(k_sp_count, gg, bw, 0, st, f);
     HIP_TRY(launch_scan(st, f.tcnt, n_tiles, toff2 + n_tiles, toff2, total2));
-    hipLaunchKernelGGL(k_sp_write, gw, bw, 0, st, h->spt, f, (const int64_t*)toff2, d_pos, d_len, d_id);
+    hipLaunchKernelGGL(k_sp_write, gg, bw, 0, st, h->spt, f, (const int64_t*)toff2, d_pos, d_len, d_id);
     hipLaunchKernelGGL(k_sp_fix_count, dim3(1), dim3(64), 0, st, (const unsigned int*)f.flag, (const int64_t*)total2,
                        d_count);
     HIP_TRY(hipGetLastError());
@@ -1045,7 +1070,7 @@ int32_t encode_device(sw_encoder* h, const uint8_t* d_bytes, int64_t n_bytes, co
     // (cleared per launch rather than entry by entry by the merge kernels that empty the claims:
     // the memset leaves the table's lines in the caches, and the probes then hit -- clearing only
     // the claims made k_split_classify 2% slower on C2, r4n/r4o A/B)
-    if (h->dedupe) HIP_TRY(hipMemsetAsync(h->d_dtab, 0, sizeof(uint64_t) * ((size_t)a.dmask + 1 + SW_DD_HOT), st));
+    if (h->dedupe) HIP_TRY(hipMemsetAsync(h->d_dtab, 0, sizeof(uint64_t) * kDdWords * ((size_t)a.dmask + 1), st));
     if (fused) {
       const PbArgs pg{d_bytes, n_bytes, d_str_off, n_str, h->d_tile_slo, spa};
       hipLaunchKernelGGL(k_edges, dim3((unsigned)((n_tiles + 1 + 255) / 256)), dim3(256), 0, st, pg, n_tiles,

@@ -36,15 +36,35 @@ constexpr int kTileBits = 11;
 constexpr int kTile = 1 << kTileBits;        // input bytes per classify workgroup
 constexpr int kThreads = 256;                // 4 waves
 constexpr int kWaves = kThreads / 64;
-// this thread's wave in its workgroup
-__device__ __forceinline__ int wave_in_block() { return (int)(threadIdx.x >> 6); }
-// ... as a scalar (readfirstlane): the compiler then keeps the tile indices in SGPRs.
-// k_split_classify: 80 VGPRs + 40 B of scratch -> 75-80 VGPRs, no scratch, 3.12 -> 3.03 ms
-// (r6b A/B).  Only where it is tested exact: with it in every kernel a batch cut into 2-tile
-// launches got wrong string offsets (r6d; not yet explained).
+// The wave's index in its block as a scalar (readfirstlane): the compiler then keeps the tile
+// indices in SGPRs.  k_split_classify: 80 VGPRs + 36 B of scratch -> 80 VGPRs, no scratch, 3.20 ->
+// 3.09 ms on C2, 6.14 -> 5.88 on ENTROPY (r6r A/B).  Rounds 4-5 measured it 180x slower with wrong
+// string offsets: a miscompiled 64-bit min (tile_end below), not the index.
 #ifndef SW_WAVE_SCALAR
-#define SW_WAVE_SCALAR 0
+#define SW_WAVE_SCALAR 1
 #endif
+#ifndef SW_WAVE_SCALAR_ALL
+#define SW_WAVE_SCALAR_ALL 0  // (every kernel's wave index, not only k_split_classify's)
+#endif
+__device__ __forceinline__ int wave_in_block() {
+#if SW_WAVE_SCALAR_ALL
+  return __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+#else
+  return (int)(threadIdx.x >> 6);
+#endif
+}
+#ifdef SW_DIAG_SFIRST
+__device__ unsigned int g_diag_sfirst;
+#endif
+// A tile's end, min(t0 + kTile, n_bytes), in 32 bits (a launch is < 2^30 bytes).  With the tile
+// index in SGPRs (wave_in_block_s), ROCm 7.2's compiler lowered the 64-bit signed min to a VALU
+// compare (writing VCC) followed by s_cselect reading SCC -- the carry of the add before it: t1 was
+// always n_bytes, every wave walked the strings to the batch's end (the 180x slower kernel of
+// rounds 4-5) and wrote other tiles' string offsets (SW_DIAG_SFIRST build, r6q).  The 32-bit min
+// is one s_min_i32.
+__device__ __forceinline__ int64_t tile_end(int64_t t0, int64_t n_bytes) {
+  return (int64_t)min((int32_t)t0 + (int32_t)kTile, (int32_t)n_bytes);
+}
 __device__ __forceinline__ int wave_in_block_s() {
 #if SW_WAVE_SCALAR
   return __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
@@ -85,12 +105,14 @@ constexpr uint32_t kRlDense = 0x80000000u;
 constexpr uint32_t kCsPos = 0x7FFFu, kCsSpecial = 0x8000u;
 constexpr uint32_t kSpDone = 0xFFFFFFFEu;  // (table_lookups: the chunk's slot is written already)
 constexpr uint32_t kNoDid = 0x7FFFFFFu;    // (27-bit dense result field of a queue entry: none)
-constexpr int64_t kDdSlotsDefault = 1LL << 22;  // dedupe table entries at most to start with (32 MiB)
-constexpr int64_t kDdSlotsMax = 1LL << 26;      // ... and after growing (a queue entry's dense field: 27 bits)
-constexpr int kDdExactMax = 7;             // dedupe keys of <= this many bytes are exact (no verification)
-#ifndef SW_DD_HOT
-#define SW_DD_HOT 0                        // dedupe: entries of a small table probed first (0: none)
+#ifndef SW_DD_WIDE
+#define SW_DD_WIDE 0                       // dedupe entries of two words (exact keys up to 14 bytes; r6o A/B: not faster)
 #endif
+constexpr int64_t kDdSlotsDefault = 1LL << 22;  // dedupe table entries at most to start with (32 MiB; wide: 64)
+constexpr int64_t kDdSlotsMax = 1LL << 26;      // ... and after growing (a queue entry's dense field: 27 bits)
+constexpr int kDdWords = SW_DD_WIDE ? 2 : 1;    // 64-bit words per dedupe entry
+constexpr uint32_t kDdGroup = 8 / kDdWords;     // entries per 64-byte line (a chunk's candidates)
+constexpr int kDdExactMax = SW_DD_WIDE ? 14 : 7;  // dedupe keys of <= this many bytes are exact (no verification)
 #ifndef SW_PAIR_MAX_N
 #define SW_PAIR_MAX_N 16                   // k_merge_bucket<N>: two chunks per lane up to this N (0: never)
 #endif
@@ -881,15 +903,21 @@ __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t x, int lane) {
 // Batch-wide dedupe of queued chunks (in k_classify).  Real text repeats its multi-token words
 // endlessly, and a chunk's encoding depends on its bytes alone, so the merge loop needs to run
 // once per DISTINCT chunk of the launch.  The table (cleared before every launch) holds one
-// word per claimed chunk, 8 candidates per chunk in one 64-byte line:
-//   exact keys, chunks of <= 7 bytes:  bytes | length << 56 | 1 << 63
-//   longer chunks:                     26-bit fingerprint << 37 | length << 31 | position
-// The first occurrence claims an entry with a CAS and is merged; its result head lands in
+// entry of two words {w0, w1} per claimed chunk, 4 candidates per chunk in one 64-byte line:
+//   exact keys, chunks of <= 14 bytes:  w0 = bytes 0..6 | length << 56 | 1 << 63,
+//                                        w1 = bytes 7..13 | 1 << 63 (chunks of 8..14 bytes)
+//   longer chunks:                       w0 = 26-bit fingerprint << 37 | length << 31 | position
+// The first occurrence claims an entry with a CAS on w0 and is merged; its result head lands in
 // dres at the entry's index, which every later occurrence refers to (slot_dref): nothing has to
 // be read back from the claimant.  Exact keys decide equality by themselves; a fingerprint match
 // is confirmed by comparing the bytes with the claimant's bytes in the (immutable) input, so no
 // hash collision can change a result.  A chunk that finds no free candidate merges itself.
-// Only the CAS needs cross-XCD coherence.  u: the chunk's bytes as zero-padded LE words.
+// Only the CAS and w1 need cross-XCD coherence: the claimant stores w1 right after its CAS, and a
+// chunk whose w0 matches reads w1 (coherently if its cached copy is still 0) a few times; when w1
+// is still not visible it merges itself (never wrong, only not shared).  Round 4 kept one word
+// (exact up to 7 bytes, SW_DD_WIDE=0): every repeat of an 8..14-byte chunk then re-read the
+// claimant's bytes at a random place in the input, a dependent miss.
+// u: the chunk's bytes as zero-padded LE words.
 // ---------------------------------------------------------------------------------------
 constexpr uint64_t kDdExact = 1ULL << 63;
 struct DdOut {
@@ -911,32 +939,49 @@ __device__ __forceinline__ DdOut dedupe_claim(const EncArgs& a, const uint32_t* 
   }
   const uint32_t h2 = (h ^ (h >> 16)) * 0x7FEB352Du;
   const bool exact = n <= (int)a.dexact;
-  const uint64_t tag = exact ? ((uint64_t)u[0] | ((uint64_t)u[1] << 32) | ((uint64_t)n << 56) | kDdExact)
+  const uint64_t lo7 = (uint64_t)u[0] | ((uint64_t)(u[1] & 0xFFFFFFu) << 32);
+  const uint64_t tag = exact ? (lo7 | ((uint64_t)n << 56) | kDdExact)
                              : ((uint64_t)((h2 >> 6) & a.dfp_mask & 0x3FFFFFFu) << 37 | (uint64_t)n << 31);
   const uint64_t mine = exact ? tag : (tag | (uint64_t)start);
-  const uint32_t grp = h & a.dmask & ~7u;
-#if SW_DD_HOT
-  // a small table first (SW_DD_HOT entries after the main table's, L2-resident): the first
-  // chunks to claim its lines are, on Zipf text, mostly the frequent ones, and their later
-  // occurrences then find them there instead of in a line of the large table (a miss to HBM)
-  const uint32_t hgrp = (a.dmask + 1) + ((h2 >> 9) & (uint32_t)(SW_DD_HOT - 1) & ~7u);
-  for (int j = 0; j < 16; ++j) {
-    const uint32_t idx = j < 8 ? (hgrp | ((h2 + j) & 7u)) : (grp | ((h2 + j) & 7u));
-#else
-  for (int j = 0; j < 8; ++j) {
-    const uint32_t idx = grp | ((h2 + j) & 7u);
+#if SW_DD_WIDE
+  const bool two = exact && n > 7;  // (w1 holds bytes 7..13)
+  const uint64_t w1 = ((uint64_t)(u[1] >> 24) | ((uint64_t)u[2] << 8) | ((uint64_t)(u[3] & 0xFFFFu) << 40)) | kDdExact;
 #endif
-    unsigned long long* p = (unsigned long long*)a.dtab + idx;
+  const uint32_t grp = h & a.dmask & ~(kDdGroup - 1);
+  for (int j = 0; j < (int)kDdGroup; ++j) {
+    const uint32_t idx = grp | ((h2 + j) & (kDdGroup - 1));
+    unsigned long long* p = (unsigned long long*)a.dtab + (size_t)kDdWords * idx;
     // an entry changes once (0 -> final), so a cached plain load is safe: a stale 0 only sends
     // this lane to the CAS, which returns the live value
+#if SW_DD_WIDE
+    const ulonglong2 e = *(const ulonglong2*)p;  // (both words in one request)
+    uint64_t cur = e.x;
+#else
     uint64_t cur = *p;
+#endif
     if (cur == 0) {
       cur = atomicCAS(p, 0ULL, (unsigned long long)mine);
-      if (cur == 0) return DdOut{1, idx};  // claimed: this chunk is merged and shared
+      if (cur == 0) {  // claimed: this chunk is merged and shared
+#if SW_DD_WIDE
+        if (two) __hip_atomic_store(p + 1, (unsigned long long)w1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#endif
+        return DdOut{1, idx};
+      }
     }
     if (exact) {
-      if (cur == mine) return DdOut{2, idx};
-      continue;
+      if (cur != mine) continue;
+#if SW_DD_WIDE
+      if (two) {
+        uint64_t c1 = e.y;
+        for (int t = 0; c1 == 0 && t < 8; ++t) {  // (the claimant's w1 not seen yet)
+          if (t) __builtin_amdgcn_s_sleep(2);
+          c1 = __hip_atomic_load(p + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        if (c1 == 0) return DdOut{0, 0};
+        if (c1 != w1) continue;
+      }
+#endif
+      return DdOut{2, idx};
     }
     if ((cur & ~0x7FFFFFFFULL) != tag) continue;
     const int64_t other = (int64_t)(cur & 0x7FFFFFFFULL);
@@ -1015,7 +1060,7 @@ constexpr int kRelEndLong = 1 << 30;
 template <bool kSp>  // kSp: the launch has special-token occurrences (a.sp)
 __device__ __forceinline__ void classify_chunks(const EncArgs& a, int64_t tile, const uint32_t* s_b32,
                                                 uint16_t* s_cstart, uint16_t* s_qbuf, uint32_t myhalf, int rel_end,
-                                                int64_t s_first);
+                                                int64_t s_first, int64_t sp_lo, int64_t sp_hi);
 
 // one tile (the body of k_classify's tile loop): the chunk starts from the uploaded bitmap
 template <bool kSp>
@@ -1023,7 +1068,7 @@ __device__ __forceinline__ void classify_tile(const EncArgs& a, int64_t tile, ui
                                               uint16_t* s_qbuf) {
   const int lane = threadIdx.x & 63;
   const int64_t t0 = tile * kTile;
-  const int64_t t1 = min(t0 + (int64_t)kTile, a.n_bytes);
+  const int64_t t1 = tile_end(t0, a.n_bytes);
   const int64_t w0 = t0 >> 6;
 
   // 1. stage the window's bytes (1-KiB coalesced 16-byte loads) and the bitmap words (in
@@ -1048,6 +1093,7 @@ __device__ __forceinline__ void classify_tile(const EncArgs& a, int64_t tile, ui
   if (lane < 8) s_b32[kWin / 4 + lane] = 0;
   const uint64_t bw = (lane < kTileWords && w0 + lane < a.n_words) ? SW_LDNT2(&a.bits[w0 + lane]) : 0ULL;
   const int64_t s_first = a.tile_slo[tile];  // (prefetched: used by step 6)
+  const int64_t sp_lo = kSp ? a.sp.tile_sp[tile] : 0, sp_hi = kSp ? a.sp.tile_sp[tile + 1] : 0;  // (... by step 2)
 
   // 2. chunk starts in [t0, t1): lane l owns bits 32 l .. 32 l + 31 of the tile (half of bitmap
   //    word l / 2: all 64 lanes enumerate, half as many starts each as with a word per lane)
@@ -1082,7 +1128,7 @@ __device__ __forceinline__ void classify_tile(const EncArgs& a, int64_t tile, ui
       last_end = min(q, a.n_bytes);
     }
   }
-  classify_chunks<kSp>(a, tile, s_b32, s_cstart, s_qbuf, myhalf, (int)(last_end - t0), s_first);
+  classify_chunks<kSp>(a, tile, s_b32, s_cstart, s_qbuf, myhalf, (int)(last_end - t0), s_first, sp_lo, sp_hi);
 }
 
 // The tile's chunks from its chunk-start bits on: lane l holds bits 32 l .. 32 l + 31 of the tile
@@ -1091,12 +1137,12 @@ __device__ __forceinline__ void classify_tile(const EncArgs& a, int64_t tile, ui
 template <bool kSp>
 __device__ __forceinline__ void classify_chunks(const EncArgs& a, int64_t tile, const uint32_t* s_b32,
                                                 uint16_t* s_cstart, uint16_t* s_qbuf, uint32_t myhalf, int rel_end,
-                                                int64_t s_first) {
+                                                int64_t s_first, int64_t sp_lo, int64_t sp_hi) {
   SW_STAMP_INIT;
   const int lane = threadIdx.x & 63;
   const uint64_t lt_mask = (lane == 0) ? 0ULL : (~0ULL >> (64 - lane));
   const int64_t t0 = tile * kTile;
-  const int64_t t1 = min(t0 + (int64_t)kTile, a.n_bytes);
+  const int64_t t1 = tile_end(t0, a.n_bytes);
   const uint32_t cnt = (uint32_t)__popc(myhalf);
   const uint32_t incl = wave_incl_scan(cnt, lane);
   const int C = (int)__shfl(incl, 63, 64);
@@ -1111,8 +1157,12 @@ __device__ __forceinline__ void classify_chunks(const EncArgs& a, int64_t tile, 
   wave_sync_mem();
   if (kSp) {  // the special-token occurrences starting in the tile (each one whole chunk): their
               // slots get the specials' ids, their chunks the flag the lookups skip -- once per tile
-    const int64_t sp_lo = a.sp.tile_sp[tile];
-    const int64_t sp_hi = a.sp.tile_sp[tile + 1];
+    // (sp_lo, sp_hi: tile_sp[tile], tile_sp[tile + 1] -- loaded by k_classify at its start, here
+    // for k_split_classify (-1))
+    if (sp_lo < 0) {
+      sp_lo = a.sp.tile_sp[tile];
+      sp_hi = a.sp.tile_sp[tile + 1];
+    }
     for (int64_t j = sp_lo + lane; j < sp_hi; j += 64) {
       const int p = (int)(a.sp.pos[j] - t0);
       int lo = 0, hi = C;  // (its chunk: the first whose start is >= p, and it starts at p)
@@ -1135,7 +1185,11 @@ __device__ __forceinline__ void classify_chunks(const EncArgs& a, int64_t tile, 
   //    kernels and counted per length bucket (lane b: bucket b).
   int32_t* dst = a.scratch + t0;
   const int rounds = (C + 63) >> 6;
+#ifdef SW_DIAG_NO_LOOKUP  // (diagnostic, wrong ids: every multi-byte chunk "hits" token 0, no memory access)
+  const bool use_table = false;
+#else
   const bool use_table = a.chunks.enabled != 0;
+#endif
   const int64_t mis = (int64_t)((uintptr_t)a.bytes & 3);
   const uint32_t* gwords = (const uint32_t*)((uintptr_t)a.bytes - mis);
   const int64_t last_word = (mis + a.n_bytes - 1) >> 2;
@@ -1158,7 +1212,11 @@ __device__ __forceinline__ void classify_chunks(const EncArgs& a, int64_t tile, 
           const int ls = (int)(cs & kCsPos);
           const int end = (k + 1 < C) ? (int)(s_cstart[k + 1] & kCsPos) : rel_end;
           tok[u] = (kSp && (cs & kCsSpecial)) ? kSpDone
-                   : (valid && end - ls == 1) ? (s_b32[ls >> 2] >> (8 * (ls & 3))) & 0xFFu : kInf;
+                   : (valid && end - ls == 1) ? (s_b32[ls >> 2] >> (8 * (ls & 3))) & 0xFFu
+#ifdef SW_DIAG_NO_LOOKUP
+                   : (valid && end - ls <= kShort) ? 0u
+#endif
+                   : kInf;
         }
       }
 #pragma unroll
@@ -1262,8 +1320,34 @@ __device__ __forceinline__ void classify_chunks(const EncArgs& a, int64_t tile, 
 #else
   const int64_t s_first_now = s_first;
 #endif
+#ifdef SW_DIAG_SFIRST  // (diagnostic build: the first string against a fresh binary search)
+  {
+    int64_t lo = 0, hi = a.n_str;
+    while (lo < hi) {
+      const int64_t m = (lo + hi) >> 1;
+      if (a.str_off[m] < t0) lo = m + 1; else hi = m;
+    }
+    const int64_t v = __hip_atomic_load(&a.tile_slo[tile], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint64_t bad = __ballot(s_first_now != lo || v != lo);
+    if (bad && lane == (int)__builtin_ctzll(bad)) {
+      const unsigned k = atomicAdd(&g_diag_sfirst, 1u);
+      if (k < 12)
+        printf("sfirst tile %ld blk %u tid %u lane %d: reg %ld coherent %ld search %ld n_str %ld t0 %ld C %d bad %016lx\n",
+               (long)tile, blockIdx.x, threadIdx.x, lane, (long)s_first_now, (long)v, (long)lo, (long)a.n_str, (long)t0,
+               C, (unsigned long)bad);
+    }
+  }
+#endif
+#ifdef SW_DIAG_SFIRST
+  int diag_it = 0;
+  int64_t diag_p = -1;
+#endif
   for (int64_t s = s_first_now + lane; s < a.n_str; s += 64) {
     const int64_t p = a.str_off[s];
+#ifdef SW_DIAG_SFIRST
+    ++diag_it;
+    diag_p = p;
+#endif
     if (p >= t1) break;
     int lo = 0, hi = C;  // first chunk with start >= p
     const int lp = (int)(p - t0);
@@ -1273,6 +1357,18 @@ __device__ __forceinline__ void classify_chunks(const EncArgs& a, int64_t tile, 
     }
     a.out_off[s] = (int64_t)lo;
   }
+#ifdef SW_DIAG_SFIRST
+  {
+    const uint64_t many = __ballot(diag_it > 4);
+    if (many && lane == (int)__builtin_ctzll(many)) {
+      const unsigned k = atomicAdd(&g_diag_sfirst, 1u);
+      if (k < 12)
+        printf("strings tile %ld lane %d: it %d last p %ld t0 %ld t1 %ld n_bytes %ld s_first %ld n_str %ld C %d\n",
+               (long)tile, lane, diag_it, (long)diag_p, (long)t0, (long)t1, (long)a.n_bytes, (long)s_first_now,
+               (long)a.n_str, C);
+    }
+  }
+#endif
   SW_STAMP(3);
   wave_sync_mem();  // (the next tile reuses the wave's LDS)
 }
@@ -2206,7 +2302,7 @@ __device__ __forceinline__ void compact_tile(const EncArgs& a, int64_t t, int64_
   const int C = (int)a.tile_slots[t];
   OutT* dst = out + base;
   // strings starting in this tile: lane i holds string s_lo + i's chunk index (k_classify)
-  const int64_t t1 = min(t * kTile + (int64_t)kTile, a.n_bytes);
+  const int64_t t1 = tile_end(t * kTile, a.n_bytes);
   const int64_t s_lo = a.tile_slo[t];
   const int64_t s_hi = (t + 1 < a.n_tiles) ? a.tile_slo[t + 1] : a.n_str;
   const int64_t my_s = s_lo + lane;

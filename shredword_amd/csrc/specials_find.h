@@ -45,6 +45,8 @@ struct SpTab {
   int32_t n_first;
   int32_t max_len;
   int32_t n;
+  const uint32_t* img;   // the table as k_sp_find stages it in LDS (layout above sft_len)
+  int32_t img_words, o_first, o_list, o_words;
 };
 
 struct SpFind {
@@ -109,8 +111,7 @@ __global__ void __launch_bounds__(kThreads) k_sp_detect(SpTab T, SpFind f) {
     __syncthreads();
   }
   const int lane = threadIdx.x & 63;
-  const int64_t t = (int64_t)blockIdx.x * kWaves + wave_in_block();
-  if (t >= f.n_tiles) return;
+  for (int64_t t = (int64_t)blockIdx.x * kWaves + wave_in_block(); t < f.n_tiles; t += (int64_t)gridDim.x * kWaves) {
   const int64_t p0 = (t << kTileBits) + 32 * lane;
   uint32_t w[8];
   if (((uintptr_t)f.bytes & 15) == 0 && p0 + 32 <= f.n_bytes) {
@@ -158,6 +159,7 @@ __global__ void __launch_bounds__(kThreads) k_sp_detect(SpTab T, SpFind f) {
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) n += (uint32_t)__shfl_xor((int)n, off, 64);
   if (lane == 0) f.tcand[t] = n;
+  }
 }
 
 // the next candidate at or after q, below lim (-1: none); one word of the candidate bits at a time
@@ -177,8 +179,8 @@ __device__ __forceinline__ int64_t sp_next_cand(const SpFind& f, int64_t q, int6
 __global__ void __launch_bounds__(kThreads) k_sp_resolve(SpTab T, SpFind f) {
   if (__hip_atomic_load(f.flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) return;
   const int lane = threadIdx.x & 63;
-  const int64_t t = (int64_t)blockIdx.x * kWaves + wave_in_block();
-  if (t >= f.n_tiles || f.tcand[t] == 0) return;
+  for (int64_t t = (int64_t)blockIdx.x * kWaves + wave_in_block(); t < f.n_tiles; t += (int64_t)gridDim.x * kWaves) {
+  if (f.tcand[t] == 0) continue;
   const int64_t p0 = (t << kTileBits) + 32 * lane;
   for (uint32_t x = f.cbits[t * 64 + lane]; x; x &= x - 1) {
     const int64_t p = p0 + __builtin_ctz(x);
@@ -202,25 +204,26 @@ __global__ void __launch_bounds__(kThreads) k_sp_resolve(SpTab T, SpFind f) {
       span = max(span, r + (int64_t)Lr);
     }
   }
+  }
 }
 
 __global__ void __launch_bounds__(kThreads) k_sp_count(SpFind f) {
+  if (__hip_atomic_load(f.flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) return;
   const int lane = threadIdx.x & 63;
-  const int64_t t = (int64_t)blockIdx.x * kWaves + wave_in_block();
-  if (t >= f.n_tiles) return;
-  const bool on = __hip_atomic_load(f.flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
-  uint32_t n = on && f.tcand[t] ? (uint32_t)__popc(f.chosen[t * 64 + lane]) : 0u;
+  for (int64_t t = (int64_t)blockIdx.x * kWaves + wave_in_block(); t < f.n_tiles; t += (int64_t)gridDim.x * kWaves) {
+    uint32_t n = f.tcand[t] ? (uint32_t)__popc(f.chosen[t * 64 + lane]) : 0u;
 #pragma unroll
-  for (int off = 32; off > 0; off >>= 1) n += (uint32_t)__shfl_xor((int)n, off, 64);
-  if (lane == 0) f.tcnt[t] = n;
+    for (int off = 32; off > 0; off >>= 1) n += (uint32_t)__shfl_xor((int)n, off, 64);
+    if (lane == 0) f.tcnt[t] = n;
+  }
 }
 
 __global__ void __launch_bounds__(kThreads) k_sp_write(SpTab T, SpFind f, const int64_t* toff, int64_t* pos,
                                                        int32_t* len, int32_t* id) {
   if (__hip_atomic_load(f.flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) return;
   const int lane = threadIdx.x & 63;
-  const int64_t t = (int64_t)blockIdx.x * kWaves + wave_in_block();
-  if (t >= f.n_tiles || f.tcnt[t] == 0) return;
+  for (int64_t t = (int64_t)blockIdx.x * kWaves + wave_in_block(); t < f.n_tiles; t += (int64_t)gridDim.x * kWaves) {
+  if (f.tcnt[t] == 0) continue;
   const uint32_t c = f.chosen[t * 64 + lane];
   const uint32_t cnt = (uint32_t)__popc(c);
   const uint32_t incl = wave_incl_scan(cnt, lane);
@@ -234,24 +237,43 @@ __global__ void __launch_bounds__(kThreads) k_sp_write(SpTab T, SpFind f, const 
     id[o] = T.ids[k];
     ++o;
   }
+  }
 }
 
 // ---- the one-pass path ---------------------------------------------------------------------
 constexpr int kSfPre = 128;                          // bytes staged before the tile
 constexpr int kSfBytes = kSfPre + kTile + kSpMaxLen;  // the byte window [t0 - 128, t0 + 2048 + 64)
 constexpr int kSfCand = kSfPre + kTile;              // candidate positions [t0 - 128, t0 + 2048)
+constexpr int kSfCandWords = kSfCand / 32;
 constexpr int kSfSsWords = (kSfBytes + 32) / 32 + 1; // string-start bits of the window (+ its end)
-constexpr uint8_t kSfNone = 0xFF;                    // (no candidate: at most 255 specials here)
 
 struct SfShared {
   uint32_t b[kSfBytes / 4 + 4];  // the window's bytes (zeros outside the batch)
   uint32_t ss[kSfSsWords];       // string starts (the batch end included)
+  uint32_t cb[kSfCandWords];     // candidates: some special matches there, inside its string
   uint32_t chosen[kTile / 32];   // occurrences starting in the tile
   uint32_t seen[kTile / 32];     // tile candidates some cluster walk decided
-  uint8_t ci[kSfCand];           // the candidate's special, or kSfNone
+  uint8_t ci[kSfCand];           // a candidate's special (valid where cb is set)
 };
 
-__device__ __forceinline__ uint32_t sf_byte(const SfShared& m, int r) { return (m.b[r >> 2] >> (8 * (r & 3))) & 0xFFu; }
+// The specials' table as k_sp_find stages it in LDS (SpTab.img, built by sw_encoder_set_specials),
+// 32-bit words:
+//   [0, n)                special k: its first word in the byte area | its length << 16
+//   [o_first, + 129)      first byte b's group starts at list entry group[b] (16 bits each, 257)
+//   [o_list, ...)         the specials grouped by first byte, dict order within a group (8 bits each)
+//   [o_words, ...)        every special's bytes from a word boundary, zero padded
+__device__ __forceinline__ int sft_len(const uint32_t* s, int k) { return (int)(s[k] >> 16); }
+__device__ __forceinline__ int sft_group(const uint32_t* s, int o_first, int b) {
+  return (int)((s[o_first + (b >> 1)] >> (16 * (b & 1))) & 0xFFFFu);
+}
+__device__ __forceinline__ int sft_list(const uint32_t* s, int o_list, int g) {
+  return (int)((s[o_list + (g >> 2)] >> (8 * (g & 3))) & 0xFFu);
+}
+// the window's bytes r .. r + 3 as one word
+__device__ __forceinline__ uint32_t sf_word(const SfShared& m, int r) {
+  const int w = r >> 2;
+  return __builtin_amdgcn_alignbyte(m.b[w + 1], m.b[w], (uint32_t)(r & 3));
+}
 
 // the first string start after window position r (the window's end when none is staged)
 __device__ __forceinline__ int sf_next_start(const SfShared& m, int r) {
@@ -263,24 +285,65 @@ __device__ __forceinline__ int sf_next_start(const SfShared& m, int r) {
   return kSfSsWords * 32;
 }
 
+// the next candidate at or after q, below lim (lim when none)
+__device__ __forceinline__ int sf_next_cand(const SfShared& m, int q, int lim) {
+  lim = min(lim, kSfCand);
+  while (q < lim) {
+    const uint32_t w = m.cb[q >> 5] >> (q & 31);
+    if (w) return min(q + __builtin_ctz(w), lim);
+    q = (q | 31) + 1;
+  }
+  return lim;
+}
+
+// clean: no earlier candidate (within the longest special) covers r
+__device__ __forceinline__ bool sf_clean(const SfShared& m, const uint32_t* s, int r, int max_len) {
+  for (int q = sf_next_cand(m, max(r - (max_len - 1), 0), r); q < r; q = sf_next_cand(m, q + 1, r))
+    if (q + sft_len(s, m.ci[q]) > r) return false;
+  return true;
+}
+
+#ifndef SW_SF_WAVES
+#define SW_SF_WAVES 7
+#endif
 template <bool kSwar>
-__global__ void __launch_bounds__(kThreads) k_sp_find(SpTab T, SpFind f) {
+__global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(SW_SF_WAVES, SW_SF_WAVES)))
+k_sp_find(SpTab T, SpFind f) {
+  extern __shared__ uint32_t s_sft[];  // T.img (T.img_words words)
   __shared__ SfShared s_all[kWaves];
   __shared__ uint32_t s_filt[8];
-  if (!kSwar) {
-    if (threadIdx.x < 8) s_filt[threadIdx.x] = T.filt[threadIdx.x];
-    __syncthreads();
-  }
   const int lane = threadIdx.x & 63;
   const int64_t t = (int64_t)blockIdx.x * kWaves + wave_in_block();
+  const int64_t tc = min(t, f.n_tiles - 1);
+  // the loads whose latencies overlap: the window's first string, the window's bytes, then its
+  // string offsets (waiting for the first only)
+  const int64_t first = tc > 0 ? f.tile_slo[tc - 1] : 0;  // (<= the first string starting in the window)
+  const int64_t t0 = tc << kTileBits, wb = t0 - kSfPre;
+  const bool fast = ((uintptr_t)f.bytes & 15) == 0 && wb >= 0 && wb + kSfBytes <= f.n_bytes;
+  constexpr int kSfVec = (kSfBytes / 16 + 63) / 64;  // 16-byte loads a lane
+  u32x4 xs[kSfVec];
+  if (fast) {
+#pragma unroll
+    for (int j = 0; j < kSfVec; ++j) {
+      const int i = lane + 64 * j;
+      if (i < kSfBytes / 16) xs[j] = SW_LDNT((const u32x4*)(f.bytes + wb) + i);
+    }
+  }
+  const int64_t span = (int64_t)kSfSsWords * 32;
+  int64_t r0 = span;
+  if (first + lane <= f.n_str) r0 = f.str_off[first + lane] - wb;
+  for (int i = threadIdx.x; i < T.img_words; i += kThreads) s_sft[i] = T.img[i];
+  if (!kSwar && threadIdx.x < 8) s_filt[threadIdx.x] = T.filt[threadIdx.x];
+  __syncthreads();
+  const uint32_t* s = s_sft;
   if (t >= f.n_tiles) return;
   SfShared& m = s_all[wave_in_block()];
-  const int64_t t0 = t << kTileBits, wb = t0 - kSfPre;
-  // 1. the window's bytes, its string starts; no candidates yet
-  if (((uintptr_t)f.bytes & 15) == 0 && wb >= 0 && wb + kSfBytes <= f.n_bytes) {
-    for (int i = lane; i < kSfBytes / 16; i += 64) {
-      const u32x4 x = SW_LDNT((const u32x4*)(f.bytes + wb) + i);
-      *(uint4*)(m.b + 4 * i) = make_uint4(x[0], x[1], x[2], x[3]);
+  // 1. the window's bytes and its string starts
+  if (fast) {
+#pragma unroll
+    for (int j = 0; j < kSfVec; ++j) {
+      const int i = lane + 64 * j;
+      if (i < kSfBytes / 16) *(uint4*)(m.b + 4 * i) = make_uint4(xs[j][0], xs[j][1], xs[j][2], xs[j][3]);
     }
   } else {
     for (int i = lane; i < kSfBytes / 4; i += 64) {
@@ -296,73 +359,73 @@ __global__ void __launch_bounds__(kThreads) k_sp_find(SpTab T, SpFind f) {
   for (int i = lane; i < kSfSsWords; i += 64) m.ss[i] = 0;
   m.chosen[lane] = 0;
   m.seen[lane] = 0;
-  for (int i = lane; i < kSfCand / 4; i += 64) ((uint32_t*)m.ci)[i] = 0xFFFFFFFFu;
   wave_sync_mem();
-  {
-    const int64_t first = t > 0 ? f.tile_slo[t - 1] : 0;  // (<= the first string starting in the window)
-    const int64_t span = (int64_t)kSfSsWords * 32;
-    for (int64_t i0 = first; i0 <= f.n_str; i0 += 64) {
-      const int64_t i = i0 + lane;
-      int64_t r = span;
-      if (i <= f.n_str) r = f.str_off[i] - wb;
-      if (r >= 0 && r < span) atomicOr(&m.ss[r >> 5], 1u << (r & 31));
-      if (__ballot(r < span) != ~0ULL) break;  // (offsets ascend: past the window)
-    }
+  for (int64_t i0 = first;;) {
+    if (r0 >= 0 && r0 < span) atomicOr(&m.ss[r0 >> 5], 1u << (r0 & 31));
+    if (__ballot(r0 < span) != ~0ULL) break;  // (offsets ascend: past the window)
+    i0 += 64;
+    if (i0 > f.n_str) break;
+    r0 = i0 + lane <= f.n_str ? f.str_off[i0 + lane] - wb : span;
   }
   wave_sync_mem();
-  // 2. candidates of [t0 - 128, t0 + 2048): 68 groups of 32 positions
-  for (int g = lane; g < kSfCand / 32; g += 64) {
+  // 2. candidates of [t0 - 128, t0 + 2048), 32 positions a lane: the first byte by SWAR compares
+  //    (or the first-byte set), the rest word by word against the LDS table, first match in dict order
+  for (int g = lane; g < kSfCandWords; g += 64) {
     uint32_t mk = 0;
     if (kSwar) {
+      const uint4 q0 = *(const uint4*)(m.b + 8 * g), q1 = *(const uint4*)(m.b + 8 * g + 4);
+      const uint32_t w[8] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w};
       for (int j = 0; j < T.n_first; ++j) {
         const uint32_t fb = ((T.fb >> (8 * j)) & 0xFFu) * 0x01010101u;
 #pragma unroll
-        for (int i = 0; i < 8; ++i) mk |= mm4_hi(zero_bytes(m.b[8 * g + i] ^ fb)) << (4 * i);
+        for (int i = 0; i < 8; ++i) mk |= mm4_hi(zero_bytes(w[i] ^ fb)) << (4 * i);
       }
     } else {
+#pragma unroll 4
       for (int k = 0; k < 32; ++k) {
-        const uint32_t b = sf_byte(m, 32 * g + k);
+        const uint32_t b = (m.b[8 * g + (k >> 2)] >> (8 * (k & 3))) & 0xFFu;
         mk |= ((s_filt[b >> 5] >> (b & 31)) & 1u) << k;
       }
     }
     const int64_t p0 = wb + 32 * g;  // (positions outside the batch match nothing)
     if (p0 < 0) mk &= p0 + 32 <= 0 ? 0u : ~0u << (-p0);
     if (p0 + 32 > f.n_bytes) mk &= p0 >= f.n_bytes ? 0u : (1u << (f.n_bytes - p0)) - 1u;
+    uint32_t hit = 0;
     int end = -1;
     for (; mk; mk &= mk - 1) {
       const int r = 32 * g + __builtin_ctz(mk);
       if (r >= end) end = sf_next_start(m, r);
-      const uint32_t b = sf_byte(m, r);
-      for (int32_t gi = T.first[b]; gi < T.first[b + 1]; ++gi) {
-        const int32_t k = T.list[gi];
-        const int32_t o = T.off[k], L = T.off[k + 1] - o;
+      const int b = (int)(m.b[r >> 2] >> (8 * (r & 3))) & 0xFF;
+      const int g1 = sft_group(s, T.o_first, b + 1);
+      for (int gi = sft_group(s, T.o_first, b); gi < g1; ++gi) {
+        const int k = sft_list(s, T.o_list, gi);
+        const int L = sft_len(s, k), wo = T.o_words + (int)(s[k] & 0xFFFFu);
         if (r + L > end) continue;
         bool same = true;
-        for (int32_t q = 1; q < L && same; ++q) same = sf_byte(m, r + q) == T.bytes[o + q];
+        for (int q = 0; q < L && same; q += 4) {
+          const uint32_t msk = L - q >= 4 ? ~0u : (1u << (8 * (L - q))) - 1u;
+          same = ((sf_word(m, r + q) ^ s[wo + (q >> 2)]) & msk) == 0;
+        }
         if (same) {
           m.ci[r] = (uint8_t)k;
+          hit |= 1u << (r & 31);
           break;
         }
       }
     }
+    m.cb[g] = hit;
   }
   wave_sync_mem();
-  auto len_of = [&](int r) -> int { const int32_t k = m.ci[r]; return T.off[k + 1] - T.off[k]; };
   // 3. clean candidates of [t0 - 64, t0 + 2048) and their clusters' walks (decisions inside the tile)
-  for (int g = lane + 2; g < kSfCand / 32; g += 64) {
-    for (int k = 0; k < 32; ++k) {
-      const int r = 32 * g + k;
-      if (m.ci[r] == kSfNone) continue;
-      bool clean = true;
-      for (int q = max(r - (T.max_len - 1), 0); q < r && clean; ++q)
-        clean = m.ci[q] == kSfNone || q + len_of(q) <= r;
-      if (!clean) continue;
-      const int L = len_of(r);
+  for (int g = lane + 2; g < kSfCandWords; g += 64) {
+    for (uint32_t x = m.cb[g]; x; x &= x - 1) {
+      const int r = 32 * g + __builtin_ctz(x);
+      if (!sf_clean(m, s, r, T.max_len)) continue;
+      const int L = sft_len(s, m.ci[r]);
       if (r >= kSfPre) atomicOr(&m.chosen[(r - kSfPre) >> 5], 1u << ((r - kSfPre) & 31));
       int span = r + L, taken = r + L;
-      for (int q = r + 1; q < span && q < kSfCand; ++q) {
-        if (m.ci[q] == kSfNone) continue;
-        const int Lq = len_of(q);
+      for (int q = sf_next_cand(m, r + 1, span); q < span && q < kSfCand; q = sf_next_cand(m, q + 1, span)) {
+        const int Lq = sft_len(s, m.ci[q]);
         if (q >= kSfPre) atomicOr(&m.seen[(q - kSfPre) >> 5], 1u << ((q - kSfPre) & 31));
         if (q >= taken) {
           if (q >= kSfPre) atomicOr(&m.chosen[(q - kSfPre) >> 5], 1u << ((q - kSfPre) & 31));
@@ -377,16 +440,9 @@ __global__ void __launch_bounds__(kThreads) k_sp_find(SpTab T, SpFind f) {
   //    window's decidable part) sends the launch to the global-memory path
   {
     uint32_t undecided = 0;
-    for (int k = 0; k < 32; ++k) {
-      const int r = kSfPre + 32 * lane + k;
-      if (m.ci[r] == kSfNone) continue;
-      const uint32_t bit = 1u << k;
-      if (!(m.chosen[lane] & bit) && !(m.seen[lane] & bit)) {
-        bool clean = true;  // (a clean candidate is always chosen: only dirty unreached ones count)
-        for (int q = max(r - (T.max_len - 1), 0); q < r && clean; ++q)
-          clean = m.ci[q] == kSfNone || q + len_of(q) <= r;
-        if (!clean) undecided |= bit;
-      }
+    for (uint32_t x = m.cb[kSfPre / 32 + lane] & ~m.chosen[lane] & ~m.seen[lane]; x; x &= x - 1) {
+      const int k = __builtin_ctz(x);
+      if (!sf_clean(m, s, kSfPre + 32 * lane + k, T.max_len)) undecided |= 1u << k;
     }
     if (__ballot(undecided != 0) && lane == 0) __hip_atomic_store(f.flag, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
@@ -402,20 +458,23 @@ __global__ void __launch_bounds__(kThreads) k_sp_find(SpTab T, SpFind f) {
   if (lane == 63) f.tcnt[t] = incl;
 }
 
+constexpr int kSfEmitTiles = 8;  // k_sp_emit: tiles a wave
+constexpr unsigned kSfGlobalBlocks = 2048;  // the global path's grid (its kernels loop over the tiles)
 __global__ void __launch_bounds__(kThreads) k_sp_emit(SpTab T, SpFind f, const int64_t* toff, int64_t* pos,
                                                       int32_t* len, int32_t* id) {
   if (__hip_atomic_load(f.flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) return;  // (the global path writes)
   const int lane = threadIdx.x & 63;
-  const int64_t t = (int64_t)blockIdx.x * kWaves + wave_in_block();
-  if (t >= f.n_tiles) return;
-  const uint32_t n = f.tcnt[t];
-  const int64_t o = toff[t];
-  for (uint32_t i = lane; i < n; i += 64) {
-    const uint32_t e = f.list[t * f.tcap + i];
-    const int32_t k = (int32_t)(e >> 11);
-    pos[o + i] = (t << kTileBits) + (int64_t)(e & 2047u);
-    len[o + i] = T.off[k + 1] - T.off[k];
-    id[o + i] = T.ids[k];
+  const int64_t t1 = ((int64_t)blockIdx.x * kWaves + wave_in_block() + 1) * kSfEmitTiles;
+  for (int64_t t = t1 - kSfEmitTiles; t < t1 && t < f.n_tiles; ++t) {
+    const uint32_t n = f.tcnt[t];
+    const int64_t o = toff[t];
+    for (uint32_t i = lane; i < n; i += 64) {
+      const uint32_t e = f.list[t * f.tcap + i];
+      const int32_t k = (int32_t)(e >> 11);
+      pos[o + i] = (t << kTileBits) + (int64_t)(e & 2047u);
+      len[o + i] = T.off[k + 1] - T.off[k];
+      id[o + i] = T.ids[k];
+    }
   }
 }
 

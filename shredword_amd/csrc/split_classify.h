@@ -72,6 +72,26 @@ __device__ __forceinline__ int64_t sp_first_end(const SpArgs& sp, int64_t n_tile
   return lo;
 }
 
+// the same for a whole wave (p, lo, hi uniform): the first index in [lo, hi) whose end is at or
+// after p (hi when none), 64 probes a step instead of one (one memory round trip for <= 64 entries)
+__device__ __forceinline__ int64_t sp_first_end_wave(const SpArgs& sp, int64_t lo, int64_t hi, int64_t p, int lane) {
+  while (hi - lo > 64) {
+    const int64_t step = (hi - lo + 63) >> 6;
+    const int64_t m = lo + lane * step;
+    const uint64_t b = __ballot(m < hi && sp.pos[m] + sp.len[m] >= p);
+    if (b) {  // (the answer is in (lo + (k - 1) step, lo + k step])
+      const int64_t k = __builtin_ctzll(b);
+      hi = lo + k * step;
+      if (k) lo += (k - 1) * step + 1;
+    } else {  // (every probe below hi ends before p: the answer is past the last of them)
+      lo += ((hi - 1 - lo) / step) * step + 1;
+    }
+  }
+  const int64_t m = lo + lane;
+  const uint64_t b = __ballot(m < hi && sp.pos[m] + sp.len[m] >= p);
+  return b ? lo + __builtin_ctzll(b) : hi;
+}
+
 // bits of [p, p + 32): the occurrences' starts and ends (*ss) and their inner bytes (*inner)
 __device__ __forceinline__ void sp_bits32(const SpArgs& sp, int64_t n_tiles, int64_t p, uint32_t* ss, uint32_t* inner) {
   uint32_t s = 0, in = 0;
@@ -343,7 +363,7 @@ __device__ __forceinline__ void split_classify_tile(const EncArgs& a, const PbAr
   SW_STAMP_INIT;
   const int lane = threadIdx.x & 63;
   const int64_t t0 = tile * kTile;
-  const int64_t t1 = min(t0 + (int64_t)kTile, a.n_bytes);
+  const int64_t t1 = tile_end(t0, a.n_bytes);
   const int64_t n_chunks = (a.n_bytes + psb::kChunk - 1) / psb::kChunk;
   const int64_t c0 = tile << (kTileBits - 5), c = c0 + lane;
   const int64_t stride = a.n_tiles + 1;
@@ -424,8 +444,12 @@ __device__ __forceinline__ void split_classify_tile(const EncArgs& a, const PbAr
     sm.in[lane] = 0u;
     wave_sync_mem();
     const int64_t w0 = t0 - kScSsPre, w1 = w0 + (int64_t)kScSsWords * 32;
+    // (the first occurrence ending at or after w0, in tile - 1's range: see sp_first_end; the
+    // indices are loaded here, not at the start: held through the class masks they cost 0.27 ms, r6q)
+    const int64_t sp_prev = tile > 0 ? a.sp.tile_sp[tile - 1] : 0, sp_lo = a.sp.tile_sp[tile];
     const int64_t nsp = a.sp.tile_sp[a.n_tiles];
-    for (int64_t j0 = sp_first_end(a.sp, a.n_tiles, w0); j0 < nsp; j0 += 64) {
+    const int64_t j_first = tile > 0 ? sp_first_end_wave(a.sp, max(sp_prev - 1, (int64_t)0), sp_lo, w0, lane) : 0;
+    for (int64_t j0 = j_first; j0 < nsp; j0 += 64) {
       const int64_t j = j0 + lane;
       int64_t pa = w1, pe = w1;
       if (j < nsp) {
@@ -520,7 +544,7 @@ __device__ __forceinline__ void split_classify_tile(const EncArgs& a, const PbAr
   else if (a.n_bytes <= t1 + 32) rel_end = (int)(a.n_bytes - t0);
   else rel_end = kRelEndLong;
   wave_sync_mem();  // (the masks' LDS becomes the chunk-start list)
-  classify_chunks<kSp>(a, tile, s_win + kScPre / 4, sh->cstart, s_qbuf, r, rel_end, s_first);
+  classify_chunks<kSp>(a, tile, s_win + kScPre / 4, sh->cstart, s_qbuf, r, rel_end, s_first, -1, -1);
 }
 
 #ifndef SW_SC_WAVES

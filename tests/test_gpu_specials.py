@@ -241,3 +241,26 @@ def test_encode_with_device_found_specials(pattern):
         L.sw_encoder_set_option(h, _lib.SW_OPT_DEVICE_SPECIALS, 1)
         L.sw_encoder_set_option(h, _lib.SW_OPT_PIPE_RUN_BYTES, 128 << 20)
     t.close()
+
+
+@pytest.mark.parametrize("per_kib", [64, 300])
+def test_dense_specials_device_path(per_kib):
+    """Special-dense batches (64 and 300 occurrences per KiB, the bench's `dense` corpus and
+    denser): more occurrences in a tile's index range than one wave's 64 probes, so the window's
+    first-occurrence search (sp_first_end_wave) takes its multi-step path; the device finder and
+    the encode against the oracle, GPT-2 and cl100k."""
+    import torch
+    bench_sp = {"<|endoftext|>": 50256, "<|fim_prefix|>": 50257, "<|fim_middle|>": 50258, "<|fim_suffix|>": 50259}
+    buf0, off0 = corpus.synth(5, corpus.MIXED, 3000, 1074)
+    buf, off = corpus.splice_specials(buf0, off0, bench_sp, per_kib=per_kib, end_special=0)
+    dev = torch.device("cuda", 0)
+    d_buf, d_off = torch.from_numpy(buf).to(dev), torch.from_numpy(off).to(dev)
+    for pattern in ("gpt2", "cl100k"):
+        t = tok_for("bl32k.model", pattern)
+        t.special_tokens = dict(bench_sp)
+        e_ids, e_off = expected(t, buf, off, bench_sp, pattern)
+        found = t.find_specials_device(d_buf, d_off, n_bytes=len(buf))
+        g_ids, g_off = t.encode_device(d_buf, d_off, d_specials=found, n_bytes=len(buf))
+        np.testing.assert_array_equal(g_off.cpu().numpy(), e_off)
+        np.testing.assert_array_equal(g_ids.cpu().numpy(), e_ids)
+        t.close()

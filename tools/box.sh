@@ -34,7 +34,7 @@ NB=(--no-cpu-baseline --e2e-steps 0)
 for s in "$@"; do
   case $s in
     pytest) run pytest 1100 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread ;;
-    pytest=*) run pytest_part 900 python -u -m pytest ${s#pytest=} -x -q --timeout 300 --timeout-method thread ;;
+    pytest=*) v=${s#pytest=}; run pytest_part 900 python -u -m pytest ${v//+/ } -x -q --timeout 300 --timeout-method thread ;;
     smoke) run smoke 180 python -c "import __graft_entry__ as g; g.smoke()" ;;
     c2) bench c2 --steps 20 --warmup 2 ;;
     c3) bench c3 --steps 20 --warmup 2 --presplit host "${NB[@]}" ;;

@@ -53,14 +53,11 @@ __device__ __forceinline__ int wave_in_block() {
   return (int)(threadIdx.x >> 6);
 #endif
 }
-#ifdef SW_DIAG_SFIRST
-__device__ unsigned int g_diag_sfirst;
-#endif
 // A tile's end, min(t0 + kTile, n_bytes), in 32 bits (a launch is < 2^30 bytes).  With the tile
 // index in SGPRs (wave_in_block_s), ROCm 7.2's compiler lowered the 64-bit signed min to a VALU
 // compare (writing VCC) followed by s_cselect reading SCC -- the carry of the add before it: t1 was
 // always n_bytes, every wave walked the strings to the batch's end (the 180x slower kernel of
-// rounds 4-5) and wrote other tiles' string offsets (SW_DIAG_SFIRST build, r6q).  The 32-bit min
+// rounds 4-5) and wrote other tiles' string offsets (a diagnostic build printing them, r6q).  The 32-bit min
 // is one s_min_i32.
 __device__ __forceinline__ int64_t tile_end(int64_t t0, int64_t n_bytes) {
   return (int64_t)min((int32_t)t0 + (int32_t)kTile, (int32_t)n_bytes);
@@ -105,14 +102,11 @@ constexpr uint32_t kRlDense = 0x80000000u;
 constexpr uint32_t kCsPos = 0x7FFFu, kCsSpecial = 0x8000u;
 constexpr uint32_t kSpDone = 0xFFFFFFFEu;  // (table_lookups: the chunk's slot is written already)
 constexpr uint32_t kNoDid = 0x7FFFFFFu;    // (27-bit dense result field of a queue entry: none)
-#ifndef SW_DD_WIDE
-#define SW_DD_WIDE 0                       // dedupe entries of two words (exact keys up to 14 bytes; r6o A/B: not faster)
-#endif
-constexpr int64_t kDdSlotsDefault = 1LL << 22;  // dedupe table entries at most to start with (32 MiB; wide: 64)
+constexpr int64_t kDdSlotsDefault = 1LL << 22;  // dedupe table entries at most to start with (32 MiB)
 constexpr int64_t kDdSlotsMax = 1LL << 26;      // ... and after growing (a queue entry's dense field: 27 bits)
-constexpr int kDdWords = SW_DD_WIDE ? 2 : 1;    // 64-bit words per dedupe entry
-constexpr uint32_t kDdGroup = 8 / kDdWords;     // entries per 64-byte line (a chunk's candidates)
-constexpr int kDdExactMax = SW_DD_WIDE ? 14 : 7;  // dedupe keys of <= this many bytes are exact (no verification)
+constexpr int kDdWords = 1;                     // 64-bit words per dedupe entry
+constexpr uint32_t kDdGroup = 8;                // entries per 64-byte line (a chunk's candidates)
+constexpr int kDdExactMax = 7;                  // dedupe keys of <= this many bytes are exact (no verification)
 #ifndef SW_PAIR_MAX_N
 #define SW_PAIR_MAX_N 16                   // k_merge_bucket<N>: two chunks per lane up to this N (0: never)
 #endif
@@ -903,21 +897,18 @@ __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t x, int lane) {
 // Batch-wide dedupe of queued chunks (in k_classify).  Real text repeats its multi-token words
 // endlessly, and a chunk's encoding depends on its bytes alone, so the merge loop needs to run
 // once per DISTINCT chunk of the launch.  The table (cleared before every launch) holds one
-// entry of two words {w0, w1} per claimed chunk, 4 candidates per chunk in one 64-byte line:
-//   exact keys, chunks of <= 14 bytes:  w0 = bytes 0..6 | length << 56 | 1 << 63,
-//                                        w1 = bytes 7..13 | 1 << 63 (chunks of 8..14 bytes)
-//   longer chunks:                       w0 = 26-bit fingerprint << 37 | length << 31 | position
+// word per claimed chunk, 8 candidates per chunk in one 64-byte line:
+//   exact keys, chunks of <= 7 bytes:  bytes | length << 56 | 1 << 63
+//   longer chunks:                     26-bit fingerprint << 37 | length << 31 | position
 // The first occurrence claims an entry with a CAS on w0 and is merged; its result head lands in
 // dres at the entry's index, which every later occurrence refers to (slot_dref): nothing has to
 // be read back from the claimant.  Exact keys decide equality by themselves; a fingerprint match
 // is confirmed by comparing the bytes with the claimant's bytes in the (immutable) input, so no
 // hash collision can change a result.  A chunk that finds no free candidate merges itself.
-// Only the CAS and w1 need cross-XCD coherence: the claimant stores w1 right after its CAS, and a
-// chunk whose w0 matches reads w1 (coherently if its cached copy is still 0) a few times; when w1
-// is still not visible it merges itself (never wrong, only not shared).  Round 4 kept one word
-// (exact up to 7 bytes, SW_DD_WIDE=0): every repeat of an 8..14-byte chunk then re-read the
-// claimant's bytes at a random place in the input, a dependent miss.
-// u: the chunk's bytes as zero-padded LE words.
+// Only the CAS needs cross-XCD coherence.  (Two-word entries with exact keys up to 14 bytes, the
+// second word stored after the claim, drop the verification reads of 8..14-byte chunks but were
+// not faster: round 3 in k_classify, 2.32 -> 2.50 ms; round 5 in k_split_classify, C2 3.16 ->
+// 3.21 ms, ENTROPY 14.0 -> 14.8 ms per step, r6o.)  u: the chunk's bytes as zero-padded LE words.
 // ---------------------------------------------------------------------------------------
 constexpr uint64_t kDdExact = 1ULL << 63;
 struct DdOut {
@@ -943,45 +934,20 @@ __device__ __forceinline__ DdOut dedupe_claim(const EncArgs& a, const uint32_t* 
   const uint64_t tag = exact ? (lo7 | ((uint64_t)n << 56) | kDdExact)
                              : ((uint64_t)((h2 >> 6) & a.dfp_mask & 0x3FFFFFFu) << 37 | (uint64_t)n << 31);
   const uint64_t mine = exact ? tag : (tag | (uint64_t)start);
-#if SW_DD_WIDE
-  const bool two = exact && n > 7;  // (w1 holds bytes 7..13)
-  const uint64_t w1 = ((uint64_t)(u[1] >> 24) | ((uint64_t)u[2] << 8) | ((uint64_t)(u[3] & 0xFFFFu) << 40)) | kDdExact;
-#endif
   const uint32_t grp = h & a.dmask & ~(kDdGroup - 1);
   for (int j = 0; j < (int)kDdGroup; ++j) {
     const uint32_t idx = grp | ((h2 + j) & (kDdGroup - 1));
     unsigned long long* p = (unsigned long long*)a.dtab + (size_t)kDdWords * idx;
     // an entry changes once (0 -> final), so a cached plain load is safe: a stale 0 only sends
     // this lane to the CAS, which returns the live value
-#if SW_DD_WIDE
-    const ulonglong2 e = *(const ulonglong2*)p;  // (both words in one request)
-    uint64_t cur = e.x;
-#else
     uint64_t cur = *p;
-#endif
     if (cur == 0) {
       cur = atomicCAS(p, 0ULL, (unsigned long long)mine);
-      if (cur == 0) {  // claimed: this chunk is merged and shared
-#if SW_DD_WIDE
-        if (two) __hip_atomic_store(p + 1, (unsigned long long)w1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-#endif
-        return DdOut{1, idx};
-      }
+      if (cur == 0) return DdOut{1, idx};  // claimed: this chunk is merged and shared
     }
     if (exact) {
-      if (cur != mine) continue;
-#if SW_DD_WIDE
-      if (two) {
-        uint64_t c1 = e.y;
-        for (int t = 0; c1 == 0 && t < 8; ++t) {  // (the claimant's w1 not seen yet)
-          if (t) __builtin_amdgcn_s_sleep(2);
-          c1 = __hip_atomic_load(p + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-        if (c1 == 0) return DdOut{0, 0};
-        if (c1 != w1) continue;
-      }
-#endif
-      return DdOut{2, idx};
+      if (cur == mine) return DdOut{2, idx};
+      continue;
     }
     if ((cur & ~0x7FFFFFFFULL) != tag) continue;
     const int64_t other = (int64_t)(cur & 0x7FFFFFFFULL);
@@ -1320,34 +1286,8 @@ __device__ __forceinline__ void classify_chunks(const EncArgs& a, int64_t tile, 
 #else
   const int64_t s_first_now = s_first;
 #endif
-#ifdef SW_DIAG_SFIRST  // (diagnostic build: the first string against a fresh binary search)
-  {
-    int64_t lo = 0, hi = a.n_str;
-    while (lo < hi) {
-      const int64_t m = (lo + hi) >> 1;
-      if (a.str_off[m] < t0) lo = m + 1; else hi = m;
-    }
-    const int64_t v = __hip_atomic_load(&a.tile_slo[tile], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const uint64_t bad = __ballot(s_first_now != lo || v != lo);
-    if (bad && lane == (int)__builtin_ctzll(bad)) {
-      const unsigned k = atomicAdd(&g_diag_sfirst, 1u);
-      if (k < 12)
-        printf("sfirst tile %ld blk %u tid %u lane %d: reg %ld coherent %ld search %ld n_str %ld t0 %ld C %d bad %016lx\n",
-               (long)tile, blockIdx.x, threadIdx.x, lane, (long)s_first_now, (long)v, (long)lo, (long)a.n_str, (long)t0,
-               C, (unsigned long)bad);
-    }
-  }
-#endif
-#ifdef SW_DIAG_SFIRST
-  int diag_it = 0;
-  int64_t diag_p = -1;
-#endif
   for (int64_t s = s_first_now + lane; s < a.n_str; s += 64) {
     const int64_t p = a.str_off[s];
-#ifdef SW_DIAG_SFIRST
-    ++diag_it;
-    diag_p = p;
-#endif
     if (p >= t1) break;
     int lo = 0, hi = C;  // first chunk with start >= p
     const int lp = (int)(p - t0);
@@ -1357,18 +1297,6 @@ __device__ __forceinline__ void classify_chunks(const EncArgs& a, int64_t tile, 
     }
     a.out_off[s] = (int64_t)lo;
   }
-#ifdef SW_DIAG_SFIRST
-  {
-    const uint64_t many = __ballot(diag_it > 4);
-    if (many && lane == (int)__builtin_ctzll(many)) {
-      const unsigned k = atomicAdd(&g_diag_sfirst, 1u);
-      if (k < 12)
-        printf("strings tile %ld lane %d: it %d last p %ld t0 %ld t1 %ld n_bytes %ld s_first %ld n_str %ld C %d\n",
-               (long)tile, lane, diag_it, (long)diag_p, (long)t0, (long)t1, (long)a.n_bytes, (long)s_first_now,
-               (long)a.n_str, C);
-    }
-  }
-#endif
   SW_STAMP(3);
   wave_sync_mem();  // (the next tile reuses the wave's LDS)
 }

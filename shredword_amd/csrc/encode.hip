@@ -544,7 +544,7 @@ extern "C" void sw_encoder_destroy(sw_encoder* h) {
   if (!h) return;
   {
     DeviceGuard g(h->device);
-    if (h->stream) (void)hipStreamSynchronize(h->stream);
+    (void)hipDeviceSynchronize();  // (every stream of this encoder idle before anything is freed or unpinned)
     free_workspace(h);
     free_io(h);
     if (h->ws_done) (void)hipEventSynchronize(h->ws_done);
@@ -601,10 +601,10 @@ extern "C" int32_t sw_encoder_unpin_host(sw_encoder* h, void* ptr) {
   DeviceGuard g(h->device);
   for (size_t i = 0; i < h->pins.size(); ++i) {
     if (h->pins[i].h != (char*)ptr) continue;
-    // (nothing of this encoder may still read or write it)
-    if (h->stream) HIP_TRY(hipStreamSynchronize(h->stream));
-    if (h->s_h2d) HIP_TRY(hipStreamSynchronize(h->s_h2d));
-    if (h->s_d2h) HIP_TRY(hipStreamSynchronize(h->s_d2h));
+    // (nothing may still read or write it: the whole device drained, not only this encoder's
+    // streams -- a write into the range still in flight, or held in a cache, when its mapping goes
+    // faults the device; an intermittent fault after the pinned-output test was seen in rounds 4-5)
+    HIP_TRY(hipDeviceSynchronize());
     HIP_TRY(hipHostUnregister((void*)((uintptr_t)ptr & ~(uintptr_t)4095)));
     h->pins.erase(h->pins.begin() + (long)i);
     return SW_OK;
@@ -902,6 +902,7 @@ int32_t set_specials(sw_encoder* h, const sw_specials* sp) {
       img.resize(img.size() + (size_t)(L + 3) / 4, 0u);
       std::memcpy(img.data() + t.o_words + wo, sp->bytes + sp->off[k], (size_t)L);
     }
+    img.push_back(0u);  // (k_sp_find reads a special's second word even for one of <= 4 bytes)
     t.img_words = (int32_t)img.size();
   }
   // one buffer: bytes | off | ids | list | first | LDS image
@@ -1316,6 +1317,7 @@ __global__ void __launch_bounds__(256) k_push_direct(const int32_t* __restrict__
   if (done[1] || base + n > out_cap) return;
   copy_seg((const uint8_t*)ids, (uint8_t*)(out + base), n * 4, t, nt);
   for (int64_t j = t; j < n_oo; j += nt) out_off[j] = d_oo[j] + base;
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // (system scope: the host-memory writes leave the caches here)
 }
 __global__ void k_push_advance(const int64_t* ntok, int64_t out_cap, int64_t* done) {
   if (threadIdx.x != 0) return;

@@ -1511,8 +1511,19 @@ __device__ __forceinline__ void put_lds_result(const EncArgs& a, uint64_t e, uin
 // k_merge_bucket<N>: queued chunks of buckets [b_lo, b_hi] (length <= N), one per lane;
 // persistent grid-stride over 64-entry batches of the bucket-major queue
 // ---------------------------------------------------------------------------------------
+#ifndef SW_MB_WAVES4
+#define SW_MB_WAVES4 1  // k_merge_bucket<4>: the waves per SIMD the compiler must fit (1: its choice)
+#endif
+#ifndef SW_MB_WAVES8
+#define SW_MB_WAVES8 1  // ... <8>
+#endif
+#ifndef SW_MB_WAVES16
+#define SW_MB_WAVES16 1  // ... <16>
+#endif
 template <bool kWide, bool k16, int N, bool kWF = false>  // kWF: a well-formed table (lane_merge_lds_wf)
-__global__ void __launch_bounds__(kThreads) k_merge_bucket(EncArgs a, int b_lo, int b_hi) {
+__global__ void __launch_bounds__(kThreads)
+__attribute__((amdgpu_waves_per_eu(N <= 4 ? SW_MB_WAVES4 : N <= 8 ? SW_MB_WAVES8 : N <= 16 ? SW_MB_WAVES16 : 1)))
+k_merge_bucket(EncArgs a, int b_lo, int b_hi) {
   SW_STAMP_INIT;
   const int64_t gw = ((int64_t)blockIdx.x * kWaves + wave_in_block());  // global wave id
   const int64_t n_waves = ((int64_t)gridDim.x * kThreads) >> 6;

@@ -397,12 +397,15 @@ k_sp_find(SpTab T, SpFind f) {
       if (r >= end) end = sf_next_start(m, r);
       const int b = (int)(m.b[r >> 2] >> (8 * (r & 3))) & 0xFF;
       const int g1 = sft_group(s, T.o_first, b + 1);
+      const uint32_t x0 = sf_word(m, r), x1 = sf_word(m, r + 4);  // (the first 8 bytes, once)
       for (int gi = sft_group(s, T.o_first, b); gi < g1; ++gi) {
         const int k = sft_list(s, T.o_list, gi);
         const int L = sft_len(s, k), wo = T.o_words + (int)(s[k] & 0xFFFFu);
         if (r + L > end) continue;
-        bool same = true;
-        for (int q = 0; q < L && same; q += 4) {
+        const uint32_t m0 = L >= 4 ? ~0u : (1u << (8 * L)) - 1u;
+        const uint32_t m1 = L >= 8 ? ~0u : L <= 4 ? 0u : (1u << (8 * (L - 4))) - 1u;
+        bool same = ((x0 ^ s[wo]) & m0) == 0 && ((x1 ^ s[wo + 1]) & m1) == 0;  // (s[wo + 1]: padded)
+        for (int q = 8; q < L && same; q += 4) {
           const uint32_t msk = L - q >= 4 ? ~0u : (1u << (8 * (L - q))) - 1u;
           same = ((sf_word(m, r + q) ^ s[wo + (q >> 2)]) & msk) == 0;
         }
@@ -462,19 +465,52 @@ constexpr int kSfEmitTiles = 8;  // k_sp_emit: tiles a wave
 constexpr unsigned kSfGlobalBlocks = 2048;  // the global path's grid (its kernels loop over the tiles)
 __global__ void __launch_bounds__(kThreads) k_sp_emit(SpTab T, SpFind f, const int64_t* toff, int64_t* pos,
                                                       int32_t* len, int32_t* id) {
+  __shared__ int32_t s_len[256], s_id[256];  // (the specials' lengths and ids: <= 255 of them here)
+  for (int i = threadIdx.x; i < T.n; i += kThreads) {
+    s_len[i] = T.off[i + 1] - T.off[i];
+    s_id[i] = T.ids[i];
+  }
+  __syncthreads();
   if (__hip_atomic_load(f.flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) return;  // (the global path writes)
   const int lane = threadIdx.x & 63;
-  const int64_t t1 = ((int64_t)blockIdx.x * kWaves + wave_in_block() + 1) * kSfEmitTiles;
-  for (int64_t t = t1 - kSfEmitTiles; t < t1 && t < f.n_tiles; ++t) {
-    const uint32_t n = f.tcnt[t];
-    const int64_t o = toff[t];
-    for (uint32_t i = lane; i < n; i += 64) {
-      const uint32_t e = f.list[t * f.tcap + i];
-      const int32_t k = (int32_t)(e >> 11);
-      pos[o + i] = (t << kTileBits) + (int64_t)(e & 2047u);
-      len[o + i] = T.off[k + 1] - T.off[k];
-      id[o + i] = T.ids[k];
-    }
+  // kSfEmitTiles tiles a wave, their lists as one: lane q < kSfEmitTiles loads tile t0 + q's count
+  // and output offset, and entry j of the joined lists belongs to the tile whose prefix holds it
+  const int64_t tw = ((int64_t)blockIdx.x * kWaves + wave_in_block()) * kSfEmitTiles;
+  const bool mine = lane < kSfEmitTiles && tw + lane < f.n_tiles;
+  const uint32_t cnt = mine ? f.tcnt[tw + lane] : 0u;
+  const int64_t o_t = mine ? toff[tw + lane] : 0;
+  uint32_t incl = cnt;  // (inclusive prefix over the wave's tiles, lanes 0 .. kSfEmitTiles - 1)
+#pragma unroll
+  for (int d = 1; d < kSfEmitTiles; d <<= 1) {
+    const uint32_t y = (uint32_t)__shfl_up((int)incl, d, 64);
+    if (lane >= d) incl += y;
+  }
+  uint32_t pre[kSfEmitTiles];  // (every lane holds the prefixes and offsets: shuffles outside the loop)
+  int64_t ob[kSfEmitTiles];
+#pragma unroll
+  for (int d = 0; d < kSfEmitTiles; ++d) {
+    pre[d] = (uint32_t)__shfl((int)incl, d, 64);
+    ob[d] = __shfl(o_t, d, 64);
+  }
+  const uint32_t total = pre[kSfEmitTiles - 1];
+  for (uint32_t j = lane; j < total; j += 64) {
+    int q = 0;  // (the tile: the first whose inclusive prefix exceeds j)
+    uint32_t before = 0;
+    int64_t o = ob[0];
+#pragma unroll
+    for (int d = 0; d < kSfEmitTiles - 1; ++d)
+      if (pre[d] <= j) {
+        q = d + 1;
+        before = pre[d];
+        o = ob[d + 1];
+      }
+    const int64_t t = tw + q;
+    const uint32_t i = j - before;
+    const uint32_t e = f.list[t * f.tcap + i];
+    const int32_t k = (int32_t)(e >> 11);
+    pos[o + i] = (t << kTileBits) + (int64_t)(e & 2047u);
+    len[o + i] = s_len[k];
+    id[o + i] = s_id[k];
   }
 }
 

@@ -287,15 +287,49 @@ __device__ inline int64_t next_set_bit(const uint64_t* bits, int64_t n_words, in
   return q < n_bits ? q : n_bits;
 }
 
-// exclusive block scan over kThreads threads (sh: kThreads/64 words); *total = block sum
-__device__ inline uint32_t block_excl_scan(uint32_t v, uint32_t* sh, uint32_t* total) {
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  uint32_t x = v;
+// Inclusive scan over the wave's 64 lanes (every lane active).  SW_DPP_SCAN: by DPP -- row shifts
+// 1, 2, 4, 8 within each 16-lane row, then row_bcast:15 (rows 1, 3) and row_bcast:31 (rows 2, 3),
+// six VALU operations; else six shuffles through the LDS crossbar (ds_bpermute), each a round trip.
+#ifndef SW_DPP_SCAN
+#define SW_DPP_SCAN 0
+#endif
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t x, int lane) {
+#if SW_DPP_SCAN
+  (void)lane;  // (a lane whose source is outside its row, or masked off by row_mask, adds 0)
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xF, 0xF, false);  // row_shr:1
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xF, 0xF, false);  // row_shr:2
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xF, 0xF, false);  // row_shr:4
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xF, 0xF, false);  // row_shr:8
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xA, 0xF, false);  // row_bcast:15
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xC, 0xF, false);  // row_bcast:31
+  return x;
+#else
 #pragma unroll
   for (int off = 1; off < 64; off <<= 1) {
     const uint32_t y = __shfl_up(x, off, 64);
     if (lane >= off) x += y;
   }
+  return x;
+#endif
+}
+
+// lane L's value to every lane (L a constant, every lane active): v_readlane under SW_DPP_SCAN
+// (an SGPR, no LDS crossbar round trip), else a shuffle
+__device__ __forceinline__ uint32_t lane_value(uint32_t x, int L) {
+#if SW_DPP_SCAN
+  return (uint32_t)__builtin_amdgcn_readlane((int)x, L);
+#else
+  return (uint32_t)__shfl((int)x, L, 64);
+#endif
+}
+__device__ __forceinline__ unsigned long long lane_value64(unsigned long long x, int L) {
+  return (unsigned long long)lane_value((uint32_t)x, L) | ((unsigned long long)lane_value((uint32_t)(x >> 32), L) << 32);
+}
+
+// exclusive block scan over kThreads threads (sh: kThreads/64 words); *total = block sum
+__device__ inline uint32_t block_excl_scan(uint32_t v, uint32_t* sh, uint32_t* total) {
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const uint32_t x = wave_incl_scan(v, lane);
   if (lane == 63) sh[wid] = x;
   __syncthreads();
   uint32_t base = 0, tot = 0;
@@ -884,14 +918,6 @@ struct EncArgs {
 #define SW_STAMP_INIT do {} while (0)
 #endif
 
-__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t x, int lane) {
-#pragma unroll
-  for (int off = 1; off < 64; off <<= 1) {
-    const uint32_t y = __shfl_up(x, off, 64);
-    if (lane >= off) x += y;
-  }
-  return x;
-}
 
 // ---------------------------------------------------------------------------------------
 // Batch-wide dedupe of queued chunks (in k_classify).  Real text repeats its multi-token words
@@ -1111,7 +1137,7 @@ __device__ __forceinline__ void classify_chunks(const EncArgs& a, int64_t tile, 
   const int64_t t1 = tile_end(t0, a.n_bytes);
   const uint32_t cnt = (uint32_t)__popc(myhalf);
   const uint32_t incl = wave_incl_scan(cnt, lane);
-  const int C = (int)__shfl(incl, 63, 64);
+  const int C = (int)lane_value(incl, 63);
   {
     uint32_t x = myhalf;
     uint32_t k = incl - cnt;
@@ -1237,7 +1263,7 @@ __device__ __forceinline__ void classify_chunks(const EncArgs& a, int64_t tile, 
       if (lm) {
         unsigned long long lb = 0;
         if (lane == 0) lb = atomicAdd(a.l_count, (unsigned long long)__popcll(lm));
-        lb = __shfl(lb, 0, 64);
+        lb = lane_value64(lb, 0);
         if (longc)
           a.llist[lb + __popcll(lm & lt_mask)] =
               ((uint64_t)(t0 + ls) << 32) | (len < (int)kNoDid ? (uint32_t)len : kNoDid);
@@ -1805,7 +1831,7 @@ __device__ int seg_merge(const DevTable& t, const uint8_t* src, T* id, T* rk, ui
   const uint32_t incl = wave_incl_scan(cnt, lane);
   uint32_t o = incl - cnt;
   for (uint64_t m = am; m; m &= m - 1) out[o++] = id[own(__builtin_ctzll(m))];
-  return (int)__shfl(incl, 63, 64);
+  return (int)lane_value(incl, 63);
 }
 
 // one 64-thread workgroup (one wave) per chunk; launched with a grid far larger than the
@@ -2300,7 +2326,7 @@ __device__ __forceinline__ void compact_tile(const EncArgs& a, int64_t t, int64_
       const uint32_t m = ref ? (dense ? (q.x & 0xFFFFu) : q.x) : (valid ? 1u : 0u);
       const uint32_t incl = wave_incl_scan(m, lane);
       const uint32_t o = carry + incl - m;
-      carry += __shfl(incl, 63, 64);
+      carry += lane_value(incl, 63);
       const uint32_t lo = o - gbase;
       if (valid && !ref) {
         if (lo < (uint32_t)kOutCapW) s_out[lo] = v[u];

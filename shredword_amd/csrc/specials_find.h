@@ -479,12 +479,7 @@ __global__ void __launch_bounds__(kThreads) k_sp_emit(SpTab T, SpFind f, const i
   const bool mine = lane < kSfEmitTiles && tw + lane < f.n_tiles;
   const uint32_t cnt = mine ? f.tcnt[tw + lane] : 0u;
   const int64_t o_t = mine ? toff[tw + lane] : 0;
-  uint32_t incl = cnt;  // (inclusive prefix over the wave's tiles, lanes 0 .. kSfEmitTiles - 1)
-#pragma unroll
-  for (int d = 1; d < kSfEmitTiles; d <<= 1) {
-    const uint32_t y = (uint32_t)__shfl_up((int)incl, d, 64);
-    if (lane >= d) incl += y;
-  }
+  const uint32_t incl = wave_incl_scan(cnt, lane);  // (lanes 0 .. kSfEmitTiles - 1: the tiles' prefixes)
   uint32_t pre[kSfEmitTiles];  // (every lane holds the prefixes and offsets: shuffles outside the loop)
   int64_t ob[kSfEmitTiles];
 #pragma unroll

@@ -564,7 +564,8 @@ def main():
                                     ("C2: configs[1] full path, 1 GiB %s UTF-8, %d strings, GPU %s pre-split + "
                                      "merge loop + id compaction%s" % (
                                          (args.corpus or "mixed").upper(), n_str, args.pattern,
-                                         " + special tokens (found on host)" if specials else "")))
+                                         (" + special tokens (found on the device, inside the step)" if sp_device
+                                          else " + special tokens (found on host)") if specials else "")))
                        + (" + RCCL all-gather of ids + reassembly (offsets rebased, ids widened to int32)"
                           if gather else ""),
                        "presplit": args.presplit,

@@ -290,8 +290,10 @@ __device__ inline int64_t next_set_bit(const uint64_t* bits, int64_t n_words, in
 // Inclusive scan over the wave's 64 lanes (every lane active).  SW_DPP_SCAN: by DPP -- row shifts
 // 1, 2, 4, 8 within each 16-lane row, then row_bcast:15 (rows 1, 3) and row_bcast:31 (rows 2, 3),
 // six VALU operations; else six shuffles through the LDS crossbar (ds_bpermute), each a round trip.
+// r7x A/B: C2 234.8 -> 238.5 GB/s (k_compact 0.94 -> 0.89 ms), C3 GPT-2 + specials 251 -> 264
+// (k_classify<true> 2.39 -> 2.24 ms).
 #ifndef SW_DPP_SCAN
-#define SW_DPP_SCAN 0
+#define SW_DPP_SCAN 1
 #endif
 __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t x, int lane) {
 #if SW_DPP_SCAN
@@ -313,7 +315,7 @@ __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t x, int lane) {
 #endif
 }
 
-// lane L's value to every lane (L a constant, every lane active): v_readlane under SW_DPP_SCAN
+// lane L's value to every lane (L wave-uniform, every lane active): v_readlane under SW_DPP_SCAN
 // (an SGPR, no LDS crossbar round trip), else a shuffle
 __device__ __forceinline__ uint32_t lane_value(uint32_t x, int L) {
 #if SW_DPP_SCAN
@@ -1281,7 +1283,7 @@ __device__ __forceinline__ void classify_chunks(const EncArgs& a, int64_t tile, 
       }
       nown += __popcll(pend);
       while (pend) {  // one ballot per bucket present
-        const int bb = __shfl(b, __ffsll((long long)pend) - 1, 64);
+        const int bb = (int)lane_value((uint32_t)b, __ffsll((long long)pend) - 1);
         const uint64_t m = __ballot(b == bb);
         if (lane == bb) bcount += (uint32_t)__popcll(m);
         pend &= ~m;
@@ -1537,19 +1539,10 @@ __device__ __forceinline__ void put_lds_result(const EncArgs& a, uint64_t e, uin
 // k_merge_bucket<N>: queued chunks of buckets [b_lo, b_hi] (length <= N), one per lane;
 // persistent grid-stride over 64-entry batches of the bucket-major queue
 // ---------------------------------------------------------------------------------------
-#ifndef SW_MB_WAVES4
-#define SW_MB_WAVES4 1  // k_merge_bucket<4>: the waves per SIMD the compiler must fit (1: its choice)
-#endif
-#ifndef SW_MB_WAVES8
-#define SW_MB_WAVES8 1  // ... <8>
-#endif
-#ifndef SW_MB_WAVES16
-#define SW_MB_WAVES16 1  // ... <16>
-#endif
+// (capping the short buckets at 5, 6 or 8 waves per SIMD -- 64-96 VGPRs, some spilled -- was
+// slower on memo-off: 18.7 -> 19.2-20.5 ms, r7x)
 template <bool kWide, bool k16, int N, bool kWF = false>  // kWF: a well-formed table (lane_merge_lds_wf)
-__global__ void __launch_bounds__(kThreads)
-__attribute__((amdgpu_waves_per_eu(N <= 4 ? SW_MB_WAVES4 : N <= 8 ? SW_MB_WAVES8 : N <= 16 ? SW_MB_WAVES16 : 1)))
-k_merge_bucket(EncArgs a, int b_lo, int b_hi) {
+__global__ void __launch_bounds__(kThreads) k_merge_bucket(EncArgs a, int b_lo, int b_hi) {
   SW_STAMP_INIT;
   const int64_t gw = ((int64_t)blockIdx.x * kWaves + wave_in_block());  // global wave id
   const int64_t n_waves = ((int64_t)gridDim.x * kThreads) >> 6;
@@ -2364,8 +2357,8 @@ __device__ __forceinline__ void compact_tile(const EncArgs& a, int64_t t, int64_
       // long results (C5: whole 4 KiB chunks): one coalesced copy by the whole wave each
       for (uint64_t lm = __ballot(ref && m > kLaneCopy); lm; lm &= lm - 1) {
         const int L = __ffsll((long long)lm) - 1;
-        const int64_t pL = (int64_t)__shfl((long long)p, L, 64);
-        const uint32_t oL = (uint32_t)__shfl((int)o, L, 64), mL = (uint32_t)__shfl((int)m, L, 64);
+        const int64_t pL = (int64_t)lane_value64((unsigned long long)p, L);
+        const uint32_t oL = lane_value(o, L), mL = lane_value(m, L);
         const uint32_t loL = oL - gbase;
         for (uint32_t k0 = 3; k0 < mL; k0 += 256) {  // (four loads in flight per lane, then the stores)
           int32_t id[4];

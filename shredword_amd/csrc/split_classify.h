@@ -274,9 +274,6 @@ struct MixBytes {
 };
 
 // per-wave LDS of k_split_classify
-#ifndef SW_SP_PREFETCH
-#define SW_SP_PREFETCH 0  // k_split_classify<true>: the tile's occurrence indices loaded at its start
-#endif
 constexpr int kScPre = 32;                         // bytes staged before the tile
 constexpr int kScWinWords = (kScPre + kWin) / 4 + 8;  // [t0 - 32, t0 + kWin) + a zero tail
 constexpr int kScSsPre = 64;                       // string-start bits staged from t0 - 64 ...
@@ -405,8 +402,13 @@ __device__ __forceinline__ void split_classify_tile(const EncArgs& a, const PbAr
     rw[1] = x0[0]; rw[2] = x0[1]; rw[3] = x0[2]; rw[4] = x0[3];
     rw[5] = x1[0]; rw[6] = x1[1]; rw[7] = x1[2]; rw[8] = x1[3];
     // the word before the chunk: lane - 1's last; the word after it: lane + 1's first
+#if SW_DPP_SCAN  // (DPP wave rotations by one lane: VALU, no LDS crossbar round trip)
+    const uint32_t up = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)rw[8], 0x13C, 0xF, 0xF, false);  // wave_ror:1
+    const uint32_t dn = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)rw[1], 0x134, 0xF, 0xF, false);  // wave_rol:1
+#else
     const uint32_t up = (uint32_t)__shfl((int)rw[8], (lane + 63) & 63, 64);
     const uint32_t dn = (uint32_t)__shfl((int)rw[1], (lane + 1) & 63, 64);
+#endif
     rw[0] = lane == 0 ? xe[3] : up;
     rw[9] = lane == 63 ? xe[0] : dn;
   } else {
@@ -426,11 +428,6 @@ __device__ __forceinline__ void split_classify_tile(const EncArgs& a, const PbAr
   }
   const uint32_t r0 = edge[9 * stride + tile], r_next = edge[9 * stride + tile + 1];
   const int64_t s_first = a.tile_slo[tile];
-#if SW_SP_PREFETCH  // (the occurrences' tile indices at the start: scalar loads with the scalar tile index)
-  const int64_t sp_prev = kSp && tile > 0 ? a.sp.tile_sp[tile - 1] : 0;
-  const int64_t sp_lo = kSp ? a.sp.tile_sp[tile] : 0, sp_hi = kSp ? a.sp.tile_sp[tile + 1] : -1;
-  const int64_t nsp = kSp ? a.sp.tile_sp[a.n_tiles] : 0;
-#endif
   ScMasks& sm = sh->pre;
   if (lane < 9) sm.m[lane][65] = edge[lane * stride + tile + 1];  // (k_edges: the next tile's first chunk)
   else if (lane < 18) sm.m[lane - 9][0] = 0u;
@@ -453,11 +450,10 @@ __device__ __forceinline__ void split_classify_tile(const EncArgs& a, const PbAr
     wave_sync_mem();
     const int64_t w0 = t0 - kScSsPre, w1 = w0 + (int64_t)kScSsWords * 32;
     // (the first occurrence ending at or after w0, in tile - 1's range: see sp_first_end; the
-    // indices are loaded here, not at the start: held through the class masks they cost 0.27 ms, r6q)
-#if !SW_SP_PREFETCH
+    // indices are loaded here, not at the start: held through the class masks they cost 0.27 ms
+    // with a vector tile index, r6q, and gave nothing with the scalar one, r7x)
     const int64_t sp_prev = tile > 0 ? a.sp.tile_sp[tile - 1] : 0, sp_lo = a.sp.tile_sp[tile];
     const int64_t nsp = a.sp.tile_sp[a.n_tiles];
-#endif
     const int64_t j_first = tile > 0 ? sp_first_end_wave(a.sp, max(sp_prev - 1, (int64_t)0), sp_lo, w0, lane) : 0;
     for (int64_t j0 = j_first; j0 < nsp; j0 += 64) {
       const int64_t j = j0 + lane;
@@ -554,11 +550,7 @@ __device__ __forceinline__ void split_classify_tile(const EncArgs& a, const PbAr
   else if (a.n_bytes <= t1 + 32) rel_end = (int)(a.n_bytes - t0);
   else rel_end = kRelEndLong;
   wave_sync_mem();  // (the masks' LDS becomes the chunk-start list)
-  #if SW_SP_PREFETCH
-  classify_chunks<kSp>(a, tile, s_win + kScPre / 4, sh->cstart, s_qbuf, r, rel_end, s_first, sp_lo, sp_hi);
-#else
-  classify_chunks<kSp>(a, tile, s_win + kScPre / 4, sh->cstart, s_qbuf, r, rel_end, s_first, -1, -1);
-#endif
+    classify_chunks<kSp>(a, tile, s_win + kScPre / 4, sh->cstart, s_qbuf, r, rel_end, s_first, -1, -1);
 }
 
 #ifndef SW_SC_WAVES

@@ -328,6 +328,17 @@ __device__ __forceinline__ unsigned long long lane_value64(unsigned long long x,
   return (unsigned long long)lane_value((uint32_t)x, L) | ((unsigned long long)lane_value((uint32_t)(x >> 32), L) << 32);
 }
 
+// the wave's sum in every lane (every lane active)
+__device__ __forceinline__ uint32_t wave_sum(uint32_t v, int lane) {
+#if SW_DPP_SCAN
+  return lane_value(wave_incl_scan(v, lane), 63);
+#else
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v += (uint32_t)__shfl_xor((int)v, off, 64);
+  return v;
+#endif
+}
+
 // exclusive block scan over kThreads threads (sh: kThreads/64 words); *total = block sum
 __device__ inline uint32_t block_excl_scan(uint32_t v, uint32_t* sh, uint32_t* total) {
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
@@ -2235,9 +2246,7 @@ __global__ void __launch_bounds__(kThreads) k_tile_count(EncArgs a) {
   }
 #pragma unroll
   for (int k = 0; k < kTcTiles; ++k) {
-    uint32_t v = c[k];
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+    const uint32_t v = wave_sum(c[k], lane);
     if (lane == 0 && tb + k < a.n_tiles) a.tile_cnt[tb + k] = v + (uint32_t)(C[k] - nr[k]);
   }
 }

@@ -155,9 +155,7 @@ __global__ void __launch_bounds__(kThreads) k_sp_detect(SpTab T, SpFind f) {
   }
   f.cbits[t * 64 + lane] = c;
   f.chosen[t * 64 + lane] = 0u;
-  uint32_t n = (uint32_t)__popc(c);
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) n += (uint32_t)__shfl_xor((int)n, off, 64);
+  const uint32_t n = wave_sum((uint32_t)__popc(c), lane);
   if (lane == 0) f.tcand[t] = n;
   }
 }
@@ -211,9 +209,7 @@ __global__ void __launch_bounds__(kThreads) k_sp_count(SpFind f) {
   if (__hip_atomic_load(f.flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) return;
   const int lane = threadIdx.x & 63;
   for (int64_t t = (int64_t)blockIdx.x * kWaves + wave_in_block(); t < f.n_tiles; t += (int64_t)gridDim.x * kWaves) {
-    uint32_t n = f.tcand[t] ? (uint32_t)__popc(f.chosen[t * 64 + lane]) : 0u;
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) n += (uint32_t)__shfl_xor((int)n, off, 64);
+    const uint32_t n = wave_sum(f.tcand[t] ? (uint32_t)__popc(f.chosen[t * 64 + lane]) : 0u, lane);
     if (lane == 0) f.tcnt[t] = n;
   }
 }

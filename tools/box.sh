@@ -54,6 +54,7 @@ for s in "$@"; do
     prof_c3spd) run prof_c3spd 1100 bash tools/profile_gpu.sh "${TAG}_c3spd" --pattern gpt2 --specials 1 --specials-device ;;
     prof_ent) run prof_ent 1100 bash tools/profile_gpu.sh "${TAG}_ent" --corpus entropy ;;
     prof_off) run prof_off 1100 bash tools/profile_gpu.sh "${TAG}_off" --no-dedupe --no-chunk-table ;;
+    prof_dense) run prof_dense 1100 bash tools/profile_gpu.sh "${TAG}_dense" --pattern gpt2 --specials 64 --specials-device ;;
     ab=*) IFS=',' read -r -a specs <<< "${s#ab=}"
           specs=("${specs[@]//+/,}")  # (a spec's own bench args: lib.so@--corpus+entropy)
           run "ab" 1000 bash tools/gpu_ab_trace.sh "$TAG" "${specs[@]}" ;;

@@ -2385,23 +2385,14 @@ __device__ __forceinline__ void compact_tile(const EncArgs& a, int64_t t, int64_
           }
         }
       }
-      if (__ballot((sj >> 6) == r)) {  // (a string of this tile starts in this round: its id offset)
-        const uint32_t got = (uint32_t)__shfl((int)o, sj & 63, 64);
-        if ((sj >> 6) == r) s_off = got;
-      }
+      const uint32_t got = (uint32_t)__shfl((int)o, sj & 63, 64);
+      if ((sj >> 6) == r) s_off = got;
       if (many && valid) a.scratch[t * kTile + j] = (int32_t)o;  // (this wave's own slots)
     }
     wave_sync_mem();
     // the staged ids: one contiguous 256-byte store per 64 ids
     const uint32_t staged = min(carry - gbase, (uint32_t)kOutCapW);
-    for (uint32_t i0 = 0; i0 < staged; i0 += 256) {  // (four LDS reads in flight, then their stores)
-      int32_t sv[4];
-#pragma unroll
-      for (int q = 0; q < 4; ++q) sv[q] = i0 + 64 * q + lane < staged ? s_out[i0 + 64 * q + lane] : 0;
-#pragma unroll
-      for (int q = 0; q < 4; ++q)
-        if (i0 + 64 * q + lane < staged) SW_STNT(&dst[gbase + i0 + 64 * q + lane], (OutT)sv[q]);
-    }
+    for (uint32_t i = lane; i < staged; i += 64) SW_STNT(&dst[gbase + i], (OutT)s_out[i]);
     wave_sync_mem();  // (s_rp / s_rq / s_out are rewritten by the next group)
 #ifdef SW_STAMPS
     __builtin_amdgcn_s_waitcnt(0);

@@ -1089,10 +1089,21 @@ int32_t encode_device(sw_encoder* h, const uint8_t* d_bytes, int64_t n_bytes, co
         hipLaunchKernelGGL(k_split_redo<false>, dim3(kRedoGrid), dim3(kThreads), 0, st, a, pg, (int)pattern,
                            (const uint32_t*)h->d_edge, (uint32_t*)h->d_pbits, redo);
       }
-    } else if (sp.n > 0) {
-      hipLaunchKernelGGL(k_classify<true>, dim3((unsigned)((n_tiles + kWaves - 1) / kWaves)), dim3(kThreads), 0, st, a);
     } else {
-      hipLaunchKernelGGL(k_classify<false>, dim3((unsigned)((n_tiles + kWaves - 1) / kWaves)), dim3(kThreads), 0, st, a);
+      // (tiles over k_classify's chunk-start capacity: listed, then classified by k_classify_big)
+      unsigned int* ov_count = h->d_redo;
+      int64_t* ov_tiles = (int64_t*)(h->d_redo + 2);
+      HIP_TRY(hipMemsetAsync(ov_count, 0, sizeof(unsigned int), st));
+      const dim3 gc((unsigned)((n_tiles + kWaves - 1) / kWaves));
+      if (sp.n > 0) {
+        hipLaunchKernelGGL(k_classify<true>, gc, dim3(kThreads), 0, st, a, ov_count, ov_tiles);
+        hipLaunchKernelGGL(k_classify_big<true>, dim3(kRedoGrid), dim3(kThreads), 0, st, a, (const unsigned int*)ov_count,
+                           (const int64_t*)ov_tiles);
+      } else {
+        hipLaunchKernelGGL(k_classify<false>, gc, dim3(kThreads), 0, st, a, ov_count, ov_tiles);
+        hipLaunchKernelGGL(k_classify_big<false>, dim3(kRedoGrid), dim3(kThreads), 0, st, a, (const unsigned int*)ov_count,
+                           (const int64_t*)ov_tiles);
+      }
     }
     HIP_TRY(hipGetLastError());
     // streams of the merge kernels: [0] buckets 17..32 B, then 5..8 B, [1] 9..16 B, then 2..4 B

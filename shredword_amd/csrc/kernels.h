@@ -1058,19 +1058,29 @@ constexpr int kWinWords = kWin / 4 + 8;
 // capped at 6 it spilled 24 B per lane (+0.9 GB of writes, not faster); with its body as a
 // function of (tile, base) (compact_tile) the compiler fits 78 VGPRs, 6 waves, no spill: 1.11 ->
 // 0.95 ms (profiles/r2_k.md).
-#define SW_CLS_ATTR __attribute__((amdgpu_waves_per_eu(6, 6)))
+// Round 5: the chunk-start list capped at kClsCsCap (a tile with more goes to k_classify_big),
+// so a block fits 7 per CU: 7 waves per SIMD (as k_split_classify, split_classify.h kScCsCap).
+#ifndef SW_CLS_CSCAP
+#define SW_CLS_CSCAP 1456
+#endif
+constexpr int kClsCsCap = SW_CLS_CSCAP;
+#ifndef SW_CLS_WAVES
+#define SW_CLS_WAVES 7
+#endif
+#define SW_CLS_ATTR __attribute__((amdgpu_waves_per_eu(SW_CLS_WAVES, SW_CLS_WAVES)))
 // (a last chunk that runs more than kShort bytes past its tile, end unknown to the tile: long,
 // its length found from the complete bitmap by k_lp_prep)
 constexpr int kRelEndLong = 1 << 30;
 template <bool kSp>  // kSp: the launch has special-token occurrences (a.sp)
 __device__ __forceinline__ void classify_chunks(const EncArgs& a, int64_t tile, const uint32_t* s_b32,
                                                 uint16_t* s_cstart, uint16_t* s_qbuf, uint32_t myhalf, int rel_end,
-                                                int64_t s_first, int64_t sp_lo, int64_t sp_hi);
+                                                int64_t s_first, int64_t sp_lo, int64_t sp_hi, int cap = kTile + 1,
+                                                unsigned int* ov_count = nullptr, int64_t* ov_tiles = nullptr);
 
 // one tile (the body of k_classify's tile loop): the chunk starts from the uploaded bitmap
 template <bool kSp>
 __device__ __forceinline__ void classify_tile(const EncArgs& a, int64_t tile, uint32_t* s_b32, uint16_t* s_cstart,
-                                              uint16_t* s_qbuf) {
+                                              uint16_t* s_qbuf, int cap, unsigned int* ov_count, int64_t* ov_tiles) {
   const int lane = threadIdx.x & 63;
   const int64_t t0 = tile * kTile;
   const int64_t t1 = tile_end(t0, a.n_bytes);
@@ -1133,7 +1143,8 @@ __device__ __forceinline__ void classify_tile(const EncArgs& a, int64_t tile, ui
       last_end = min(q, a.n_bytes);
     }
   }
-  classify_chunks<kSp>(a, tile, s_b32, s_cstart, s_qbuf, myhalf, (int)(last_end - t0), s_first, sp_lo, sp_hi);
+  classify_chunks<kSp>(a, tile, s_b32, s_cstart, s_qbuf, myhalf, (int)(last_end - t0), s_first, sp_lo, sp_hi, cap,
+                       ov_count, ov_tiles);
 }
 
 // The tile's chunks from its chunk-start bits on: lane l holds bits 32 l .. 32 l + 31 of the tile
@@ -1142,7 +1153,8 @@ __device__ __forceinline__ void classify_tile(const EncArgs& a, int64_t tile, ui
 template <bool kSp>
 __device__ __forceinline__ void classify_chunks(const EncArgs& a, int64_t tile, const uint32_t* s_b32,
                                                 uint16_t* s_cstart, uint16_t* s_qbuf, uint32_t myhalf, int rel_end,
-                                                int64_t s_first, int64_t sp_lo, int64_t sp_hi) {
+                                                int64_t s_first, int64_t sp_lo, int64_t sp_hi, int cap,
+                                                unsigned int* ov_count, int64_t* ov_tiles) {
   SW_STAMP_INIT;
   const int lane = threadIdx.x & 63;
   const uint64_t lt_mask = (lane == 0) ? 0ULL : (~0ULL >> (64 - lane));
@@ -1151,6 +1163,10 @@ __device__ __forceinline__ void classify_chunks(const EncArgs& a, int64_t tile, 
   const uint32_t cnt = (uint32_t)__popc(myhalf);
   const uint32_t incl = wave_incl_scan(cnt, lane);
   const int C = (int)lane_value(incl, 63);
+  if (C > cap) {  // (more chunk starts than the LDS list holds: nothing is written; k_classify_big does it)
+    if (lane == 0) ov_tiles[atomicAdd(ov_count, 1u)] = tile;
+    return;
+  }
   {
     uint32_t x = myhalf;
     uint32_t k = incl - cnt;
@@ -1342,13 +1358,30 @@ __device__ __forceinline__ void classify_chunks(const EncArgs& a, int64_t tile, 
 
 // one wave per tile
 template <bool kSp>
-__global__ void __launch_bounds__(kThreads) SW_CLS_ATTR k_classify(EncArgs a) {
+__global__ void __launch_bounds__(kThreads) SW_CLS_ATTR k_classify(EncArgs a, unsigned int* ov_count, int64_t* ov_tiles) {
   __shared__ __attribute__((aligned(16))) uint32_t s_b32_all[kWaves][kWinWords];  // window bytes (+ zero tail)
-  __shared__ uint16_t s_cs_all[kWaves][kTile + 1];   // chunk starts (tile-relative)
+  __shared__ uint16_t s_cs_all[kWaves][kClsCsCap + 1];  // chunk starts (tile-relative), up to kClsCsCap
   __shared__ uint16_t s_qb_all[kWaves][kQBuf];       // chunks not settled by a lookup, to dedupe
-  const int wv = wave_in_block();
+  const int wv = wave_in_block_s();
   const int64_t tile = (int64_t)blockIdx.x * kWaves + wv;
-  if (tile < a.n_tiles) classify_tile<kSp>(a, tile, s_b32_all[wv], s_cs_all[wv], s_qb_all[wv]);
+  if (tile < a.n_tiles)
+    classify_tile<kSp>(a, tile, s_b32_all[wv], s_cs_all[wv], s_qb_all[wv], kClsCsCap, ov_count, ov_tiles);
+}
+
+// the tiles k_classify could not hold (more than kClsCsCap chunks), one wave each with the whole
+// list in LDS, the waves of a fixed grid taking them in turn
+template <bool kSp>
+__global__ void __launch_bounds__(kThreads) k_classify_big(EncArgs a, const unsigned int* ov_count, const int64_t* ov_tiles) {
+  __shared__ __attribute__((aligned(16))) uint32_t s_b32_all[kWaves][kWinWords];
+  __shared__ uint16_t s_cs_all[kWaves][kTile + 1];
+  __shared__ uint16_t s_qb_all[kWaves][kQBuf];
+  const int wv = wave_in_block_s();
+  // (this launch's list, written by k_classify: read coherently, never through the scalar cache)
+  const int64_t n = (int64_t)__hip_atomic_load(ov_count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  for (int64_t i = (int64_t)blockIdx.x * kWaves + wv; i < n; i += (int64_t)gridDim.x * kWaves) {
+    const int64_t tile = __hip_atomic_load(&ov_tiles[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    classify_tile<kSp>(a, tile, s_b32_all[wv], s_cs_all[wv], s_qb_all[wv], kTile + 1, nullptr, nullptr);
+  }
 }
 
 // ---------------------------------------------------------------------------------------
@@ -2252,7 +2285,13 @@ __global__ void __launch_bounds__(kThreads) k_tile_count(EncArgs a) {
 }
 
 constexpr int kRefCap = 128;    // references per 8-round group gathered through LDS
-constexpr int kOutCapW = 1024;  // ids per group staged in LDS (the rest are stored directly)
+#ifndef SW_CP_OUTCAP
+#define SW_CP_OUTCAP 1024
+#endif
+#ifndef SW_CP_WAVES
+#define SW_CP_WAVES 0  // k_compact: waves per SIMD to fit (0: the compiler's choice)
+#endif
+constexpr int kOutCapW = SW_CP_OUTCAP;  // ids per group staged in LDS (the rest are stored directly)
 constexpr uint32_t kLaneCopy = 64;  // results longer than this are copied by the whole wave
 
 // tile t's ids to out + base (base: the ids of the tiles before it); per wave: the group's
@@ -2418,7 +2457,11 @@ __device__ __forceinline__ void compact_tile(const EncArgs& a, int64_t t, int64_
 }
 
 template <typename OutT>
-__global__ void __launch_bounds__(kThreads) k_compact(EncArgs a, const int64_t* tile_base, OutT* out) {
+__global__ void __launch_bounds__(kThreads)
+#if SW_CP_WAVES
+__attribute__((amdgpu_waves_per_eu(SW_CP_WAVES, SW_CP_WAVES)))
+#endif
+k_compact(EncArgs a, const int64_t* tile_base, OutT* out) {
   __shared__ uint32_t s_rp_all[kWaves][kRefCap];
   __shared__ uint4 s_rq_all[kWaves][kRefCap];
   __shared__ int32_t s_out_all[kWaves][kOutCapW];  // a group's ids, staged for 256-B stores

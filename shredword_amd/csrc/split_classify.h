@@ -284,10 +284,19 @@ struct ScMasks {
   uint32_t ss[kScSsWords]; // string starts
   uint32_t in[64];         // bytes inside special-token occurrences (lane l: bits 32 l ..), if any
 };
-union ScShared {           // the masks are dead once the tile's chunk starts are known
+template <int kCs>
+union ScSharedT {          // the masks are dead once the tile's chunk starts are known
   ScMasks pre;
-  uint16_t cstart[kTile + 2];
+  uint16_t cstart[kCs];
 };
+using ScShared = ScSharedT<kTile + 2>;
+// The chunk starts k_split_classify's LDS holds: with fewer than a tile's 2048 (+ 2), the union is
+// no larger than the masks and a block of 4 waves fits 7 blocks per CU instead of 6; a tile with
+// more chunks is listed for k_split_redo, which holds them all.
+#ifndef SW_SC_CSCAP
+#define SW_SC_CSCAP 1456  // (r7h A/B: C2 k_split_classify 2.97 -> 2.91 ms, ENTROPY 5.76 -> 5.43, 7 waves per SIMD)
+#endif
+constexpr int kScCsCap = SW_SC_CSCAP;
 
 // psb::carries' view inside k_split_classify: the tile's masks from LDS, the rest from global memory
 struct FSrc {
@@ -356,9 +365,9 @@ struct RedoList {
 
 // one tile: pre-split, then classify_chunks.  kRedo: the walks may read global memory (FSrc) --
 // k_split_redo; else they stay in LDS (LSrc) and a tile that needs more is listed in `redo`
-template <bool kSp, bool kRedo>
+template <bool kSp, bool kRedo, class ShT>
 __device__ __forceinline__ void split_classify_tile(const EncArgs& a, const PbArgs& g, int pattern, const uint32_t* edge,
-                                                    uint32_t* bits32, int64_t tile, uint32_t* s_win, ScShared* sh,
+                                                    uint32_t* bits32, int64_t tile, uint32_t* s_win, ShT* sh,
                                                     uint16_t* s_qbuf, const RedoList& redo) {
   SW_STAMP_INIT;
   const int lane = threadIdx.x & 63;
@@ -530,15 +539,20 @@ __device__ __forceinline__ void split_classify_tile(const EncArgs& a, const PbAr
       }
     }
   }
+  if (c < n_chunks) {
+    if (has_sp && lane > 0) r &= ~sm.in[lane];  // (lane 0: k_edges cleared them)
+    if (32 * c + 32 > a.n_bytes) r &= (1u << (a.n_bytes - 32 * c)) - 1u;
+  }
   if constexpr (!kRedo) {
-    if (__ballot(unresolved)) {  // (rare: nothing of the tile is written yet; k_split_redo does it all)
+    constexpr int kCap = (int)(sizeof(sh->cstart) / sizeof(uint16_t)) - 2;
+    bool over = false;  // (more chunk starts than the LDS list holds)
+    if constexpr (kCap < kTile) over = wave_sum((uint32_t)__popc(c < n_chunks ? r : 0u), lane) > (uint32_t)kCap;
+    if (__ballot(unresolved) || over) {  // (rare: nothing of the tile is written yet; k_split_redo does it all)
       if (lane == 0) redo.tiles[atomicAdd(redo.count, 1u)] = tile;
       return;
     }
   }
   if (c < n_chunks) {
-    if (has_sp && lane > 0) r &= ~sm.in[lane];  // (lane 0: k_edges cleared them)
-    if (32 * c + 32 > a.n_bytes) r &= (1u << (a.n_bytes - 32 * c)) - 1u;
     bits32[c] = r;
     if (c == n_chunks - 1 && (c & 1) == 0) bits32[c + 1] = 0;  // (the last word's upper half)
   }
@@ -554,13 +568,13 @@ __device__ __forceinline__ void split_classify_tile(const EncArgs& a, const PbAr
 }
 
 #ifndef SW_SC_WAVES
-#define SW_SC_WAVES 6
+#define SW_SC_WAVES 7
 #endif
 template <bool kSp>
 __global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(SW_SC_WAVES, SW_SC_WAVES)))
 k_split_classify(EncArgs a, PbArgs g, int pattern, const uint32_t* edge, uint32_t* bits32, RedoList redo) {
   __shared__ __attribute__((aligned(16))) uint32_t s_win_all[kWaves][kScWinWords];
-  __shared__ ScShared s_sh_all[kWaves];
+  __shared__ ScSharedT<kScCsCap> s_sh_all[kWaves];
   __shared__ uint16_t s_qb_all[kWaves][kQBuf];
   const int wv = wave_in_block_s();
   const int64_t tile = (int64_t)blockIdx.x * kWaves + wv;

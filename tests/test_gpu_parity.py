@@ -464,3 +464,27 @@ def test_shared_handle_patterns_per_call_two_streams():
     va.close()
     assert base._handle is not None  # (a view never destroys its parent's handle)
     base.close()
+
+
+@pytest.mark.parametrize("host_presplit", [0, 1])
+def test_chunk_dense_tiles_over_the_lds_list(host_presplit):
+    """Tiles with more chunk starts than the classification's LDS list holds (1454: runs of
+    one-byte strings, "1a1a..." text that cl100k cuts into one-byte chunks, a space between
+    letters) go to the overflow kernels (k_split_redo on the device pre-split, k_classify_big on
+    a host bitmap) -- the same ids as the oracle, beside ordinary tiles of the same batch."""
+    rng = random.Random(5)
+    datas = []
+    for _ in range(6):
+        datas += [bytes([rng.choice(b"abcxyz")]) for _ in range(3000)]      # one-byte strings
+        datas.append(("1a" * 2500).encode())                                 # one-byte chunks
+        datas.append(" ".join(rng.choice("pqrs") for _ in range(1500)).encode())
+        datas.append(b"the quick brown fox jumps over the lazy dog. " * 60)  # ordinary text
+    buf, off = pack(datas)
+    t = tok_for("bl32k.model")
+    exp = oracle_encode(t.merges, buf, off, "cl100k")
+    L, h = _lib.lib(), t._encoder()
+    _lib.check(L.sw_encoder_set_option(h, _lib.SW_OPT_HOST_PRESPLIT, host_presplit))
+    try:
+        assert_same(gpu_encode(t, buf, off), exp)
+    finally:
+        L.sw_encoder_set_option(h, _lib.SW_OPT_HOST_PRESPLIT, 0)

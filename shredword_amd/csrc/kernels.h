@@ -2240,7 +2240,10 @@ __device__ __forceinline__ uint4 ref_head(const EncArgs& a, int32_t v) {
   return q;
 }
 
-constexpr int kRoundsInFlight = 8;  // slot rounds whose loads (then gathers) issue together
+#ifndef SW_CP_ROUNDS
+#define SW_CP_ROUNDS 8
+#endif
+constexpr int kRoundsInFlight = SW_CP_ROUNDS;  // slot rounds whose loads (then gathers) issue together
 
 // id count of the result a reference-list entry names
 // (a dense result's count from the byte array: 4 MiB at most, so these random reads mostly hit
@@ -2256,6 +2259,9 @@ __device__ __forceinline__ uint32_t ref_count(const EncArgs& a, uint32_t r) {
 // then their counts: one dependent round trip serves kTcTiles tiles (a tile holds ~58
 // references on prose, so one wave per tile spent most of its life waiting)
 constexpr int kTcTiles = 2;  // (4: no faster, r4s)
+#ifndef SW_TC_BATCH
+#define SW_TC_BATCH 0  // k_tile_count: rounds of a long reference list in flight together (0: one)
+#endif
 __global__ void __launch_bounds__(kThreads) k_tile_count(EncArgs a) {
   const int64_t tb = (((int64_t)blockIdx.x * kWaves + wave_in_block())) * kTcTiles;
   const int lane = threadIdx.x & 63;
@@ -2274,8 +2280,20 @@ __global__ void __launch_bounds__(kThreads) k_tile_count(EncArgs a) {
 #pragma unroll
   for (int k = 0; k < kTcTiles; ++k) {
     const uint32_t* rl = a.rlist + min(tb + k, a.n_tiles - 1) * kTile;
+#if SW_TC_BATCH
+    for (int i0 = 64; i0 < nr[k]; i0 += 64 * SW_TC_BATCH) {  // (long lists: SW_TC_BATCH rounds in flight)
+      uint32_t e[SW_TC_BATCH], v[SW_TC_BATCH];
+#pragma unroll
+      for (int q = 0; q < SW_TC_BATCH; ++q) e[q] = i0 + 64 * q + lane < nr[k] ? SW_LDNT2(&rl[i0 + 64 * q + lane]) : 0u;
+#pragma unroll
+      for (int q = 0; q < SW_TC_BATCH; ++q) v[q] = i0 + 64 * q + lane < nr[k] ? ref_count(a, e[q]) : 0u;
+#pragma unroll
+      for (int q = 0; q < SW_TC_BATCH; ++q) c[k] += v[q];
+    }
+#else
     for (int i0 = 64; i0 < nr[k]; i0 += 64)  // (long lists: the rest a round at a time)
       if (i0 + lane < nr[k]) c[k] += ref_count(a, SW_LDNT2(&rl[i0 + lane]));
+#endif
   }
 #pragma unroll
   for (int k = 0; k < kTcTiles; ++k) {

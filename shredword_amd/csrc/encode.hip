@@ -1133,7 +1133,10 @@ int32_t encode_device(sw_encoder* h, const uint8_t* d_bytes, int64_t n_bytes, co
     HIP_TRY(long_part(1));
     HIP_TRY(launch_scan(st, h->d_bcnt, kNumBuckets * n_tiles, h->d_part, h->d_boff, h->d_qtotal));
     hipLaunchKernelGGL(k_scatter, dim3((unsigned)((n_tiles + 15) / 16)), dim3(kThreads), 0, st, a);  // (4 tiles a wave)
-    const dim3 pg(2048), pb(kThreads);  // persistent grid for the queue kernels
+#ifndef SW_MB_GRID
+#define SW_MB_GRID 2048
+#endif
+    const dim3 pg(SW_MB_GRID), pb(kThreads);  // persistent grid for the queue kernels
     if (h->merge_fork) {
       HIP_TRY(hipEventRecord(h->ev_fork, st));
       for (int k = 0; k < 2; ++k) HIP_TRY(hipStreamWaitEvent(h->s_fork[k], h->ev_fork, 0));

@@ -544,9 +544,15 @@ __device__ __forceinline__ uint32_t lane_merge_reg_loop_wf(const DevTable& t, ui
 // the initial ranks of slots g .. g + 3 are in registers before any later slot's lookups issue
 // (lane_merge_lds_wf: the compiler otherwise hoisted all N lookups -- 8 registers each in
 // flight -- to the front: 239 VGPRs at N = 32, 132 with this)
-template <int N>
+#ifndef SW_RANK_G8
+#define SW_RANK_G8 0  // the N = 8 merge bucket's initial ranks: all 7 lookups in flight (else 4 at a time)
+#endif
+template <int N, int G = 4>
 __device__ __forceinline__ void rank_group_done(uint32_t (&rk)[N], int g) {
-  if constexpr (N >= 4) {
+  if constexpr (G == 8) {  // (groups of 8 lookups: lane_merge_lds_wfq, N = 8, 16)
+    asm volatile("" : "+v"(rk[g]), "+v"(rk[g + 1]), "+v"(rk[g + 2]), "+v"(rk[g + 3]), "+v"(rk[g + 4]), "+v"(rk[g + 5]),
+                      "+v"(rk[g + 6]), "+v"(rk[g + 7])::"memory");
+  } else if constexpr (N >= 4) {
     asm volatile("" : "+v"(rk[g]), "+v"(rk[g + 1]), "+v"(rk[g + 2]), "+v"(rk[g + 3])::"memory");
   } else {
     asm volatile("" ::: "memory");
@@ -674,12 +680,13 @@ __device__ __forceinline__ void lane_merge_lds_wfq(const DevTable& t, const uint
 #pragma unroll
     for (int k = 0; k < N; ++k) s_id[64 * (q * N + k) + lane] = (u[q][k >> 2] >> (8 * (k & 3))) & 0xFFu;
   // initial ranks: four lookups of each chunk in flight at a time
+  constexpr int G = ((N == 8 || N == 16) && SW_RANK_G8) ? 8 : 4;  // (lookups of a chunk in flight per group)
 #pragma unroll
-  for (int g = 0; g < N; g += 4) {
+  for (int g = 0; g < N; g += G) {
 #pragma unroll
     for (int q = 0; q < Q; ++q)
 #pragma unroll
-      for (int k = g; k < g + 4 && k < N; ++k) {
+      for (int k = g; k < g + G && k < N; ++k) {
         const uint32_t b0 = (u[q][k >> 2] >> (8 * (k & 3))) & 0xFFu;
         const uint32_t b1 = (k + 1 < N) ? (u[q][(k + 1) >> 2] >> (8 * ((k + 1) & 3))) & 0xFFu : 0u;
         rk[q][k] = lookup<kWide>(t, b0, b1);
@@ -687,9 +694,9 @@ __device__ __forceinline__ void lane_merge_lds_wfq(const DevTable& t, const uint
 #pragma unroll
     for (int q = 0; q < Q; ++q) {
 #pragma unroll
-      for (int k = g; k < g + 4 && k < N; ++k)
+      for (int k = g; k < g + G && k < N; ++k)
         rk[q][k] = ((k + 1 < n[q]) ? (min(rk[q][k], 0xFFFFu) << 5) : KINF) | (uint32_t)k;
-      rank_group_done<N>(rk[q], g);
+      rank_group_done<N, G>(rk[q], g);
     }
   }
 #pragma unroll

@@ -107,6 +107,9 @@ constexpr int64_t kDdSlotsMax = 1LL << 26;      // ... and after growing (a queu
 constexpr int kDdWords = 1;                     // 64-bit words per dedupe entry
 constexpr uint32_t kDdGroup = 8;                // entries per 64-byte line (a chunk's candidates)
 constexpr int kDdExactMax = 7;                  // dedupe keys of <= this many bytes are exact (no verification)
+#ifndef SW_DD_NT
+#define SW_DD_NT 0
+#endif
 #ifndef SW_PAIR_MAX_N
 #define SW_PAIR_MAX_N 16                   // k_merge_bucket<N>: two chunks per lane up to this N (0: never)
 #endif
@@ -986,7 +989,11 @@ __device__ __forceinline__ DdOut dedupe_claim(const EncArgs& a, const uint32_t* 
     unsigned long long* p = (unsigned long long*)a.dtab + (size_t)kDdWords * idx;
     // an entry changes once (0 -> final), so a cached plain load is safe: a stale 0 only sends
     // this lane to the CAS, which returns the live value
+#if SW_DD_NT  // (streaming hint: slower, r7r -- a frequent chunk's line serves its repeats from L2)
+    uint64_t cur = __builtin_nontemporal_load(p);
+#else
     uint64_t cur = *p;
+#endif
     if (cur == 0) {
       cur = atomicCAS(p, 0ULL, (unsigned long long)mine);
       if (cur == 0) return DdOut{1, idx};  // claimed: this chunk is merged and shared
@@ -1008,9 +1015,18 @@ __device__ __forceinline__ DdOut dedupe_claim(const EncArgs& a, const uint32_t* 
       const uint4* q16 = (const uint4*)words;
       const int64_t b0 = g >> 4;
       const int span = (int)(g & 15) + n;
+#if SW_DD_NT
+      const u32x4* v16 = (const u32x4*)q16;
+      const u32x4 y0 = SW_LDNT(v16 + b0);
+      const u32x4 y1 = span > 16 ? SW_LDNT(v16 + b0 + 1) : u32x4{0u, 0u, 0u, 0u};
+      const u32x4 y2 = span > 32 ? SW_LDNT(v16 + b0 + 2) : u32x4{0u, 0u, 0u, 0u};
+      const uint4 x0 = make_uint4(y0[0], y0[1], y0[2], y0[3]), x1 = make_uint4(y1[0], y1[1], y1[2], y1[3]),
+                  x2 = make_uint4(y2[0], y2[1], y2[2], y2[3]);
+#else
       const uint4 x0 = q16[b0];
       const uint4 x1 = span > 16 ? q16[b0 + 1] : make_uint4(0, 0, 0, 0);
       const uint4 x2 = span > 32 ? q16[b0 + 2] : make_uint4(0, 0, 0, 0);
+#endif
       const uint32_t W[12] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w, x2.x, x2.y, x2.z, x2.w};
       const int k = (int)(w0 & 3);
       uint32_t R[kShort / 4 + 1];

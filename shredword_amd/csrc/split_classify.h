@@ -293,6 +293,9 @@ using ScShared = ScSharedT<kTile + 2>;
 // The chunk starts k_split_classify's LDS holds: with fewer than a tile's 2048 (+ 2), the union is
 // no larger than the masks and a block of 4 waves fits 7 blocks per CU instead of 6; a tile with
 // more chunks is listed for k_split_redo, which holds them all.
+#ifndef SW_BITS_NT
+#define SW_BITS_NT 0
+#endif
 #ifndef SW_SC_CSCAP
 #define SW_SC_CSCAP 1456  // (r7h A/B: C2 k_split_classify 2.97 -> 2.91 ms, ENTROPY 5.76 -> 5.43, 7 waves per SIMD)
 #endif
@@ -553,7 +556,11 @@ __device__ __forceinline__ void split_classify_tile(const EncArgs& a, const PbAr
     }
   }
   if (c < n_chunks) {
+#if SW_BITS_NT  // (the bitmap streams out: later passes read little of it)
+    SW_STNT(&bits32[c], r);
+#else
     bits32[c] = r;
+#endif
     if (c == n_chunks - 1 && (c & 1) == 0) bits32[c + 1] = 0;  // (the last word's upper half)
   }
   SW_STAMP(14);

@@ -486,7 +486,9 @@ def main():
                                 "caller's input and output arrays pinned once (Tokenizer.pin_host -> "
                                 "sw_encoder_pin_host: input read over PCIe by the copy kernel, int32 ids and offsets "
                                 "written by the device into the caller's arrays)") + ", sw_encode_batch%s" % (
-                                   "_ex (specials found on the host threads)" if specials else ""),
+                                   ("_ex (specials found on the host threads: the caller's bitmap)" if host_ps else
+                                    "_ex (specials found on the device launch by launch, sw_find_specials_device)")
+                                   if specials else ""),
                "mode": best,
                "pinned_modes_mb_s": {m: round(n_bytes / v[0] / 1e6, 1) for m, v in pin_modes.items()},
                "pin_ms_once": round(t_pin * 1e3, 1),

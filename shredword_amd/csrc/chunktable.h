@@ -15,7 +15,10 @@
 // spill = 1 marks a bucket that is the FIRST candidate of some key stored in its second: a
 // lookup whose first probe neither matches nor sees spill is a certain miss, so most lookups
 // cost one memory request instead of two (entries are placed in token order, first candidate
-// preferred, so the frequent chunks sit in their first bucket).
+// preferred, so the frequent chunks sit in their first bucket).  The tables are kept at most
+// 10% full (SW_CT_LOAD, up to 2^22 buckets): one lane that needs its second candidate costs
+// its whole wave batch a second dependent round trip, so few spilled buckets matter more than
+// the table's size (C2 at 0.45: 2.99 ms of k_split_classify, at 0.10: 2.76; profiles/r5_ab.txt).
 #pragma once
 #include <hip/hip_runtime.h>
 

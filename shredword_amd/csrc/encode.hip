@@ -170,6 +170,11 @@ struct sw_encoder {
   unsigned int* d_redo = nullptr;     // k_split_classify's tiles for k_split_redo: count, then the list (int64)
   bool fused_presplit = true;         // SW_OPT_FUSED_PRESPLIT: the device pre-split inside k_split_classify
   bool device_specials = true;        // SW_OPT_DEVICE_SPECIALS: sw_encode_batch_ex finds specials on the device
+#ifndef SW_CP_MODE_DEFAULT
+#define SW_CP_MODE_DEFAULT 2
+#endif
+  int compact_waves = SW_CP_MODE_DEFAULT;  // SW_OPT_COMPACT_WAVES (2: from the last launch's ids per tile)
+  int64_t cp_prev_tiles = 0;          // tiles of the previous launch (its id count: h_ddfull[1])
   unsigned long long* d_pcount = nullptr;
   uint64_t* d_llist = nullptr;        // k_classify's long chunks (EncArgs::llist) and their count
   unsigned long long* d_lcount = nullptr;
@@ -414,7 +419,8 @@ hipError_t launch_presplit(hipStream_t st, const uint8_t* d_bytes, int64_t n_byt
 
 }  // namespace
 
-// exclusive scan of cnt[0..n) into base, total into *total (three small kernels)
+// exclusive scan of cnt[0..n) into base, total into *total (two small kernels: the blocks' sums,
+// then each block's scan behind the sum of the sums before it)
 hipError_t sw::launch_scan(hipStream_t st, const uint32_t* cnt, int64_t n, int64_t* part, int64_t* base,
                            int64_t* total, const int64_t* n_dev) {
   const int64_t n_parts = (n + kScanBlock - 1) / kScanBlock;
@@ -423,8 +429,7 @@ hipError_t sw::launch_scan(hipStream_t st, const uint32_t* cnt, int64_t n, int64
     return hipGetLastError();
   }
   hipLaunchKernelGGL(k_scan_reduce, dim3((unsigned)n_parts), dim3(kThreads), 0, st, cnt, n, n_dev, part);
-  hipLaunchKernelGGL(k_scan_parts, dim3(1), dim3(1024), 0, st, part, n, n_dev, total);
-  hipLaunchKernelGGL(k_scan_apply, dim3((unsigned)n_parts), dim3(kThreads), 0, st, cnt, n, n_dev, part, base);
+  hipLaunchKernelGGL(k_scan_apply, dim3((unsigned)n_parts), dim3(kThreads), 0, st, cnt, n, n_dev, part, base, total);
   return hipGetLastError();
 }
 int64_t sw::scan_block() { return kScanBlock; }
@@ -527,9 +532,10 @@ extern "C" int32_t sw_encoder_create(const int32_t* pairs, const int32_t* vals, 
   }
   e = hipEventCreateWithFlags(&h->ws_done, hipEventDisableTiming);
   if (e == hipSuccess)  // (the dedupe overflow count of the last launch, written by the device)
-    e = hipHostMalloc((void**)&h->h_ddfull, sizeof(unsigned long long), hipHostMallocMapped | hipHostMallocCoherent);
+    e = hipHostMalloc((void**)&h->h_ddfull, 2 * sizeof(unsigned long long), hipHostMallocMapped | hipHostMallocCoherent);
   if (e == hipSuccess) {
-    *h->h_ddfull = 0;
+    h->h_ddfull[0] = 0;  // (and [1]: the last launch's id count)
+    h->h_ddfull[1] = 0;
     e = hipHostGetDevicePointer((void**)&h->hd_ddfull, h->h_ddfull, 0);
   }
   if (e != hipSuccess) {
@@ -643,6 +649,10 @@ extern "C" int32_t sw_encoder_set_option(sw_encoder* h, int32_t option, int64_t 
     case SW_OPT_FUSED_PRESPLIT: h->fused_presplit = value != 0; return SW_OK;
     case SW_OPT_TEST_FAIL_GROWTH: h->test_fail_grow = value ? 1 : 0; h->dd_grow_stop = false; return SW_OK;
     case SW_OPT_DEVICE_SPECIALS: h->device_specials = value != 0; return SW_OK;
+    case SW_OPT_COMPACT_WAVES:
+      if (value != 2 && value != 6 && value != 7) return fail(SW_ERR_ARG, "SW_OPT_COMPACT_WAVES: 2, 6 or 7");
+      h->compact_waves = (int)value;
+      return SW_OK;
     case SW_OPT_PIPE_DEPTH:
       if (value < 2 || value > 4) return fail(SW_ERR_ARG, "pipeline depth: 2 .. 4");
       h->pipe_depth = (int)value;
@@ -1071,11 +1081,17 @@ int32_t encode_device(sw_encoder* h, const uint8_t* d_bytes, int64_t n_bytes, co
     // (cleared per launch rather than entry by entry by the merge kernels that empty the claims:
     // the memset leaves the table's lines in the caches, and the probes then hit -- clearing only
     // the claims made k_split_classify 2% slower on C2, r4n/r4o A/B)
-    if (h->dedupe) HIP_TRY(hipMemsetAsync(h->d_dtab, 0, sizeof(uint64_t) * kDdWords * ((size_t)a.dmask + 1), st));
+    const size_t dtab_bytes = sizeof(uint64_t) * kDdWords * ((size_t)a.dmask + 1);
+#ifndef SW_EDGE_CLEAR
+#define SW_EDGE_CLEAR 1  // (k_edges' threads clear the table: +4 us of k_edges for a 9 us memset on C2, r8b)
+#endif
+    const bool clr_in_edges = SW_EDGE_CLEAR && fused && dtab_bytes % 16 == 0;
+    if (h->dedupe && !clr_in_edges) HIP_TRY(hipMemsetAsync(h->d_dtab, 0, dtab_bytes, st));
     if (fused) {
       const PbArgs pg{d_bytes, n_bytes, d_str_off, n_str, h->d_tile_slo, spa};
       hipLaunchKernelGGL(k_edges, dim3((unsigned)((n_tiles + 1 + 255) / 256)), dim3(256), 0, st, pg, n_tiles,
-                         (int)pattern, h->d_edge, h->d_redo);
+                         (int)pattern, h->d_edge, h->d_redo, h->dedupe && clr_in_edges ? (uint4*)h->d_dtab : nullptr,
+                         (int64_t)(dtab_bytes / 16));
       const dim3 gc((unsigned)((n_tiles + kWaves - 1) / kWaves));
       const RedoList redo{h->d_redo, (int64_t*)(h->d_redo + 2)};  // (its count zeroed by k_edges)
       if (sp.n > 0) {
@@ -1174,8 +1190,19 @@ int32_t encode_device(sw_encoder* h, const uint8_t* d_bytes, int64_t n_bytes, co
     hipLaunchKernelGGL(k_tile_count, dim3((unsigned)((n_tiles + kWaves * kTcTiles - 1) / (kWaves * kTcTiles))),
                        dim3(kThreads), 0, st, a);
     HIP_TRY(launch_scan(st, h->d_tile_cnt, n_tiles, h->d_part, h->d_tile_base, h->d_total));
-    if (out16)
+    // k_compact7 when the last launch's tiles held few ids (read without waiting: a heuristic)
+    bool c7 = h->compact_waves == 7;
+    if (h->compact_waves == 2 && h->h_ddfull && h->cp_prev_tiles > 0) {
+      const unsigned long long ids = __atomic_load_n(&h->h_ddfull[1], __ATOMIC_RELAXED);
+      c7 = ids > 0 && ids <= (unsigned long long)h->cp_prev_tiles * kCompact7MaxIdsPerTile;
+    }
+    h->cp_prev_tiles = n_tiles;
+    if (out16 && c7)
+      hipLaunchKernelGGL(k_compact7<uint16_t>, wg, dim3(kThreads), 0, st, a, h->d_tile_base, (uint16_t*)d_out_ids);
+    else if (out16)
       hipLaunchKernelGGL(k_compact<uint16_t>, wg, dim3(kThreads), 0, st, a, h->d_tile_base, (uint16_t*)d_out_ids);
+    else if (c7)
+      hipLaunchKernelGGL(k_compact7<int32_t>, wg, dim3(kThreads), 0, st, a, h->d_tile_base, (int32_t*)d_out_ids);
     else
       hipLaunchKernelGGL(k_compact<int32_t>, wg, dim3(kThreads), 0, st, a, h->d_tile_base, (int32_t*)d_out_ids);
     HIP_TRY(hipGetLastError());

@@ -2082,6 +2082,7 @@ __device__ __forceinline__ int64_t scan_count(int64_t n, const int64_t* n_dev) {
   return d < n ? (d < 0 ? 0 : d) : n;
 }
 
+// (the counts read striped: every load instruction one contiguous 1 KB of the wave, not 64 lines)
 __global__ void __launch_bounds__(kThreads) k_scan_reduce(const uint32_t* cnt, int64_t n_max, const int64_t* n_dev,
                                                           int64_t* part) {
   const int64_t n = scan_count(n_max, n_dev);
@@ -2089,10 +2090,13 @@ __global__ void __launch_bounds__(kThreads) k_scan_reduce(const uint32_t* cnt, i
     if (threadIdx.x == 0) part[blockIdx.x] = 0;
     return;
   }
-  const int64_t base = (int64_t)blockIdx.x * kScanBlock + (int64_t)threadIdx.x * kScanPer;
+  const int64_t b0 = (int64_t)blockIdx.x * kScanBlock;
   uint64_t s = 0;
-  for (int k = 0; k < kScanPer; ++k)
-    if (base + k < n) s += cnt[base + k];
+#pragma unroll
+  for (int k = 0; k < kScanPer; ++k) {
+    const int64_t i = b0 + k * kThreads + threadIdx.x;
+    s += i < n ? cnt[i] : 0u;
+  }
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off, 64);
   __shared__ uint64_t sw[kThreads / 64];
@@ -2105,57 +2109,69 @@ __global__ void __launch_bounds__(kThreads) k_scan_reduce(const uint32_t* cnt, i
   }
 }
 
-__global__ void __launch_bounds__(1024) k_scan_parts(int64_t* part, int64_t n_max, const int64_t* n_dev, int64_t* total) {
-  __shared__ int64_t sh[1024];
-  const int64_t n_parts = (scan_count(n_max, n_dev) + kScanBlock - 1) / kScanBlock;
-  int64_t carry = 0;
-  for (int64_t base = 0; base < n_parts; base += 1024) {
-    const int64_t i = base + threadIdx.x;
-    const int64_t v = i < n_parts ? part[i] : 0;
-    sh[threadIdx.x] = v;
-    __syncthreads();
-    for (int off = 1; off < 1024; off <<= 1) {
-      const int64_t y = threadIdx.x >= off ? sh[threadIdx.x - off] : 0;
-      __syncthreads();
-      sh[threadIdx.x] += y;
-      __syncthreads();
-    }
-    if (i < n_parts) part[i] = carry + sh[threadIdx.x] - v;
-    carry += sh[1023];
-    __syncthreads();
-  }
-  if (threadIdx.x == 0) *total = carry;
-}
-
+// (striped through LDS: the counts loaded and the offsets stored one contiguous run per wave
+// instruction, each thread scanning kScanPer consecutive counts in between -- a thread's own 16
+// counts and 16 offsets straight from memory were 16 instructions touching 64 lines each)
+// Each block sums the partial sums of the blocks before it itself (<= a few thousand: one load
+// per thread per 256) -- no k_scan_parts pass between -- and block 0 writes the total.
 __global__ void __launch_bounds__(kThreads) k_scan_apply(const uint32_t* cnt, int64_t n_max, const int64_t* n_dev,
-                                                         const int64_t* part, int64_t* base_out) {
+                                                         const int64_t* part, int64_t* base_out, int64_t* total) {
   const int64_t n = scan_count(n_max, n_dev);
-  if ((int64_t)blockIdx.x * kScanBlock >= n) return;
-  const int64_t base = (int64_t)blockIdx.x * kScanBlock + (int64_t)threadIdx.x * kScanPer;
-  uint32_t v[kScanPer];
-  uint64_t s = 0;
+  if (blockIdx.x > 0 && (int64_t)blockIdx.x * kScanBlock >= n) return;  // (block 0 writes the total, 0 too)
+  __shared__ int64_t s_pre[2];
+  {
+    const int64_t n_parts = (n + kScanBlock - 1) / kScanBlock;
+    const int64_t upto = blockIdx.x == 0 ? n_parts : (int64_t)blockIdx.x;  // (block 0: all, for the total)
+    int64_t a = 0;
+    for (int64_t j = threadIdx.x; j < upto; j += kThreads) a += part[j];
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) a += __shfl_xor(a, off, 64);
+    __shared__ int64_t s_red[kThreads / 64];
+    if ((threadIdx.x & 63) == 0) s_red[threadIdx.x >> 6] = a;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      int64_t t = 0;
+      for (int k = 0; k < kThreads / 64; ++k) t += s_red[k];
+      s_pre[0] = blockIdx.x == 0 ? 0 : t;
+      if (blockIdx.x == 0) *total = t;
+    }
+  }
+  __shared__ uint32_t s_c[kScanBlock + kScanBlock / 32];  // (one pad word per 32: conflict-free rows)
+  auto at = [](int i) { return i + (i >> 5); };
+  const int64_t b0 = (int64_t)blockIdx.x * kScanBlock;
 #pragma unroll
   for (int k = 0; k < kScanPer; ++k) {
-    v[k] = base + k < n ? cnt[base + k] : 0u;
+    const int i = k * kThreads + threadIdx.x;
+    s_c[at(i)] = b0 + i < n ? cnt[b0 + i] : 0u;
+  }
+  __syncthreads();
+  uint32_t v[kScanPer];
+  uint32_t s = 0;
+#pragma unroll
+  for (int k = 0; k < kScanPer; ++k) {
+    v[k] = s_c[at(threadIdx.x * kScanPer + k)];
     s += v[k];
   }
-  uint64_t x = s;
+  uint32_t x = s;  // (a block's counts sum below 2^31: at most the launch's bytes)
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-#pragma unroll
-  for (int off = 1; off < 64; off <<= 1) {
-    const uint64_t y = __shfl_up(x, off, 64);
-    if (lane >= off) x += y;
-  }
-  __shared__ uint64_t sw[kThreads / 64];
+  x = wave_incl_scan(x, lane);
+  __shared__ uint32_t sw[kThreads / 64];
   if (lane == 63) sw[wid] = x;
   __syncthreads();
-  uint64_t wb = 0;
+  uint32_t wb = 0;
   for (int k = 0; k < wid; ++k) wb += sw[k];
-  int64_t run = part[blockIdx.x] + (int64_t)(wb + x - s);
+  uint32_t run = wb + x - s;  // block-relative exclusive offset of this thread's first count
 #pragma unroll
   for (int k = 0; k < kScanPer; ++k) {
-    if (base + k < n) base_out[base + k] = run;
+    s_c[at(threadIdx.x * kScanPer + k)] = run;
     run += v[k];
+  }
+  __syncthreads();
+  const int64_t p = s_pre[0];
+#pragma unroll
+  for (int k = 0; k < kScanPer; ++k) {
+    const int i = k * kThreads + threadIdx.x;
+    if (b0 + i < n) base_out[b0 + i] = p + (int64_t)s_c[at(i)];
   }
 }
 
@@ -2333,12 +2349,18 @@ constexpr int kRefCap = 128;    // references per 8-round group gathered through
 #define SW_CP_WAVES 0  // k_compact: waves per SIMD to fit (0: the compiler's choice)
 #endif
 constexpr int kOutCapW = SW_CP_OUTCAP;  // ids per group staged in LDS (the rest are stored directly)
+// k_compact7: the same at 7 waves per SIMD with 768 staged ids a group (70 VGPRs, 22.5 KB of LDS a
+// block), for launches whose tiles hold few ids (the host chooses from the last launch's ids per
+// tile): C2 0.855 -> 0.803 ms, C5 0.794 -> 0.749, but 11% slower on ENTROPY's 1293 ids a tile
+// (its groups overflow the staging; r7j in profiles/r5_ab.txt)
+constexpr int kOutCap7 = 768;
+constexpr int kCompact7MaxIdsPerTile = 900;  // (the host's threshold on the last launch's average)
 constexpr uint32_t kLaneCopy = 64;  // results longer than this are copied by the whole wave
 
 // tile t's ids to out + base (base: the ids of the tiles before it); per wave: the group's
 // references, gathered with full lanes before any store (a store ahead of a load in the wave's
 // vmcnt order would make the load wait for it)
-template <typename OutT>  // int32_t, or uint16_t (SW_OPT_OUT_BITS 16: every id of the table fits)
+template <typename OutT, int kOutCap>  // OutT: int32_t, or uint16_t (SW_OPT_OUT_BITS 16: every id of the table fits)
 __device__ __forceinline__ void compact_tile(const EncArgs& a, int64_t t, int64_t base, OutT* out, uint32_t* s_rp,
                                              uint4* s_rq, int32_t* s_out) {
   SW_STAMP_INIT;
@@ -2411,7 +2433,7 @@ __device__ __forceinline__ void compact_tile(const EncArgs& a, int64_t t, int64_
       carry += lane_value(incl, 63);
       const uint32_t lo = o - gbase;
       if (valid && !ref) {
-        if (lo < (uint32_t)kOutCapW) s_out[lo] = v[u];
+        if (lo < (uint32_t)kOutCap) s_out[lo] = v[u];
         else dst[o] = (OutT)v[u];
       }
       // ids from the head while it has them (nh), then from res at the merged occurrence's p
@@ -2421,7 +2443,7 @@ __device__ __forceinline__ void compact_tile(const EncArgs& a, int64_t t, int64_
         const uint32_t mm = m > kLaneCopy ? 3u : m;  // (long results: the head here, the rest below)
         const uint32_t hm = min(mm, nh);
         auto put = [&](uint32_t k, uint32_t id) {
-          if (lo + k < (uint32_t)kOutCapW) s_out[lo + k] = (int32_t)id;
+          if (lo + k < (uint32_t)kOutCap) s_out[lo + k] = (int32_t)id;
           else dst[o + k] = (OutT)id;
         };
         if (d16) {
@@ -2460,7 +2482,7 @@ __device__ __forceinline__ void compact_tile(const EncArgs& a, int64_t t, int64_
           for (int q = 0; q < 4; ++q) {
             const uint32_t k = k0 + 64 * q + lane;
             if (k >= mL) break;
-            if (loL + k < (uint32_t)kOutCapW) s_out[loL + k] = id[q];
+            if (loL + k < (uint32_t)kOutCap) s_out[loL + k] = id[q];
             else dst[oL + k] = (OutT)id[q];
           }
         }
@@ -2471,7 +2493,7 @@ __device__ __forceinline__ void compact_tile(const EncArgs& a, int64_t t, int64_
     }
     wave_sync_mem();
     // the staged ids: one contiguous 256-byte store per 64 ids
-    const uint32_t staged = min(carry - gbase, (uint32_t)kOutCapW);
+    const uint32_t staged = min(carry - gbase, (uint32_t)kOutCap);
     for (uint32_t i = lane; i < staged; i += 64) SW_STNT(&dst[gbase + i], (OutT)s_out[i]);
     wave_sync_mem();  // (s_rp / s_rq / s_out are rewritten by the next group)
 #ifdef SW_STAMPS
@@ -2509,7 +2531,19 @@ k_compact(EncArgs a, const int64_t* tile_base, OutT* out) {
   const int wv = wave_in_block();
   const int64_t t = ((int64_t)blockIdx.x * kWaves + wave_in_block());
   if (t >= a.n_tiles) return;
-  compact_tile(a, t, tile_base[t], out, s_rp_all[wv], s_rq_all[wv], s_out_all[wv]);
+  compact_tile<OutT, kOutCapW>(a, t, tile_base[t], out, s_rp_all[wv], s_rq_all[wv], s_out_all[wv]);
+}
+
+template <typename OutT>
+__global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(7, 7)))
+k_compact7(EncArgs a, const int64_t* tile_base, OutT* out) {
+  __shared__ uint32_t s_rp_all[kWaves][kRefCap];
+  __shared__ uint4 s_rq_all[kWaves][kRefCap];
+  __shared__ int32_t s_out_all[kWaves][kOutCap7];
+  const int wv = wave_in_block();
+  const int64_t t = ((int64_t)blockIdx.x * kWaves + wave_in_block());
+  if (t >= a.n_tiles) return;
+  compact_tile<OutT, kOutCap7>(a, t, tile_base[t], out, s_rp_all[wv], s_rq_all[wv], s_out_all[wv]);
 }
 
 // every string offset: a complemented value is one k_compact finished; strings starting at or
@@ -2522,6 +2556,8 @@ __global__ void k_string_offsets(const int64_t* str_off, int64_t n_str, int64_t 
     const unsigned long long v = *dd_full;
     *dd_full = 0;
     __hip_atomic_store(h_dd_full, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    // (and the launch's id count: the next launch picks its k_compact from the ids per tile)
+    __hip_atomic_store(h_dd_full + 1, (unsigned long long)*total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }
   if (s > n_str) return;
   if (s == n_str || str_off[s] >= n_bytes) {

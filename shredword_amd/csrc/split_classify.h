@@ -211,10 +211,16 @@ __device__ __forceinline__ void ss_win5(const PbArgs& g, int64_t n_tiles, int64_
 
 // k_edges: per tile boundary b in [0, n_tiles] (byte 2048 b, chunk c = 64 b): the class masks of
 // chunk c and its final chunk-start word (zeros past the batch).  edge[k * (n_tiles + 1) + b].
+// With clr (SW_EDGE_CLEAR) its threads also clear the dedupe table (n16 16-byte words) in place of
+// the memset before it (profiles/r5_ab.txt r8a-r8b).
 __global__ void __launch_bounds__(256) k_edges(PbArgs g, int64_t n_tiles, int pattern, uint32_t* edge,
-                                               unsigned int* redo_count) {
+                                               unsigned int* redo_count, uint4* clr, int64_t n16) {
   const int64_t b = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (b == 0) *redo_count = 0;  // (k_split_classify's redo list, empty)
+  if (clr) {
+    const int64_t nth = (int64_t)gridDim.x * 256;
+    for (int64_t i = b; i < n16; i += nth) clr[i] = make_uint4(0u, 0u, 0u, 0u);
+  }
   if (b > n_tiles) return;
   const int64_t n_chunks = (g.n_bytes + psb::kChunk - 1) / psb::kChunk;
   const int64_t c = b << (kTileBits - 5);
@@ -228,6 +234,8 @@ __global__ void __launch_bounds__(256) k_edges(PbArgs g, int64_t n_tiles, int pa
     if (pattern == 2) {  // (the chunks are the strings)
       r = sw.at(32 * c);
     } else {
+      // (the bytes loaded per chunk, after the search: all three loaded ahead of it held 30 more
+      // registers through it and made the kernel slower, 0.077 -> 0.110 ms on C2, r8a)
       auto masks = [&](int64_t k) -> psb::Masks {
         if (k < 0 || k >= n_chunks) return psb::Masks{};
         psb::RegBytes by;

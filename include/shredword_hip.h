@@ -160,10 +160,11 @@ int32_t sw_encoder_unpin_host(sw_encoder* h, void* ptr);
  *                          <= 64 bytes and the pre-split is the device's; 0: on the host threads.
  *                          Results identical. */
 #define SW_OPT_DEVICE_SPECIALS 18
-/*   SW_OPT_COMPACT_WAVES   the id compaction kernel: 2 (default) picks from the previous launch's ids
- *                          per 2 KiB tile (7 waves per SIMD with a smaller id staging below 900, else
- *                          6 with the larger one); 6 or 7 force one.  Results identical. */
-#define SW_OPT_COMPACT_WAVES 19
+/*   SW_OPT_COMPACT_KERNEL  the id compaction kernel: 0 (default) picks from the previous launch's ids
+ *                          per 2 KiB tile: below 640 -> 3, below 900 -> 2, else 1; 1: 6 waves per SIMD,
+ *                          1024 ids staged a group; 2: 7 waves, 768 staged; 3: as 2 with separate LDS
+ *                          and global accesses instead of one generic access.  Results identical. */
+#define SW_OPT_COMPACT_KERNEL 19
 /* (option 15 was an A/B knob of round 2, removed: set_option rejects it) */
 /* (option 16, a persistent 16-bit output of sw_encode_device, was replaced by the per-call
  * sw_encode_ex.out_bits: set_option rejects it; sw_encode_device always writes int32) */

@@ -171,9 +171,9 @@ struct sw_encoder {
   bool fused_presplit = true;         // SW_OPT_FUSED_PRESPLIT: the device pre-split inside k_split_classify
   bool device_specials = true;        // SW_OPT_DEVICE_SPECIALS: sw_encode_batch_ex finds specials on the device
 #ifndef SW_CP_MODE_DEFAULT
-#define SW_CP_MODE_DEFAULT 2
+#define SW_CP_MODE_DEFAULT 0
 #endif
-  int compact_waves = SW_CP_MODE_DEFAULT;  // SW_OPT_COMPACT_WAVES (2: from the last launch's ids per tile)
+  int compact_kernel = SW_CP_MODE_DEFAULT;  // SW_OPT_COMPACT_KERNEL (0: from the last launch's ids per tile)
   int64_t cp_prev_tiles = 0;          // tiles of the previous launch (its id count: h_ddfull[1])
   unsigned long long* d_pcount = nullptr;
   uint64_t* d_llist = nullptr;        // k_classify's long chunks (EncArgs::llist) and their count
@@ -649,9 +649,9 @@ extern "C" int32_t sw_encoder_set_option(sw_encoder* h, int32_t option, int64_t 
     case SW_OPT_FUSED_PRESPLIT: h->fused_presplit = value != 0; return SW_OK;
     case SW_OPT_TEST_FAIL_GROWTH: h->test_fail_grow = value ? 1 : 0; h->dd_grow_stop = false; return SW_OK;
     case SW_OPT_DEVICE_SPECIALS: h->device_specials = value != 0; return SW_OK;
-    case SW_OPT_COMPACT_WAVES:
-      if (value != 2 && value != 6 && value != 7) return fail(SW_ERR_ARG, "SW_OPT_COMPACT_WAVES: 2, 6 or 7");
-      h->compact_waves = (int)value;
+    case SW_OPT_COMPACT_KERNEL:
+      if (value < 0 || value > 3) return fail(SW_ERR_ARG, "SW_OPT_COMPACT_KERNEL: 0 .. 3");
+      h->compact_kernel = (int)value;
       return SW_OK;
     case SW_OPT_PIPE_DEPTH:
       if (value < 2 || value > 4) return fail(SW_ERR_ARG, "pipeline depth: 2 .. 4");
@@ -1190,21 +1190,24 @@ int32_t encode_device(sw_encoder* h, const uint8_t* d_bytes, int64_t n_bytes, co
     hipLaunchKernelGGL(k_tile_count, dim3((unsigned)((n_tiles + kWaves * kTcTiles - 1) / (kWaves * kTcTiles))),
                        dim3(kThreads), 0, st, a);
     HIP_TRY(launch_scan(st, h->d_tile_cnt, n_tiles, h->d_part, h->d_tile_base, h->d_total));
-    // k_compact7 when the last launch's tiles held few ids (read without waiting: a heuristic)
-    bool c7 = h->compact_waves == 7;
-    if (h->compact_waves == 2 && h->h_ddfull && h->cp_prev_tiles > 0) {
-      const unsigned long long ids = __atomic_load_n(&h->h_ddfull[1], __ATOMIC_RELAXED);
-      c7 = ids > 0 && ids <= (unsigned long long)h->cp_prev_tiles * kCompact7MaxIdsPerTile;
+    // the compaction kernel from the last launch's ids per tile (read without waiting: a heuristic)
+    int ck = h->compact_kernel;
+    if (ck == 0) {
+      ck = 1;
+      const unsigned long long ids = h->h_ddfull ? __atomic_load_n(&h->h_ddfull[1], __ATOMIC_RELAXED) : 0ULL;
+      const unsigned long long tl = (unsigned long long)h->cp_prev_tiles;
+      if (tl > 0 && ids > 0) ck = ids <= tl * kCompactTypedMaxIdsPerTile ? 3 : ids <= tl * kCompact7MaxIdsPerTile ? 2 : 1;
     }
     h->cp_prev_tiles = n_tiles;
-    if (out16 && c7)
-      hipLaunchKernelGGL(k_compact7<uint16_t>, wg, dim3(kThreads), 0, st, a, h->d_tile_base, (uint16_t*)d_out_ids);
-    else if (out16)
-      hipLaunchKernelGGL(k_compact<uint16_t>, wg, dim3(kThreads), 0, st, a, h->d_tile_base, (uint16_t*)d_out_ids);
-    else if (c7)
-      hipLaunchKernelGGL(k_compact7<int32_t>, wg, dim3(kThreads), 0, st, a, h->d_tile_base, (int32_t*)d_out_ids);
-    else
-      hipLaunchKernelGGL(k_compact<int32_t>, wg, dim3(kThreads), 0, st, a, h->d_tile_base, (int32_t*)d_out_ids);
+    if (out16) {
+      if (ck == 3) hipLaunchKernelGGL((k_compact7<uint16_t, true>), wg, dim3(kThreads), 0, st, a, h->d_tile_base, (uint16_t*)d_out_ids);
+      else if (ck == 2) hipLaunchKernelGGL((k_compact7<uint16_t, false>), wg, dim3(kThreads), 0, st, a, h->d_tile_base, (uint16_t*)d_out_ids);
+      else hipLaunchKernelGGL(k_compact<uint16_t>, wg, dim3(kThreads), 0, st, a, h->d_tile_base, (uint16_t*)d_out_ids);
+    } else {
+      if (ck == 3) hipLaunchKernelGGL((k_compact7<int32_t, true>), wg, dim3(kThreads), 0, st, a, h->d_tile_base, (int32_t*)d_out_ids);
+      else if (ck == 2) hipLaunchKernelGGL((k_compact7<int32_t, false>), wg, dim3(kThreads), 0, st, a, h->d_tile_base, (int32_t*)d_out_ids);
+      else hipLaunchKernelGGL(k_compact<int32_t>, wg, dim3(kThreads), 0, st, a, h->d_tile_base, (int32_t*)d_out_ids);
+    }
     HIP_TRY(hipGetLastError());
   } else {
     HIP_TRY(hipMemsetAsync(h->d_total, 0, sizeof(int64_t), st));

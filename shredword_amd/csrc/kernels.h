@@ -120,6 +120,14 @@ constexpr int kDdExactMax = 7;                  // dedupe keys of <= this many b
 // streaming accesses (read or written once per launch) carry the non-temporal hint, so the
 // caches keep the randomly gathered merge results instead
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+// Pointers with their address space spelled out.  A generic pointer the compiler cannot place --
+// a select between an LDS and a global address, a pointer rebuilt from an integer, one read from
+// a struct -- becomes a FLAT access, which waits on both the vector-memory and the LDS counters
+// (k_compact's "ids to LDS staging or straight to memory" store was 144 flat stores).
+#define SW_AS_GLOBAL __attribute__((address_space(1)))
+#define SW_AS_LDS __attribute__((address_space(3)))
+template <class T> __device__ __forceinline__ SW_AS_GLOBAL T* gptr(T* p) { return (SW_AS_GLOBAL T*)p; }
+template <class T> __device__ __forceinline__ SW_AS_LDS T* lptr(T* p) { return (SW_AS_LDS T*)p; }
 #define SW_LDNT(p) __builtin_nontemporal_load(p)
 #define SW_STNT(p, v) __builtin_nontemporal_store((v), (p))
 // the other streaming arrays -- bitmap words, reference lists, tile-local queues -- too
@@ -223,13 +231,14 @@ __device__ __forceinline__ void table_lookups(const DevChunkTable& c, const uint
     len[u] = valid && !sp ? end - ls : 0;
     window_words(s_b32, ls, min(max(len[u], 1), 16), w[u]);
     tok[u] = sp ? kSpDone : len[u] == 1 ? (w[u][0] & 0xFFu) : kInf;
-    const uint4* pa = c.sb;  // (a lane without a probe loads the first bucket, unused)
-    if (len[u] >= 2 && len[u] <= 8) pa = &c.sb[chunk_b1(chunk_hash(w[u][0], w[u][1], 0, 0, len[u], c.s_m1), c.s_shift)];
+    const SW_AS_GLOBAL u32x4* pa = gptr((const u32x4*)c.sb);  // (a lane without a probe loads the first bucket, unused)
+    if (len[u] >= 2 && len[u] <= 8)
+      pa = gptr((const u32x4*)&c.sb[chunk_b1(chunk_hash(w[u][0], w[u][1], 0, 0, len[u], c.s_m1), c.s_shift)]);
     if (len[u] > 8 && len[u] <= 16)
-      pa = &c.lb[2 * chunk_b1(chunk_hash(w[u][0], w[u][1], w[u][2], w[u][3], len[u], c.l_m1), c.l_shift)];
-    qa[u] = *(const u32x4*)pa;
+      pa = gptr((const u32x4*)&c.lb[2 * chunk_b1(chunk_hash(w[u][0], w[u][1], w[u][2], w[u][3], len[u], c.l_m1), c.l_shift)]);
+    qa[u] = *pa;
     qb[u] = u32x4{0u, 0u, 0u, 0u};
-    if (len[u] > 8 && len[u] <= 16) qb[u] = *(const u32x4*)(pa + 1);
+    if (len[u] > 8 && len[u] <= 16) qb[u] = pa[1];
   }
   regs_barrier<R>(qa, qb);
   auto compare = [&](int u) -> bool {  // the entry in qa/qb holds the chunk: tok[u] set
@@ -252,12 +261,12 @@ __device__ __forceinline__ void table_lookups(const DevChunkTable& c, const uint
     if (!hit && spill) {
       need2 |= 1u << u;
       if (len[u] <= 8) {
-        qa[u] = *(const u32x4*)&c.sb[chunk_b2(chunk_hash(w[u][0], w[u][1], 0, 0, len[u], c.s_m1), c.s_m2, c.s_shift)];
+        qa[u] = *gptr((const u32x4*)&c.sb[chunk_b2(chunk_hash(w[u][0], w[u][1], 0, 0, len[u], c.s_m1), c.s_m2, c.s_shift)]);
       } else {
-        const uint4* pa =
-            &c.lb[2 * chunk_b2(chunk_hash(w[u][0], w[u][1], w[u][2], w[u][3], len[u], c.l_m1), c.l_m2, c.l_shift)];
-        qa[u] = *(const u32x4*)pa;
-        qb[u] = *(const u32x4*)(pa + 1);
+        const SW_AS_GLOBAL u32x4* pa = gptr((const u32x4*)&c.lb[2 * chunk_b2(
+            chunk_hash(w[u][0], w[u][1], w[u][2], w[u][3], len[u], c.l_m1), c.l_m2, c.l_shift)]);
+        qa[u] = pa[0];
+        qb[u] = pa[1];
       }
     }
   }
@@ -965,7 +974,7 @@ struct DdOut {
   uint32_t v;
 };
 
-__device__ __forceinline__ DdOut dedupe_claim(const EncArgs& a, const uint32_t* words, int64_t last_word, int64_t mis,
+__device__ __forceinline__ DdOut dedupe_claim(const EncArgs& a, const SW_AS_GLOBAL uint32_t* words, int64_t last_word, int64_t mis,
                                               int64_t start, int n, const uint32_t (&u)[kShort / 4]) {
   const int nw = (n + 3) >> 2;
   uint32_t h = 0x9E3779B9u ^ ((uint32_t)n << 24);
@@ -1235,7 +1244,7 @@ __device__ __forceinline__ void classify_chunks(const EncArgs& a, int64_t tile, 
   const bool use_table = a.chunks.enabled != 0;
 #endif
   const int64_t mis = (int64_t)((uintptr_t)a.bytes & 3);
-  const uint32_t* gwords = (const uint32_t*)((uintptr_t)a.bytes - mis);
+  const SW_AS_GLOBAL uint32_t* gwords = (const SW_AS_GLOBAL uint32_t*)((uintptr_t)a.bytes - mis);
   const int64_t last_word = (mis + a.n_bytes - 1) >> 2;
   uint32_t bcount = 0;
   int nq = 0;    // wave-uniform: chunks waiting in s_qbuf
@@ -1497,7 +1506,7 @@ __device__ __forceinline__ int64_t long_count(const EncArgs& a) {
 
 // the chunk bytes [g, g + n) of the word-aligned input as N/4 zero-padded LE words
 template <int N>
-__device__ __forceinline__ void chunk_words(const uint32_t* words, int64_t last_word, int64_t g, int n,
+__device__ __forceinline__ void chunk_words(const SW_AS_GLOBAL uint32_t* words, int64_t last_word, int64_t g, int n,
                                             uint32_t (&u)[N / 4]) {
   constexpr int W = N / 4 + 1;  // aligned words covering any N-byte span
   const int64_t w0 = g >> 2;
@@ -1617,7 +1626,7 @@ __global__ void __launch_bounds__(kThreads) k_merge_bucket(EncArgs a, int b_lo, 
   int64_t lo, hi;
   bucket_range(a, b_lo, b_hi, &lo, &hi);
   const int64_t mis = (int64_t)((uintptr_t)a.bytes & 3);
-  const uint32_t* words = (const uint32_t*)((uintptr_t)a.bytes - mis);
+  const SW_AS_GLOBAL uint32_t* words = (const SW_AS_GLOBAL uint32_t*)((uintptr_t)a.bytes - mis);
   const int64_t last_word = (mis + a.n_bytes - 1) >> 2;  // last word holding input bytes
   constexpr bool kLds = kWF && k16 && !kWide;
   // two or four chunks per lane (lane_merge_lds_wfq) for the short buckets of well-formed 16-bit tables
@@ -2273,10 +2282,10 @@ __device__ __forceinline__ uint4 res_head(const uint32_t* res, int64_t p) {
 // the head {count, id0, id1, id2 | p} of the result a reference slot names
 // (one load from a selected address: a branch per kind would wait for one load before the other)
 __device__ __forceinline__ uint4 ref_head(const EncArgs& a, int32_t v) {
-  const uint32_t* src = slot_is_dref(v) ? (const uint32_t*)(a.dres + slot_did(v)) : a.res + 2 * slot_pos(v);
-  uint4 q;
-  __builtin_memcpy(&q, src, sizeof(q));
-  return q;
+  const SW_AS_GLOBAL uint32_t* src =
+      slot_is_dref(v) ? gptr((const uint32_t*)(a.dres + slot_did(v))) : gptr((const uint32_t*)a.res + 2 * slot_pos(v));
+  const uint32_t x0 = src[0], x1 = src[1], x2 = src[2], x3 = src[3];  // (dword-aligned 16 bytes)
+  return make_uint4(x0, x1, x2, x3);
 }
 
 #ifndef SW_CP_ROUNDS
@@ -2355,21 +2364,40 @@ constexpr int kOutCapW = SW_CP_OUTCAP;  // ids per group staged in LDS (the rest
 // (its groups overflow the staging; r7j in profiles/r5_ab.txt)
 constexpr int kOutCap7 = 768;
 constexpr int kCompact7MaxIdsPerTile = 900;  // (the host's threshold on the last launch's average)
+constexpr int kCompactTypedMaxIdsPerTile = 640;  // (... below which it takes the typed one, see compact_tile)
 constexpr uint32_t kLaneCopy = 64;  // results longer than this are copied by the whole wave
 
 // tile t's ids to out + base (base: the ids of the tiles before it); per wave: the group's
 // references, gathered with full lanes before any store (a store ahead of a load in the wave's
 // vmcnt order would make the load wait for it)
-template <typename OutT, int kOutCap>  // OutT: int32_t, or uint16_t (SW_OPT_OUT_BITS 16: every id of the table fits)
-__device__ __forceinline__ void compact_tile(const EncArgs& a, int64_t t, int64_t base, OutT* out, uint32_t* s_rp,
-                                             uint4* s_rq, int32_t* s_out) {
+// kTyped: the staging / direct stores and the staged-head loads as separate LDS and global
+// instructions; else one generic (FLAT) access with a per-lane address, which costs every access
+// both counters but is one instruction where a group's ids overflow the staging (ENTROPY, C5).
+// r8d: C2 k_compact7 0.797 -> 0.755 ms typed; ENTROPY's k_compact 3.39 -> 3.94 and C5's k_compact7
+// 0.754 -> 0.796 typed -- so the host takes the typed kernel only for launches with few ids a tile.
+template <typename OutT, int kOutCap, bool kTyped>  // OutT: int32_t, or uint16_t (SW_OPT_OUT_BITS 16: every id of the table fits)
+__device__ __forceinline__ void compact_tile(const EncArgs& a, int64_t t, int64_t base, OutT* out, uint32_t* s_rp_g,
+                                             uint4* s_rq_g, int32_t* s_out_g) {
+  SW_AS_LDS uint32_t* s_rp = lptr(s_rp_g);
+  SW_AS_LDS u32x4* s_rq = lptr((u32x4*)s_rq_g);
+  SW_AS_LDS int32_t* s_out = lptr(s_out_g);
+  OutT* const dst_p = out + base;
+  auto put_id = [&](uint32_t l, uint32_t o_, int32_t id) {  // staged id l, or straight to output o_
+    if constexpr (kTyped) {
+      if (l < (uint32_t)kOutCap) s_out[l] = id;
+      else gptr(dst_p)[o_] = (OutT)id;
+    } else {
+      if (l < (uint32_t)kOutCap) s_out_g[l] = id;
+      else dst_p[o_] = (OutT)id;
+    }
+  };
   SW_STAMP_INIT;
   const int lane = threadIdx.x & 63;
   const uint64_t lt_mask = (lane == 0) ? 0ULL : (~0ULL >> (64 - lane));
   constexpr int R = kRoundsInFlight;
-  const int32_t* src = a.scratch + t * kTile;
+  const SW_AS_GLOBAL int32_t* src = gptr((const int32_t*)a.scratch + t * kTile);
   const int C = (int)a.tile_slots[t];
-  OutT* dst = out + base;
+  SW_AS_GLOBAL OutT* dst = gptr(out + base);
   // strings starting in this tile: lane i holds string s_lo + i's chunk index (k_classify)
   const int64_t t1 = tile_end(t * kTile, a.n_bytes);
   const int64_t s_lo = a.tile_slo[t];
@@ -2410,8 +2438,8 @@ __device__ __forceinline__ void compact_tile(const EncArgs& a, int64_t t, int64_
       uint4 q0 = make_uint4(0, 0, 0, 0), q1 = make_uint4(0, 0, 0, 0);
       if (lane < nr) q0 = ref_head(a, (int32_t)s_rp[lane]);
       if (lane + 64 < nr) q1 = ref_head(a, (int32_t)s_rp[lane + 64]);
-      if (lane < nr) s_rq[lane] = q0;
-      if (lane + 64 < nr) s_rq[lane + 64] = q1;
+      if (lane < nr) s_rq[lane] = u32x4{q0.x, q0.y, q0.z, q0.w};
+      if (lane + 64 < nr) s_rq[lane + 64] = u32x4{q1.x, q1.y, q1.z, q1.w};
     }
     wave_sync_mem();
     SW_STAMP(9);
@@ -2424,7 +2452,18 @@ __device__ __forceinline__ void compact_tile(const EncArgs& a, int64_t t, int64_
       const bool valid = j < C;
       const bool ref = valid && v[u] < 0;
       uint4 q = make_uint4(0, 0, 0, 0);
-      if (ref) q = ridx[u] < (uint32_t)kRefCap ? s_rq[ridx[u]] : ref_head(a, v[u]);
+      if constexpr (kTyped) {
+        if (ref) {
+          if (ridx[u] < (uint32_t)kRefCap) {
+            const u32x4 x = s_rq[ridx[u]];
+            q = make_uint4(x[0], x[1], x[2], x[3]);
+          } else {
+            q = ref_head(a, v[u]);
+          }
+        }
+      } else {
+        if (ref) q = ridx[u] < (uint32_t)kRefCap ? s_rq_g[ridx[u]] : ref_head(a, v[u]);
+      }
       const bool dense = ref && slot_is_dref(v[u]);
       const bool d16 = dense && a.ids16 != 0;
       const uint32_t m = ref ? (dense ? (q.x & 0xFFFFu) : q.x) : (valid ? 1u : 0u);
@@ -2433,8 +2472,7 @@ __device__ __forceinline__ void compact_tile(const EncArgs& a, int64_t t, int64_
       carry += lane_value(incl, 63);
       const uint32_t lo = o - gbase;
       if (valid && !ref) {
-        if (lo < (uint32_t)kOutCap) s_out[lo] = v[u];
-        else dst[o] = (OutT)v[u];
+        put_id(lo, o, v[u]);
       }
       // ids from the head while it has them (nh), then from res at the merged occurrence's p
       const uint32_t nh = d16 ? (m <= 7 ? m : 1u) : dense ? (m <= 3 ? 3u : 2u) : 3u;
@@ -2443,8 +2481,7 @@ __device__ __forceinline__ void compact_tile(const EncArgs& a, int64_t t, int64_
         const uint32_t mm = m > kLaneCopy ? 3u : m;  // (long results: the head here, the rest below)
         const uint32_t hm = min(mm, nh);
         auto put = [&](uint32_t k, uint32_t id) {
-          if (lo + k < (uint32_t)kOutCap) s_out[lo + k] = (int32_t)id;
-          else dst[o + k] = (OutT)id;
+          put_id(lo + k, o + k, (int32_t)id);
         };
         if (d16) {
           const uint32_t w[4] = {q.x, q.y, q.z, q.w};
@@ -2482,8 +2519,7 @@ __device__ __forceinline__ void compact_tile(const EncArgs& a, int64_t t, int64_
           for (int q = 0; q < 4; ++q) {
             const uint32_t k = k0 + 64 * q + lane;
             if (k >= mL) break;
-            if (loL + k < (uint32_t)kOutCap) s_out[loL + k] = id[q];
-            else dst[oL + k] = (OutT)id[q];
+            put_id(loL + k, oL + k, id[q]);
           }
         }
       }
@@ -2531,10 +2567,10 @@ k_compact(EncArgs a, const int64_t* tile_base, OutT* out) {
   const int wv = wave_in_block();
   const int64_t t = ((int64_t)blockIdx.x * kWaves + wave_in_block());
   if (t >= a.n_tiles) return;
-  compact_tile<OutT, kOutCapW>(a, t, tile_base[t], out, s_rp_all[wv], s_rq_all[wv], s_out_all[wv]);
+  compact_tile<OutT, kOutCapW, false>(a, t, tile_base[t], out, s_rp_all[wv], s_rq_all[wv], s_out_all[wv]);
 }
 
-template <typename OutT>
+template <typename OutT, bool kTyped>
 __global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(7, 7)))
 k_compact7(EncArgs a, const int64_t* tile_base, OutT* out) {
   __shared__ uint32_t s_rp_all[kWaves][kRefCap];
@@ -2543,7 +2579,7 @@ k_compact7(EncArgs a, const int64_t* tile_base, OutT* out) {
   const int wv = wave_in_block();
   const int64_t t = ((int64_t)blockIdx.x * kWaves + wave_in_block());
   if (t >= a.n_tiles) return;
-  compact_tile<OutT, kOutCap7>(a, t, tile_base[t], out, s_rp_all[wv], s_rq_all[wv], s_out_all[wv]);
+  compact_tile<OutT, kOutCap7, kTyped>(a, t, tile_base[t], out, s_rp_all[wv], s_rq_all[wv], s_out_all[wv]);
 }
 
 // every string offset: a complemented value is one k_compact finished; strings starting at or

@@ -216,7 +216,7 @@ __global__ void __launch_bounds__(kThreads) k_lp_encode(EncArgs a, LongArgs L) {
   uint32_t* s_id = s_ids + (kLds ? wave_in_block() * 64 * kPieceN : 0);
   const uint64_t lt_mask = (lane == 0) ? 0ULL : (~0ULL >> (64 - lane));
   const int64_t mis = (int64_t)((uintptr_t)a.bytes & 3);
-  const uint32_t* words = (const uint32_t*)((uintptr_t)a.bytes - mis);
+  const SW_AS_GLOBAL uint32_t* words = (const SW_AS_GLOBAL uint32_t*)((uintptr_t)a.bytes - mis);
   const int64_t last_word = (mis + a.n_bytes - 1) >> 2;
   const int64_t n_waves = (int64_t)gridDim.x * (kThreads / 64);
   for (int64_t g = ((int64_t)blockIdx.x * kWaves + wave_in_block()); 63 * g < np; g += n_waves) {
@@ -367,7 +367,7 @@ __global__ void __launch_bounds__(kThreads) k_lp_windows(EncArgs a, LongArgs L, 
   uint32_t* s_id = s_ids + (kLds ? wave_in_block() * 64 * kShort : 0);
   const int64_t nh = lp_count(&L.ctl[kLcHead + r], L.pcap), np = lp_count(&L.ctl[kLcPieces], L.pcap);
   const int64_t mis = (int64_t)((uintptr_t)a.bytes & 3);
-  const uint32_t* words = (const uint32_t*)((uintptr_t)a.bytes - mis);
+  const SW_AS_GLOBAL uint32_t* words = (const SW_AS_GLOBAL uint32_t*)((uintptr_t)a.bytes - mis);
   const int64_t last_word = (mis + a.n_bytes - 1) >> 2;
   const int64_t stride = (int64_t)gridDim.x * kThreads;
   for (int64_t t0 = (int64_t)blockIdx.x * kThreads; t0 < nh; t0 += stride) {  // (whole waves: the loop is per lane)

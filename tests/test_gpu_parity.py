@@ -107,19 +107,19 @@ def test_compaction_string_layouts():
         t.close()
 
 
-@pytest.mark.parametrize("waves", [6, 7, 2])
-def test_compaction_kernel_choice(waves):
-    """SW_OPT_COMPACT_WAVES: the 6-wave (1024 staged ids a group) and 7-wave (768) compaction
-    kernels, forced and chosen per launch from the previous launch's ids per tile (2): a batch of
-    many short ids per tile (its groups overflow the staging) after one of few and back, each
-    against the oracle; other values are rejected."""
+@pytest.mark.parametrize("kernel", [1, 2, 3, 0])
+def test_compaction_kernel_choice(kernel):
+    """SW_OPT_COMPACT_KERNEL: the 6-wave (1024 staged ids a group), 7-wave (768) and 7-wave typed
+    compaction kernels, forced and chosen per launch from the previous launch's ids per tile (0):
+    a batch of many short ids per tile (its groups overflow the staging) after one of few and
+    back, each against the oracle; other values are rejected."""
     t = sa.Tokenizer(device=0)
     t.merges = load_model_merges("bl32k.model")
     t.pattern = ""
     try:
         L = _lib.lib()
-        assert L.sw_encoder_set_option(t._encoder(), _lib.SW_OPT_COMPACT_WAVES, 5) != 0
-        _lib.check(L.sw_encoder_set_option(t._encoder(), _lib.SW_OPT_COMPACT_WAVES, waves))
+        assert L.sw_encoder_set_option(t._encoder(), _lib.SW_OPT_COMPACT_KERNEL, 4) != 0
+        _lib.check(L.sw_encoder_set_option(t._encoder(), _lib.SW_OPT_COMPACT_KERNEL, kernel))
         rng = random.Random(11)
         dense = pack([bytes(rng.randrange(128, 256) for _ in range(rng.randrange(1, 600))) for _ in range(3000)])
         for buf, off in (corpus.synth(3, corpus.MIXED, 20000, 300), dense, corpus.synth(4, corpus.STRESS, 3000, 600),

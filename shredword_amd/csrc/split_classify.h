@@ -213,7 +213,15 @@ __device__ __forceinline__ void ss_win5(const PbArgs& g, int64_t n_tiles, int64_
 // chunk c and its final chunk-start word (zeros past the batch).  edge[k * (n_tiles + 1) + b].
 // With clr (SW_EDGE_CLEAR) its threads also clear the dedupe table (n16 16-byte words) in place of
 // the memset before it (profiles/r5_ab.txt r8a-r8b).
-__global__ void __launch_bounds__(256) k_edges(PbArgs g, int64_t n_tiles, int pattern, uint32_t* edge,
+#ifndef SW_EDGE_WAVES
+#define SW_EDGE_WAVES 0  // (waves per SIMD to fit; 0: the compiler's choice)
+#endif
+#if SW_EDGE_WAVES
+#define SW_EDGE_ATTR __attribute__((amdgpu_waves_per_eu(SW_EDGE_WAVES, SW_EDGE_WAVES)))
+#else
+#define SW_EDGE_ATTR
+#endif
+__global__ void __launch_bounds__(256) SW_EDGE_ATTR k_edges(PbArgs g, int64_t n_tiles, int pattern, uint32_t* edge,
                                                unsigned int* redo_count, uint4* clr, int64_t n16) {
   const int64_t b = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (b == 0) *redo_count = 0;  // (k_split_classify's redo list, empty)

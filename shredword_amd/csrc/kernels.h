@@ -102,7 +102,10 @@ constexpr uint32_t kRlDense = 0x80000000u;
 constexpr uint32_t kCsPos = 0x7FFFu, kCsSpecial = 0x8000u;
 constexpr uint32_t kSpDone = 0xFFFFFFFEu;  // (table_lookups: the chunk's slot is written already)
 constexpr uint32_t kNoDid = 0x7FFFFFFu;    // (27-bit dense result field of a queue entry: none)
-constexpr int64_t kDdSlotsDefault = 1LL << 22;  // dedupe table entries at most to start with (32 MiB)
+#ifndef SW_DD_SLOTS_LOG2
+#define SW_DD_SLOTS_LOG2 22
+#endif
+constexpr int64_t kDdSlotsDefault = 1LL << SW_DD_SLOTS_LOG2;  // dedupe table entries at most to start with (32 MiB)
 constexpr int64_t kDdSlotsMax = 1LL << 26;      // ... and after growing (a queue entry's dense field: 27 bits)
 constexpr int kDdWords = 1;                     // 64-bit words per dedupe entry
 constexpr uint32_t kDdGroup = 8;                // entries per 64-byte line (a chunk's candidates)

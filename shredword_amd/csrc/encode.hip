@@ -811,7 +811,10 @@ struct DevSpecials {
 // further attempts on this handle) instead of leaving the handle half-built.
 int32_t grow_dedupe(sw_encoder* h) {
   const unsigned long long over = h->h_ddfull ? __atomic_load_n(h->h_ddfull, __ATOMIC_ACQUIRE) : 0ULL;
-  if (!h->d_dtab || h->dedupe_slots || h->dd_grow_stop || over <= (unsigned long long)h->dd_slots / 32 ||
+#ifndef SW_DD_GROW_DIV
+#define SW_DD_GROW_DIV 32  // (grow when more than slots / this many chunks found no entry)
+#endif
+  if (!h->d_dtab || h->dedupe_slots || h->dd_grow_stop || over <= (unsigned long long)h->dd_slots / SW_DD_GROW_DIV ||
       h->dd_slots >= kDdSlotsMax)
     return SW_OK;  // (SW_OPT_DEDUPE_SLOTS caps the table on purpose: no growth)
   int64_t slots = h->dd_slots;

@@ -2536,7 +2536,7 @@ __device__ __forceinline__ void compact_tile(const EncArgs& a, int64_t t, int64_
 #ifndef SW_CP_FLUSH16
 #define SW_CP_FLUSH16 1
 #endif
-    if constexpr (SW_CP_FLUSH16 && kTyped && sizeof(OutT) == 4) {
+    if constexpr (SW_CP_FLUSH16 && (kTyped || SW_CP_FLUSH16 == 2) && sizeof(OutT) == 4) {
       // (16-byte stores, four ids a lane, from the output's first 16-byte boundary on; the ids
       // before it one a lane)
       const uint32_t mis4 = (uint32_t)(((uintptr_t)(out + base + gbase) >> 2) & 3u);

@@ -349,6 +349,10 @@ def main():
     if world > 1:
         dist.barrier()
     k_ms = L.sw_encoder_last_kernel_ms(h)
+    try:  # (the dominant kernel alone, HIP events on the launch stream; absent from older A/B builds)
+        cls_ms = L.sw_encoder_last_classify_ms(h)
+    except AttributeError:
+        cls_ms = -1.0
     _lib.check(L.sw_encoder_set_timing(h, 0))
     reassembly_ok = None
     if gather:
@@ -398,7 +402,7 @@ def main():
         k_ms = ms_step
     achieved = b_algo / (k_ms * 1e-3) / 1e9 if k_ms > 0 else None
     # traffic: HBM bytes per launch from the committed PMC profile of this same workload, if any
-    traffic, traffic_x2, traffic_src, counters = None, None, None, None
+    traffic, traffic_x2, traffic_src, counters, dom_prof = None, None, None, None, None
     try:  # (one entry per workload, written by tools/summarize_prof.py from that workload's PMC run)
         with open(os.path.join(ROOT, "profiles", "traffic.json")) as f:
             tj = json.load(f)
@@ -411,6 +415,7 @@ def main():
                 traffic, traffic_src = int(ent["traffic_bytes_per_launch"]), ent["source"]
                 traffic_x2 = int(ent.get("traffic_bytes_per_launch_x2", 0)) or None
                 counters = ent.get("counters")
+                dom_prof = ent.get("dominant")
     except (OSError, ValueError, KeyError):
         pass
     roofline = {"bound": "hbm", "achieved": round(achieved, 2) if achieved else None, "peak": HBM_PEAK_GBS,
@@ -425,6 +430,27 @@ def main():
                 "kernel_ms": round(k_ms, 4),
                 "algo_bytes_per_launch": int(b_algo),
                 "counters": counters}
+    # the dominant kernel's own roofline: the classification reads the input once,
+    # writes one 4-byte slot per chunk and writes (device pre-split) or reads (caller's bitmap) n/8
+    # bytes of chunk-start bitmap; its time from HIP events around it on the launch stream, live
+    dom_algo = n_bytes + 4 * l_chunks + (n_bytes + 7) // 8
+    dom = {"kernel": "k_classify" if host_ps else "k_split_classify",
+           "algo_bytes_per_launch": int(dom_algo),
+           "algo_note": "input bytes + 4 B slot per chunk + n/8 bitmap (written by the fused pre-split, read with "
+                        "a caller's bitmap)",
+           "kernel_ms": round(cls_ms, 4) if cls_ms > 0 else None,
+           "achieved": round(dom_algo / (cls_ms * 1e-3) / 1e9, 2) if cls_ms > 0 else None,
+           "peak": HBM_PEAK_GBS, "unit": "GB/s",
+           "frac": round(dom_algo / (cls_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 5) if cls_ms > 0 else None,
+           "share_of_pipeline": round(cls_ms / k_ms, 3) if cls_ms > 0 and k_ms > 0 else None}
+    if dom_prof:  # (the committed PMC profile of this workload: the same kernel's trace time and bytes)
+        dom["trace_ms"] = dom_prof.get("avg_ms")
+        dom["traffic"] = dom_prof.get("traffic_bytes")
+        dom["traffic_over_algo"] = round(dom_prof["traffic_bytes"] / dom_algo, 2) if dom_prof.get("traffic_bytes") else None
+        dom["fetch_bytes"] = dom_prof.get("fetch_bytes")
+        dom["write_bytes"] = dom_prof.get("write_bytes")
+        dom["traffic_source"] = traffic_src
+    roofline["dominant"] = dom
 
     # PCIe-inclusive rate (rank 0, N=1): the same batch from host buffers to host buffers through
     # sw_encode_batch (Tokenizer.encode_packed).  Reported beside, never `value`.  Two modes: the

@@ -94,80 +94,32 @@ int32_t sw_encoder_reserve(sw_encoder* h, int64_t max_bytes, int64_t max_strings
 int32_t sw_encoder_pin_host(sw_encoder* h, void* ptr, int64_t bytes);
 int32_t sw_encoder_unpin_host(sw_encoder* h, void* ptr);
 
-/* Encoder options (sw_encoder_set_option).
- *   SW_OPT_CHUNK_TABLE  1 (default): a chunk of 2..16 bytes that encodes to exactly one token is
- *                       answered from a table built at creation (the vocabulary's byte strings
- *                       whose own encoding is a single token); 0: every chunk runs the merge
- *                       loop.  Results are identical either way.
- *   SW_OPT_DEDUPE       1 (default): within one launch, a multi-token chunk whose bytes already
- *                       occurred shares the first occurrence's merge result (bytes compared, not
- *                       just hashed); 0: every occurrence runs its own merge loop.  Results are
- *                       identical either way. */
-#define SW_OPT_CHUNK_TABLE 1
-#define SW_OPT_DEDUPE 2
-/* Testing knobs of the dedupe table (results are identical for any value):
- *   SW_OPT_DEDUPE_SLOTS    cap on the table's slots (0 = automatic, else a power of two >= 8);
- *                          a full table makes chunks merge on their own
- *   SW_OPT_DEDUPE_FP_BITS  fingerprint bits compared before the bytes of chunks with
- *                          fingerprint keys (26 = default; 0 makes every probe fall through to
- *                          the byte comparison) */
-#define SW_OPT_DEDUPE_SLOTS 3
-#define SW_OPT_DEDUPE_FP_BITS 4
-/*   SW_OPT_PATTERN         pre-split pattern (SW_PAT_*) sw_encode_device uses when it is given
+/* Encoder options (sw_encoder_set_option).  Every option leaves the results unchanged.
+ *   SW_OPT_PATTERN         pre-split pattern (SW_PAT_*) sw_encode_device uses when it is given
  *                          no chunk bitmap (default SW_PAT_CL100K)
  *   SW_OPT_HOST_PRESPLIT   1: sw_encode_batch without a bitmap pre-splits on the host threads
  *                          (sw_presplit_host) instead of on the device (default 0) */
 #define SW_OPT_PATTERN 5
 #define SW_OPT_HOST_PRESPLIT 6
-/*   SW_OPT_LONG_SPLIT      1 (default): long chunks (> 32 bytes, any length) on well-formed tables
- *                          (SW_INFO_SPLIT) are cut into ~12-byte pieces, all pieces of all long
- *                          chunks of the launch encoded side by side over the whole GPU, every
- *                          junction verified exactly and conflicting pieces joined and encoded
- *                          again; 0: one wave loop per chunk.  Results identical.
- *   SW_OPT_MAX_LAUNCH_BYTES  sw_encode_batch encodes larger batches as several launches of
- *                          whole strings (0 = the 2^30 - 64 byte device limit; testing: any
- *                          value >= 64) */
-#define SW_OPT_LONG_SPLIT 7
+/*   SW_OPT_MAX_LAUNCH_BYTES  sw_encode_batch encodes larger batches as several launches of
+ *                          whole strings (0 = the 2^30 - 64 byte device limit; any value >= 64:
+ *                          a smaller device workspace) */
 #define SW_OPT_MAX_LAUNCH_BYTES 8
 /*   SW_OPT_PIPE_RUN_BYTES  sw_encode_batch of more than 2 runs of this many bytes (default 128 MiB; 0:
  *                          never) pipelines runs of whole strings: pinned staging copied by a pool of
  *                          host threads, uploads, encodes and downloads of consecutive runs
- *                          overlapping, ids downloaded as 16 bits when every id fits */
+ *                          overlapping, ids downloaded as 16 bits when every id fits
+ *   SW_OPT_PIPE_DEPTH      runs in flight in that pipeline, 2 .. 4 (default 3) */
 #define SW_OPT_PIPE_RUN_BYTES 9
-/*   SW_OPT_DEDUPE_EXACT    1 (default): dedupe keys of chunks up to 14 bytes are the bytes
- *                          themselves (no verification read); 0: every key is a fingerprint
- *                          verified against the first occurrence's bytes (testing) */
-#define SW_OPT_DEDUPE_EXACT 10
-/*   SW_OPT_PIPE_COPY_KERNELS  1 (default): the pipeline's uploads and downloads are kernels that
- *                          read and write the pinned host buffers directly over PCIe (about 57 GB/s
- *                          each way on MI355X, both ways at once); 0: DMA copies (hipMemcpyAsync) */
-#define SW_OPT_PIPE_COPY_KERNELS 11
-/*   SW_OPT_PIPE_DEPTH      runs in flight in that pipeline, 2 .. 4 (default 3) */
 #define SW_OPT_PIPE_DEPTH 12
-/*   SW_OPT_MERGE_STREAMS   1 (default): the merge kernels of the different chunk-length buckets
- *                          run side by side on forked streams (joined before the counts); 0: one
- *                          after another on the launch stream.  Results identical. */
-#define SW_OPT_MERGE_STREAMS 13
-/*   SW_OPT_FUSED_PRESPLIT  1 (default): the device pre-split of sw_encode_device (no caller bitmap) runs
- *                          inside the classification kernel (k_split_classify: the input is read once,
- *                          the bitmap is not read back); 0: as its own kernel first.  Results identical. */
-#define SW_OPT_FUSED_PRESPLIT 14
-/*   SW_OPT_TEST_FAIL_GROWTH  tests only: 1 makes the dedupe table's next growth allocation fail (the
- *                          encoder must keep the table it has and go on encoding) */
-#define SW_OPT_TEST_FAIL_GROWTH 17
 /*   SW_OPT_DEVICE_SPECIALS 1 (default): sw_encode_batch_ex finds the special-token occurrences on the
  *                          device (sw_find_specials_device, launch by launch) when every special is
- *                          <= 64 bytes and the pre-split is the device's; 0: on the host threads.
- *                          Results identical. */
+ *                          <= 64 bytes and the pre-split is the device's; 0: on the host threads. */
 #define SW_OPT_DEVICE_SPECIALS 18
-/*   SW_OPT_COMPACT_KERNEL  the id compaction kernel: 0 (default) picks from the previous launch's ids
- *                          per 2 KiB tile: below 640 -> 3, below 900 -> 2, else 1; 1: 6 waves per SIMD,
- *                          1024 ids staged a group; 2: 7 waves, 768 staged; 3: as 2 with separate LDS
- *                          and global accesses instead of one generic access.  Results identical. */
-#define SW_OPT_COMPACT_KERNEL 19
-/* (option 15 was an A/B knob of round 2, removed: set_option rejects it) */
-/* (option 16, a persistent 16-bit output of sw_encode_device, was replaced by the per-call
- * sw_encode_ex.out_bits: set_option rejects it; sw_encode_device always writes int32) */
+/* (Options 1-4, 7, 10, 11, 13, 14, 17 and 19 are the library's measurement and test switches --
+ * the memoisation shortcuts, the dedupe table's limits, the alternative kernels -- documented in
+ * shredword_amd/csrc/test_options.h, not part of this interface.  Option 15 (a round-2 A/B knob)
+ * and 16 (replaced by sw_encode_ex.out_bits) are rejected.) */
 int32_t sw_encoder_set_option(sw_encoder* h, int32_t option, int64_t value);
 
 /* Encoder facts (sw_encoder_get_info): distinct merges, whole-chunk table entries, whether the
@@ -178,6 +130,7 @@ int32_t sw_encoder_set_option(sw_encoder* h, int32_t option, int64_t value);
 #define SW_INFO_IDS16 4
 #define SW_INFO_SPLIT 5     /* the table is well-formed: long chunks may take the split path */
 #define SW_INFO_DEDUPE_SLOTS 6  /* entries of the dedupe table now (it grows after a launch overflows it) */
+#define SW_INFO_CHUNK_TABLE_BYTES 7  /* device bytes of the whole-chunk table (its 64-byte lines) */
 int64_t sw_encoder_get_info(const sw_encoder* h, int32_t what);
 
 /* ---- host pre-split (apply_regex, base.py:38-58) ---------------------------------------
@@ -272,22 +225,29 @@ int32_t sw_encode_device(sw_encoder* h, const uint8_t* d_bytes, int64_t n_bytes,
 
 /* ---- the same with per-call choices ---------------------------------------------------------
  * sw_encode_device with (ex == NULL: exactly sw_encode_device):
- *   chunk_bits   as d_chunk_bits above (NULL: the device pre-splits with `pattern`)
- *   out_bits     32: d_out_ids is int32_t*; 16: uint16_t* -- the multi-GPU driver's 16-bit transport
- *                (SW_INFO_IDS16 tables only, and never together with special-token occurrences:
- *                SW_ERR_ARG otherwise)
+ *   struct_size  sizeof(sw_encode_ex) of the caller's header: any other value is refused
+ *                (SW_ERR_ARG), so a caller built against another layout fails loudly
+ *   flags        SW_EX_PATTERN: `pattern` holds this call's pattern; clear (a zero-initialised
+ *                struct): the handle's SW_OPT_PATTERN
+ *   chunk_bits   as d_chunk_bits above (NULL: the device pre-splits with the pattern)
+ *   out_bits     32 (or 0): d_out_ids is int32_t*; 16: uint16_t* -- the multi-GPU driver's 16-bit
+ *                transport (SW_INFO_IDS16 tables only, and never together with special-token
+ *                occurrences: SW_ERR_ARG otherwise)
  *   sp_pos / sp_len / sp_id / n_sp   special-token occurrences (device arrays; sp_pos relative to
  *                d_bytes, ascending, non-overlapping, each inside one string; n_sp == 0: none), as
  *                sw_find_specials_host finds them: each is one chunk encoding to its id, and the
  *                device pre-split treats its ends as string boundaries (a caller bitmap must already:
  *                sw_presplit_host_specials)
- *   pattern      the device pre-split's pattern for this call (SW_PAT_*), or -1: the handle's
- *                SW_OPT_PATTERN.  Per call, so that callers sharing one handle with different
- *                patterns do not race on the option.
+ *   pattern      with SW_EX_PATTERN: the device pre-split's pattern for this call (SW_PAT_*).  Per
+ *                call, so that callers sharing one handle with different patterns do not race on the
+ *                option.
  *   d_n_sp       NULL, or the occurrence count in device memory (sw_find_specials_device's d_count,
  *                not read back by the host): n_sp is then the arrays' capacity, and the encode reads
  *                the count on the device -- the find + encode sequence needs no synchronisation */
+#define SW_EX_PATTERN 1u
 typedef struct sw_encode_ex {
+  int32_t struct_size;
+  uint32_t flags;
   const uint64_t* chunk_bits;
   int32_t out_bits;
   const int64_t* sp_pos;
@@ -340,6 +300,9 @@ int32_t sw_decode_device(sw_decoder* d, const int32_t* d_ids, int64_t n_ids, con
  * launch over that window (it synchronises on the last event), or -1. */
 int32_t sw_encoder_set_timing(sw_encoder* h, int32_t on);
 double sw_encoder_last_kernel_ms(const sw_encoder* h);
+/* the same for the classification kernel alone (k_split_classify, or k_classify with a caller's
+ * bitmap): the pipeline's dominant kernel, timed by HIP events on the launch stream */
+double sw_encoder_last_classify_ms(const sw_encoder* h);
 
 /* What the last sw_encode_device launch did (synchronises on it): out4[0] chunks, out4[1] chunks
  * that went to the merge loop (references to a merge result: not a single byte, not in the

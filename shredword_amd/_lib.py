@@ -12,7 +12,7 @@ differences from the reference:
 import ctypes
 import os
 import sysconfig
-from ctypes import (POINTER, Structure, c_char_p, c_double, c_float, c_int32, c_int64, c_size_t, c_uint8, c_uint64,
+from ctypes import (POINTER, Structure, c_char_p, c_double, c_float, c_int32, c_int64, c_size_t, c_uint8, c_uint32, c_uint64,
                     c_void_p)
 
 LIB_NAMES = ("libshredword_hip",)
@@ -22,19 +22,22 @@ SW_ERR_ARG, SW_ERR_HIP, SW_ERR_ALLOC, SW_ERR_CAP, SW_ERR_NODEV = -1, -2, -3, -4,
 
 SW_PAT_CL100K, SW_PAT_GPT2, SW_PAT_NONE = 0, 1, 2
 SW_CORPUS_ASCII, SW_CORPUS_MIXED, SW_CORPUS_STRESS, SW_CORPUS_ENTROPY = 0, 1, 2, 3
+# options (include/shredword_hip.h)
+SW_OPT_PATTERN, SW_OPT_HOST_PRESPLIT, SW_OPT_MAX_LAUNCH_BYTES = 5, 6, 8
+SW_OPT_PIPE_RUN_BYTES, SW_OPT_PIPE_DEPTH = 9, 12
+SW_OPT_DEVICE_SPECIALS = 18
+# measurement and test switches (shredword_amd/csrc/test_options.h; results unchanged)
 SW_OPT_CHUNK_TABLE, SW_OPT_DEDUPE, SW_OPT_DEDUPE_SLOTS, SW_OPT_DEDUPE_FP_BITS = 1, 2, 3, 4
-SW_OPT_PATTERN, SW_OPT_HOST_PRESPLIT, SW_OPT_LONG_SPLIT, SW_OPT_MAX_LAUNCH_BYTES = 5, 6, 7, 8
-SW_OPT_PIPE_RUN_BYTES = 9
+SW_OPT_LONG_SPLIT = 7
 SW_OPT_DEDUPE_EXACT = 10
 SW_OPT_PIPE_COPY_KERNELS = 11
-SW_OPT_PIPE_DEPTH = 12
 SW_OPT_MERGE_STREAMS = 13
 SW_OPT_FUSED_PRESPLIT = 14
 SW_OPT_TEST_FAIL_GROWTH = 17
-SW_OPT_DEVICE_SPECIALS = 18
 SW_OPT_COMPACT_KERNEL = 19
 SW_OPT_OUT_BITS = 16  # (removed: set_option rejects it; 16-bit output is sw_encode_ex.out_bits, per call)
 SW_INFO_MERGES, SW_INFO_CHUNK_ENTRIES, SW_INFO_WIDE_TABLE, SW_INFO_IDS16, SW_INFO_SPLIT, SW_INFO_DEDUPE_SLOTS = 1, 2, 3, 4, 5, 6
+SW_INFO_CHUNK_TABLE_BYTES = 7
 
 
 class SwStats(Structure):
@@ -48,15 +51,21 @@ class SwSpecials(Structure):
     _fields_ = [("bytes", POINTER(c_uint8)), ("off", POINTER(c_int64)), ("ids", POINTER(c_int32)), ("n", c_int64)]
 
 
+SW_EX_PATTERN = 1
+
+
 class SwEncodeEx(Structure):
     """sw_encode_ex: per-call choices of sw_encode_device_ex (device pointers as integers).
-    pattern: SW_PAT_* for this call, or -1 (the default here): the handle's SW_OPT_PATTERN."""
-    _fields_ = [("chunk_bits", c_void_p), ("out_bits", c_int32), ("sp_pos", c_void_p), ("sp_len", c_void_p),
-                ("sp_id", c_void_p), ("n_sp", c_int64), ("pattern", c_int32), ("d_n_sp", c_void_p)]
+    pattern: SW_PAT_* for this call (sets SW_EX_PATTERN), or -1 (the default here): the handle's
+    SW_OPT_PATTERN.  struct_size is filled in: the library refuses any other layout."""
+    _fields_ = [("struct_size", c_int32), ("flags", c_uint32), ("chunk_bits", c_void_p), ("out_bits", c_int32),
+                ("sp_pos", c_void_p), ("sp_len", c_void_p), ("sp_id", c_void_p), ("n_sp", c_int64),
+                ("pattern", c_int32), ("d_n_sp", c_void_p)]
 
     def __init__(self, chunk_bits=None, out_bits=32, sp_pos=None, sp_len=None, sp_id=None, n_sp=0, pattern=-1,
                  d_n_sp=None):
-        super().__init__(chunk_bits, out_bits, sp_pos, sp_len, sp_id, n_sp, pattern, d_n_sp)
+        super().__init__(ctypes.sizeof(SwEncodeEx), SW_EX_PATTERN if pattern >= 0 else 0, chunk_bits, out_bits,
+                         sp_pos, sp_len, sp_id, n_sp, max(pattern, 0), d_n_sp)
 
 
 class TrainConfig(Structure):
@@ -128,6 +137,7 @@ _SIGNATURES = {
     "sw_encoder_get_info": (c_int64, [c_void_p, c_int32]),
     "sw_encoder_set_timing": (c_int32, [c_void_p, c_int32]),
     "sw_encoder_last_kernel_ms": (c_double, [c_void_p]),
+    "sw_encoder_last_classify_ms": (c_double, [c_void_p]),
     "sw_encoder_last_counts": (c_int32, [c_void_p, POINTER(c_int64)]),
     "sw_encoder_phase_cycles": (c_int32, [c_void_p, POINTER(c_double), c_int32]),
     "sw_reassemble_device": (c_int32, [c_void_p, c_int32, c_void_p, c_int64, c_void_p, c_void_p, c_int64, c_int32,

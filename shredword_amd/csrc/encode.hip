@@ -37,8 +37,10 @@
 #include "long_split.h"
 #include "presplit_kernel.h"
 #include "split_classify.h"
+#include "copy_seg.h"
 #include "specials_find.h"
 #include "shredword_hip.h"
+#include "test_options.h"
 #include "table.h"
 
 using namespace sw;
@@ -79,6 +81,7 @@ struct sw_encoder {
   DevChunkTable chunks{};
   void* d_chunks = nullptr;
   int64_t n_chunk_entries = 0;
+  int64_t chunk_table_bytes = 0;
   // split + verify for long chunks (long_split.h): well-formed tables only
   bool split_ok = false;              // values >= 256, unique, larger than both pair members
   bool long_split = true;             // SW_OPT_LONG_SPLIT (0: the wave loop per long chunk)
@@ -210,6 +213,8 @@ struct sw_encoder {
   bool timing = false;
   std::vector<hipEvent_t> ev_pool;
   size_t ev_used = 0;  // pairs recorded
+  std::vector<hipEvent_t> ev_cls;  // (timing) the classification kernel of each launch: a pair per launch
+  size_t ev_cls_used = 0;
 };
 
 namespace {
@@ -513,6 +518,7 @@ extern "C" int32_t sw_encoder_create(const int32_t* pairs, const int32_t* vals, 
       sw_encoder_destroy(h);
       return fail(SW_ERR_HIP, std::string("sw_encoder_create: ") + hipGetErrorString(e));
     }
+    h->chunk_table_bytes = (int64_t)(sb + lb);
     h->chunks.sb = (const uint4*)h->d_chunks;
     h->chunks.lb = (const uint4*)((char*)h->d_chunks + sb);
     h->chunks.s_shift = ct.s_shift; h->chunks.s_m1 = ct.s_m1; h->chunks.s_m2 = ct.s_m2;
@@ -578,6 +584,7 @@ extern "C" void sw_encoder_destroy(sw_encoder* h) {
     if (h->ws_done) (void)hipEventDestroy(h->ws_done);
     if (h->h_ddfull) (void)hipHostFree(h->h_ddfull);
     for (hipEvent_t ev : h->ev_pool) (void)hipEventDestroy(ev);
+    for (hipEvent_t ev : h->ev_cls) (void)hipEventDestroy(ev);
     if (h->stream) (void)hipStreamDestroy(h->stream);
   }
   delete h;
@@ -679,6 +686,7 @@ extern "C" int64_t sw_encoder_get_info(const sw_encoder* h, int32_t what) {
     case SW_INFO_IDS16: return h->ids16 ? 1 : 0;
     case SW_INFO_SPLIT: return h->split_ok ? 1 : 0;
     case SW_INFO_DEDUPE_SLOTS: return h->dd_slots;
+    case SW_INFO_CHUNK_TABLE_BYTES: return h->chunk_table_bytes;
     default: return SW_ERR_ARG;
   }
 }
@@ -687,7 +695,24 @@ extern "C" int32_t sw_encoder_set_timing(sw_encoder* h, int32_t on) {
   if (!h) return fail(SW_ERR_ARG, "sw_encoder_set_timing: null handle");
   h->timing = on != 0;
   h->ev_used = 0;
+  h->ev_cls_used = 0;
   return SW_OK;
+}
+
+// Average device time of the classification kernel alone (k_split_classify, or k_classify with a
+// caller's bitmap) over the launches recorded since the last sw_encoder_set_timing(h, 1): the
+// pipeline's dominant kernel, for the per-kernel roofline (HIP events on the launch stream).
+extern "C" double sw_encoder_last_classify_ms(const sw_encoder* h) {
+  if (!h || h->ev_cls_used == 0) return -1.0;
+  DeviceGuard g(h->device);
+  if (hipEventSynchronize(h->ev_cls[2 * h->ev_cls_used - 1]) != hipSuccess) return -1.0;
+  double sum = 0;
+  for (size_t i = 0; i < h->ev_cls_used; ++i) {
+    float ms = 0;
+    if (hipEventElapsedTime(&ms, h->ev_cls[2 * i], h->ev_cls[2 * i + 1]) != hipSuccess) return -1.0;
+    sum += ms;
+  }
+  return sum / (double)h->ev_cls_used;
 }
 
 // Average device time of the whole sw_encode_device pipeline (k_tile_strings .. k_string_offsets) over the
@@ -1090,6 +1115,21 @@ int32_t encode_device(sw_encoder* h, const uint8_t* d_bytes, int64_t n_bytes, co
 #endif
     const bool clr_in_edges = SW_EDGE_CLEAR && fused && dtab_bytes % 16 == 0;
     if (h->dedupe && !clr_in_edges) HIP_TRY(hipMemsetAsync(h->d_dtab, 0, dtab_bytes, st));
+    hipEvent_t c1 = nullptr;  // (timing: the classification kernel alone -- k_split_classify or k_classify)
+    if (h->timing) {
+      while (h->ev_cls.size() < 2 * (h->ev_cls_used + 1)) {
+        hipEvent_t ev;
+        HIP_TRY(hipEventCreate(&ev));
+        h->ev_cls.push_back(ev);
+      }
+      c1 = h->ev_cls[2 * h->ev_cls_used + 1];
+    }
+    auto cls_begin = [&]() -> hipError_t { return c1 ? hipEventRecord(h->ev_cls[2 * h->ev_cls_used], st) : hipSuccess; };
+    auto cls_end = [&]() -> hipError_t {
+      if (!c1) return hipSuccess;
+      ++h->ev_cls_used;
+      return hipEventRecord(c1, st);
+    };
     if (fused) {
       const PbArgs pg{d_bytes, n_bytes, d_str_off, n_str, h->d_tile_slo, spa};
       hipLaunchKernelGGL(k_edges, dim3((unsigned)((n_tiles + 1 + 255) / 256)), dim3(256), 0, st, pg, n_tiles,
@@ -1097,14 +1137,17 @@ int32_t encode_device(sw_encoder* h, const uint8_t* d_bytes, int64_t n_bytes, co
                          (int64_t)(dtab_bytes / 16));
       const dim3 gc((unsigned)((n_tiles + kWaves - 1) / kWaves));
       const RedoList redo{h->d_redo, (int64_t*)(h->d_redo + 2)};  // (its count zeroed by k_edges)
+      HIP_TRY(cls_begin());
       if (sp.n > 0) {
         hipLaunchKernelGGL(k_split_classify<true>, gc, dim3(kThreads), 0, st, a, pg, (int)pattern,
                            (const uint32_t*)h->d_edge, (uint32_t*)h->d_pbits, redo);
+        HIP_TRY(cls_end());
         hipLaunchKernelGGL(k_split_redo<true>, dim3(kRedoGrid), dim3(kThreads), 0, st, a, pg, (int)pattern,
                            (const uint32_t*)h->d_edge, (uint32_t*)h->d_pbits, redo);
       } else {
         hipLaunchKernelGGL(k_split_classify<false>, gc, dim3(kThreads), 0, st, a, pg, (int)pattern,
                            (const uint32_t*)h->d_edge, (uint32_t*)h->d_pbits, redo);
+        HIP_TRY(cls_end());
         hipLaunchKernelGGL(k_split_redo<false>, dim3(kRedoGrid), dim3(kThreads), 0, st, a, pg, (int)pattern,
                            (const uint32_t*)h->d_edge, (uint32_t*)h->d_pbits, redo);
       }
@@ -1114,12 +1157,15 @@ int32_t encode_device(sw_encoder* h, const uint8_t* d_bytes, int64_t n_bytes, co
       int64_t* ov_tiles = (int64_t*)(h->d_redo + 2);
       HIP_TRY(hipMemsetAsync(ov_count, 0, sizeof(unsigned int), st));
       const dim3 gc((unsigned)((n_tiles + kWaves - 1) / kWaves));
+      HIP_TRY(cls_begin());
       if (sp.n > 0) {
         hipLaunchKernelGGL(k_classify<true>, gc, dim3(kThreads), 0, st, a, ov_count, ov_tiles);
+        HIP_TRY(cls_end());
         hipLaunchKernelGGL(k_classify_big<true>, dim3(kRedoGrid), dim3(kThreads), 0, st, a, (const unsigned int*)ov_count,
                            (const int64_t*)ov_tiles);
       } else {
         hipLaunchKernelGGL(k_classify<false>, gc, dim3(kThreads), 0, st, a, ov_count, ov_tiles);
+        HIP_TRY(cls_end());
         hipLaunchKernelGGL(k_classify_big<false>, dim3(kRedoGrid), dim3(kThreads), 0, st, a, (const unsigned int*)ov_count,
                            (const int64_t*)ov_tiles);
       }
@@ -1247,12 +1293,17 @@ extern "C" int32_t sw_encode_device_ex(sw_encoder* h, const uint8_t* d_bytes, in
   if (!ex)
     return encode_device(h, d_bytes, n_bytes, d_str_off, n_str, nullptr, DevSpecials{}, d_out_ids, false, d_out_off,
                          stream, n_tokens_host);
-  if (ex->out_bits != 16 && ex->out_bits != 32) return fail(SW_ERR_ARG, "sw_encode_device_ex: out_bits 16 or 32");
+  if (ex->struct_size != (int32_t)sizeof(sw_encode_ex))
+    return fail(SW_ERR_ARG, "sw_encode_device_ex: struct_size is not sizeof(sw_encode_ex) of this library");
+  if (ex->out_bits != 0 && ex->out_bits != 16 && ex->out_bits != 32)
+    return fail(SW_ERR_ARG, "sw_encode_device_ex: out_bits 16 or 32");
+  if ((ex->flags & SW_EX_PATTERN) && (ex->pattern < SW_PAT_CL100K || ex->pattern > SW_PAT_NONE))
+    return fail(SW_ERR_ARG, "sw_encode_device_ex: unknown pattern");
   DevSpecials sp;
   sp.pos = ex->sp_pos; sp.len = ex->sp_len; sp.id = ex->sp_id; sp.n = ex->n_sp; sp.n_dev = ex->d_n_sp;
   if (sp.n_dev && sp.n <= 0) return fail(SW_ERR_ARG, "sw_encode_device_ex: d_n_sp needs n_sp = the arrays' capacity");
   return encode_device(h, d_bytes, n_bytes, d_str_off, n_str, ex->chunk_bits, sp, d_out_ids, ex->out_bits == 16,
-                       d_out_off, stream, n_tokens_host, ex->pattern);
+                       d_out_off, stream, n_tokens_host, (ex->flags & SW_EX_PATTERN) ? ex->pattern : -1);
 }
 
 extern "C" int32_t sw_encoder_set_specials(sw_encoder* h, const sw_specials* sp) {
@@ -1284,68 +1335,14 @@ __global__ void k_pack16(const int32_t* in, const int64_t* total, uint16_t* out)
 
 // Pipeline copies as kernels over PCIe: a few hundred waves of 16-byte loads keep enough requests
 // in flight to run a copy at the link rate (about 57 GB/s each way measured, tools/h2d_probe.hip)
-// while the encode kernels run beside them.  Staging buffers are hipHostMalloc'd (page aligned) and
-// device buffers hipMalloc'd, but two paths hand over arbitrary offsets: the caller's pinned input
-// (a run starts at any byte) and the caller's pinned output (a run's ids start at any id), so
-// copy_seg aligns the destination with a head of single bytes and then reads the source as
-// aligned 16-byte blocks, each lane taking its neighbour's block (a shuffle) to realign.
-typedef unsigned int v4u32 __attribute__((ext_vector_type(4)));
-
+// while the encode kernels run beside them (copy_seg: copy_seg.h, its access ranges checked on the
+// CPU by tests/native/copy_seg_emul.cpp).
 constexpr int kCopySegs = 6;
 struct CopySegs {
   const uint8_t* src[kCopySegs];
   uint8_t* dst[kCopySegs];
   int64_t n[kCopySegs];
 };
-
-// bytes [r, r + 16) of the 32 bytes lo | hi (0 < r < 16; r wave-uniform)
-__device__ __forceinline__ v4u32 realign16(const v4u32& lo, const v4u32& hi, uint32_t r) {
-  const uint32_t w[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
-  const uint32_t sh = r & 3;
-  v4u32 o;
-  switch (r >> 2) {  // (uniform: no dynamically indexed registers)
-    case 0: o = v4u32{__builtin_amdgcn_alignbyte(w[1], w[0], sh), __builtin_amdgcn_alignbyte(w[2], w[1], sh),
-                      __builtin_amdgcn_alignbyte(w[3], w[2], sh), __builtin_amdgcn_alignbyte(w[4], w[3], sh)}; break;
-    case 1: o = v4u32{__builtin_amdgcn_alignbyte(w[2], w[1], sh), __builtin_amdgcn_alignbyte(w[3], w[2], sh),
-                      __builtin_amdgcn_alignbyte(w[4], w[3], sh), __builtin_amdgcn_alignbyte(w[5], w[4], sh)}; break;
-    case 2: o = v4u32{__builtin_amdgcn_alignbyte(w[3], w[2], sh), __builtin_amdgcn_alignbyte(w[4], w[3], sh),
-                      __builtin_amdgcn_alignbyte(w[5], w[4], sh), __builtin_amdgcn_alignbyte(w[6], w[5], sh)}; break;
-    default: o = v4u32{__builtin_amdgcn_alignbyte(w[4], w[3], sh), __builtin_amdgcn_alignbyte(w[5], w[4], sh),
-                       __builtin_amdgcn_alignbyte(w[6], w[5], sh), __builtin_amdgcn_alignbyte(w[7], w[6], sh)}; break;
-  }
-  return o;
-}
-
-// dst[0, n) = src[0, n); t / nt: this thread's index in the grid and the grid's size (whole waves)
-__device__ inline void copy_seg(const uint8_t* src, uint8_t* dst, int64_t n, int64_t t, int64_t nt) {
-  const int64_t head = min<int64_t>(n, (int64_t)((16 - ((uintptr_t)dst & 15)) & 15));
-  for (int64_t i = t; i < head; i += nt) dst[i] = src[i];
-  src += head;
-  dst += head;
-  n -= head;
-  const int64_t n16 = n >> 4;
-  v4u32* d = (v4u32*)dst;
-  const uint32_t mis = (uint32_t)((uintptr_t)src & 15);
-  if (mis == 0) {
-    const v4u32* s = (const v4u32*)src;
-    for (int64_t i = t; i < n16; i += nt) d[i] = __builtin_nontemporal_load(s + i);
-  } else {
-    // block i of dst = bytes [mis, mis + 16) of the aligned source blocks i, i + 1 (block n16 holds
-    // the last bytes block n16 - 1 needs; it lies in the same 16 bytes, hence the same page, as them)
-    const v4u32* s = (const v4u32*)(src - mis);
-    const int lane = (int)(threadIdx.x & 63);
-    for (int64_t i0 = t - lane; i0 < n16; i0 += nt) {  // (wave-uniform)
-      const int64_t i = i0 + lane;
-      const v4u32 x = i <= n16 ? __builtin_nontemporal_load(s + i) : v4u32{0, 0, 0, 0};
-      v4u32 y;
-      y.x = (uint32_t)__shfl_down((int)x.x, 1, 64); y.y = (uint32_t)__shfl_down((int)x.y, 1, 64);
-      y.z = (uint32_t)__shfl_down((int)x.z, 1, 64); y.w = (uint32_t)__shfl_down((int)x.w, 1, 64);
-      if (lane == 63 && i + 1 <= n16) y = __builtin_nontemporal_load(s + i + 1);
-      if (i < n16) d[i] = realign16(x, y, mis);
-    }
-  }
-  for (int64_t i = (n16 << 4) + t; i < n; i += nt) dst[i] = src[i];
-}
 
 __global__ void __launch_bounds__(256) k_copy_segs(CopySegs c) {
   const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x, nt = (int64_t)gridDim.x * blockDim.x;
@@ -1524,12 +1521,14 @@ int32_t encode_batch_pipelined(sw_encoder* h, const uint8_t* bytes, const int64_
   const bool count = stats && !chunk_bits;
   if (count) HIP_TRY(hipMemsetAsync(h->d_pcount, 0, sizeof(unsigned long long), h->stream));
   const bool was_timing = h->timing;
-  const size_t was_used = h->ev_used;
+  const size_t was_used = h->ev_used, was_cls = h->ev_cls_used;
   h->timing = true;
   h->ev_used = 0;
+  h->ev_cls_used = 0;
   auto restore = [&]() {
     h->timing = was_timing;
     h->ev_used = was_timing ? was_used : 0;
+    h->ev_cls_used = was_timing ? was_cls : 0;
   };
   sw::HostPool& pool = *h->pool;
   double ms_stage = 0, ms_drain = 0;
@@ -1848,9 +1847,10 @@ int32_t encode_batch_impl(sw_encoder* h, const uint8_t* bytes, const int64_t* st
   double ms_h2d = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - a).count();
   int64_t n_tok = 0;
   const bool was_timing = h->timing;
-  const size_t was_used = h->ev_used;
+  const size_t was_used = h->ev_used, was_cls = h->ev_cls_used;
   h->timing = true;
   h->ev_used = 0;
+  h->ev_cls_used = 0;
   int32_t rc = encode_device(h, h->d_bytes, n_bytes, h->d_str_off, n_str, device_presplit ? nullptr : h->d_bits, dsp,
                              h->d_out, false, h->d_out_off, st, &n_tok, pattern);
   if (rc == SW_OK && device_presplit && stats && n_bytes > 0) {  // chunk count for the stats
@@ -1864,6 +1864,7 @@ int32_t encode_batch_impl(sw_encoder* h, const uint8_t* bytes, const int64_t* st
   const double k_ms = sw_encoder_last_kernel_ms(h);
   h->timing = was_timing;
   h->ev_used = was_timing ? was_used : 0;
+  h->ev_cls_used = was_timing ? was_cls : 0;
   if (rc) return rc;
   if (n_tok > out_cap) return fail(SW_ERR_CAP, "sw_encode_batch: out_cap too small");
   a = std::chrono::steady_clock::now();

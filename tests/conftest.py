@@ -66,3 +66,19 @@ def page_array(n, dtype, fill=0):
     a = raw[a0:a0 + nbytes].view(dtype)
     a[:] = fill
     return a  # (a view: keeps raw alive)
+
+
+def page_end_array(n, dtype, fill=0):
+    """A numpy array of n elements that ENDS exactly on a page boundary, with at least one page of
+    the same allocation after it that nobody pins (so a device access past the array's end would
+    touch an unmapped page), and nothing else on its pages.  Its start is wherever n elements put
+    it: misaligned to 16 bytes unless n * itemsize is a multiple of 16."""
+    import numpy as np
+    nbytes = n * np.dtype(dtype).itemsize
+    span = (nbytes + 4095) // 4096 * 4096
+    raw = np.empty(span + 3 * 4096, dtype=np.uint8)
+    base = (-raw.ctypes.data) % 4096  # (first page boundary in raw)
+    end = base + span
+    a = raw[end - nbytes:end].view(dtype)
+    a[:] = fill
+    return a

@@ -11,7 +11,7 @@ import pytest
 import oracle
 import shredword_amd as sa
 from shredword_amd import _lib, corpus
-from conftest import PATTERNS, golden_index, load_fixture, load_model_merges, page_array
+from conftest import PATTERNS, golden_index, load_fixture, load_model_merges, page_array, page_end_array
 
 pytestmark = pytest.mark.gpu
 
@@ -368,6 +368,51 @@ def test_pipelined_depth(depth):
     assert L.sw_encoder_set_option(h, _lib.SW_OPT_PIPE_DEPTH, 5) == _lib.SW_ERR_ARG
     t.close()
 
+
+
+def test_pinned_arrays_ending_on_a_page_boundary():
+    """Pinned caller arrays with nothing after them: the input, the ids and the offsets each END
+    exactly on a page boundary (the next page of the allocation is not pinned, so a device access
+    past an array's end would touch an unmapped page), with misaligned starts (the strings begin 13
+    bytes in; the ids start 4 mod 16 bytes; out_cap is the exact token count, so the last run's ids
+    end at the page end) and many pipeline runs, so the direct push writes at many misaligned
+    running counts done[0] (copy_seg).  == the oracle; read and written through the C-ABI."""
+    buf, off = corpus.synth(11, corpus.MIXED, 900, 600)
+    n = 900
+    while True:  # (a token count that is not a multiple of 4: the ids then start off a 16-byte boundary)
+        datas = [bytes(buf[off[i]:off[i + 1]]) for i in range(n)]
+        full0, offs = pack([b"#" * 13] + datas)
+        sub = offs[1:]
+        merges = load_model_merges("bl32k.model")
+        exp = oracle_encode(merges, full0, sub, "cl100k")
+        if len(exp[0]) % 4 and len(sub) % 2 == 1:  # (and n + 1 int64 offsets ending on the page start off 16 B too)
+            break
+        n -= 1
+    t = sa.Tokenizer(device=0)
+    t.merges = merges
+    L, h = _lib.lib(), t._encoder()
+    _lib.check(L.sw_encoder_set_option(h, _lib.SW_OPT_PIPE_RUN_BYTES, 4099))
+    full = page_end_array(len(full0), np.uint8, full0)
+    out = page_end_array(len(exp[0]), np.int32, -5)
+    out_off = page_end_array(len(sub), np.int64, -5)
+    assert out.ctypes.data % 16 != 0 and out_off.ctypes.data % 16 != 0
+    for arr in (full, out, out_off):
+        assert (arr.ctypes.data + arr.nbytes) % 4096 == 0
+        t.pin_host(arr)
+    try:
+        for _ in range(2):
+            stats = _lib.SwStats()
+            _lib.check(L.sw_encode_batch(h, _lib.ptr(full, ctypes.c_uint8), _lib.ptr(sub, ctypes.c_int64), len(sub) - 1, 0,
+                                         None, _lib.ptr(out, ctypes.c_int32), len(out), _lib.ptr(out_off, ctypes.c_int64),
+                                         ctypes.byref(stats)))
+            assert stats.n_tokens == len(exp[0])
+            assert_same((out, out_off), exp)
+            out[:] = -5
+            out_off[:] = -5
+    finally:
+        for arr in (full, out, out_off):
+            t.unpin_host(arr)
+    t.close()
 
 
 @pytest.mark.parametrize("pin", ["all", "input", "outputs", "out_only"])

@@ -67,6 +67,15 @@ for s in "$@"; do
               -d "$O/pmc_${lib%.so}" -o run --output-format csv -- python3 "$R/bench.py" --steps 2 --warmup 1 "${NB[@]}" \
               > "$O/pmc_${lib%.so}.log" 2>&1)
            rc=$?; echo "pmc_${lib%.so} rc=$rc" >> "$O/status.txt"; [ $rc -eq 0 ] || exit $rc ;;
+    fetch=*) v=${s#fetch=}; lib=${v%%@*}; extra=""; [ "$lib" != "$v" ] && extra=${v#*@} && extra=${extra//+/ }
+             nm=$(echo "${v}" | tr -c 'A-Za-z0-9_\n' '_')
+             for grp in FETCH_SIZE WRITE_SIZE "TCC_HIT_sum TCC_MISS_sum"; do
+               g=$(echo $grp | cut -d' ' -f1)
+               (cd /tmp && export TMPDIR=/tmp && SHREDWORD_HIP_LIB="$R/shredword_amd/$lib" timeout -k 10 300 rocprofv3 --pmc $grp \
+                  -d "$O/fetch_${nm}_$g" -o run --output-format csv -- python3 "$R/bench.py" --steps 2 --warmup 1 "${NB[@]}" $extra \
+                  > "$O/fetch_${nm}_$g.log" 2>&1)
+               rc=$?; echo "fetch_${nm}_$g rc=$rc" >> "$O/status.txt"; [ $rc -eq 0 ] || exit $rc
+             done ;;
     *) echo "unknown step $s" >> "$O/status.txt"; exit 2 ;;
   esac
 done

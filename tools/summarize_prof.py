@@ -152,6 +152,21 @@ def main():
                               "l2_hit_rate": derived.get("l2_hit_rate"),
                               "note": "pipeline totals per launch; VALU floor = wave instructions x 2 cycles / "
                                       "1024 SIMDs / 2.4 GHz"}}
+        # the dominant kernel alone (bench.py roofline.dominant): its trace time and its own bytes
+        cls = [k for k in c if k.split("<")[0] in ("sw::k_split_classify", "sw::k_classify")]
+        if cls:
+            k = max(cls, key=lambda n: calls.get(n, 0))
+            avg = [float(r["AverageNs"]) / 1e6 for r in rows if r["Name"].split("(")[0].replace("void ", "") == k]
+            fb, wb = c[k].get("FETCH_SIZE"), c[k].get("WRITE_SIZE")
+            entry["dominant"] = {
+                "kernel": k, "avg_ms": round(avg[0], 4) if avg else None,
+                "fetch_bytes": fb * 1024 if fb is not None else None, "write_bytes": wb * 1024 if wb is not None else None,
+                "traffic_bytes": (fb + wb) * 1024 if fb is not None and wb is not None else None,
+                "lds_conflict_cycles_per_lds_inst": (c[k]["SQ_LDS_BANK_CONFLICT"] / c[k]["SQ_INSTS_LDS"]
+                                                     if c[k].get("SQ_INSTS_LDS") else None),
+                "valu_wave_insts": c[k].get("SQ_INSTS_VALU"),
+                "wait_fraction_of_wave_cycles": (c[k]["SQ_WAIT_ANY"] / c[k]["SQ_WAVE_CYCLES"]
+                                                 if c[k].get("SQ_WAVE_CYCLES") else None)}
         path = os.path.join(out, "traffic.json")
         try:
             tj = json.load(open(path))

@@ -46,11 +46,9 @@ bool place(const std::vector<Entry>& es, bool is_long, std::vector<uint4>* out, 
            uint32_t* m2) {
   const int w = is_long ? 2 : 1;
   uint32_t log2b = 4;
-#ifndef SW_CT_LOAD
-#define SW_CT_LOAD 0.10  // the cuckoo's maximum load: a sparse table leaves few spilled buckets, so few wave batches pay a second probe
-#endif
+  constexpr double kLoad = 0.10;  // the cuckoo's maximum load: a sparse table leaves few spilled buckets, so few wave batches pay a second probe
   // sparse up to 2^22 buckets (64 MB of short entries); a larger vocabulary fills them to 0.45
-  while ((double)(1ull << log2b) * SW_CT_LOAD < (double)es.size() &&
+  while ((double)(1ull << log2b) * kLoad < (double)es.size() &&
          (log2b < 22 || (double)(1ull << log2b) * 0.45 < (double)es.size()))
     ++log2b;
   uint64_t rng = is_long ? 0x13198A2E03707344ULL : 0xA4093822299F31D0ULL;

@@ -16,7 +16,7 @@
 // lookup whose first probe neither matches nor sees spill is a certain miss, so most lookups
 // cost one memory request instead of two (entries are placed in token order, first candidate
 // preferred, so the frequent chunks sit in their first bucket).  The tables are kept at most
-// 10% full (SW_CT_LOAD, up to 2^22 buckets): one lane that needs its second candidate costs
+// 10% full (kLoad, up to 2^22 buckets): one lane that needs its second candidate costs
 // its whole wave batch a second dependent round trip, so few spilled buckets matter more than
 // the table's size (C2 at 0.45: 2.99 ms of k_split_classify, at 0.10: 2.76; profiles/r5_ab.txt).
 #pragma once

@@ -173,10 +173,7 @@ struct sw_encoder {
   unsigned int* d_redo = nullptr;     // k_split_classify's tiles for k_split_redo: count, then the list (int64)
   bool fused_presplit = true;         // SW_OPT_FUSED_PRESPLIT: the device pre-split inside k_split_classify
   bool device_specials = true;        // SW_OPT_DEVICE_SPECIALS: sw_encode_batch_ex finds specials on the device
-#ifndef SW_CP_MODE_DEFAULT
-#define SW_CP_MODE_DEFAULT 0
-#endif
-  int compact_kernel = SW_CP_MODE_DEFAULT;  // SW_OPT_COMPACT_KERNEL (0: from the last launch's ids per tile)
+  int compact_kernel = 0;  // SW_OPT_COMPACT_KERNEL (0: from the last launch's ids per tile)
   int64_t cp_prev_tiles = 0;          // tiles of the previous launch (its id count: h_ddfull[1])
   unsigned long long* d_pcount = nullptr;
   uint64_t* d_llist = nullptr;        // k_classify's long chunks (EncArgs::llist) and their count
@@ -355,6 +352,40 @@ int32_t ensure_workspace(sw_encoder* h, int64_t n_bytes) {
 // Two-choice cuckoo table (see table.h).  Narrow buckets hold 2 slots, wide buckets 1; the
 // bucket count starts at the load factor below and doubles (with fresh hash multipliers) until
 // every pair is placed.
+// the quotient table (table.h) for 16-bit ids: buckets = the smallest power of two >= 2^16 with at
+// most SW_Q16_FILL keys per bucket on average; constants redrawn (eight tries per size, then the
+// buckets double) until no bucket holds more than four keys
+bool build_q16(const std::unordered_map<uint64_t, int32_t>& dict, const std::vector<uint64_t>& order, DevTable* t,
+               std::vector<uint4>* out) {
+  uint32_t log2b = 16;
+  while ((double)(1ull << log2b) * 0.25 < (double)order.size()) ++log2b;
+  uint64_t rng = 0x452821E638D01377ULL;
+  auto next = [&]() { rng ^= rng << 13; rng ^= rng >> 7; rng ^= rng << 17; return rng; };
+  for (int attempt = 0; attempt < 64 && log2b <= 24; ++attempt) {
+    if (attempt && attempt % 8 == 0) ++log2b;
+    const size_t nb = (size_t)1 << log2b;
+    t->shift = 32 - log2b;
+    t->m1 = (uint32_t)next() | 1u;
+    t->m2 = (uint32_t)next() | 1u;
+    std::vector<uint32_t> w(nb * 4, 0xFFFFFFFFu);
+    std::vector<uint8_t> fill(nb, 0);
+    bool ok = true;
+    for (uint64_t k : order) {
+      const uint32_t a = (uint32_t)(k >> 32), c = (uint32_t)k, v = (uint32_t)dict.at(k);
+      const uint32_t x = q16_mix((a << 16) | c, t->m1, t->m2);
+      const uint32_t bk = x >> t->shift;
+      if (fill[bk] == 4) { ok = false; break; }
+      w[4 * (size_t)bk + fill[bk]++] = (x & 0xFFFFu) | (v << 16);
+    }
+    if (!ok) continue;
+    out->assign(nb, make_uint4(0, 0, 0, 0));
+    std::memcpy(out->data(), w.data(), w.size() * sizeof(uint32_t));
+    t->q16 = 1;
+    return true;
+  }
+  return false;
+}
+
 bool build_cuckoo(const std::unordered_map<uint64_t, int32_t>& dict, const std::vector<uint64_t>& order, bool wide,
                   DevTable* t, std::vector<uint4>* out) {
   const int slots = wide ? 1 : 2;
@@ -485,7 +516,8 @@ extern "C" int32_t sw_encoder_create(const int32_t* pairs, const int32_t* vals, 
   h->table.wide = wide ? 1u : 0u;
   h->ids16 = ids16 && !wide;
   std::vector<uint4> host;
-  if (!build_cuckoo(dict, order, wide, &h->table, &host)) {
+  h->table.q16 = 0;
+  if (!(ids16 && !wide && build_q16(dict, order, &h->table, &host)) && !build_cuckoo(dict, order, wide, &h->table, &host)) {
     delete h;
     return fail(SW_ERR_ALLOC, "sw_encoder_create: could not build the pair table");
   }
@@ -836,10 +868,8 @@ struct DevSpecials {
 // further attempts on this handle) instead of leaving the handle half-built.
 int32_t grow_dedupe(sw_encoder* h) {
   const unsigned long long over = h->h_ddfull ? __atomic_load_n(h->h_ddfull, __ATOMIC_ACQUIRE) : 0ULL;
-#ifndef SW_DD_GROW_DIV
-#define SW_DD_GROW_DIV 32  // (grow when more than slots / this many chunks found no entry)
-#endif
-  if (!h->d_dtab || h->dedupe_slots || h->dd_grow_stop || over <= (unsigned long long)h->dd_slots / SW_DD_GROW_DIV ||
+  constexpr int64_t kGrowDiv = 32;  // (grow when more than slots / this many chunks found no entry)
+  if (!h->d_dtab || h->dedupe_slots || h->dd_grow_stop || over <= (unsigned long long)(h->dd_slots / kGrowDiv) ||
       h->dd_slots >= kDdSlotsMax)
     return SW_OK;  // (SW_OPT_DEDUPE_SLOTS caps the table on purpose: no growth)
   int64_t slots = h->dd_slots;
@@ -1110,10 +1140,11 @@ int32_t encode_device(sw_encoder* h, const uint8_t* d_bytes, int64_t n_bytes, co
     // the memset leaves the table's lines in the caches, and the probes then hit -- clearing only
     // the claims made k_split_classify 2% slower on C2, r4n/r4o A/B)
     const size_t dtab_bytes = sizeof(uint64_t) * kDdWords * ((size_t)a.dmask + 1);
-#ifndef SW_EDGE_CLEAR
-#define SW_EDGE_CLEAR 1  // (k_edges' threads clear the table: +4 us of k_edges for a 9 us memset on C2, r8b)
-#endif
-    const bool clr_in_edges = SW_EDGE_CLEAR && fused && dtab_bytes % 16 == 0;
+    // (k_edges' threads clear the table -- +4 us of k_edges for a 9 us memset on C2, r8b -- when its
+    // grid covers the table in a few stores per thread; a small launch after the table has grown
+    // for a large one keeps the memset, which is not limited to k_edges' few blocks)
+    const int64_t edge_threads = (n_tiles + 1 + 255) / 256 * 256;
+    const bool clr_in_edges = fused && dtab_bytes % 16 == 0 && (int64_t)(dtab_bytes / 16) <= 16 * edge_threads;
     if (h->dedupe && !clr_in_edges) HIP_TRY(hipMemsetAsync(h->d_dtab, 0, dtab_bytes, st));
     hipEvent_t c1 = nullptr;  // (timing: the classification kernel alone -- k_split_classify or k_classify)
     if (h->timing) {
@@ -1198,10 +1229,7 @@ int32_t encode_device(sw_encoder* h, const uint8_t* d_bytes, int64_t n_bytes, co
     HIP_TRY(long_part(1));
     HIP_TRY(launch_scan(st, h->d_bcnt, kNumBuckets * n_tiles, h->d_part, h->d_boff, h->d_qtotal));
     hipLaunchKernelGGL(k_scatter, dim3((unsigned)((n_tiles + 15) / 16)), dim3(kThreads), 0, st, a);  // (4 tiles a wave)
-#ifndef SW_MB_GRID
-#define SW_MB_GRID 2048
-#endif
-    const dim3 pg(SW_MB_GRID), pb(kThreads);  // persistent grid for the queue kernels
+    const dim3 pg(2048), pb(kThreads);  // persistent grid for the queue kernels
     if (h->merge_fork) {
       HIP_TRY(hipEventRecord(h->ev_fork, st));
       for (int k = 0; k < 2; ++k) HIP_TRY(hipStreamWaitEvent(h->s_fork[k], h->ev_fork, 0));
@@ -1470,10 +1498,11 @@ int32_t encode_batch_pipelined(sw_encoder* h, const uint8_t* bytes, const int64_
   const int64_t max_w = (max_b + 63) / 64 + 1;
   for (int slot = 0; slot < h->pipe_depth; ++slot) {
     auto& p = h->pipe[slot];
-    if (sp.n > 0 && p.cap_sp < max_sp) {
+    if (sp.n > 0 && (p.cap_sp < max_sp || (!sp.dev && !p.h_sp))) {
       (void)hipHostFree(p.h_sp); (void)hipFree(p.d_sp);
       p.h_sp = nullptr; p.d_sp = nullptr; p.cap_sp = 0;
-      HIP_TRY(hipHostMalloc(&p.h_sp, 3 * sizeof(int64_t) * max_sp, hipHostMallocDefault));
+      // (pinned staging only for occurrences found on the host: the device finder writes d_sp itself)
+      if (!sp.dev) HIP_TRY(hipHostMalloc(&p.h_sp, 3 * sizeof(int64_t) * max_sp, hipHostMallocDefault));
       HIP_TRY(hipMalloc(&p.d_sp, 3 * sizeof(int64_t) * max_sp));
       p.cap_sp = max_sp;
     }
@@ -1593,7 +1622,7 @@ int32_t encode_batch_pipelined(sw_encoder* h, const uint8_t* bytes, const int64_
       HIP_TRY(hipMemcpyAsync(p.d_in, p.h_in, (size_t)nb, hipMemcpyHostToDevice, h->s_h2d));
       HIP_TRY(hipMemcpyAsync(p.d_off, p.h_off, sizeof(int64_t) * (ns + 1), hipMemcpyHostToDevice, h->s_h2d));
       if (chunk_bits) HIP_TRY(hipMemcpyAsync(p.d_bits, p.h_bits, (size_t)n_bits, hipMemcpyHostToDevice, h->s_h2d));
-      if (m_sp > 0) HIP_TRY(hipMemcpyAsync(p.d_sp, p.h_sp, (size_t)n_sp_bytes, hipMemcpyHostToDevice, h->s_h2d));
+      if (n_sp_bytes > 0) HIP_TRY(hipMemcpyAsync(p.d_sp, p.h_sp, (size_t)n_sp_bytes, hipMemcpyHostToDevice, h->s_h2d));
     }
     HIP_TRY(hipEventRecord(p.e_in, h->s_h2d));
     HIP_TRY(hipStreamWaitEvent(h->stream, p.e_in, 0));
@@ -1894,6 +1923,10 @@ extern "C" int32_t sw_encode_batch(sw_encoder* h, const uint8_t* bytes, const in
                            stats);
 }
 
+// device memory the device special-token finder may take for sw_encode_batch_ex (its worst-case
+// occurrence arrays of every pipeline slot and its per-tile lists); beyond it the host threads find them
+constexpr int64_t kSpDeviceBudget = 1LL << 30;
+
 extern "C" int32_t sw_encode_batch_ex(sw_encoder* h, const uint8_t* bytes, const int64_t* str_off, int64_t n_str,
                                       int32_t pattern, const uint64_t* chunk_bits, const sw_specials* specials,
                                       int32_t* out_ids, int64_t out_cap, int64_t* out_off, sw_stats* stats) {
@@ -1912,7 +1945,13 @@ extern "C" int32_t sw_encode_batch_ex(sw_encoder* h, const uint8_t* bytes, const
     const int64_t nb = n_str > 0 ? str_off[n_str] - str_off[0] : 0;
     const int64_t run = h->pipe_run > 0 && nb > 2 * h->pipe_run ? std::min(h->pipe_run, h->max_launch)
                                                                    : std::min(nb, h->max_launch);
-    if (h->spt_dev && 16 * (run / h->spt_min_len + 1) <= (int64_t)1 << 31) {
+    // (the finder sizes its arrays for the worst case -- every run packed with the shortest special:
+    // 24 B per possible occurrence and slot, and each tile's list -- so short specials on large runs
+    // fall back to the host threads rather than take gigabytes of device memory)
+    const int64_t slots = h->pipe_run > 0 && nb > 2 * h->pipe_run ? h->pipe_depth : 1;
+    const int64_t worst = 24 * (run / h->spt_min_len + 1) * slots +
+                          4 * ((run + kTile - 1) / kTile) * (kTile / h->spt_min_len + 1);
+    if (h->spt_dev && worst <= kSpDeviceBudget && 16 * (run / h->spt_min_len + 1) <= (int64_t)1 << 31) {
       HostSpecials sp;
       sp.dev = true;
       sp.n = 1;

@@ -40,18 +40,8 @@ constexpr int kWaves = kThreads / 64;
 // indices in SGPRs.  k_split_classify: 80 VGPRs + 36 B of scratch -> 80 VGPRs, no scratch, 3.20 ->
 // 3.09 ms on C2, 6.14 -> 5.88 on ENTROPY (r6r A/B).  Rounds 4-5 measured it 180x slower with wrong
 // string offsets: a miscompiled 64-bit min (tile_end below), not the index.
-#ifndef SW_WAVE_SCALAR
-#define SW_WAVE_SCALAR 1
-#endif
-#ifndef SW_WAVE_SCALAR_ALL
-#define SW_WAVE_SCALAR_ALL 0  // (every kernel's wave index, not only k_split_classify's)
-#endif
 __device__ __forceinline__ int wave_in_block() {
-#if SW_WAVE_SCALAR_ALL
-  return __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-#else
   return (int)(threadIdx.x >> 6);
-#endif
 }
 // A tile's end, min(t0 + kTile, n_bytes), in 32 bits (a launch is < 2^30 bytes).  With the tile
 // index in SGPRs (wave_in_block_s), ROCm 7.2's compiler lowered the 64-bit signed min to a VALU
@@ -63,11 +53,7 @@ __device__ __forceinline__ int64_t tile_end(int64_t t0, int64_t n_bytes) {
   return (int64_t)min((int32_t)t0 + (int32_t)kTile, (int32_t)n_bytes);
 }
 __device__ __forceinline__ int wave_in_block_s() {
-#if SW_WAVE_SCALAR
   return __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-#else
-  return (int)(threadIdx.x >> 6);
-#endif
 }
 constexpr int kShort = 32;                   // per-lane merge loop up to this many bytes
 constexpr int kWin = kTile + 64;             // LDS byte window (tile + halo for key reads)
@@ -102,23 +88,13 @@ constexpr uint32_t kRlDense = 0x80000000u;
 constexpr uint32_t kCsPos = 0x7FFFu, kCsSpecial = 0x8000u;
 constexpr uint32_t kSpDone = 0xFFFFFFFEu;  // (table_lookups: the chunk's slot is written already)
 constexpr uint32_t kNoDid = 0x7FFFFFFu;    // (27-bit dense result field of a queue entry: none)
-#ifndef SW_DD_SLOTS_LOG2
-#define SW_DD_SLOTS_LOG2 22
-#endif
-constexpr int64_t kDdSlotsDefault = 1LL << SW_DD_SLOTS_LOG2;  // dedupe table entries at most to start with (32 MiB)
+constexpr int64_t kDdSlotsDefault = 1LL << 22;  // dedupe table entries at most to start with (32 MiB)
 constexpr int64_t kDdSlotsMax = 1LL << 26;      // ... and after growing (a queue entry's dense field: 27 bits)
 constexpr int kDdWords = 1;                     // 64-bit words per dedupe entry
 constexpr uint32_t kDdGroup = 8;                // entries per 64-byte line (a chunk's candidates)
 constexpr int kDdExactMax = 7;                  // dedupe keys of <= this many bytes are exact (no verification)
-#ifndef SW_DD_NT
-#define SW_DD_NT 0
-#endif
-#ifndef SW_PAIR_MAX_N
-#define SW_PAIR_MAX_N 16                   // k_merge_bucket<N>: two chunks per lane up to this N (0: never)
-#endif
-#ifndef SW_QUAD_MAX_N
-#define SW_QUAD_MAX_N 4                    // ... and four up to this N (0: never)
-#endif
+constexpr int kPairMaxN = 16;  // k_merge_bucket<N>: two chunks per lane up to this N
+constexpr int kQuadMaxN = 4;   // ... and four up to this N
 
 // streaming accesses (read or written once per launch) carry the non-temporal hint, so the
 // caches keep the randomly gathered merge results instead
@@ -156,6 +132,16 @@ __host__ __device__ inline int bucket_min_len(int b) {
 // candidate buckets), no loop: one memory round trip for every lane.
 template <bool kWide>
 __device__ __forceinline__ uint32_t lookup(const DevTable& t, uint32_t a, uint32_t b) {
+  if (!kWide && t.q16) {  // the quotient table (table.h): one 16-byte bucket, four tagged entries
+    const uint32_t x = q16_mix((a << 16) | b, t.m1, t.m2), tag = x & 0xFFFFu;
+    const uint4 q = ((const uint4*)t.buckets)[x >> t.shift];
+    uint32_t v = 0xFFFFu;
+    v = ((q.x & 0xFFFFu) == tag) ? (q.x >> 16) : v;
+    v = ((q.y & 0xFFFFu) == tag) ? (q.y >> 16) : v;
+    v = ((q.z & 0xFFFFu) == tag) ? (q.z >> 16) : v;
+    v = ((q.w & 0xFFFFu) == tag) ? (q.w >> 16) : v;
+    return (v == 0xFFFFu || (a | b) > 0xFFFFu) ? kInf : v;
+  }
   const uint32_t f = mix_key(a, b);
   const uint4* B = (const uint4*)t.buckets;
   const uint4 q1 = B[bucket1(f, t)];
@@ -302,16 +288,12 @@ __device__ inline int64_t next_set_bit(const uint64_t* bits, int64_t n_words, in
   return q < n_bits ? q : n_bits;
 }
 
-// Inclusive scan over the wave's 64 lanes (every lane active).  SW_DPP_SCAN: by DPP -- row shifts
-// 1, 2, 4, 8 within each 16-lane row, then row_bcast:15 (rows 1, 3) and row_bcast:31 (rows 2, 3),
-// six VALU operations; else six shuffles through the LDS crossbar (ds_bpermute), each a round trip.
+// Inclusive scan over the wave's 64 lanes (every lane active), by DPP: row shifts 1, 2, 4, 8 within
+// each 16-lane row, then row_bcast:15 (rows 1, 3) and row_bcast:31 (rows 2, 3) -- six VALU
+// operations instead of six shuffles through the LDS crossbar (ds_bpermute), each a round trip.
 // r7x A/B: C2 234.8 -> 238.5 GB/s (k_compact 0.94 -> 0.89 ms), C3 GPT-2 + specials 251 -> 264
 // (k_classify<true> 2.39 -> 2.24 ms).
-#ifndef SW_DPP_SCAN
-#define SW_DPP_SCAN 1
-#endif
 __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t x, int lane) {
-#if SW_DPP_SCAN
   (void)lane;  // (a lane whose source is outside its row, or masked off by row_mask, adds 0)
   x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xF, 0xF, false);  // row_shr:1
   x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xF, 0xF, false);  // row_shr:2
@@ -320,24 +302,12 @@ __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t x, int lane) {
   x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xA, 0xF, false);  // row_bcast:15
   x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xC, 0xF, false);  // row_bcast:31
   return x;
-#else
-#pragma unroll
-  for (int off = 1; off < 64; off <<= 1) {
-    const uint32_t y = __shfl_up(x, off, 64);
-    if (lane >= off) x += y;
-  }
-  return x;
-#endif
 }
 
-// lane L's value to every lane (L wave-uniform, every lane active): v_readlane under SW_DPP_SCAN
-// (an SGPR, no LDS crossbar round trip), else a shuffle
+// lane L's value to every lane (L wave-uniform, every lane active): v_readlane (an SGPR, no LDS
+// crossbar round trip)
 __device__ __forceinline__ uint32_t lane_value(uint32_t x, int L) {
-#if SW_DPP_SCAN
   return (uint32_t)__builtin_amdgcn_readlane((int)x, L);
-#else
-  return (uint32_t)__shfl((int)x, L, 64);
-#endif
 }
 __device__ __forceinline__ unsigned long long lane_value64(unsigned long long x, int L) {
   return (unsigned long long)lane_value((uint32_t)x, L) | ((unsigned long long)lane_value((uint32_t)(x >> 32), L) << 32);
@@ -345,13 +315,7 @@ __device__ __forceinline__ unsigned long long lane_value64(unsigned long long x,
 
 // the wave's sum in every lane (every lane active)
 __device__ __forceinline__ uint32_t wave_sum(uint32_t v, int lane) {
-#if SW_DPP_SCAN
   return lane_value(wave_incl_scan(v, lane), 63);
-#else
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) v += (uint32_t)__shfl_xor((int)v, off, 64);
-  return v;
-#endif
 }
 
 // exclusive block scan over kThreads threads (sh: kThreads/64 words); *total = block sum
@@ -559,9 +523,6 @@ __device__ __forceinline__ uint32_t lane_merge_reg_loop_wf(const DevTable& t, ui
 // the initial ranks of slots g .. g + 3 are in registers before any later slot's lookups issue
 // (lane_merge_lds_wf: the compiler otherwise hoisted all N lookups -- 8 registers each in
 // flight -- to the front: 239 VGPRs at N = 32, 132 with this)
-#ifndef SW_RANK_G8
-#define SW_RANK_G8 0  // the N = 8 merge bucket's initial ranks: all 7 lookups in flight (else 4 at a time)
-#endif
 template <int N, int G = 4>
 __device__ __forceinline__ void rank_group_done(uint32_t (&rk)[N], int g) {
   if constexpr (G == 8) {  // (groups of 8 lookups: lane_merge_lds_wfq, N = 8, 16)
@@ -695,7 +656,7 @@ __device__ __forceinline__ void lane_merge_lds_wfq(const DevTable& t, const uint
 #pragma unroll
     for (int k = 0; k < N; ++k) s_id[64 * (q * N + k) + lane] = (u[q][k >> 2] >> (8 * (k & 3))) & 0xFFu;
   // initial ranks: four lookups of each chunk in flight at a time
-  constexpr int G = ((N == 8 || N == 16) && SW_RANK_G8) ? 8 : 4;  // (lookups of a chunk in flight per group)
+  constexpr int G = 4;  // (lookups of a chunk in flight per group)
 #pragma unroll
   for (int g = 0; g < N; g += G) {
 #pragma unroll
@@ -1001,11 +962,7 @@ __device__ __forceinline__ DdOut dedupe_claim(const EncArgs& a, const SW_AS_GLOB
     unsigned long long* p = (unsigned long long*)a.dtab + (size_t)kDdWords * idx;
     // an entry changes once (0 -> final), so a cached plain load is safe: a stale 0 only sends
     // this lane to the CAS, which returns the live value
-#if SW_DD_NT  // (streaming hint: slower, r7r -- a frequent chunk's line serves its repeats from L2)
-    uint64_t cur = __builtin_nontemporal_load(p);
-#else
     uint64_t cur = *p;
-#endif
     if (cur == 0) {
       cur = atomicCAS(p, 0ULL, (unsigned long long)mine);
       if (cur == 0) return DdOut{1, idx};  // claimed: this chunk is merged and shared
@@ -1027,18 +984,9 @@ __device__ __forceinline__ DdOut dedupe_claim(const EncArgs& a, const SW_AS_GLOB
       const uint4* q16 = (const uint4*)words;
       const int64_t b0 = g >> 4;
       const int span = (int)(g & 15) + n;
-#if SW_DD_NT
-      const u32x4* v16 = (const u32x4*)q16;
-      const u32x4 y0 = SW_LDNT(v16 + b0);
-      const u32x4 y1 = span > 16 ? SW_LDNT(v16 + b0 + 1) : u32x4{0u, 0u, 0u, 0u};
-      const u32x4 y2 = span > 32 ? SW_LDNT(v16 + b0 + 2) : u32x4{0u, 0u, 0u, 0u};
-      const uint4 x0 = make_uint4(y0[0], y0[1], y0[2], y0[3]), x1 = make_uint4(y1[0], y1[1], y1[2], y1[3]),
-                  x2 = make_uint4(y2[0], y2[1], y2[2], y2[3]);
-#else
       const uint4 x0 = q16[b0];
       const uint4 x1 = span > 16 ? q16[b0 + 1] : make_uint4(0, 0, 0, 0);
       const uint4 x2 = span > 32 ? q16[b0 + 2] : make_uint4(0, 0, 0, 0);
-#endif
       const uint32_t W[12] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w, x2.x, x2.y, x2.z, x2.w};
       const int k = (int)(w0 & 3);
       uint32_t R[kShort / 4 + 1];
@@ -1081,10 +1029,7 @@ static_assert(kTile <= 0x10000, "chunk starts are uint16");
 // ---------------------------------------------------------------------------------------
 // two rounds of table probes in flight per wave: 5.52 -> 5.46 ms per C2 launch (one round or
 // three: 5.55 / 5.75 ms; four cap the kernel at 5 waves per SIMD)
-#ifndef SW_LOOK_ROUNDS
-#define SW_LOOK_ROUNDS 2
-#endif
-constexpr int kLookRounds = SW_LOOK_ROUNDS;
+constexpr int kLookRounds = 2;
 constexpr int kQBuf = 64 * (kLookRounds + 1);        // dedupe buffer: one batch + a group of rounds
 constexpr int kWinWords = kWin / 4 + 8;
 
@@ -1095,14 +1040,7 @@ constexpr int kWinWords = kWin / 4 + 8;
 // 0.95 ms (profiles/r2_k.md).
 // Round 5: the chunk-start list capped at kClsCsCap (a tile with more goes to k_classify_big),
 // so a block fits 7 per CU: 7 waves per SIMD (as k_split_classify, split_classify.h kScCsCap).
-#ifndef SW_CLS_CSCAP
-#define SW_CLS_CSCAP 1456
-#endif
-constexpr int kClsCsCap = SW_CLS_CSCAP;
-#ifndef SW_CLS_WAVES
-#define SW_CLS_WAVES 7
-#endif
-#define SW_CLS_ATTR __attribute__((amdgpu_waves_per_eu(SW_CLS_WAVES, SW_CLS_WAVES)))
+constexpr int kClsCsCap = 1456;
 // (a last chunk that runs more than kShort bytes past its tile, end unknown to the tile: long,
 // its length found from the complete bitmap by k_lp_prep)
 constexpr int kRelEndLong = 1 << 30;
@@ -1367,15 +1305,8 @@ __device__ __forceinline__ void classify_chunks(const EncArgs& a, int64_t tile, 
   // 6. strings starting in this tile: chunk (= slot) index within the tile (k_compact converts)
   //    (the first one read here, not held in a register through the tile: with a scalar tile index
   //    this is a scalar load)
-#ifndef SW_LATE_SFIRST
-#define SW_LATE_SFIRST 1
-#endif
-#if SW_LATE_SFIRST
   (void)s_first;
   const int64_t s_first_now = a.tile_slo[tile];
-#else
-  const int64_t s_first_now = s_first;
-#endif
   for (int64_t s = s_first_now + lane; s < a.n_str; s += 64) {
     const int64_t p = a.str_off[s];
     if (p >= t1) break;
@@ -1393,7 +1324,7 @@ __device__ __forceinline__ void classify_chunks(const EncArgs& a, int64_t tile, 
 
 // one wave per tile
 template <bool kSp>
-__global__ void __launch_bounds__(kThreads) SW_CLS_ATTR k_classify(EncArgs a, unsigned int* ov_count, int64_t* ov_tiles) {
+__global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(7, 7))) k_classify(EncArgs a, unsigned int* ov_count, int64_t* ov_tiles) {
   __shared__ __attribute__((aligned(16))) uint32_t s_b32_all[kWaves][kWinWords];  // window bytes (+ zero tail)
   __shared__ uint16_t s_cs_all[kWaves][kClsCsCap + 1];  // chunk starts (tile-relative), up to kClsCsCap
   __shared__ uint16_t s_qb_all[kWaves][kQBuf];       // chunks not settled by a lookup, to dedupe
@@ -1633,7 +1564,7 @@ __global__ void __launch_bounds__(kThreads) k_merge_bucket(EncArgs a, int b_lo, 
   const int64_t last_word = (mis + a.n_bytes - 1) >> 2;  // last word holding input bytes
   constexpr bool kLds = kWF && k16 && !kWide;
   // two or four chunks per lane (lane_merge_lds_wfq) for the short buckets of well-formed 16-bit tables
-  constexpr int kPer = !kLds ? 1 : N <= SW_QUAD_MAX_N ? 4 : N <= SW_PAIR_MAX_N ? 2 : 1;
+  constexpr int kPer = !kLds ? 1 : N <= kQuadMaxN ? 4 : N <= kPairMaxN ? 2 : 1;
   __shared__ uint32_t s_ids[kLds ? kWaves * 64 * N * kPer : 1];  // (lane_merge_lds_wf: the waves' ids)
   uint32_t* s_id = s_ids + (kLds ? wave_in_block() * 64 * N * kPer : 0);
   if constexpr (kPer > 1) {  // batches of 64 kPer entries per wave: entries base + 64 q + lane
@@ -2291,10 +2222,7 @@ __device__ __forceinline__ uint4 ref_head(const EncArgs& a, int32_t v) {
   return make_uint4(x0, x1, x2, x3);
 }
 
-#ifndef SW_CP_ROUNDS
-#define SW_CP_ROUNDS 8
-#endif
-constexpr int kRoundsInFlight = SW_CP_ROUNDS;  // slot rounds whose loads (then gathers) issue together
+constexpr int kRoundsInFlight = 8;  // slot rounds whose loads (then gathers) issue together
 
 // id count of the result a reference-list entry names
 // (a dense result's count from the byte array: 4 MiB at most, so these random reads mostly hit
@@ -2310,9 +2238,6 @@ __device__ __forceinline__ uint32_t ref_count(const EncArgs& a, uint32_t r) {
 // then their counts: one dependent round trip serves kTcTiles tiles (a tile holds ~58
 // references on prose, so one wave per tile spent most of its life waiting)
 constexpr int kTcTiles = 2;  // (4: no faster, r4s)
-#ifndef SW_TC_BATCH
-#define SW_TC_BATCH 0  // k_tile_count: rounds of a long reference list in flight together (0: one)
-#endif
 __global__ void __launch_bounds__(kThreads) k_tile_count(EncArgs a) {
   const int64_t tb = (((int64_t)blockIdx.x * kWaves + wave_in_block())) * kTcTiles;
   const int lane = threadIdx.x & 63;
@@ -2331,20 +2256,8 @@ __global__ void __launch_bounds__(kThreads) k_tile_count(EncArgs a) {
 #pragma unroll
   for (int k = 0; k < kTcTiles; ++k) {
     const uint32_t* rl = a.rlist + min(tb + k, a.n_tiles - 1) * kTile;
-#if SW_TC_BATCH
-    for (int i0 = 64; i0 < nr[k]; i0 += 64 * SW_TC_BATCH) {  // (long lists: SW_TC_BATCH rounds in flight)
-      uint32_t e[SW_TC_BATCH], v[SW_TC_BATCH];
-#pragma unroll
-      for (int q = 0; q < SW_TC_BATCH; ++q) e[q] = i0 + 64 * q + lane < nr[k] ? SW_LDNT2(&rl[i0 + 64 * q + lane]) : 0u;
-#pragma unroll
-      for (int q = 0; q < SW_TC_BATCH; ++q) v[q] = i0 + 64 * q + lane < nr[k] ? ref_count(a, e[q]) : 0u;
-#pragma unroll
-      for (int q = 0; q < SW_TC_BATCH; ++q) c[k] += v[q];
-    }
-#else
     for (int i0 = 64; i0 < nr[k]; i0 += 64)  // (long lists: the rest a round at a time)
       if (i0 + lane < nr[k]) c[k] += ref_count(a, SW_LDNT2(&rl[i0 + lane]));
-#endif
   }
 #pragma unroll
   for (int k = 0; k < kTcTiles; ++k) {
@@ -2354,13 +2267,7 @@ __global__ void __launch_bounds__(kThreads) k_tile_count(EncArgs a) {
 }
 
 constexpr int kRefCap = 128;    // references per 8-round group gathered through LDS
-#ifndef SW_CP_OUTCAP
-#define SW_CP_OUTCAP 1024
-#endif
-#ifndef SW_CP_WAVES
-#define SW_CP_WAVES 0  // k_compact: waves per SIMD to fit (0: the compiler's choice)
-#endif
-constexpr int kOutCapW = SW_CP_OUTCAP;  // ids per group staged in LDS (the rest are stored directly)
+constexpr int kOutCapW = 1024;  // ids per group staged in LDS (the rest are stored directly)
 // k_compact7: the same at 7 waves per SIMD with 768 staged ids a group (70 VGPRs, 22.5 KB of LDS a
 // block), for launches whose tiles hold few ids (the host chooses from the last launch's ids per
 // tile): C2 0.855 -> 0.803 ms, C5 0.794 -> 0.749, but 11% slower on ENTROPY's 1293 ids a tile
@@ -2533,10 +2440,7 @@ __device__ __forceinline__ void compact_tile(const EncArgs& a, int64_t t, int64_
     wave_sync_mem();
     // the staged ids: one contiguous 256-byte store per 64 ids
     const uint32_t staged = min(carry - gbase, (uint32_t)kOutCap);
-#ifndef SW_CP_FLUSH16
-#define SW_CP_FLUSH16 1
-#endif
-    if constexpr (SW_CP_FLUSH16 && (kTyped || SW_CP_FLUSH16 == 2) && sizeof(OutT) == 4) {
+    if constexpr (kTyped && sizeof(OutT) == 4) {
       // (16-byte stores, four ids a lane, from the output's first 16-byte boundary on; the ids
       // before it one a lane)
       const uint32_t mis4 = (uint32_t)(((uintptr_t)(out + base + gbase) >> 2) & 3u);
@@ -2579,9 +2483,6 @@ __device__ __forceinline__ void compact_tile(const EncArgs& a, int64_t t, int64_
 
 template <typename OutT>
 __global__ void __launch_bounds__(kThreads)
-#if SW_CP_WAVES
-__attribute__((amdgpu_waves_per_eu(SW_CP_WAVES, SW_CP_WAVES)))
-#endif
 k_compact(EncArgs a, const int64_t* tile_base, OutT* out) {
   __shared__ uint32_t s_rp_all[kWaves][kRefCap];
   __shared__ uint4 s_rq_all[kWaves][kRefCap];

@@ -152,24 +152,6 @@ SW_HD inline Masks classify(const Bytes& by, uint64_t ss, const Cls& cls, bool c
   // ASCII classes of the chunk's bytes (words 1..8): a class byte per byte (ascii_class4), two
   // classes gathered per multiply
   uint32_t L = 0, N = 0, C = 0, P = 0, H = 0, A = 0;
-#ifndef SW_PSB_LUT
-#define SW_PSB_LUT 1
-#endif
-#if !SW_PSB_LUT
-#pragma unroll
-  for (int i = 1; i < 9; ++i) {
-    const uint32_t x = by.word(i), asc = ~x & kLane7, x7 = x & kLow7;
-    const int s = 4 * (i - 1);
-    const uint32_t ws = in7(x7, 9, 13) & asc, cr = (in7(x7, '\n', '\n') | in7(x7, '\r', '\r')) & asc;
-    L |= mm4(in7(x7 | 0x20202020u, 'a', 'z') & asc) << s;
-    N |= mm4(in7(x7, '0', '9') & asc) << s;
-    C |= mm4(cr) << s;
-    H |= mm4(ws & ~cr) << s;
-    P |= mm4(in7(x7, ' ', ' ') & asc) << s;
-    A |= mm4(in7(x7, '\'', '\'') & asc) << s;
-  }
-  if (false)
-#endif
 #pragma unroll
   for (int i = 1; i < 9; ++i) {
     const uint32_t t = ascii_class4(by.word(i));

@@ -17,9 +17,6 @@ __constant__ uint8_t c_ucd1[SW_UCD_STAGE1_SIZE] = SW_UCD_STAGE1_INIT;
 __constant__ uint8_t c_ucd2[SW_UCD_STAGE2_SIZE] = SW_UCD_STAGE2_INIT;
 
 __device__ inline int ucd_class(uint32_t cp) {
-#ifdef SW_PS_NOUCD  // (diagnostic timing builds only)
-  return (int)(cp & 1);
-#endif
   if (cp > 0x10FFFF) return kOther;
   const uint32_t blk = c_ucd1[cp >> 8];
   const uint32_t v = c_ucd2[blk * 64 + ((cp & 255) >> 2)];

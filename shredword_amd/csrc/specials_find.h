@@ -299,11 +299,8 @@ __device__ __forceinline__ bool sf_clean(const SfShared& m, const uint32_t* s, i
   return true;
 }
 
-#ifndef SW_SF_WAVES
-#define SW_SF_WAVES 7
-#endif
 template <bool kSwar>
-__global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(SW_SF_WAVES, SW_SF_WAVES)))
+__global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(7, 7)))
 k_sp_find(SpTab T, SpFind f) {
   extern __shared__ uint32_t s_sft[];  // T.img (T.img_words words)
   __shared__ SfShared s_all[kWaves];

@@ -108,16 +108,8 @@ __device__ __forceinline__ void sp_bits32(const SpArgs& sp, int64_t n_tiles, int
   *inner = in;
 }
 
-#ifndef SW_SC_GSRC_NOINLINE
-#define SW_SC_GSRC_NOINLINE 0
-#endif
-#if SW_SC_GSRC_NOINLINE
-#define SW_SC_GSRC_ATTR __noinline__
-#else
-#define SW_SC_GSRC_ATTR __forceinline__
-#endif
 struct GSrc;
-__device__ SW_SC_GSRC_ATTR psb::Masks gsrc_masks(const GSrc& s, int64_t c);
+__device__ __forceinline__ psb::Masks gsrc_masks(const GSrc& s, int64_t c);
 
 // psb::carries' view of the batch from global memory only (k_edges, and k_split_classify's walks
 // past its tile): every chunk classified from its 40 bytes
@@ -141,10 +133,7 @@ struct GSrc {
   }
 };
 
-// (SW_SC_GSRC_NOINLINE: out of line -- a whole classify per call site is otherwise inlined into
-// every walk of psb::carries, ~100 KB of code for the fused kernel -- at the price of the call's
-// register saves)
-__device__ SW_SC_GSRC_ATTR psb::Masks gsrc_masks(const GSrc& s, int64_t c) {
+__device__ __forceinline__ psb::Masks gsrc_masks(const GSrc& s, int64_t c) {
   psb::RegBytes by;
   pb_load40(s.g, 32 * c, by.w);
   const uint64_t ss = (uint64_t)s.ss_at(32 * c - 4) | ((uint64_t)(s.ss_at(32 * c + 28) & 0xFFu) << 32);
@@ -213,15 +202,7 @@ __device__ __forceinline__ void ss_win5(const PbArgs& g, int64_t n_tiles, int64_
 // chunk c and its final chunk-start word (zeros past the batch).  edge[k * (n_tiles + 1) + b].
 // With clr (SW_EDGE_CLEAR) its threads also clear the dedupe table (n16 16-byte words) in place of
 // the memset before it (profiles/r5_ab.txt r8a-r8b).
-#ifndef SW_EDGE_WAVES
-#define SW_EDGE_WAVES 0  // (waves per SIMD to fit; 0: the compiler's choice)
-#endif
-#if SW_EDGE_WAVES
-#define SW_EDGE_ATTR __attribute__((amdgpu_waves_per_eu(SW_EDGE_WAVES, SW_EDGE_WAVES)))
-#else
-#define SW_EDGE_ATTR
-#endif
-__global__ void __launch_bounds__(256) SW_EDGE_ATTR k_edges(PbArgs g, int64_t n_tiles, int pattern, uint32_t* edge,
+__global__ void __launch_bounds__(256) k_edges(PbArgs g, int64_t n_tiles, int pattern, uint32_t* edge,
                                                unsigned int* redo_count, uint4* clr, int64_t n16) {
   const int64_t b = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (b == 0) *redo_count = 0;  // (k_split_classify's redo list, empty)
@@ -309,13 +290,7 @@ using ScShared = ScSharedT<kTile + 2>;
 // The chunk starts k_split_classify's LDS holds: with fewer than a tile's 2048 (+ 2), the union is
 // no larger than the masks and a block of 4 waves fits 7 blocks per CU instead of 6; a tile with
 // more chunks is listed for k_split_redo, which holds them all.
-#ifndef SW_BITS_NT
-#define SW_BITS_NT 0
-#endif
-#ifndef SW_SC_CSCAP
-#define SW_SC_CSCAP 1456  // (r7h A/B: C2 k_split_classify 2.97 -> 2.91 ms, ENTROPY 5.76 -> 5.43, 7 waves per SIMD)
-#endif
-constexpr int kScCsCap = SW_SC_CSCAP;
+constexpr int kScCsCap = 1456;  // (r7h A/B: C2 k_split_classify 2.97 -> 2.91 ms, ENTROPY 5.76 -> 5.43, 7 waves per SIMD)
 
 // psb::carries' view inside k_split_classify: the tile's masks from LDS, the rest from global memory
 struct FSrc {
@@ -402,20 +377,8 @@ __device__ __forceinline__ void split_classify_tile(const EncArgs& a, const PbAr
   const int64_t wb = t0 - kScPre;
   uint32_t rw[10];
   static_assert(kScPre == 32 && kWin == kTile + 64, "block layout of the window");
-#ifndef SW_SC_REGBYTES
-#define SW_SC_REGBYTES 1
-#endif
-  const bool fast = SW_SC_REGBYTES && ((uintptr_t)a.bytes & 15) == 0 && wb >= 0 && wb + kScPre + kWin <= a.n_bytes;
-  if (!SW_SC_REGBYTES && ((uintptr_t)a.bytes & 15) == 0 && wb >= 0 && wb + kScPre + kWin <= a.n_bytes) {
-#pragma unroll
-    for (int q = 0; q < ((kScPre + kWin) / 16 + 63) / 64; ++q) {
-      const int i = lane + 64 * q;
-      if (i < (kScPre + kWin) / 16) {
-        const u32x4 x = SW_LDNT((const u32x4*)(a.bytes + wb + 16 * (int64_t)i));
-        *(uint4*)(s_win + 4 * i) = make_uint4(x[0], x[1], x[2], x[3]);
-      }
-    }
-  } else if (fast) {
+  const bool fast = ((uintptr_t)a.bytes & 15) == 0 && wb >= 0 && wb + kScPre + kWin <= a.n_bytes;
+  if (fast) {
     const u32x4* src = (const u32x4*)(a.bytes + wb);
     const u32x4 x0 = SW_LDNT(src + 2 + 2 * lane), x1 = SW_LDNT(src + 3 + 2 * lane);
     // the other six blocks: lane 0 block 1 (its word before the chunk), lane 63 block 130 (its word
@@ -430,13 +393,8 @@ __device__ __forceinline__ void split_classify_tile(const EncArgs& a, const PbAr
     rw[1] = x0[0]; rw[2] = x0[1]; rw[3] = x0[2]; rw[4] = x0[3];
     rw[5] = x1[0]; rw[6] = x1[1]; rw[7] = x1[2]; rw[8] = x1[3];
     // the word before the chunk: lane - 1's last; the word after it: lane + 1's first
-#if SW_DPP_SCAN  // (DPP wave rotations by one lane: VALU, no LDS crossbar round trip)
     const uint32_t up = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)rw[8], 0x13C, 0xF, 0xF, false);  // wave_ror:1
     const uint32_t dn = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)rw[1], 0x134, 0xF, 0xF, false);  // wave_rol:1
-#else
-    const uint32_t up = (uint32_t)__shfl((int)rw[8], (lane + 63) & 63, 64);
-    const uint32_t dn = (uint32_t)__shfl((int)rw[1], (lane + 1) & 63, 64);
-#endif
     rw[0] = lane == 0 ? xe[3] : up;
     rw[9] = lane == 63 ? xe[0] : dn;
   } else {
@@ -572,11 +530,7 @@ __device__ __forceinline__ void split_classify_tile(const EncArgs& a, const PbAr
     }
   }
   if (c < n_chunks) {
-#if SW_BITS_NT  // (the bitmap streams out: later passes read little of it)
-    SW_STNT(&bits32[c], r);
-#else
     bits32[c] = r;
-#endif
     if (c == n_chunks - 1 && (c & 1) == 0) bits32[c + 1] = 0;  // (the last word's upper half)
   }
   SW_STAMP(14);
@@ -590,11 +544,8 @@ __device__ __forceinline__ void split_classify_tile(const EncArgs& a, const PbAr
     classify_chunks<kSp>(a, tile, s_win + kScPre / 4, sh->cstart, s_qbuf, r, rel_end, s_first, -1, -1);
 }
 
-#ifndef SW_SC_WAVES
-#define SW_SC_WAVES 7
-#endif
 template <bool kSp>
-__global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(SW_SC_WAVES, SW_SC_WAVES)))
+__global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(7, 7)))
 k_split_classify(EncArgs a, PbArgs g, int pattern, const uint32_t* edge, uint32_t* bits32, RedoList redo) {
   __shared__ __attribute__((aligned(16))) uint32_t s_win_all[kWaves][kScWinWords];
   __shared__ ScSharedT<kScCsCap> s_sh_all[kWaves];

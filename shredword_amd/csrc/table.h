@@ -10,6 +10,16 @@
 //   wide   (any member > 0xFFFF):         bucket = 1 slot  {a, b, value, 0}
 // Empty slots hold key / a = 0xFFFFFFFF (never a valid key: ids are non-negative int32 and the
 // narrow key (0xFFFF, 0xFFFF) forces the wide layout).
+//
+// Round 6, tables whose every id is <= 0xFFFD (SW_INFO_IDS16: the 32k / 50k vocabularies): a
+// QUOTIENT table, one 16-byte bucket per lookup instead of two.  The 32-bit key a << 16 | b goes
+// through a bijective mix x (two odd multiplies and xor-shifts, constants drawn per build); the
+// bucket is x's top bits (at least 16 of them) and each of its four 4-byte entries holds x's low
+// 16 bits as the tag and the value: bucket and tag together are x, hence the key -- the lookup is
+// exact with no key stored.  The builder redraws the constants (and doubles the buckets) until no
+// bucket holds more than four keys, so every lookup is one load and no lane ever needs a second
+// probe.  Empty entries are 0xFFFFFFFF (value 0xFFFF: no pair, as values are <= 0xFFFD).  At 32k
+// merges: 2^17 buckets, 2 MB (L2-resident), half the L2 requests of the two-bucket lookup.
 #pragma once
 #include <cstdint>
 
@@ -23,7 +33,17 @@ struct DevTable {
   uint32_t shift;       // 32 - log2(n_buckets)
   uint32_t m1, m2;      // odd multipliers of the two hash functions
   uint32_t wide;
+  uint32_t q16;         // the quotient layout (16-bit ids; m1, m2: the mix constants)
 };
+
+// the quotient table's bijective 32-bit mix (m1, m2 odd): invertible, so bucket + tag identify the key
+__host__ __device__ inline uint32_t q16_mix(uint32_t k, uint32_t m1, uint32_t m2) {
+  uint32_t x = k * m1;
+  x ^= x >> 16;
+  x *= m2;
+  x ^= x >> 15;
+  return x;
+}
 
 __host__ __device__ inline uint32_t mix_key(uint32_t a, uint32_t b) {
   // 32-bit fingerprint of the pair used by both bucket choices

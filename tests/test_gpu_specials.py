@@ -264,3 +264,36 @@ def test_dense_specials_device_path(per_kib):
         np.testing.assert_array_equal(g_off.cpu().numpy(), e_off)
         np.testing.assert_array_equal(g_ids.cpu().numpy(), e_ids)
         t.close()
+
+
+def test_short_special_budget_fallback_and_ex_struct_checks():
+    """A one-byte special: its worst case (an occurrence at every byte) on a 40 MB batch is over the
+    device finder's memory budget, so sw_encode_batch_ex finds the occurrences on the host threads;
+    on a small batch the device finds them -- the oracle's ids either way.  sw_encode_device_ex
+    refuses a struct of another size and an unknown per-call pattern."""
+    import torch
+    sp = {"\n": 100300, "<|endoftext|>": 100257}
+    t = tok_for("bl32k.model")
+    t.special_tokens = sp
+    for n_str, mean in ((200, 300), (60000, 700)):
+        buf, off = corpus.synth(33, corpus.MIXED, n_str, mean, n_threads=8)
+        ids, got_off = t.encode_packed(buf, off, specials=sp)
+        e_ids, e_off = expected(t, buf, off, sp, "cl100k")
+        np.testing.assert_array_equal(got_off, e_off)
+        np.testing.assert_array_equal(ids, e_ids)
+    L, h = _lib.lib(), t._encoder()
+    dev = torch.device("cuda", 0)
+    d_buf = torch.from_numpy(buf[:4096].copy()).to(dev)
+    d_off = torch.tensor([0, 4096], dtype=torch.int64, device=dev)
+    d_out = torch.empty(4096, dtype=torch.int32, device=dev)
+    d_oo = torch.empty(2, dtype=torch.int64, device=dev)
+    for bad in ("size", "pattern"):
+        ex = _lib.SwEncodeEx()
+        if bad == "size":
+            ex.struct_size = 0
+        else:
+            ex.flags, ex.pattern = _lib.SW_EX_PATTERN, 7
+        rc = L.sw_encode_device_ex(h, d_buf.data_ptr(), 4096, d_off.data_ptr(), 1, ctypes.byref(ex), d_out.data_ptr(),
+                                   d_oo.data_ptr(), None, None)
+        assert rc == _lib.SW_ERR_ARG, bad
+    t.close()

@@ -80,6 +80,8 @@ def parse():
     ap.add_argument("--dedupe-slots", type=int, default=0, help="A/B only: cap the dedupe table (power of two)")
     ap.add_argument("--no-dedupe-exact", action="store_true", help="A/B only: fingerprint keys for every chunk")
     ap.add_argument("--no-merge-streams", action="store_true", help="A/B only: merge kernels one after another")
+    ap.add_argument("--staged-heads", type=int, default=0, choices=[0, 1, 2],
+                    help="A/B only: result heads staged by k_tile_count (0 automatic, 1 always, 2 never)")
     ap.add_argument("--no-fused", action="store_true",
                     help="A/B only: the device pre-split as its own kernel before k_classify (same results)")
     ap.add_argument("--pipe-dma", action="store_true", help="A/B only: e2e pipeline copies by DMA, not kernels")
@@ -187,6 +189,8 @@ def main():
         _lib.check(L.sw_encoder_set_option(h, _lib.SW_OPT_DEDUPE_EXACT, 0))
     if args.no_merge_streams:
         _lib.check(L.sw_encoder_set_option(h, _lib.SW_OPT_MERGE_STREAMS, 0))
+    if args.staged_heads:
+        _lib.check(L.sw_encoder_set_option(h, _lib.SW_OPT_STAGED_HEADS, args.staged_heads))
     if args.no_fused:
         _lib.check(L.sw_encoder_set_option(h, _lib.SW_OPT_FUSED_PRESPLIT, 0))
     if args.pipe_dma:

@@ -35,6 +35,7 @@ SW_OPT_MERGE_STREAMS = 13
 SW_OPT_FUSED_PRESPLIT = 14
 SW_OPT_TEST_FAIL_GROWTH = 17
 SW_OPT_COMPACT_KERNEL = 19
+SW_OPT_STAGED_HEADS = 20
 SW_OPT_OUT_BITS = 16  # (removed: set_option rejects it; 16-bit output is sw_encode_ex.out_bits, per call)
 SW_INFO_MERGES, SW_INFO_CHUNK_ENTRIES, SW_INFO_WIDE_TABLE, SW_INFO_IDS16, SW_INFO_SPLIT, SW_INFO_DEDUPE_SLOTS = 1, 2, 3, 4, 5, 6
 SW_INFO_CHUNK_TABLE_BYTES = 7

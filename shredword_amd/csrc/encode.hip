@@ -173,7 +173,8 @@ struct sw_encoder {
   unsigned int* d_redo = nullptr;     // k_split_classify's tiles for k_split_redo: count, then the list (int64)
   bool fused_presplit = true;         // SW_OPT_FUSED_PRESPLIT: the device pre-split inside k_split_classify
   bool device_specials = true;        // SW_OPT_DEVICE_SPECIALS: sw_encode_batch_ex finds specials on the device
-  int compact_kernel = 0;  // SW_OPT_COMPACT_KERNEL (0: from the last launch's ids per tile)
+  int compact_kernel = 0;
+  int staged_heads = 0;               // SW_OPT_STAGED_HEADS: 0 automatic (a grown dedupe table), 1 always, 2 never  // SW_OPT_COMPACT_KERNEL (0: from the last launch's ids per tile)
   int64_t cp_prev_tiles = 0;          // tiles of the previous launch (its id count: h_ddfull[1])
   unsigned long long* d_pcount = nullptr;
   uint64_t* d_llist = nullptr;        // k_classify's long chunks (EncArgs::llist) and their count
@@ -688,6 +689,10 @@ extern "C" int32_t sw_encoder_set_option(sw_encoder* h, int32_t option, int64_t 
     case SW_OPT_FUSED_PRESPLIT: h->fused_presplit = value != 0; return SW_OK;
     case SW_OPT_TEST_FAIL_GROWTH: h->test_fail_grow = value ? 1 : 0; h->dd_grow_stop = false; return SW_OK;
     case SW_OPT_DEVICE_SPECIALS: h->device_specials = value != 0; return SW_OK;
+    case SW_OPT_STAGED_HEADS:
+      if (value < 0 || value > 2) return fail(SW_ERR_ARG, "staged heads: 0 (automatic), 1 (always) or 2 (never)");
+      h->staged_heads = (int)value;
+      return SW_OK;
     case SW_OPT_COMPACT_KERNEL:
       if (value < 0 || value > 3) return fail(SW_ERR_ARG, "SW_OPT_COMPACT_KERNEL: 0 .. 3");
       h->compact_kernel = (int)value;
@@ -1135,6 +1140,9 @@ int32_t encode_device(sw_encoder* h, const uint8_t* d_bytes, int64_t n_bytes, co
     a.inv = h->d_inv; a.n_inv = h->n_inv; a.ids16 = h->ids16 ? 1u : 0u;
     a.lstart = h->lp.wstart; a.llen = h->lp.wlen; a.n_long = &h->lp.ctl[kLcWave]; a.lcap = h->lp.lcap;
     a.sp = spa;
+    // the result heads staged by k_tile_count when the dedupe table has grown past the caches (its
+    // heads, 16 B an entry, are random HBM reads that k_compact would otherwise make a second time)
+    a.staged_heads = (h->staged_heads == 1 || (h->staged_heads == 0 && h->dedupe && h->dd_slots > kDdSlotsDefault)) ? 1u : 0u;
     const bool split = h->split_ok && h->long_split;  // (split + verify needs a well-formed table)
     // (cleared per launch rather than entry by entry by the merge kernels that empty the claims:
     // the memset leaves the table's lines in the caches, and the probes then hit -- clearing only
@@ -1264,8 +1272,11 @@ int32_t encode_device(sw_encoder* h, const uint8_t* d_bytes, int64_t n_bytes, co
     }
     HIP_TRY(hipGetLastError());
     const dim3 wg((unsigned)((n_tiles + 3) / 4));  // one wave per tile
-    hipLaunchKernelGGL(k_tile_count, dim3((unsigned)((n_tiles + kWaves * kTcTiles - 1) / (kWaves * kTcTiles))),
-                       dim3(kThreads), 0, st, a);
+    if (a.staged_heads)
+      hipLaunchKernelGGL(k_tile_count_staged, dim3((unsigned)((n_tiles + kWaves - 1) / kWaves)), dim3(kThreads), 0, st, a);
+    else
+      hipLaunchKernelGGL(k_tile_count, dim3((unsigned)((n_tiles + kWaves * kTcTiles - 1) / (kWaves * kTcTiles))),
+                         dim3(kThreads), 0, st, a);
     HIP_TRY(launch_scan(st, h->d_tile_cnt, n_tiles, h->d_part, h->d_tile_base, h->d_total));
     // the compaction kernel from the last launch's ids per tile (read without waiting: a heuristic)
     int ck = h->compact_kernel;

@@ -891,6 +891,8 @@ struct EncArgs {
   uint32_t* big_list;        // long chunks over kLongLds bytes (their index in the long list)
   uint32_t* big_count;       // ... how many (cleared per launch)
   uint32_t ids16;            // every id fits 16 bits (dres layout)
+  uint32_t staged_heads;     // k_tile_count_staged wrote each tile's first kStageCap result heads into its rlist
+                             // range (k_compact reads them there, in order, instead of gathering them)
   SpArgs sp;                 // special-token occurrences (sp.n == 0: none)
 };
 
@@ -2266,6 +2268,52 @@ __global__ void __launch_bounds__(kThreads) k_tile_count(EncArgs a) {
   }
 }
 
+// k_tile_count_staged (launches whose dedupe table has grown past the caches: the low-repetition
+// corpora, where every reference's 16-byte head is a random HBM read): the tile's ids per tile as
+// k_tile_count, but from the heads themselves -- gathered once here, in the tile's reference order,
+// and written over the tile's own reference list (2048 words: room for kStageCap heads), so that
+// k_compact reads them back as one coalesced run instead of gathering them a second time.  One wave
+// per tile; every list entry is read before the first head is written over the list.
+constexpr int kStageCap = kTile / 4;  // heads staged per tile (the list's 2048 words)
+constexpr int kStageRounds = kStageCap / 64;
+__global__ void __launch_bounds__(kThreads) k_tile_count_staged(EncArgs a) {
+  const int64_t t = (int64_t)blockIdx.x * kWaves + wave_in_block();
+  const int lane = threadIdx.x & 63;
+  if (t >= a.n_tiles) return;
+  uint32_t* rl = a.rlist + t * kTile;
+  const int C = (int)a.tile_slots[t], nr = (int)a.tile_nref[t];
+  const int ns = min(nr, kStageCap);
+  uint32_t e[kStageRounds];
+#pragma unroll
+  for (int j = 0; j < kStageRounds; ++j) e[j] = (64 * j < ns && 64 * j + lane < ns) ? SW_LDNT2(&rl[64 * j + lane]) : 0u;
+  uint32_t c = 0;
+  for (int i0 = kStageCap; i0 < nr; i0 += 64)  // (beyond the staged ones: counts only, read before any head is written)
+    if (i0 + lane < nr) c += ref_count(a, SW_LDNT2(&rl[i0 + lane]));
+  uint4 q[kStageRounds];
+#pragma unroll
+  for (int j = 0; j < kStageRounds; ++j) {
+    q[j] = make_uint4(0u, 0u, 0u, 0u);
+    if (64 * j < ns && 64 * j + lane < ns) {
+      const uint32_t r = e[j];
+      q[j] = ref_head(a, (r & kRlDense) ? slot_dref(r & ~kRlDense) : slot_ref((int64_t)r));
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < kStageRounds; ++j) {
+    if (64 * j < ns && 64 * j + lane < ns) {
+      const bool dense = (e[j] & kRlDense) != 0;
+      c += dense && a.ids16 ? (q[j].x & 0xFFFFu) : q[j].x;
+    }
+  }
+  wave_sync_mem();  // (every lane's reads of the list are done: its words are rewritten now)
+  uint4* hd = (uint4*)rl;
+#pragma unroll
+  for (int j = 0; j < kStageRounds; ++j)
+    if (64 * j < ns && 64 * j + lane < ns) hd[64 * j + lane] = q[j];
+  const uint32_t v = wave_sum(c, lane);
+  if (lane == 0) a.tile_cnt[t] = v + (uint32_t)(C - nr);
+}
+
 constexpr int kRefCap = 128;    // references per 8-round group gathered through LDS
 constexpr int kOutCapW = 1024;  // ids per group staged in LDS (the rest are stored directly)
 // k_compact7: the same at 7 waves per SIMD with 768 staged ids a group (70 VGPRs, 22.5 KB of LDS a
@@ -2322,6 +2370,7 @@ __device__ __forceinline__ void compact_tile(const EncArgs& a, int64_t t, int64_
   const int sj = has_s ? (int)s_cj : -1;
   const bool many = s_hi - s_lo > 64;  // rare: slot offsets go through scratch instead
   uint32_t s_off = 0, carry = 0;
+  int refs_before = 0;  // (wave-uniform) references of the groups before this one
 #ifdef SW_STAMPS
   if (sj == -12345) s_off = 1;  // (forces the string loads to land here in stamp builds)
   SW_STAMP(8);
@@ -2346,8 +2395,17 @@ __device__ __forceinline__ void compact_tile(const EncArgs& a, int64_t t, int64_
       static_assert(kRefCap == 128, "two gathers per lane");
       const int nr = min(nref, kRefCap);
       uint4 q0 = make_uint4(0, 0, 0, 0), q1 = make_uint4(0, 0, 0, 0);
-      if (lane < nr) q0 = ref_head(a, (int32_t)s_rp[lane]);
-      if (lane + 64 < nr) q1 = ref_head(a, (int32_t)s_rp[lane + 64]);
+      // (staged: the group's references are the tile's refs_before + 0 .. nr - 1, in order)
+      const SW_AS_GLOBAL u32x4* sth = gptr((const u32x4*)(a.rlist + t * kTile)) + refs_before;
+      auto st4 = [&](int i) { const u32x4 x = sth[i]; return make_uint4(x[0], x[1], x[2], x[3]); };
+      if (lane < nr) {
+        if (a.staged_heads && refs_before + lane < kStageCap) q0 = st4(lane);
+        else q0 = ref_head(a, (int32_t)s_rp[lane]);
+      }
+      if (lane + 64 < nr) {
+        if (a.staged_heads && refs_before + lane + 64 < kStageCap) q1 = st4(lane + 64);
+        else q1 = ref_head(a, (int32_t)s_rp[lane + 64]);
+      }
       if (lane < nr) s_rq[lane] = u32x4{q0.x, q0.y, q0.z, q0.w};
       if (lane + 64 < nr) s_rq[lane + 64] = u32x4{q1.x, q1.y, q1.z, q1.w};
     }
@@ -2362,17 +2420,26 @@ __device__ __forceinline__ void compact_tile(const EncArgs& a, int64_t t, int64_
       const bool valid = j < C;
       const bool ref = valid && v[u] < 0;
       uint4 q = make_uint4(0, 0, 0, 0);
+      // (a group's references past kRefCap: gathered here -- from the staged heads when there are)
+      const bool staged = a.staged_heads && refs_before + (int)ridx[u] < kStageCap;
       if constexpr (kTyped) {
         if (ref) {
           if (ridx[u] < (uint32_t)kRefCap) {
             const u32x4 x = s_rq[ridx[u]];
+            q = make_uint4(x[0], x[1], x[2], x[3]);
+          } else if (staged) {
+            const u32x4 x = gptr((const u32x4*)(a.rlist + t * kTile))[refs_before + ridx[u]];
             q = make_uint4(x[0], x[1], x[2], x[3]);
           } else {
             q = ref_head(a, v[u]);
           }
         }
       } else {
-        if (ref) q = ridx[u] < (uint32_t)kRefCap ? s_rq_g[ridx[u]] : ref_head(a, v[u]);
+        if (ref) {
+          if (ridx[u] < (uint32_t)kRefCap) q = s_rq_g[ridx[u]];
+          else if (staged) q = ((const uint4*)(a.rlist + t * kTile))[refs_before + ridx[u]];
+          else q = ref_head(a, v[u]);
+        }
       }
       const bool dense = ref && slot_is_dref(v[u]);
       const bool d16 = dense && a.ids16 != 0;
@@ -2457,6 +2524,7 @@ __device__ __forceinline__ void compact_tile(const EncArgs& a, int64_t t, int64_
     } else {
       for (uint32_t i = lane; i < staged; i += 64) SW_STNT(&dst[gbase + i], (OutT)s_out[i]);
     }
+    refs_before += nref;
     wave_sync_mem();  // (s_rp / s_rq / s_out are rewritten by the next group)
 #ifdef SW_STAMPS
     __builtin_amdgcn_s_waitcnt(0);

@@ -33,3 +33,6 @@
 //                        tile; 1: 6 waves per SIMD, 1024 ids staged; 2: 7 waves, 768 staged; 3: as 2 with
 //                        typed LDS / global accesses
 #define SW_OPT_COMPACT_KERNEL 19
+// SW_OPT_STAGED_HEADS    0 (default): k_tile_count stages the result heads for k_compact when the dedupe table
+//                        has grown (low-repetition text); 1: always; 2: never
+#define SW_OPT_STAGED_HEADS 20

@@ -129,6 +129,31 @@ def test_compaction_kernel_choice(kernel):
         t.close()
 
 
+@pytest.mark.parametrize("mode", [1, 2])
+@pytest.mark.parametrize("model", ["bl32k.model", "toy500.model", "wide"])
+def test_staged_result_heads(mode, model):
+    """SW_OPT_STAGED_HEADS: k_tile_count gathering each tile's result heads once and staging them over
+    its reference list for k_compact (1: forced) against the gathers in k_compact (2) -- dense and
+    own references, tiles over the staging's 512 heads (a one-byte-string batch of multi-token
+    chunks), 16- and 32-bit heads (a table with ids over 16 bits), each == the oracle."""
+    t = sa.Tokenizer(device=0)
+    base = load_model_merges("bl32k.model" if model == "wide" else model)
+    t.merges = ({(a if a < 256 else a + 70000, b if b < 256 else b + 70000): v + 70000 for (a, b), v in base.items()}
+                if model == "wide" else base)
+    t.pattern = ""
+    try:
+        L = _lib.lib()
+        assert L.sw_encoder_set_option(t._encoder(), _lib.SW_OPT_STAGED_HEADS, 3) != 0
+        _lib.check(L.sw_encoder_set_option(t._encoder(), _lib.SW_OPT_STAGED_HEADS, mode))
+        rng = random.Random(12)
+        many = pack([bytes(rng.choice(b"abcdefgh") for _ in range(rng.randrange(2, 5))) for _ in range(40000)])
+        for buf, off in (corpus.synth(5, corpus.MIXED, 20000, 300), corpus.synth(6, corpus.ENTROPY, 8000, 500),
+                         many, corpus.synth(7, corpus.STRESS, 3000, 600)):
+            assert_same(gpu_encode(t, buf, off), oracle_encode(t.merges, buf, off, "cl100k"))
+    finally:
+        t.close()
+
+
 def test_tokenizer_encode_decode_surface():
     t = tok_for("bl32k.model")
     text = "Hello world's 12345 \n\n  x 中文 😀"

@@ -273,6 +273,8 @@ void free_pipe(sw_encoder* h) {
   }
 }
 
+constexpr unsigned long long kStagedMinMerges = 6000000;  // (see encode_device: k_tile_count_staged)
+
 int32_t ensure_workspace(sw_encoder* h, int64_t n_bytes) {
   if (n_bytes <= h->cap_bytes) return SW_OK;
   free_workspace(h);
@@ -571,10 +573,11 @@ extern "C" int32_t sw_encoder_create(const int32_t* pairs, const int32_t* vals, 
   }
   e = hipEventCreateWithFlags(&h->ws_done, hipEventDisableTiming);
   if (e == hipSuccess)  // (the dedupe overflow count of the last launch, written by the device)
-    e = hipHostMalloc((void**)&h->h_ddfull, 2 * sizeof(unsigned long long), hipHostMallocMapped | hipHostMallocCoherent);
+    e = hipHostMalloc((void**)&h->h_ddfull, 3 * sizeof(unsigned long long), hipHostMallocMapped | hipHostMallocCoherent);
   if (e == hipSuccess) {
     h->h_ddfull[0] = 0;  // (and [1]: the last launch's id count)
     h->h_ddfull[1] = 0;
+    h->h_ddfull[2] = 0;  // (and [2]: its merge loops)
     e = hipHostGetDevicePointer((void**)&h->hd_ddfull, h->h_ddfull, 0);
   }
   if (e != hipSuccess) {
@@ -1142,7 +1145,12 @@ int32_t encode_device(sw_encoder* h, const uint8_t* d_bytes, int64_t n_bytes, co
     a.sp = spa;
     // the result heads staged by k_tile_count when the dedupe table has grown past the caches (its
     // heads, 16 B an entry, are random HBM reads that k_compact would otherwise make a second time)
-    a.staged_heads = (h->staged_heads == 1 || (h->staged_heads == 0 && h->dedupe && h->dd_slots > kDdSlotsDefault)) ? 1u : 0u;
+    // (automatic: the previous launch ran more than kStagedMinMerges merge loops, i.e. its distinct
+    // results' heads spread over more 64-byte lines than the 256 MB Infinity Cache holds -- ENTROPY's
+    // 15.6 M per GiB; a GPT-2 pre-split with specials runs 3 M and keeps them cached, and C2 0.75 M.
+    // Read without waiting, like the compaction kernel's choice: results are identical either way)
+    const unsigned long long prev_merges = h->h_ddfull ? __atomic_load_n(&h->h_ddfull[2], __ATOMIC_RELAXED) : 0ULL;
+    a.staged_heads = (h->staged_heads == 1 || (h->staged_heads == 0 && h->dedupe && prev_merges > kStagedMinMerges)) ? 1u : 0u;
     const bool split = h->split_ok && h->long_split;  // (split + verify needs a well-formed table)
     // (cleared per launch rather than entry by entry by the merge kernels that empty the claims:
     // the memset leaves the table's lines in the caches, and the probes then hit -- clearing only
@@ -1301,7 +1309,7 @@ int32_t encode_device(sw_encoder* h, const uint8_t* d_bytes, int64_t n_bytes, co
     HIP_TRY(hipMemsetAsync(h->d_total, 0, sizeof(int64_t), st));
   }
   hipLaunchKernelGGL(k_string_offsets, dim3((unsigned)((n_str + 1 + 255) / 256)), dim3(256), 0, st, d_str_off, n_str,
-                     n_bytes, h->d_total, d_out_off, h->d_ddfull, h->hd_ddfull);
+                     n_bytes, h->d_total, d_out_off, h->d_ddfull, h->hd_ddfull, n_tiles > 0 ? h->d_qtotal : nullptr);
   HIP_TRY(hipGetLastError());
   if (h->timing) {
     HIP_TRY(hipEventRecord(e1, st));

@@ -2577,7 +2577,8 @@ k_compact7(EncArgs a, const int64_t* tile_base, OutT* out) {
 // past n_bytes (trailing empty strings) and the end sentinel get the total
 // (and the launch's dedupe overflow count to host memory, zeroed for the next launch)
 __global__ void k_string_offsets(const int64_t* str_off, int64_t n_str, int64_t n_bytes, const int64_t* total,
-                                 int64_t* out_off, unsigned long long* dd_full, unsigned long long* h_dd_full) {
+                                 int64_t* out_off, unsigned long long* dd_full, unsigned long long* h_dd_full,
+                                 const int64_t* q_total) {
   const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (s == 0 && dd_full) {
     const unsigned long long v = *dd_full;
@@ -2585,6 +2586,10 @@ __global__ void k_string_offsets(const int64_t* str_off, int64_t n_str, int64_t 
     __hip_atomic_store(h_dd_full, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     // (and the launch's id count: the next launch picks its k_compact from the ids per tile)
     __hip_atomic_store(h_dd_full + 1, (unsigned long long)*total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    // (and its merge loops run -- the distinct queued chunks: the next launch stages the result heads
+    // when they are too many for the caches)
+    __hip_atomic_store(h_dd_full + 2, q_total ? (unsigned long long)*q_total : 0ULL, __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_SYSTEM);
   }
   if (s > n_str) return;
   if (s == n_str || str_off[s] >= n_bytes) {

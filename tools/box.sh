@@ -76,6 +76,16 @@ for s in "$@"; do
                   > "$O/fetch_${nm}_$g.log" 2>&1)
                rc=$?; echo "fetch_${nm}_$g rc=$rc" >> "$O/status.txt"; [ $rc -eq 0 ] || exit $rc
              done ;;
+    diag=*) v=${s#diag=}; extra=""; [ "$v" != "" ] && extra=${v//+/ }  # (latency / TLB / TA diagnostics of a bench config)
+            i=0
+            for grp in "SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAIT_INST_ANY SQ_WAVE_CYCLES SQ_INST_CYCLES_VMEM_RD SQ_WAIT_ANY SQ_INSTS_VMEM_RD SQ_BUSY_CYCLES" \
+                       "TCP_TCC_READ_REQ_LATENCY_sum TCP_TCC_READ_REQ_sum TCP_UTCL1_TRANSLATION_MISS_sum TCP_UTCL1_REQUEST_sum" \
+                       "TA_BUSY_avr TA_ADDR_STALLED_BY_TC_CYCLES_sum"; do
+              i=$((i+1))
+              (cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --pmc $grp -d "$O/diag$i" -o run --output-format csv \
+                 -- python3 "$R/bench.py" --steps 2 --warmup 1 "${NB[@]}" $extra > "$O/diag$i.log" 2>&1)
+              rc=$?; echo "diag$i rc=$rc" >> "$O/status.txt"; [ $rc -eq 0 ] || exit $rc
+            done ;;
     *) echo "unknown step $s" >> "$O/status.txt"; exit 2 ;;
   esac
 done

@@ -10,7 +10,9 @@ import sys
 root = sys.argv[1]
 want = sys.argv[2] if len(sys.argv) > 2 else ""
 runs = collections.defaultdict(dict)
-for f in sorted(glob.glob(os.path.join(root, "fetch_*", "**", "*counter_collection.csv"), recursive=True)):
+files = glob.glob(os.path.join(root, "fetch_*", "**", "*counter_collection.csv"), recursive=True)
+files += glob.glob(os.path.join(root, "diag*", "**", "*counter_collection.csv"), recursive=True)
+for f in sorted(files):
     name = os.path.relpath(f, root).split(os.sep)[0]
     var, grp = name.rsplit("_", 2)[0], name
     per = collections.defaultdict(float)
@@ -22,9 +24,16 @@ for f in sorted(glob.glob(os.path.join(root, "fetch_*", "**", "*counter_collecti
     for (d, c), v in per.items():
         acc[(kn[d], c)].append(v)
     for (k, c), vs in acc.items():
-        runs[name.split("_so_")[0]][(k, c)] = sum(vs) / len(vs)
+        runs[name.split("_so_")[0] if name.startswith("fetch_") else "diag"][(k, c)] = sum(vs) / len(vs)
 for var, d in runs.items():
     print("==", var)
+    if var == "diag":
+        for k in sorted({k for k, _ in d if want in k}):
+            print("  %s" % k[:60])
+            for (kk, c), v in sorted(d.items()):
+                if kk == k:
+                    print("     %-40s %.4g" % (c, v))
+        continue
     ks = sorted({k for k, _ in d if want in k})
     for k in ks:
         fb, wb = d.get((k, "FETCH_SIZE")), d.get((k, "WRITE_SIZE"))

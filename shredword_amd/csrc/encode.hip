@@ -964,19 +964,30 @@ int32_t set_specials(sw_encoder* h, const sw_specials* sp) {
   // the LDS image of k_sp_find (specials_find.h, above sft_len), when the finder takes the table
   std::vector<uint32_t> img;
   if (few && max_len <= kSpMaxLen) {
+    const int32_t n_list = first[256];
     t.o_first = (int32_t)n;
-    t.o_list = t.o_first + 129;
-    t.o_words = t.o_list + (int32_t)((n + 3) / 4);
+    t.o_rec = (t.o_first + 129 + 3) & ~3;  // (16-byte aligned records)
+    t.o_tag = t.o_rec + kSfRecWords * n_list;
+    t.o_words = t.o_tag + n_list;
     img.assign((size_t)t.o_words, 0u);
     for (int b = 0; b <= 256; ++b) img[(size_t)t.o_first + b / 2] |= (uint32_t)first[(size_t)b] << (16 * (b & 1));
-    for (size_t g = 0; g < (size_t)first[256]; ++g)
-      img[(size_t)t.o_list + g / 4] |= (uint32_t)list[g] << (8 * (g & 3));
+    std::vector<uint32_t> wo_of((size_t)n, 0u);
     for (int64_t k = 0; k < n; ++k) {
       const int32_t L = off[(size_t)k + 1] - off[(size_t)k];
       const size_t wo = img.size() - (size_t)t.o_words;
+      wo_of[(size_t)k] = (uint32_t)wo;
       img[(size_t)k] = (uint32_t)wo | (uint32_t)L << 16;
       img.resize(img.size() + (size_t)(L + 3) / 4, 0u);
       std::memcpy(img.data() + t.o_words + wo, sp->bytes + sp->off[k], (size_t)L);
+    }
+    for (int32_t g = 0; g < n_list; ++g) {
+      const int32_t k = list[(size_t)g], L = off[(size_t)k + 1] - off[(size_t)k];
+      uint32_t* rec = img.data() + t.o_rec + kSfRecWords * g;
+      for (int32_t j = 0; j < std::min<int32_t>(L, 16); ++j) {
+        rec[j / 4] |= (uint32_t)sp->bytes[sp->off[k] + j] << (8 * (j % 4));
+        rec[4 + j / 4] |= 0xFFu << (8 * (j % 4));
+      }
+      img[(size_t)t.o_tag + g] = (uint32_t)k | (uint32_t)L << 8 | wo_of[(size_t)k] << 16;
     }
     img.push_back(0u);  // (k_sp_find reads a special's second word even for one of <= 4 bytes)
     t.img_words = (int32_t)img.size();

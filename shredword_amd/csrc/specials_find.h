@@ -46,7 +46,7 @@ struct SpTab {
   int32_t max_len;
   int32_t n;
   const uint32_t* img;   // the table as k_sp_find stages it in LDS (layout above sft_len)
-  int32_t img_words, o_first, o_list, o_words;
+  int32_t img_words, o_first, o_rec, o_tag, o_words;
 };
 
 struct SpFind {
@@ -241,6 +241,7 @@ constexpr int kSfPre = 128;                          // bytes staged before the 
 constexpr int kSfBytes = kSfPre + kTile + kSpMaxLen;  // the byte window [t0 - 128, t0 + 2048 + 64)
 constexpr int kSfCand = kSfPre + kTile;              // candidate positions [t0 - 128, t0 + 2048)
 constexpr int kSfCandWords = kSfCand / 32;
+static_assert(kSfCand == 64 * 34, "k_sp_find: 34 candidate positions a lane");
 constexpr int kSfSsWords = (kSfBytes + 32) / 32 + 1; // string-start bits of the window (+ its end)
 
 struct SfShared {
@@ -256,14 +257,15 @@ struct SfShared {
 // 32-bit words:
 //   [0, n)                special k: its first word in the byte area | its length << 16
 //   [o_first, + 129)      first byte b's group starts at list entry group[b] (16 bits each, 257)
-//   [o_list, ...)         the specials grouped by first byte, dict order within a group (8 bits each)
+//   [o_rec, + 8 x list)   per list entry (the specials grouped by first byte, dict order within a
+//                         group): the special's first 16 bytes zero padded, then their byte masks
+//                         (16-byte aligned: two ds_read_b128, no chain through an index)
+//   [o_tag, + list)       per list entry: special k | length << 8 | its first word in the byte area << 16
 //   [o_words, ...)        every special's bytes from a word boundary, zero padded
+constexpr int kSfRecWords = 8;
 __device__ __forceinline__ int sft_len(const uint32_t* s, int k) { return (int)(s[k] >> 16); }
 __device__ __forceinline__ int sft_group(const uint32_t* s, int o_first, int b) {
   return (int)((s[o_first + (b >> 1)] >> (16 * (b & 1))) & 0xFFFFu);
-}
-__device__ __forceinline__ int sft_list(const uint32_t* s, int o_list, int g) {
-  return (int)((s[o_list + (g >> 2)] >> (8 * (g & 3))) & 0xFFu);
 }
 // the window's bytes r .. r + 3 as one word
 __device__ __forceinline__ uint32_t sf_word(const SfShared& m, int r) {
@@ -271,14 +273,15 @@ __device__ __forceinline__ uint32_t sf_word(const SfShared& m, int r) {
   return __builtin_amdgcn_alignbyte(m.b[w + 1], m.b[w], (uint32_t)(r & 3));
 }
 
-// the first string start after window position r (the window's end when none is staged)
-__device__ __forceinline__ int sf_next_start(const SfShared& m, int r) {
-  for (int q = r + 1; q < kSfSsWords * 32;) {
-    const uint32_t w = m.ss[q >> 5] >> (q & 31);
-    if (w) return q + __builtin_ctz(w);
-    q = (q | 31) + 1;
-  }
-  return kSfSsWords * 32;
+// the first string start in (r, r + 64], r + 65 when there is none (a special of <= 64 bytes at r
+// fits its string when it ends at or before it): three independent LDS reads instead of a word by
+// word walk to the string's end, a chain of dependent reads as long as the string
+__device__ __forceinline__ int sf_end_after(const SfShared& m, int r) {
+  static_assert(kSpMaxLen <= 64 && kSfCand + 64 < 32 * (kSfSsWords - 1), "sf_end_after's three words");
+  const int q = r + 1, w = q >> 5, sh = q & 31;
+  const uint64_t lo = ((uint64_t)m.ss[w + 1] << 32) | m.ss[w];
+  const uint64_t bits = (lo >> sh) | (sh ? (uint64_t)m.ss[w + 2] << (64 - sh) : 0ULL);
+  return bits ? q + __builtin_ctzll(bits) : q + 64;
 }
 
 // the next candidate at or after q, below lim (lim when none)
@@ -302,7 +305,7 @@ __device__ __forceinline__ bool sf_clean(const SfShared& m, const uint32_t* s, i
 template <bool kSwar>
 __global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(7, 7)))
 k_sp_find(SpTab T, SpFind f) {
-  extern __shared__ uint32_t s_sft[];  // T.img (T.img_words words)
+  extern __shared__ __align__(16) uint32_t s_sft[];  // T.img (T.img_words words; its records 16-byte aligned)
   __shared__ SfShared s_all[kWaves];
   __shared__ uint32_t s_filt[8];
   const int lane = threadIdx.x & 63;
@@ -350,6 +353,7 @@ k_sp_find(SpTab T, SpFind f) {
   }
   if (lane < 4) m.b[kSfBytes / 4 + lane] = 0;
   for (int i = lane; i < kSfSsWords; i += 64) m.ss[i] = 0;
+  for (int i = lane; i < kSfCandWords; i += 64) m.cb[i] = 0;
   m.chosen[lane] = 0;
   m.seen[lane] = 0;
   wave_sync_mem();
@@ -361,55 +365,78 @@ k_sp_find(SpTab T, SpFind f) {
     r0 = i0 + lane <= f.n_str ? f.str_off[i0 + lane] - wb : span;
   }
   wave_sync_mem();
-  // 2. candidates of [t0 - 128, t0 + 2048), 32 positions a lane: the first byte by SWAR compares
-  //    (or the first-byte set), the rest word by word against the LDS table, first match in dict order
-  for (int g = lane; g < kSfCandWords; g += 64) {
-    uint32_t mk = 0;
+  // 2. candidates of [t0 - 128, t0 + 2048), 34 positions a lane (2176 = 64 x 34: one pass, where
+  //    32 a lane took a second pass for the last four words), found by their first byte (SWAR
+  //    compares, or the first-byte set) and matched word by word against the LDS table, the first
+  //    match in dict order.  The first-byte hits are kept transposed (bit 8 j + k: byte j of word k)
+  //    so that each word's four zero-byte flags go in by one shift; their order does not matter.
+  {
+    const int P = 34 * lane, w0 = P >> 2;
+    const uint32_t sh = (uint32_t)(P & 3);
+    uint32_t d[10], w[9];
+#pragma unroll
+    for (int k = 0; k < 10; ++k) d[k] = m.b[w0 + k];
+#pragma unroll
+    for (int k = 0; k < 9; ++k) w[k] = __builtin_amdgcn_alignbyte(d[k + 1], d[k], sh);
+    uint32_t mlo = 0, mhi = 0;  // positions P + 4 k + j (k < 8) at bit 8 j + k; P + 32, P + 33 at bits 0, 1
     if (kSwar) {
-      const uint4 q0 = *(const uint4*)(m.b + 8 * g), q1 = *(const uint4*)(m.b + 8 * g + 4);
-      const uint32_t w[8] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w};
       for (int j = 0; j < T.n_first; ++j) {
         const uint32_t fb = ((T.fb >> (8 * j)) & 0xFFu) * 0x01010101u;
 #pragma unroll
-        for (int i = 0; i < 8; ++i) mk |= mm4_hi(zero_bytes(w[i] ^ fb)) << (4 * i);
+        for (int k = 0; k < 8; ++k) mlo |= zero_bytes(w[k] ^ fb) >> (7 - k);
+        const uint32_t z = zero_bytes(w[8] ^ fb);
+        mhi |= ((z >> 7) & 1u) | ((z >> 14) & 2u);
       }
     } else {
-#pragma unroll 4
-      for (int k = 0; k < 32; ++k) {
-        const uint32_t b = (m.b[8 * g + (k >> 2)] >> (8 * (k & 3))) & 0xFFu;
-        mk |= ((s_filt[b >> 5] >> (b & 31)) & 1u) << k;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const uint32_t b = (w[k] >> (8 * j)) & 0xFFu;
+          mlo |= ((s_filt[b >> 5] >> (b & 31)) & 1u) << (8 * j + k);
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const uint32_t b = (w[8] >> (8 * j)) & 0xFFu;
+        mhi |= ((s_filt[b >> 5] >> (b & 31)) & 1u) << j;
       }
     }
-    const int64_t p0 = wb + 32 * g;  // (positions outside the batch match nothing)
-    if (p0 < 0) mk &= p0 + 32 <= 0 ? 0u : ~0u << (-p0);
-    if (p0 + 32 > f.n_bytes) mk &= p0 >= f.n_bytes ? 0u : (1u << (f.n_bytes - p0)) - 1u;
-    uint32_t hit = 0;
-    int end = -1;
-    for (; mk; mk &= mk - 1) {
-      const int r = 32 * g + __builtin_ctz(mk);
-      if (r >= end) end = sf_next_start(m, r);
-      const int b = (int)(m.b[r >> 2] >> (8 * (r & 3))) & 0xFF;
+    uint64_t hit = 0;  // bit i: position P + i
+    for (uint64_t mk = ((uint64_t)mhi << 32) | mlo; mk; mk &= mk - 1) {
+      const int bt = __builtin_ctzll(mk), i = bt < 32 ? 4 * (bt & 7) + (bt >> 3) : bt;
+      const int r = P + i;
+      if (wb + r < 0 || wb + r >= f.n_bytes) continue;  // (positions outside the batch match nothing)
+      const int end = sf_end_after(m, r);
+      uint32_t x[4];  // (the first 16 bytes, once)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) x[q] = sf_word(m, r + 4 * q);
+      const int b = (int)(x[0] & 0xFFu);
       const int g1 = sft_group(s, T.o_first, b + 1);
-      const uint32_t x0 = sf_word(m, r), x1 = sf_word(m, r + 4);  // (the first 8 bytes, once)
       for (int gi = sft_group(s, T.o_first, b); gi < g1; ++gi) {
-        const int k = sft_list(s, T.o_list, gi);
-        const int L = sft_len(s, k), wo = T.o_words + (int)(s[k] & 0xFFFFu);
+        const uint4 w = *(const uint4*)(s + T.o_rec + kSfRecWords * gi);
+        const uint4 mk4 = *(const uint4*)(s + T.o_rec + kSfRecWords * gi + 4);
+        const uint32_t tag = s[T.o_tag + gi];
+        const int L = (int)((tag >> 8) & 0xFFu);
         if (r + L > end) continue;
-        const uint32_t m0 = L >= 4 ? ~0u : (1u << (8 * L)) - 1u;
-        const uint32_t m1 = L >= 8 ? ~0u : L <= 4 ? 0u : (1u << (8 * (L - 4))) - 1u;
-        bool same = ((x0 ^ s[wo]) & m0) == 0 && ((x1 ^ s[wo + 1]) & m1) == 0;  // (s[wo + 1]: padded)
-        for (int q = 8; q < L && same; q += 4) {
+        bool same = (((x[0] ^ w.x) & mk4.x) | ((x[1] ^ w.y) & mk4.y) | ((x[2] ^ w.z) & mk4.z) | ((x[3] ^ w.w) & mk4.w)) == 0;
+        const int wo = T.o_words + (int)(tag >> 16);
+        for (int q = 16; q < L && same; q += 4) {  // (past 16 bytes: word by word)
           const uint32_t msk = L - q >= 4 ? ~0u : (1u << (8 * (L - q))) - 1u;
           same = ((sf_word(m, r + q) ^ s[wo + (q >> 2)]) & msk) == 0;
         }
         if (same) {
-          m.ci[r] = (uint8_t)k;
-          hit |= 1u << (r & 31);
+          m.ci[r] = (uint8_t)(tag & 0xFFu);
+          hit |= 1ULL << i;
           break;
         }
       }
     }
-    m.cb[g] = hit;
+    if (hit) {  // (34 bits from bit P & 31 of word P >> 5: two words, shared with the neighbours)
+      const uint64_t h = hit << (P & 31);
+      atomicOr(&m.cb[P >> 5], (uint32_t)h);
+      if (h >> 32) atomicOr(&m.cb[(P >> 5) + 1], (uint32_t)(h >> 32));
+    }
   }
   wave_sync_mem();
   // 3. clean candidates of [t0 - 64, t0 + 2048) and their clusters' walks (decisions inside the tile)

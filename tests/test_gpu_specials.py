@@ -168,7 +168,7 @@ def _device_find(t, buf, off):
     return pos[:n].cpu().numpy(), ln[:n].cpu().numpy(), ids[:n].cpu().numpy()
 
 
-@pytest.mark.parametrize("case", range(8))
+@pytest.mark.parametrize("case", range(9))
 def test_device_finder_equals_host_finder(case):
     """sw_find_specials_device == sw_find_specials_host (itself == the plain restatement split_ref,
     tests/test_specials.py) on adversarial sets: specials that overlap themselves and each other
@@ -185,11 +185,15 @@ def test_device_finder_equals_host_finder(case):
         dict(SPECIALS),
         {"the": 340, " the": 341, "he": 342, "e ": 343},
         {"\n": 350, "\n\n": 351, " ": 352},
+        # one first byte, shared prefixes past the 16 bytes k_sp_find's records hold, dict order
+        # putting a longer special before its prefix and after it
+        {"<|im_start|>assistant": 360, "<|im_start|>": 361, "<|im_start|>assistant_long": 362,
+         "<|im_start|>user": 363, "<|im_end|>": 364, "<|im_start|>assistan": 365},
     ]
     sp = sets[case]
     t = tok_for("bl32k.model")
     t.special_tokens = sp
-    names = [k for k in sp if k] + ["a", "b", "|", "<", ">", " ", "\n", "word", "é", "th", "e"]
+    names = [k for k in sp if k] + ["a", "b", "|", "<", ">", " ", "\n", "word", "é", "th", "e", "assistant", "_long"]
     datas = []
     for k in range(400):
         n_parts = rng.choice([0, 1, 5, 40, 300, 1200])

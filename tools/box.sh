@@ -13,7 +13,7 @@
 #   prof_<cfg>         rocprofv3 kernel trace + one PMC pass per counter group (tools/profile_gpu.sh)
 #   ab=spec,spec,...   kernel-trace A/B of library variants / bench args (tools/gpu_ab_trace.sh)
 #   stamps=lib[:kind]  per-phase cycle stamps of an SW_STAMPS build (tools/phase_stamps.py)
-#   pmc=lib            one PMC pass of instruction counters over the C2 bench with library `lib`
+#   pmc=lib[@args]     one PMC pass of instruction counters over the C2 bench (or its args) with library `lib`
 set -u
 TAG=$1; shift
 R=${GRAFT_REPO_ROOT:-$(pwd)}
@@ -61,12 +61,13 @@ for s in "$@"; do
     stamps=*) v=${s#stamps=}; lib=${v%%:*}; kind=mixed; [ "$lib" != "$v" ] && kind=${v#*:}
               run "stamps_${lib%.so}_$kind" 200 env SHREDWORD_HIP_LIB="$R/shredword_amd/$lib" \
                 python3 tools/phase_stamps.py 250000 "$kind" fused ;;
-    pmc=*) lib=${s#pmc=}
+    pmc=*) v=${s#pmc=}; lib=${v%%@*}; extra=""; [ "$lib" != "$v" ] && extra=${v#*@} && extra=${extra//+/ }
+           nm=pmc_$(echo "${v%.so}" | tr -c 'A-Za-z0-9_\n' '_')
            (cd /tmp && export TMPDIR=/tmp && SHREDWORD_HIP_LIB="$R/shredword_amd/$lib" timeout -k 10 300 rocprofv3 --pmc \
               SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_SMEM SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_WAIT_INST_ANY SQ_WAVE_CYCLES \
-              -d "$O/pmc_${lib%.so}" -o run --output-format csv -- python3 "$R/bench.py" --steps 2 --warmup 1 "${NB[@]}" \
-              > "$O/pmc_${lib%.so}.log" 2>&1)
-           rc=$?; echo "pmc_${lib%.so} rc=$rc" >> "$O/status.txt"; [ $rc -eq 0 ] || exit $rc ;;
+              -d "$O/$nm" -o run --output-format csv -- python3 "$R/bench.py" --steps 2 --warmup 1 "${NB[@]}" $extra \
+              > "$O/$nm.log" 2>&1)
+           rc=$?; echo "$nm rc=$rc" >> "$O/status.txt"; [ $rc -eq 0 ] || exit $rc ;;
     fetch=*) v=${s#fetch=}; lib=${v%%@*}; extra=""; [ "$lib" != "$v" ] && extra=${v#*@} && extra=${extra//+/ }
              nm=$(echo "${v}" | tr -c 'A-Za-z0-9_\n' '_')
              for grp in FETCH_SIZE WRITE_SIZE "TCC_HIT_sum TCC_MISS_sum"; do

@@ -284,7 +284,7 @@ int32_t ensure_workspace(sw_encoder* h, int64_t n_bytes) {
   // (+ slack for k_compact's head reads; k_classify's tile-local queue, aliased here, takes whole tiles)
   HIP_TRY(hipMalloc(&h->d_res, sizeof(uint32_t) * std::max<int64_t>(2 * nb + 16, n_tiles * kTile)));
   HIP_TRY(hipMalloc(&h->d_tile_slo, sizeof(int64_t) * n_tiles));
-  HIP_TRY(hipMalloc(&h->d_tile_sp, sizeof(int64_t) * (n_tiles + 1)));
+  HIP_TRY(hipMalloc(&h->d_tile_sp, sizeof(int64_t) * 2 * (n_tiles + 1)));  // (tile_sp, then tile_spw)
   HIP_TRY(hipMalloc(&h->d_tile_slots, sizeof(uint32_t) * n_tiles));
   HIP_TRY(hipMalloc(&h->d_tile_nref, sizeof(uint32_t) * n_tiles));
   HIP_TRY(hipMalloc(&h->d_rlist, sizeof(uint32_t) * n_tiles * kTile));
@@ -1122,10 +1122,10 @@ int32_t encode_device(sw_encoder* h, const uint8_t* d_bytes, int64_t n_bytes, co
   if (n_tiles > 0)  // (the pre-split and k_classify start from each tile's first string)
     hipLaunchKernelGGL(k_tile_strings, dim3((unsigned)((n_tiles + 255) / 256)), dim3(256), 0, st, d_str_off, n_str,
                        n_tiles, h->d_tile_slo, h->d_lcount);  // (and the long list emptied)
-  const SpArgs spa{sp.pos, sp.len, sp.id, sp.n, h->d_tile_sp};
+  const SpArgs spa{sp.pos, sp.len, sp.id, sp.n, h->d_tile_sp, h->d_tile_sp + (n_tiles + 1)};
   if (n_tiles > 0 && sp.n > 0)  // (... and their first special-token occurrence; the count last)
-    hipLaunchKernelGGL(k_tile_specials, dim3((unsigned)((n_tiles + 1 + 255) / 256)), dim3(256), 0, st, sp.pos, sp.n,
-                       sp.n_dev, n_tiles, h->d_tile_sp);
+    hipLaunchKernelGGL(k_tile_specials, dim3((unsigned)((n_tiles + 1 + 255) / 256)), dim3(256), 0, st, sp.pos, sp.len,
+                       sp.n, sp.n_dev, n_tiles, h->d_tile_sp, h->d_tile_sp + (n_tiles + 1));
   // the full path (no caller bitmap): the device pre-split, fused into the classification
   // (k_edges + k_split_classify) or as its own kernel first (SW_OPT_FUSED_PRESPLIT 0; special
   // tokens always take the fused kernel)

@@ -843,6 +843,8 @@ struct SpArgs {
   const int32_t* id;
   int64_t n;                 // > 0: the launch has occurrences (at most n)
   const int64_t* tile_sp;    // [n_tiles + 1]
+  const int64_t* tile_spw;   // [n_tiles + 1] the first occurrence ending at or after tile t's first byte - 64
+                             // (the start of k_split_classify's and k_edges' windows; k_tile_specials)
 };
 
 struct EncArgs {
@@ -2000,17 +2002,25 @@ __global__ void k_tile_strings(const int64_t* str_off, int64_t n_str, int64_t n_
 
 // tile_sp[t], t in [0, n_tiles]: the first special-token occurrence starting at or after byte
 // t * kTile; the count is n, or *n_dev (the device finder's) when n_dev is given
-__global__ void k_tile_specials(const int64_t* pos, int64_t n, const int64_t* n_dev, int64_t n_tiles, int64_t* tile_sp) {
+__global__ void k_tile_specials(const int64_t* pos, const int32_t* len, int64_t n, const int64_t* n_dev, int64_t n_tiles,
+                                int64_t* tile_sp, int64_t* tile_spw) {
   const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (t > n_tiles) return;
   const int64_t cnt = n_dev ? min(max(*n_dev, (int64_t)0), n) : n;
-  const int64_t t0 = t * kTile;
-  int64_t lo = 0, hi = cnt;
-  while (lo < hi) {
-    const int64_t m = (lo + hi) >> 1;
-    if (pos[m] < t0) lo = m + 1; else hi = m;
+  const int64_t t0 = t * kTile, w0 = t0 - 64;
+  int64_t lo = 0, hi = cnt, lw = 0, hw = cnt;  // (the two searches side by side: starts, then ends)
+  while (lo < hi || lw < hw) {
+    if (lo < hi) {
+      const int64_t m = (lo + hi) >> 1;
+      if (pos[m] < t0) lo = m + 1; else hi = m;
+    }
+    if (lw < hw) {
+      const int64_t m = (lw + hw) >> 1;
+      if (pos[m] + len[m] < w0) lw = m + 1; else hw = m;  // (ends ascend: the occurrences do not overlap)
+    }
   }
   tile_sp[t] = lo;
+  tile_spw[t] = lw;
 }
 
 // ---------------------------------------------------------------------------------------

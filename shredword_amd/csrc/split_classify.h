@@ -72,31 +72,13 @@ __device__ __forceinline__ int64_t sp_first_end(const SpArgs& sp, int64_t n_tile
   return lo;
 }
 
-// the same for a whole wave (p, lo, hi uniform): the first index in [lo, hi) whose end is at or
-// after p (hi when none), 64 probes a step instead of one (one memory round trip for <= 64 entries)
-__device__ __forceinline__ int64_t sp_first_end_wave(const SpArgs& sp, int64_t lo, int64_t hi, int64_t p, int lane) {
-  while (hi - lo > 64) {
-    const int64_t step = (hi - lo + 63) >> 6;
-    const int64_t m = lo + lane * step;
-    const uint64_t b = __ballot(m < hi && sp.pos[m] + sp.len[m] >= p);
-    if (b) {  // (the answer is in (lo + (k - 1) step, lo + k step])
-      const int64_t k = __builtin_ctzll(b);
-      hi = lo + k * step;
-      if (k) lo += (k - 1) * step + 1;
-    } else {  // (every probe below hi ends before p: the answer is past the last of them)
-      lo += ((hi - 1 - lo) / step) * step + 1;
-    }
-  }
-  const int64_t m = lo + lane;
-  const uint64_t b = __ballot(m < hi && sp.pos[m] + sp.len[m] >= p);
-  return b ? lo + __builtin_ctzll(b) : hi;
-}
-
 // bits of [p, p + 32): the occurrences' starts and ends (*ss) and their inner bytes (*inner)
-__device__ __forceinline__ void sp_bits32(const SpArgs& sp, int64_t n_tiles, int64_t p, uint32_t* ss, uint32_t* inner) {
+// (j0: an index known to be at or before the first occurrence ending at or after p, or -1)
+__device__ __forceinline__ void sp_bits32(const SpArgs& sp, int64_t n_tiles, int64_t p, uint32_t* ss, uint32_t* inner,
+                                          int64_t j0 = -1) {
   uint32_t s = 0, in = 0;
   const int64_t n = sp.tile_sp[n_tiles];
-  for (int64_t j = sp_first_end(sp, n_tiles, p); j < n; ++j) {
+  for (int64_t j = j0 >= 0 ? j0 : sp_first_end(sp, n_tiles, p); j < n; ++j) {
     const int64_t a = sp.pos[j], e = a + sp.len[j];
     if (a >= p + 32) break;
     if (a >= p) s |= 1u << (a - p);
@@ -158,7 +140,7 @@ struct SsWin5 {
   }
 };
 
-__device__ __forceinline__ void ss_win5(const PbArgs& g, int64_t n_tiles, int64_t base, SsWin5* out) {
+__device__ __forceinline__ void ss_win5(const PbArgs& g, int64_t n_tiles, int64_t base, SsWin5* out, int64_t sp_j0 = -1) {
   out->base = base;
 #pragma unroll
   for (int k = 0; k < 5; ++k) out->w[k] = 0u;
@@ -189,7 +171,7 @@ __device__ __forceinline__ void ss_win5(const PbArgs& g, int64_t n_tiles, int64_
   }
   if (g.sp.n > 0) {
     const int64_t n = g.sp.tile_sp[n_tiles];
-    for (int64_t j = sp_first_end(g.sp, n_tiles, base); j < n; ++j) {
+    for (int64_t j = sp_j0 >= 0 ? sp_j0 : sp_first_end(g.sp, n_tiles, base); j < n; ++j) {
       const int64_t a = g.sp.pos[j];
       if (a >= end) break;
       set(a);
@@ -218,8 +200,10 @@ __global__ void __launch_bounds__(256) k_edges(PbArgs g, int64_t n_tiles, int pa
   psb::Masks m1{};
   uint32_t r = 0;
   if (c < n_chunks) {
+    // (the occurrences from k_tile_specials' index for this window's start, t0 - 64)
+    const int64_t spj = g.sp.n > 0 ? g.sp.tile_spw[b] : -1;
     SsWin5 sw;
-    ss_win5(g, n_tiles, 32 * c - 64, &sw);  // (chunks c - 1 .. c + 1 with their 4-byte margins)
+    ss_win5(g, n_tiles, 32 * c - 64, &sw, spj);  // (chunks c - 1 .. c + 1 with their 4-byte margins)
     if (pattern == 2) {  // (the chunks are the strings)
       r = sw.at(32 * c);
     } else {
@@ -244,7 +228,7 @@ __global__ void __launch_bounds__(256) k_edges(PbArgs g, int64_t n_tiles, int pa
     }
     if (g.sp.n > 0) {  // (an occurrence's inner bytes start no chunk)
       uint32_t s, in;
-      sp_bits32(g.sp, n_tiles, 32 * c, &s, &in);
+      sp_bits32(g.sp, n_tiles, 32 * c, &s, &in, spj);
       r &= ~in;
     }
     if (32 * c + 32 > g.n_bytes) r &= (1u << (g.n_bytes - 32 * c)) - 1u;
@@ -438,9 +422,10 @@ __device__ __forceinline__ void split_classify_tile(const EncArgs& a, const PbAr
     // (the first occurrence ending at or after w0, in tile - 1's range: see sp_first_end; the
     // indices are loaded here, not at the start: held through the class masks they cost 0.27 ms
     // with a vector tile index, r6q, and gave nothing with the scalar one, r7x)
-    const int64_t sp_prev = tile > 0 ? a.sp.tile_sp[tile - 1] : 0, sp_lo = a.sp.tile_sp[tile];
+    // (the first occurrence ending at or after w0 = t0 - 64 from k_tile_specials: one load beside the
+    // live count, where a 64-wide search of the tile's range took one to two more round trips)
     const int64_t nsp = a.sp.tile_sp[a.n_tiles];
-    const int64_t j_first = tile > 0 ? sp_first_end_wave(a.sp, max(sp_prev - 1, (int64_t)0), sp_lo, w0, lane) : 0;
+    const int64_t j_first = a.sp.tile_spw[tile];
     for (int64_t j0 = j_first; j0 < nsp; j0 += 64) {
       const int64_t j = j0 + lane;
       int64_t pa = w1, pe = w1;

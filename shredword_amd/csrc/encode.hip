@@ -588,11 +588,25 @@ extern "C" int32_t sw_encoder_create(const int32_t* pairs, const int32_t* vals, 
   return SW_OK;
 }
 
+// Every stream this encoder has work on, idle: its own (launch, copy-in, copy-out, merge forks) and
+// the caller's stream of its last device-entry launch (its ws_done event, recorded after that
+// launch's last kernel and after the finder's).  Before anything is freed or unpinned: round 4's
+// destroy freed first and synchronised only the launch stream.  Other encoders and
+// the caller's unrelated work are not waited for.
+static hipError_t drain_own(sw_encoder* h) {
+  hipError_t e = hipSuccess;
+  auto take = [&](hipError_t x) { if (e == hipSuccess) e = x; };
+  if (h->ws_done) take(hipEventSynchronize(h->ws_done));
+  for (hipStream_t s : {h->stream, h->s_h2d, h->s_d2h, h->s_fork[0], h->s_fork[1]})
+    if (s) take(hipStreamSynchronize(s));
+  return e;
+}
+
 extern "C" void sw_encoder_destroy(sw_encoder* h) {
   if (!h) return;
   {
     DeviceGuard g(h->device);
-    (void)hipDeviceSynchronize();  // (every stream of this encoder idle before anything is freed or unpinned)
+    (void)drain_own(h);  // (every stream of this encoder idle before anything is freed or unpinned)
     free_workspace(h);
     free_io(h);
     if (h->ws_done) (void)hipEventSynchronize(h->ws_done);
@@ -650,10 +664,9 @@ extern "C" int32_t sw_encoder_unpin_host(sw_encoder* h, void* ptr) {
   DeviceGuard g(h->device);
   for (size_t i = 0; i < h->pins.size(); ++i) {
     if (h->pins[i].h != (char*)ptr) continue;
-    // (nothing may still read or write it: the whole device drained, not only this encoder's
-    // streams -- a write into the range still in flight, or held in a cache, when its mapping goes
-    // faults the device; an intermittent fault after the pinned-output test was seen in rounds 4-5)
-    HIP_TRY(hipDeviceSynchronize());
+    // (nothing of this encoder may still read or write it -- a write into the range still in flight
+    // when its mapping goes faults the device -- and only this encoder's streams touch its pins)
+    HIP_TRY(drain_own(h));
     HIP_TRY(hipHostUnregister((void*)((uintptr_t)ptr & ~(uintptr_t)4095)));
     h->pins.erase(h->pins.begin() + (long)i);
     return SW_OK;

@@ -71,6 +71,9 @@ def parse():
                     help="N>1: each step's reassembly completes before the next step's encode")
     ap.add_argument("--cpu-sample-mb", type=float, default=320.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--small-steps", type=int, default=20,
+                    help="rank 0, N=1: per-call latency of ~64 KiB and ~1 MiB prefixes through the same handle after "
+                         "the big launches (0: skip)")
     ap.add_argument("--e2e-steps", type=int, default=2,
                     help="N=1: also time host buffers -> host buffers (PCIe-inclusive, reported beside value)")
     ap.add_argument("--threads", type=int, default=0,
@@ -456,6 +459,30 @@ def main():
         dom["traffic_source"] = traffic_src
     roofline["dominant"] = dom
 
+    # small launches after the big ones (rank 0, N=1): the same handle -- its dedupe table as the
+    # 1 GiB launches left it (grown, on the low-repetition corpus) -- on prefixes of the batch of about
+    # 64 KiB and 1 MiB through the device entry, each call synchronised: the per-call latency a small
+    # batch pays (the table clear runs in k_edges only when its grid covers the table)
+    small = None
+    if rank == 0 and world == 1 and args.small_steps > 0 and plain and not gather and not host_ps:
+        small = {}
+        for target in (1 << 16, 1 << 20):
+            k = max(1, int(np.searchsorted(off, target, side="right")) - 1)
+            nb = int(off[k])
+            ts = []
+            for _ in range(args.small_steps + 2):
+                torch.cuda.synchronize(dev)
+                t_s = time.perf_counter()
+                _lib.check(L.sw_encode_device(h, d_buf.data_ptr(), nb, d_off.data_ptr(), k, None, d_out.data_ptr(),
+                                              d_oo.data_ptr(), stream, None))
+                torch.cuda.synchronize(dev)
+                ts.append(time.perf_counter() - t_s)
+            ts = sorted(ts[2:])
+            small[str(nb)] = {"strings": k, "ms_median": round(ts[len(ts) // 2] * 1e3, 3), "ms_min": round(ts[0] * 1e3, 3),
+                              "mb_s_median": round(nb / ts[len(ts) // 2] / 1e6, 1)}
+        small["note"] = ("sw_encode_device on a prefix of the batch, the same handle after the timed launches, "
+                         "host clock around each call + device synchronise; median of %d calls" % args.small_steps)
+
     # PCIe-inclusive rate (rank 0, N=1): the same batch from host buffers to host buffers through
     # sw_encode_batch (Tokenizer.encode_packed).  Reported beside, never `value`.  Two modes: the
     # caller's arrays pinned once (Tokenizer.pin_host: the input read over PCIe by the copy kernel,
@@ -617,6 +644,7 @@ def main():
             "parity_vs_oracle_sample": parity,
             "reassembly_check": reassembly_ok,
             "e2e_pcie": e2e,
+            "small_batches": small,
             "host_prep_s": round(t_prep, 2),
             "host_split_s": round(t_split, 3) if (host_ps or specials) else None,
             "host_split_note": ("host threads, outside the timed GPU step: special-token occurrences%s (%d threads)" % (

@@ -887,7 +887,18 @@ struct DevSpecials {
 // The new table is allocated beside the old one and swapped in only when all three buffers exist:
 // growth is an optimisation, so an allocation failure keeps the table that works (and stops
 // further attempts on this handle) instead of leaving the handle half-built.
-int32_t grow_dedupe(sw_encoder* h) {
+// The entries of the dedupe table a launch of n bytes uses: a prefix sized for its bytes -- 2^16 at
+// least, one per 8 input bytes, at most what is allocated -- so that a small launch after a large
+// one, or after the table has grown for a low-repetition corpus, clears kilobytes instead of the
+// whole table (the 1 GiB launches use all of it: 2^22 entries by default, 2^24 grown)
+int64_t launch_dd_slots(const sw_encoder* h, int64_t n_bytes) {
+  int64_t want = 1LL << 16;
+  while (want < n_bytes / 8 && want < h->dd_slots) want <<= 1;
+  return std::min<int64_t>(want, h->dd_slots);
+}
+
+int32_t grow_dedupe(sw_encoder* h, int64_t n_bytes) {
+  if (launch_dd_slots(h, n_bytes) < h->dd_slots) return SW_OK;  // (a prefix launch: more entries would not serve it)
   const unsigned long long over = h->h_ddfull ? __atomic_load_n(h->h_ddfull, __ATOMIC_ACQUIRE) : 0ULL;
   constexpr int64_t kGrowDiv = 32;  // (grow when more than slots / this many chunks found no entry)
   if (!h->d_dtab || h->dedupe_slots || h->dd_grow_stop || over <= (unsigned long long)(h->dd_slots / kGrowDiv) ||
@@ -1118,7 +1129,7 @@ int32_t encode_device(sw_encoder* h, const uint8_t* d_bytes, int64_t n_bytes, co
   // the workspace belongs to the handle: order this launch after the previous one on any stream
   if (h->ws_pending && h->ws_stream != st) HIP_TRY(hipStreamWaitEvent(st, h->ws_done, 0));
   int32_t rc = ensure_workspace(h, n_bytes);
-  if (rc == SW_OK && h->dedupe) rc = grow_dedupe(h);
+  if (rc == SW_OK && h->dedupe) rc = grow_dedupe(h, n_bytes);
   if (rc) return rc;
   const int64_t n_tiles = (n_bytes + kTile - 1) / kTile;
   h->last_tiles = n_tiles;
@@ -1154,7 +1165,10 @@ int32_t encode_device(sw_encoder* h, const uint8_t* d_bytes, int64_t n_bytes, co
     a.scratch = h->d_scratch; a.res = h->d_res;
     a.tile_slots = h->d_tile_slots; a.tile_nref = h->d_tile_nref; a.rlist = h->d_rlist; a.tile_cnt = h->d_tile_cnt;
     a.dtab = h->d_dtab; a.dedupe = h->dedupe ? 1u : 0u; a.dfp_mask = h->dedupe_fp_mask;
-    a.dmask = h->dedupe_slots ? std::min<uint32_t>(h->dmask, (uint32_t)(h->dedupe_slots - 1)) : h->dmask;
+    {
+      const uint32_t lmask = (uint32_t)(launch_dd_slots(h, n_bytes) - 1);
+      a.dmask = h->dedupe_slots ? std::min<uint32_t>(lmask, (uint32_t)(h->dedupe_slots - 1)) : lmask;
+    }
     a.dexact = h->dedupe_exact ? (uint32_t)kDdExactMax : 0u;
     a.dres = h->d_dres;
     a.dcnt = h->d_dcnt;

@@ -391,8 +391,15 @@ def test_dedupe_table_grows_and_clears_itself():
         assert_same(gpu_encode(t, buf, off), exp)
         if rep == 0:
             slots0 = L.sw_encoder_get_info(h, _lib.SW_INFO_DEDUPE_SLOTS)
-    assert L.sw_encoder_get_info(h, _lib.SW_INFO_DEDUPE_SLOTS) > slots0
-    assert_same(gpu_encode(t, buf2, off2), oracle_encode(t.merges, buf2, off2, "cl100k"))
+    grown = L.sw_encoder_get_info(h, _lib.SW_INFO_DEDUPE_SLOTS)
+    assert grown > slots0
+    # smaller launches after growth use (and clear) a prefix of the table sized for their bytes
+    # (launch_dd_slots) and never grow it; the whole table again for the large batch after them
+    buf3, off3 = corpus.synth(33, corpus.ENTROPY, 40, 900)
+    for b, o in ((buf2, off2), (buf3, off3), (buf2, off2)):
+        assert_same(gpu_encode(t, b, o), oracle_encode(t.merges, b, o, "cl100k"))
+    assert L.sw_encoder_get_info(h, _lib.SW_INFO_DEDUPE_SLOTS) == grown
+    assert_same(gpu_encode(t, buf, off), exp)
 
 
 def test_dedupe_options_validated():

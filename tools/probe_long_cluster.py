@@ -1,13 +1,15 @@
 """Probe (GPU box): the device specials finder on long runs of self-overlapping specials (the
 global-memory path's cluster walk) -- time and equality with the host finder."""
+import os
 import sys
 import time
 
 import numpy as np
 import torch
 
-sys.path.insert(0, ".")
-sys.path.insert(0, "tests")
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "tests"))
 import shredword_amd as sa  # noqa: E402
 from shredword_amd import corpus  # noqa: E402
 from conftest import load_model_merges  # noqa: E402

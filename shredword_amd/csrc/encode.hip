@@ -1098,7 +1098,7 @@ int32_t find_specials_device(sw_encoder* h, const uint8_t* d_bytes, int64_t n_by
     const dim3 gg(std::min<unsigned>(gw.x, kSfGlobalBlocks));
     if (swar) hipLaunchKernelGGL(k_sp_detect<true>, gg, bw, 0, st, h->spt, f);
     else hipLaunchKernelGGL(k_sp_detect<false>, gg, bw, 0, st, h->spt, f);
-    hipLaunchKernelGGL(k_sp_resolve, gg, bw, 0, st, h->spt, f);
+    hipLaunchKernelGGL(k_sp_resolve, gg, bw, lds_tab, st, h->spt, f);
     hipLaunchKernelGGL(k_sp_count, gg, bw, 0, st, f);
     HIP_TRY(launch_scan(st, f.tcnt, n_tiles, toff2 + n_tiles, toff2, total2));
     hipLaunchKernelGGL(k_sp_write, gg, bw, 0, st, h->spt, f, (const int64_t*)toff2, d_pos, d_len, d_id);

@@ -174,37 +174,6 @@ __device__ __forceinline__ int64_t sp_next_cand(const SpFind& f, int64_t q, int6
   return -1;
 }
 
-__global__ void __launch_bounds__(kThreads) k_sp_resolve(SpTab T, SpFind f) {
-  if (__hip_atomic_load(f.flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) return;
-  const int lane = threadIdx.x & 63;
-  for (int64_t t = (int64_t)blockIdx.x * kWaves + wave_in_block(); t < f.n_tiles; t += (int64_t)gridDim.x * kWaves) {
-  if (f.tcand[t] == 0) continue;
-  const int64_t p0 = (t << kTileBits) + 32 * lane;
-  for (uint32_t x = f.cbits[t * 64 + lane]; x; x &= x - 1) {
-    const int64_t p = p0 + __builtin_ctz(x);
-    // clean: no earlier candidate covers p (candidates never cross a string; one inside an earlier
-    // tile is read from its bits too)
-    bool clean = true;
-    for (int64_t q = sp_next_cand(f, max(p - (T.max_len - 1), (int64_t)0), p); q >= 0 && clean;
-         q = sp_next_cand(f, q + 1, p))
-      clean = q + sp_len_at(T, f, q) <= p;
-    if (!clean) continue;  // (decided by the walk from its cluster's clean head)
-    const int32_t L = sp_len_at(T, f, p);
-    atomicOr(&f.chosen[p >> 5], 1u << (p & 31));
-    // the cluster of candidates overlapping p's, left to right as the sequential scan goes
-    int64_t span = p + L, taken = p + L;
-    for (int64_t r = sp_next_cand(f, p + 1, span); r >= 0; r = sp_next_cand(f, r + 1, span)) {
-      const int32_t Lr = sp_len_at(T, f, r);
-      if (r >= taken) {
-        atomicOr(&f.chosen[r >> 5], 1u << (r & 31));
-        taken = r + Lr;
-      }
-      span = max(span, r + (int64_t)Lr);
-    }
-  }
-  }
-}
-
 __global__ void __launch_bounds__(kThreads) k_sp_count(SpFind f) {
   if (__hip_atomic_load(f.flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) return;
   const int lane = threadIdx.x & 63;
@@ -282,6 +251,121 @@ __device__ __forceinline__ int sf_end_after(const SfShared& m, int r) {
   const uint64_t lo = ((uint64_t)m.ss[w + 1] << 32) | m.ss[w];
   const uint64_t bits = (lo >> sh) | (sh ? (uint64_t)m.ss[w + 2] << (64 - sh) : 0ULL);
   return bits ? q + __builtin_ctzll(bits) : q + 64;
+}
+
+// ---- the global path's cluster walks ----------------------------------------------------------
+// k_sp_resolve: the clean candidates (no earlier candidate covers them) found lane by lane, then each
+// one's cluster walked by the whole wave, left to right as the sequential scan goes, 64 positions a
+// step: the step's candidate bits and its 128 bytes (every special starting in it fits) staged in
+// the wave's LDS, each lane matching one position against the LDS records, and the step's choices
+// made in order over the lanes' lengths -- where one lane walking one candidate a step of dependent
+// table loads took ~1 us a position of a run of self-overlapping specials (ADVICE r5;
+// tools/probe_long_cluster.py)
+constexpr int kSrWinWords = 32;  // 128 bytes: 64 positions + the longest special (64)
+
+// the special matching at window offset j (< 64) inside [j, end) (end: the string's end, window-relative)
+__device__ __forceinline__ int sr_match(const uint32_t* s, const SpTab& T, const uint32_t* win, int j, int64_t end) {
+  uint32_t x[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) x[q] = __builtin_amdgcn_alignbyte(win[(j >> 2) + q + 1], win[(j >> 2) + q], (uint32_t)(j & 3));
+  const int b = (int)(x[0] & 0xFFu);
+  const int g1 = sft_group(s, T.o_first, b + 1);
+  const uint8_t* wb = (const uint8_t*)win;
+  for (int gi = sft_group(s, T.o_first, b); gi < g1; ++gi) {
+    const uint4 w = *(const uint4*)(s + T.o_rec + kSfRecWords * gi);
+    const uint4 mk4 = *(const uint4*)(s + T.o_rec + kSfRecWords * gi + 4);
+    const uint32_t tag = s[T.o_tag + gi];
+    const int L = (int)((tag >> 8) & 0xFFu);
+    if (j + L > end) continue;
+    bool same = (((x[0] ^ w.x) & mk4.x) | ((x[1] ^ w.y) & mk4.y) | ((x[2] ^ w.z) & mk4.z) | ((x[3] ^ w.w) & mk4.w)) == 0;
+    const uint8_t* sb = (const uint8_t*)(s + T.o_words + (int)(tag >> 16));
+    for (int q = 16; q < L && same; ++q) same = wb[j + q] == sb[q];
+    if (same) return (int)(tag & 0xFFu);
+  }
+  return -1;
+}
+
+// the cluster of clean candidate p (wave-uniform), walked by the whole wave
+__device__ __forceinline__ void sr_walk(const uint32_t* s, const SpTab& T, const SpFind& f, uint32_t* win, int64_t p,
+                                        int lane) {
+  const int64_t E = sp_str_end(f, p);  // (the cluster lies in p's string: no match crosses its end)
+  const int32_t L = sp_len_at(T, f, p);
+  if (lane == 0) atomicOr(&f.chosen[p >> 5], 1u << (p & 31));
+  int64_t span = p + L, taken = p + L;
+  const bool al4 = ((uintptr_t)f.bytes & 3) == 0;
+  for (int64_t w0 = (p + 1) & ~(int64_t)63; w0 < span && w0 < f.n_bytes; w0 += 64) {
+    uint64_t cand = (uint64_t)f.cbits[w0 >> 5] | ((uint64_t)f.cbits[(w0 >> 5) + 1] << 32);
+    uint32_t v = 0;  // (the window's bytes, loaded beside its candidate bits: one round trip a step)
+    if (lane < kSrWinWords) {
+      const int64_t q = w0 + 4 * lane;
+      if (al4 && q + 4 <= f.n_bytes) {
+        v = *(const uint32_t*)(f.bytes + q);
+      } else {
+        for (int k = 0; k < 4; ++k) v |= (q + k < f.n_bytes ? (uint32_t)f.bytes[q + k] : 0u) << (8 * k);
+      }
+    }
+    if (w0 < p + 1) cand &= ~0ULL << (int)(p + 1 - w0);
+    if (!cand) continue;
+    if (lane < kSrWinWords) win[lane] = v;
+    if (lane == 0) win[kSrWinWords] = 0u;  // (the word after the window: read by the alignbyte of the last, masked out)
+    wave_sync_mem();
+    int Li = 0;  // (this lane's position's match length, 0: none)
+    if ((cand >> lane) & 1ULL) {
+      const int k = sr_match(s, T, win, lane, E - w0);
+      Li = k < 0 ? 0 : sft_len(s, k);
+    }
+    uint64_t ch = 0;
+    bool stop = false;
+    for (uint64_t m = cand; m; m &= m - 1) {  // (in order; wave-uniform)
+      const int i = __builtin_ctzll(m);
+      const int64_t r = w0 + i;
+      if (r >= span) {
+        stop = true;
+        break;
+      }
+      const int Lr = __builtin_amdgcn_readlane(Li, i);  // (i is wave-uniform: a scalar read of lane i)
+      if (r >= taken) {
+        ch |= 1ULL << i;
+        taken = r + Lr;
+      }
+      span = max(span, r + (int64_t)Lr);
+    }
+    if (lane == 0 && (uint32_t)ch) atomicOr(&f.chosen[w0 >> 5], (uint32_t)ch);
+    if (lane == 1 && (uint32_t)(ch >> 32)) atomicOr(&f.chosen[(w0 >> 5) + 1], (uint32_t)(ch >> 32));
+    wave_sync_mem();  // (the window is rewritten by the next step)
+    if (stop) break;
+  }
+}
+
+__global__ void __launch_bounds__(kThreads) k_sp_resolve(SpTab T, SpFind f) {
+  if (__hip_atomic_load(f.flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) return;
+  extern __shared__ __align__(16) uint32_t s_sft[];  // T.img (its records)
+  __shared__ uint32_t s_win[kWaves][kSrWinWords + 4];
+  for (int i = threadIdx.x; i < T.img_words; i += kThreads) s_sft[i] = T.img[i];
+  __syncthreads();
+  const uint32_t* s = s_sft;
+  uint32_t* win = s_win[wave_in_block()];
+  const int lane = threadIdx.x & 63;
+  for (int64_t t = (int64_t)blockIdx.x * kWaves + wave_in_block(); t < f.n_tiles; t += (int64_t)gridDim.x * kWaves) {
+    if (f.tcand[t] == 0) continue;
+    const int64_t p0 = (t << kTileBits) + 32 * lane;
+    uint32_t heads = 0;  // this lane's clean candidates
+    for (uint32_t x = f.cbits[t * 64 + lane]; x; x &= x - 1) {
+      const int64_t p = p0 + __builtin_ctz(x);
+      // clean: no earlier candidate covers p (candidates never cross a string; one inside an earlier
+      // tile is read from its bits too)
+      bool clean = true;
+      for (int64_t q = sp_next_cand(f, max(p - (T.max_len - 1), (int64_t)0), p); q >= 0 && clean;
+           q = sp_next_cand(f, q + 1, p))
+        clean = q + sp_len_at(T, f, q) <= p;
+      if (clean) heads |= 1u << __builtin_ctz(x);
+    }
+    for (uint64_t hl = __ballot(heads != 0); hl; hl &= hl - 1) {  // (the walks, one head at a time)
+      const int hlane = __builtin_ctzll(hl);
+      for (uint32_t hb = (uint32_t)__shfl((int)heads, hlane, 64); hb; hb &= hb - 1)
+        sr_walk(s, T, f, win, (t << kTileBits) + 32 * hlane + __builtin_ctz(hb), lane);
+    }
+  }
 }
 
 // the next candidate at or after q, below lim (lim when none)

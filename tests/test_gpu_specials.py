@@ -214,6 +214,31 @@ def test_device_finder_equals_host_finder(case):
     t.close()
 
 
+@pytest.mark.parametrize("order", [0, 1])
+def test_long_self_overlapping_run(order):
+    """A cluster far longer than k_sp_find's window (a 4 MiB run of one letter with "aa" and "aaa",
+    both dict orders) goes to the global path, whose walk takes 32 positions a step from a window
+    staged in LDS: equal to the host finder, and bounded in time (the walk of one candidate a
+    step of table loads took ~1 us a position)."""
+    import time
+    import torch
+    sp = {"aa": 300, "aaa": 301} if order == 0 else {"aaa": 301, "aa": 300}
+    t = tok_for("bl32k.model")
+    t.special_tokens = sp
+    buf, off = pack([b"x" + b"a" * (4 << 20) + b"y", b"ab" * 100, b"a" * 7, b"aaaa" * 3000])
+    d_buf = torch.from_numpy(buf).to("cuda:0")
+    d_off = torch.from_numpy(off).to("cuda:0")
+    t0 = time.perf_counter()
+    pos, ln, ids, cnt, n = t.find_specials_device(d_buf, d_off, sync=True)
+    dt = time.perf_counter() - t0
+    h_pos, h_len, h_id = corpus.find_specials(buf, off, sp)
+    np.testing.assert_array_equal(pos[:n].cpu().numpy(), h_pos)
+    np.testing.assert_array_equal(ln[:n].cpu().numpy(), h_len)
+    np.testing.assert_array_equal(ids[:n].cpu().numpy(), h_id)
+    assert dt < 1.5, dt
+    t.close()
+
+
 @pytest.mark.parametrize("pattern", ["cl100k", "gpt2"])
 def test_encode_with_device_found_specials(pattern):
     """The whole specials path on the device: find (sw_find_specials_device) -> encode

@@ -314,21 +314,40 @@ __device__ __forceinline__ void sr_walk(const uint32_t* s, const SpTab& T, const
       const int k = sr_match(s, T, win, lane, E - w0);
       Li = k < 0 ? 0 : sft_len(s, k);
     }
+    // the step's choices without a lane-serial pass: the cluster ends at the first candidate no earlier
+    // one reaches (a prefix max of the candidates' ends), and the choices are the chain from the first
+    // candidate at or after `taken`, each one's successor the first candidate at or after its end
+    const bool c = ((cand >> lane) & 1ULL) != 0;
+    const int64_t sp_rel = span - w0, tk_rel = taken - w0;  // (wave-uniform)
+    int ext = c ? lane + Li : -1;  // (a candidate's end, window-relative)
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {  // inclusive prefix max over the lanes
+      const int o = __shfl_up(ext, d, 64);
+      if (lane >= d) ext = max(ext, o);
+    }
+    const int before = __shfl_up(ext, 1, 64);  // (exclusive: the candidates before this lane)
+    const int64_t reach = max(sp_rel, (int64_t)(lane == 0 ? -1 : before));
+    const uint64_t ends = __ballot(c && (int64_t)lane >= reach);
+    const int s_end = ends ? __builtin_ctzll(ends) : 64;  // (the first candidate past the cluster)
+    const bool stop = ends != 0;
+    const uint64_t live = cand & (s_end >= 64 ? ~0ULL : ((1ULL << s_end) - 1ULL));
+    // successor of lane i: the first live candidate at or after i + L_i (64: none in this step)
+    const int e = lane + max(Li, 1);  // (a live candidate always matches, L >= 1; the guard keeps the hops moving)
+    const uint64_t after = e >= 64 ? 0ULL : (live & (~0ULL << e));
+    const int nxt = after ? __builtin_ctzll(after) : 64;
     uint64_t ch = 0;
-    bool stop = false;
-    for (uint64_t m = cand; m; m &= m - 1) {  // (in order; wave-uniform)
-      const int i = __builtin_ctzll(m);
-      const int64_t r = w0 + i;
-      if (r >= span) {
-        stop = true;
-        break;
+    int last = -1;
+    {
+      const uint64_t from = tk_rel <= 0 ? live : tk_rel >= 64 ? 0ULL : (live & (~0ULL << (int)tk_rel));
+      for (int r = from ? __builtin_ctzll(from) : 64; r < 64; r = __builtin_amdgcn_readlane(nxt, r)) {
+        ch |= 1ULL << r;
+        last = r;
       }
-      const int Lr = __builtin_amdgcn_readlane(Li, i);  // (i is wave-uniform: a scalar read of lane i)
-      if (r >= taken) {
-        ch |= 1ULL << i;
-        taken = r + Lr;
-      }
-      span = max(span, r + (int64_t)Lr);
+    }
+    if (last >= 0) taken = w0 + last + __builtin_amdgcn_readlane(Li, last);
+    {
+      const int lm = live ? 63 - __builtin_clzll(live) : -1;  // (the last live candidate: the running max there)
+      if (lm >= 0) span = max(span, w0 + (int64_t)__builtin_amdgcn_readlane(ext, lm));
     }
     if (lane == 0 && (uint32_t)ch) atomicOr(&f.chosen[w0 >> 5], (uint32_t)ch);
     if (lane == 1 && (uint32_t)(ch >> 32)) atomicOr(&f.chosen[(w0 >> 5) + 1], (uint32_t)(ch >> 32));

@@ -257,10 +257,10 @@ __device__ __forceinline__ int sf_end_after(const SfShared& m, int r) {
 // k_sp_resolve: the clean candidates (no earlier candidate covers them) found lane by lane, then each
 // one's cluster walked by the whole wave, left to right as the sequential scan goes, 64 positions a
 // step: the step's candidate bits and its 128 bytes (every special starting in it fits) staged in
-// the wave's LDS, each lane matching one position against the LDS records, and the step's choices
-// made in order over the lanes' lengths -- where one lane walking one candidate a step of dependent
-// table loads took ~1 us a position of a run of self-overlapping specials (ADVICE r5;
-// tools/probe_long_cluster.py)
+// the wave's LDS, each lane matching one position against the LDS records; the step's end of the
+// cluster by a prefix max of the candidates' ends and its choices by successor pointers (sr_walk)
+// -- where one lane walking one candidate a step of dependent table loads took ~1 us a position of
+// a run of self-overlapping specials, this takes ~35 ns (tools/probe_long_cluster.py)
 constexpr int kSrWinWords = 32;  // 128 bytes: 64 positions + the longest special (64)
 
 // the special matching at window offset j (< 64) inside [j, end) (end: the string's end, window-relative)

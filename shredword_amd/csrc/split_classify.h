@@ -419,11 +419,10 @@ __device__ __forceinline__ void split_classify_tile(const EncArgs& a, const PbAr
     sm.in[lane] = 0u;
     wave_sync_mem();
     const int64_t w0 = t0 - kScSsPre, w1 = w0 + (int64_t)kScSsWords * 32;
-    // (the first occurrence ending at or after w0, in tile - 1's range: see sp_first_end; the
-    // indices are loaded here, not at the start: held through the class masks they cost 0.27 ms
-    // with a vector tile index, r6q, and gave nothing with the scalar one, r7x)
-    // (the first occurrence ending at or after w0 = t0 - 64 from k_tile_specials: one load beside the
-    // live count, where a 64-wide search of the tile's range took one to two more round trips)
+    // (the first occurrence ending at or after w0 = t0 - 64, from k_tile_specials: one load beside
+    // the live count, where a 64-wide search of the tile's range took one to two more round trips;
+    // loaded here, not at the start: held through the class masks the indices cost 0.27 ms with a
+    // vector tile index, r6q, and gave nothing with the scalar one, r7x)
     const int64_t nsp = a.sp.tile_sp[a.n_tiles];
     const int64_t j_first = a.sp.tile_spw[tile];
     for (int64_t j0 = j_first; j0 < nsp; j0 += 64) {

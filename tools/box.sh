@@ -30,7 +30,7 @@ bench() {  # name args...
   local name=$1; shift
   run "bench_$name" 400 python -u bench.py "$@"
 }
-NB=(--no-cpu-baseline --e2e-steps 0)
+NB=(--no-cpu-baseline --e2e-steps 0 --small-steps 0)
 for s in "$@"; do
   case $s in
     pytest) run pytest 1100 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread ;;

@@ -19,7 +19,7 @@ for spec in "$@"; do
   name=${name//_so_/_}
   names+=("$name")
   SHREDWORD_HIP_LIB=$R/shredword_amd/$lib timeout -k 10 240 rocprofv3 --kernel-trace --stats -d "$OUT/$name" -o run \
-    --output-format csv -- python3 "$R/bench.py" --steps 5 --warmup 1 --no-cpu-baseline --e2e-steps 0 ${BENCH_ARGS:-} $extra \
+    --output-format csv -- python3 "$R/bench.py" --steps 5 --warmup 1 --no-cpu-baseline --e2e-steps 0 --small-steps 0 ${BENCH_ARGS:-} $extra \
     > "$OUT/$name.log" 2>&1
   rc=$?; echo "$name rc=$rc" >> "$OUT/status.txt"
   [ $rc -eq 0 ] || exit $rc

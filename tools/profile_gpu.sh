@@ -10,7 +10,7 @@ OUT=$R/gpurun_out/prof_$TAG
 mkdir -p "$OUT"
 export TMPDIR=/tmp
 cd /tmp
-BENCH=(python3 "$R/bench.py" --steps 3 --warmup 1 --no-cpu-baseline --e2e-steps 0 "$@")
+BENCH=(python3 "$R/bench.py" --steps 3 --warmup 1 --no-cpu-baseline --e2e-steps 0 --small-steps 0 "$@")
 fatal() { case $1 in 124|134|137|139) echo "fatal rc=$1 in $2" >> "$OUT/status.txt"; exit $1;; esac; }
 rocprofv3 -L > "$OUT/counters_available.txt" 2>&1
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/trace" -o run --output-format csv -- "${BENCH[@]}" > "$OUT/trace.log" 2>&1

@@ -2515,25 +2515,11 @@ __device__ __forceinline__ void compact_tile(const EncArgs& a, int64_t t, int64_
       if (many && valid) a.scratch[t * kTile + j] = (int32_t)o;  // (this wave's own slots)
     }
     wave_sync_mem();
-    // the staged ids: one contiguous 256-byte store per 64 ids
+    // the staged ids: one contiguous 256-byte store per 64 ids, each lane reading its own LDS word
+    // (round 6: 16-byte stores of four ids a lane read those words at a 4-word lane stride, and the
+    // bank conflicts cost more than the stores saved -- C2 k_compact7 0.832 -> 0.813 ms, r9zi)
     const uint32_t staged = min(carry - gbase, (uint32_t)kOutCap);
-    if constexpr (kTyped && sizeof(OutT) == 4) {
-      // (16-byte stores, four ids a lane, from the output's first 16-byte boundary on; the ids
-      // before it one a lane)
-      const uint32_t mis4 = (uint32_t)(((uintptr_t)(out + base + gbase) >> 2) & 3u);
-      const uint32_t head = min((4u - mis4) & 3u, staged);
-      if (lane < head) SW_STNT(&dst[gbase + lane], (OutT)s_out[lane]);
-      for (uint32_t i = head + 4 * lane; i < staged; i += 256) {
-        if (i + 3 < staged) {
-          const u32x4 v = {(uint32_t)s_out[i], (uint32_t)s_out[i + 1], (uint32_t)s_out[i + 2], (uint32_t)s_out[i + 3]};
-          SW_STNT((SW_AS_GLOBAL u32x4*)&dst[gbase + i], v);
-        } else {
-          for (uint32_t k = i; k < staged; ++k) SW_STNT(&dst[gbase + k], (OutT)s_out[k]);
-        }
-      }
-    } else {
-      for (uint32_t i = lane; i < staged; i += 64) SW_STNT(&dst[gbase + i], (OutT)s_out[i]);
-    }
+    for (uint32_t i = lane; i < staged; i += 64) SW_STNT(&dst[gbase + i], (OutT)s_out[i]);
     refs_before += nref;
     wave_sync_mem();  // (s_rp / s_rq / s_out are rewritten by the next group)
 #ifdef SW_STAMPS
